@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: minisched's scheduling cycle on MI355X.
+
+Metric (BASELINE.json): pod x node filter+score evals/sec (and pods scheduled/sec)
+at 100k nodes on 1/2/4/8 GPUs -> workload = config C: 100,000 nodes x
+100,000 pods, NodeUnschedulable + NodeNumber, node-sharded across ranks with
+one RCCL MAX all-reduce of the packed keys per step.
+
+One step = the whole batch through the hot path with inputs resident in HBM:
+  ms_sweep_device (fused filter->score->argmax over this rank's node shard)
+  -> all_reduce(keys, MAX) over RCCL (N > 1)
+  -> ms_decode_device (packed key -> node / code / score / FitError mask).
+value = P * N_total / step time (max over ranks), i.e. whole-job evals/s.
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver
+uses torch.distributed.run with one rank per GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
+
+METRIC = "pod×node filter+score evals/sec and pods scheduled/sec at 100k nodes, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+BYTES_PER_EVAL = {"NU+NN": 2, "NU+NRF+NN+LA": 58}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C", choices=["B", "C", "D"])
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_C.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(n_nodes, seed, target_s):
+    """Oracle (C restatement, OpenMP) on all nodes x a pod prefix, host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle  # checker only; never on the measured GPU path
+
+    from minisched_amd import synth
+
+    threads = min(16, os.cpu_count() or 1)  # the box's CPU share is 16
+    nr = synth.nodes(n_nodes, seed=seed)
+    probe = synth.pods(64, seed=seed)
+    t0 = time.perf_counter()
+    _oracle.schedule_nunn_omp(nr, probe, seed=seed, threads=threads)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    n_pods = int(min(200_000, max(64, 64 * target_s / dt)))
+    pr = synth.pods(n_pods, seed=seed)
+    t0 = time.perf_counter()
+    _oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": n_pods * n_nodes / dt,
+        "unit": "pod×node evals/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle/ms_oracle.c msor_schedule_nunn_omp, {n_nodes} nodes x first {n_pods} pods "
+        f"({dt:.1f} s, OpenMP {threads} threads); Go reference not buildable offline (GOMAXPROCS n/a)",
+        "pods_per_s": n_pods / dt,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from minisched_amd import _lib, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = synth.CONFIGS[args.config]
+    N, P = cfg["nodes"], cfg["pods"]
+    plugins = cfg["plugins"]
+    lo, hi = rank * N // world, (rank + 1) * N // world  # this rank's node shard
+
+    eng = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NN, node_base=lo, seed=args.seed,
+                      device=local)
+    eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=args.seed, start=lo))
+    eng.flush()
+
+    pods_np = synth.pods(P, seed=args.seed)
+    pods = torch.from_numpy(pods_np.view(np.uint8).copy()).to(dev)
+    keys = torch.empty(P, dtype=torch.int64, device=dev)
+    results = torch.empty(P * _lib.RESULT.itemsize, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    sweep_events = []
+
+    def step(timed):
+        if timed:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        eng.sweep_device(P, pods.data_ptr(), keys.data_ptr(), 0, sp)
+        if timed:
+            b.record(stream)
+            sweep_events.append((a, b))
+        if world > 1:
+            dist.all_reduce(keys, op=dist.ReduceOp.MAX)
+        eng.decode_device(P, pods.data_ptr(), keys.data_ptr(), 0, N, results.data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in sweep_events]))
+    res = results.cpu().numpy().view(_lib.RESULT)
+    ok = int((res["code"] == _lib.CODE_SUCCESS).sum())
+
+    if rank == 0:
+        ms_step = elapsed * 1e3 / args.steps
+        evals = float(P) * float(N)
+        value = evals * args.steps / elapsed
+        local_evals = float(P) * float(hi - lo)
+        achieved = local_evals * BYTES_PER_EVAL[plugins] / (sweep_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json) and world == 1:
+            try:
+                traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "pod×node evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": f"synthetic (splitmix64 seed {args.seed}, BASELINE.md §3)",
+            "config": {
+                "workload": f"{args.config}: {N} nodes x {P} pods, {plugins}, batched, node-sharded over {world} GPU",
+                "nodes": N,
+                "pods": P,
+                "plugins": plugins,
+                "parallelism": f"node-shard{world}",
+            },
+            "pods_per_s": P * args.steps / elapsed,
+            "pods_scheduled": ok,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_sweep_nunn",
+                "kernel_ms": sweep_ms,
+                "algorithmic_bytes_per_launch": local_evals * BYTES_PER_EVAL[plugins],
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

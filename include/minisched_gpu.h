@@ -1,0 +1,190 @@
+/*
+ * minisched_gpu.h — C ABI of the MI355X scheduling-cycle engine.
+ *
+ * This is the drop-in boundary for minisched's per-pod scheduling cycle
+ * (reference: /root/reference/minisched/minisched.go). In the reference one
+ * goroutine runs, per pod:
+ *     Nodes().List            minisched.go:40
+ *     RunFilterPlugins        minisched.go:115-151  (NodeUnschedulable)
+ *     RunPreScorePlugins      minisched.go:153-162  (NodeNumber.PreScore)
+ *     RunScorePlugins         minisched.go:164-199  (NodeNumber.Score, unweighted sum)
+ *     selectHost              minisched.go:304-325  (argmax, random tie-break)
+ * A cgo shim calls ms_schedule_batch() in place of minisched.go:40-85 and
+ * keeps the queue (:34), Permit (:89-94), the bind goroutine (:96-112) and
+ * ErrorFunc (:283-298) in Go. INTEGRATION.md shows that shim.
+ *
+ * Plain C types only: no HIP, torch or C++ types cross this boundary. Every
+ * function returns 0 (MS_OK) or a negative MS_E_* code and never aborts the
+ * process; per-pod outcomes are data in ms_result, not errors.
+ *
+ * Node ordinals are global (0 .. 2^20-2). A context owns the contiguous
+ * ordinal range [node_base, node_base + max_nodes) — one shard when nodes are
+ * split across GPUs. The tie-break that replaces rand.Intn
+ * (minisched.go:316-321) is the packed key
+ *     key = score<<52 | h32(seed,pod,node)<<20 | (0xFFFFF - node),
+ *     h32 = fmix32(fmix32(seed32 ^ pod_ordinal) ^ (node * 0x9E3779B1)),
+ *     seed32 = (uint32)(seed ^ seed>>32),
+ * maximum wins; it is a pure function of (seed, pod, node) so the result does
+ * not depend on scan order, sharding or reduction tree.
+ */
+#ifndef MINISCHED_GPU_H
+#define MINISCHED_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MS_ABI_VERSION 1
+
+/* ---- return codes -------------------------------------------------------- */
+#define MS_OK 0
+#define MS_E_INVAL (-1)    /* bad argument / state                         */
+#define MS_E_HIP (-2)      /* a HIP runtime call failed                    */
+#define MS_E_RCCL (-3)     /* reserved: in-library collectives             */
+#define MS_E_OOM (-4)      /* device or pinned allocation failed          */
+#define MS_E_CAPACITY (-5) /* ordinal outside this context's node range    */
+#define MS_E_NODEV (-6)    /* no usable gfx950 device                      */
+
+/* ---- plugin sets (minisched/initialize.go:80-138 hard-codes the first) --- */
+#define MS_PLUGINS_NU_NN 0        /* Filter[NodeUnschedulable]; Score[NodeNumber]            */
+#define MS_PLUGINS_NU_NRF_NN_LA 1 /* Filter[NU, NodeResourcesFit]; Score[NN, LeastAllocated] */
+
+/* ---- modes --------------------------------------------------------------- */
+#define MS_MODE_BATCHED 0    /* all pods of the call see the same node state               */
+#define MS_MODE_SEQUENTIAL 1 /* queue order; each winner's NodeInfo.AddPod lands before the
+                                next pod is decided (assume-on-select)                       */
+
+/* ---- per-pod outcome (ms_result.code) ------------------------------------ */
+#define MS_CODE_SUCCESS 0       /* node selected                                        */
+#define MS_CODE_ERROR 1         /* framework.Error from a score plugin: NodeNumber with a
+                                   non-digit pod name (nodenumber.go:53-56,74-77); the
+                                   reference's ErrorFunc sees a non-FitError              */
+#define MS_CODE_UNSCHEDULABLE 2 /* *framework.FitError (minisched.go:143-148)            */
+
+/* ms_result.plugin_mask = FitError Diagnosis.UnschedulablePlugins */
+#define MS_MASK_NODE_UNSCHEDULABLE (1u << 0) /* "NodeUnschedulable" */
+#define MS_MASK_NODE_RESOURCES_FIT (1u << 1) /* "NodeResourcesFit"  */
+
+#define MS_MAX_ORDINAL 0xFFFFEu
+
+/* Flat node record (v1.Node + framework.NodeInfo columns the plugins read).
+ * 64 bytes. Resource columns are ignored by MS_PLUGINS_NU_NN. */
+typedef struct ms_node_rec {
+    uint8_t unschedulable; /* node.Spec.Unschedulable                              */
+    uint8_t name_digit;    /* last char of node name as 0..9; 0xFF = not a digit     */
+    uint8_t _pad0[2];
+    int32_t allowed_pods;  /* NodeInfo.Allocatable.AllowedPodNumber                 */
+    int32_t pod_count;     /* len(NodeInfo.Pods)                                    */
+    int32_t _pad1;
+    int64_t alloc_milli_cpu, alloc_memory;     /* NodeInfo.Allocatable             */
+    int64_t req_milli_cpu, req_memory;         /* NodeInfo.Requested               */
+    int64_t nonzero_milli_cpu, nonzero_memory; /* NodeInfo.NonZeroRequested        */
+} ms_node_rec;
+
+/* Flat pod record. 40 bytes. */
+typedef struct ms_pod_rec {
+    uint32_t ordinal;                /* stable pod id fed to the tie-break           */
+    int8_t name_digit;               /* last char of pod name as 0..9; -1 = not     */
+    uint8_t tolerates_unschedulable; /* TolerationsTolerateTaint(unschedulable:NoSchedule) */
+    uint8_t _pad[2];
+    int64_t req_milli_cpu, req_memory;         /* Fit PreFilter request              */
+    int64_t nonzero_milli_cpu, nonzero_memory; /* GetNonzeroRequests sum            */
+} ms_pod_rec;
+
+/* Per-pod result. 24 bytes. */
+typedef struct ms_result {
+    int32_t node;         /* global ordinal of the selected node; -1 if none     */
+    int32_t code;         /* MS_CODE_*                                            */
+    int64_t score;        /* summed score of the selected node                    */
+    uint32_t plugin_mask; /* MS_MASK_* when code == MS_CODE_UNSCHEDULABLE, else 0 */
+    uint32_t _pad;
+} ms_result;
+
+typedef struct ms_config {
+    int32_t device;      /* HIP device ordinal (within HIP_VISIBLE_DEVICES)     */
+    int32_t plugin_set;  /* MS_PLUGINS_*                                        */
+    uint32_t max_nodes;  /* node capacity of this context                       */
+    uint32_t node_base;  /* global ordinal of local node 0 (shard offset)       */
+    uint32_t max_batch;  /* pods per internal chunk of ms_schedule_batch        */
+    uint32_t _reserved;
+    uint64_t seed;       /* tie-break seed                                      */
+} ms_config;
+
+typedef struct ms_info {
+    uint32_t max_nodes, node_base;
+    uint32_t present_nodes;  /* nodes currently in the table (not tombstoned)  */
+    uint32_t pending_deltas; /* queued upserts/deletes not yet on the device   */
+    int32_t device, plugin_set;
+    uint64_t seed;
+} ms_info;
+
+typedef struct ms_ctx ms_ctx;
+
+int ms_abi_version(void);
+int ms_device_count(int *out_count);
+
+int ms_create(const ms_config *cfg, ms_ctx **out_ctx);
+int ms_destroy(ms_ctx *ctx);
+/* Message of the last failure on ctx (or of the last failed ms_create on this
+ * thread when ctx is NULL). Never NULL. */
+const char *ms_last_error(const ms_ctx *ctx);
+int ms_get_info(const ms_ctx *ctx, ms_info *out);
+
+/* ---- node deltas (informer Add/Update/Delete, eventhandler.go:60-76) ------
+ * Enqueued under a mutex (safe from informer goroutines while another thread
+ * schedules); drained stream-ordered at the start of the next schedule call
+ * or by ms_nodes_flush. Later deltas to one ordinal win. */
+int ms_nodes_upsert(ms_ctx *ctx, uint32_t n, const uint32_t *ordinals, const ms_node_rec *recs);
+int ms_nodes_delete(ms_ctx *ctx, uint32_t n, const uint32_t *ordinals);
+int ms_nodes_flush(ms_ctx *ctx);
+/* Device -> host read-back of [first, first+n) (global ordinals); absent
+ * nodes read back with allowed_pods = -1. */
+int ms_nodes_read(ms_ctx *ctx, uint32_t first, uint32_t n, ms_node_rec *out);
+
+/* ---- the scheduling cycle ---------------------------------------------------
+ * Replaces minisched.go:40-85 for n_pods pods in queue order. Host arrays,
+ * copied through pinned staging; out[i] is written before return. With
+ * MS_MODE_SEQUENTIAL every SUCCESS commits NodeInfo.AddPod on its node before
+ * the next pod is decided (bit-exact to the one-at-a-time loop). */
+int ms_schedule_batch(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode,
+                      ms_result *out);
+
+/* Assume / forget for the live scheduler (upstream cache.AssumePod/ForgetPod):
+ * add / remove one pod's requests on a node. */
+int ms_commit_bind(ms_ctx *ctx, uint32_t ordinal, const ms_pod_rec *pod);
+int ms_uncommit_bind(ms_ctx *ctx, uint32_t ordinal, const ms_pod_rec *pod);
+
+/* ---- device-resident entry points (bench, node-sharded multi-GPU) ---------
+ * Pointers are device pointers; `stream` is a hipStream_t (NULL = the
+ * context's own stream). Nothing is synchronised: the caller orders work on
+ * the stream.
+ *
+ * ms_sweep_device: this shard's part of filter+score+selectHost for a batch.
+ *   keys[i]  = max packed key over this shard's feasible nodes (0 = none)
+ *   flags[i] = byte 0: some node here rejected by NodeUnschedulable (0/1),
+ *              byte 1: some node here rejected by NodeResourcesFit  (0/1)
+ *   Both arrays are overwritten. flags may be NULL for MS_PLUGINS_NU_NN.
+ *   Shards combine keys with an element-wise uint64 MAX and flags with a
+ *   byte-wise uint8 MAX (= OR of 0/1 bytes): one all-reduce each.
+ * ms_decode_device: combined keys/flags -> ms_result. present_nodes is the
+ *   global count of present nodes (used when flags is NULL).
+ * ms_apply_binds_device: NodeInfo.AddPod on this shard for every SUCCESS
+ *   in results (the batched-mode bind commit). */
+int ms_sweep_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint64_t *keys_dev,
+                    uint32_t *flags_dev, void *stream);
+int ms_decode_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
+                     const uint64_t *keys_dev, const uint32_t *flags_dev, uint32_t present_nodes,
+                     ms_result *results_dev, void *stream);
+int ms_apply_binds_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
+                          const ms_result *results_dev, void *stream);
+/* Whole exact sequential cycle on device-resident pods (single shard). */
+int ms_schedule_sequential_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
+                                  ms_result *results_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

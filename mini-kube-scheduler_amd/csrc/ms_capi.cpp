@@ -1,0 +1,490 @@
+// ms_capi.cpp — C ABI of the scheduling-cycle engine (include/minisched_gpu.h).
+//
+// Owns one device's node table (a shard of global ordinals), the node-delta
+// queue fed by informer callbacks, pinned staging for the cgo caller, and the
+// stream everything is ordered on. It never aborts: every HIP failure becomes
+// MS_E_HIP with the message kept for ms_last_error.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ms_internal.h"
+
+using namespace msgpu;
+
+struct ms_ctx {
+    ms_config cfg{};
+    hipStream_t stream = nullptr;
+    int num_cus = 0;
+    NodeTable t{};
+
+    // node deltas (informer goroutines) — guarded by delta_mu
+    std::mutex delta_mu;
+    std::vector<NodeDelta> pending;
+    std::vector<uint8_t> present;  // host mirror of presence, updated at enqueue
+    uint32_t present_count = 0;
+    uint32_t rows_used = 0;  // high-water mark of upserted rows (sweep extent)
+
+    // one scheduling caller at a time (minisched.go:28-30 runs one goroutine)
+    std::mutex sched_mu;
+
+    // staging
+    uint32_t batch_cap = 0;
+    ms_pod_rec *h_pods = nullptr;
+    ms_result *h_res = nullptr;
+    ms_pod_rec *d_pods = nullptr;
+    ms_result *d_res = nullptr;
+    unsigned long long *d_keys = nullptr;
+    uint32_t *d_flags = nullptr;
+    NodeDelta *h_deltas = nullptr;
+    NodeDelta *d_deltas = nullptr;
+    uint32_t delta_cap = 0;
+    ms_pod_rec *d_one = nullptr;  // commit/uncommit staging
+
+    // sequential engine scratch
+    unsigned long long *d_tile_keys = nullptr;
+    uint32_t *d_tile_flags = nullptr;
+    uint32_t tile_cap = 0;  // tiles allocated per pod
+    uint32_t *d_overflow = nullptr;
+
+    std::string err;
+};
+
+namespace {
+
+thread_local std::string g_create_err;
+
+int fail(ms_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    else g_create_err = msg;
+    return code;
+}
+
+#define MS_HIP(c, call)                                                                          \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail((c), MS_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+void free_all(ms_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
+                   c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
+                   c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
+                   c->d_tile_keys, c->d_tile_flags, c->d_overflow};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    if (c->h_pods) (void)hipHostFree(c->h_pods);
+    if (c->h_res) (void)hipHostFree(c->h_res);
+    if (c->h_deltas) (void)hipHostFree(c->h_deltas);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+int ensure_delta_cap(ms_ctx *c, uint32_t n) {
+    if (n <= c->delta_cap) return MS_OK;
+    uint32_t cap = std::max<uint32_t>(n, std::max<uint32_t>(1024, c->delta_cap * 2));
+    if (c->h_deltas) (void)hipHostFree(c->h_deltas);
+    if (c->d_deltas) (void)hipFree(c->d_deltas);
+    c->h_deltas = nullptr;
+    c->d_deltas = nullptr;
+    c->delta_cap = 0;
+    if (hipHostMalloc((void **)&c->h_deltas, sizeof(NodeDelta) * cap) != hipSuccess)
+        return fail(c, MS_E_OOM, "pinned delta staging");
+    if (hipMalloc((void **)&c->d_deltas, sizeof(NodeDelta) * cap) != hipSuccess)
+        return fail(c, MS_E_OOM, "device delta staging");
+    c->delta_cap = cap;
+    return MS_OK;
+}
+
+// Drains the delta queue onto the stream (caller holds sched_mu).
+int flush_locked(ms_ctx *c) {
+    std::vector<NodeDelta> batch;
+    {
+        std::lock_guard<std::mutex> g(c->delta_mu);
+        batch.swap(c->pending);
+    }
+    if (batch.empty()) return MS_OK;
+    // later deltas to one row win: keep the last occurrence only
+    std::unordered_map<uint32_t, uint32_t> last;
+    last.reserve(batch.size() * 2);
+    for (uint32_t i = 0; i < batch.size(); ++i) last[batch[i].local] = i;
+    std::vector<NodeDelta> uniq;
+    uniq.reserve(last.size());
+    for (uint32_t i = 0; i < batch.size(); ++i)
+        if (last[batch[i].local] == i) uniq.push_back(batch[i]);
+    int rc = ensure_delta_cap(c, (uint32_t)uniq.size());
+    if (rc) return rc;
+    // the previous use of h_deltas must be complete before it is overwritten
+    MS_HIP(c, hipStreamSynchronize(c->stream));
+    std::memcpy(c->h_deltas, uniq.data(), sizeof(NodeDelta) * uniq.size());
+    MS_HIP(c, hipMemcpyAsync(c->d_deltas, c->h_deltas, sizeof(NodeDelta) * uniq.size(),
+                             hipMemcpyHostToDevice, c->stream));
+    MS_HIP(c, launch_apply_deltas(c->t, c->d_deltas, (uint32_t)uniq.size(), c->stream));
+    return MS_OK;
+}
+
+hipStream_t pick_stream(ms_ctx *c, void *s) { return s ? (hipStream_t)s : c->stream; }
+
+// Makes work later enqueued on s wait for everything already on the context stream.
+int order_after_ctx_stream(ms_ctx *c, hipStream_t s) {
+    if (s == c->stream) return MS_OK;
+    hipEvent_t ev;
+    MS_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+    (void)hipEventDestroy(ev);
+    if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("stream ordering: ") + hipGetErrorString(e));
+    return MS_OK;
+}
+
+int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
+    if (n_tiles <= c->tile_cap) return MS_OK;
+    if (c->d_tile_keys) (void)hipFree(c->d_tile_keys);
+    if (c->d_tile_flags) (void)hipFree(c->d_tile_flags);
+    c->d_tile_keys = nullptr;
+    c->d_tile_flags = nullptr;
+    c->tile_cap = 0;
+    const size_t n = (size_t)seq_batch_limit() * n_tiles;
+    if (hipMalloc((void **)&c->d_tile_keys, n * sizeof(unsigned long long)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sequential tile keys");
+    if (hipMalloc((void **)&c->d_tile_flags, n * sizeof(uint32_t)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sequential tile flags");
+    c->tile_cap = n_tiles;
+    return MS_OK;
+}
+
+// Exact sequential engine: speculative per-tile sweep + in-order validation,
+// batch after batch on one stream.
+int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s) {
+    const uint32_t rows = c->rows_used;
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    if (rows == 0) {  // no node listed: every pod is a FitError with an empty mask
+        for (uint32_t s0 = 0; s0 < n_pods; s0 += c->batch_cap) {
+            const uint32_t nb = std::min(c->batch_cap, n_pods - s0);
+            MS_HIP(c, hipMemsetAsync(c->d_keys, 0, sizeof(unsigned long long) * nb, s));
+            MS_HIP(c, launch_decode(d_pods + s0, nb, c->d_keys, nullptr, 0, d_res + s0, s));
+        }
+        return MS_OK;
+    }
+    const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
+    int rc = ensure_tiles(c, n_tiles);
+    if (rc) return rc;
+    const uint32_t B = seq_batch_limit();
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
+                                          n_tiles, s));
+        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
+                                      n_tiles, d_res + s0, c->d_overflow, s));
+    }
+    return MS_OK;
+}
+
+int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
+                 hipStream_t s) {
+    MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
+    if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN)
+        MS_HIP(c, launch_sweep_nunn(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
+    else
+        MS_HIP(c, launch_sweep_full(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
+    return MS_OK;
+}
+
+bool valid_ctx(const ms_ctx *c) { return c != nullptr; }
+
+}  // namespace
+
+extern "C" {
+
+int ms_abi_version(void) { return MS_ABI_VERSION; }
+
+int ms_device_count(int *out) {
+    if (!out) return MS_E_INVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return MS_OK;
+}
+
+int ms_create(const ms_config *cfg, ms_ctx **out) {
+    if (!cfg || !out) return fail(nullptr, MS_E_INVAL, "ms_create: null argument");
+    *out = nullptr;
+    if (cfg->plugin_set != MS_PLUGINS_NU_NN && cfg->plugin_set != MS_PLUGINS_NU_NRF_NN_LA)
+        return fail(nullptr, MS_E_INVAL, "ms_create: unknown plugin_set");
+    if (cfg->max_nodes == 0 || (uint64_t)cfg->node_base + cfg->max_nodes > (uint64_t)MS_MAX_ORDINAL + 1)
+        return fail(nullptr, MS_E_INVAL, "ms_create: node range must be non-empty and end at or below 0xFFFFF");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, MS_E_NODEV, "ms_create: no HIP device visible");
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, MS_E_NODEV, "ms_create: device out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess)
+        return fail(nullptr, MS_E_NODEV, "ms_create: hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, MS_E_NODEV, std::string("ms_create: built for gfx950, device is ") + prop.gcnArchName);
+
+    ms_ctx *c = new (std::nothrow) ms_ctx();
+    if (!c) return fail(nullptr, MS_E_OOM, "ms_create: host allocation");
+    c->cfg = *cfg;
+    if (c->cfg.max_batch == 0) c->cfg.max_batch = 1u << 16;
+    c->num_cus = prop.multiProcessorCount;
+    c->batch_cap = c->cfg.max_batch;
+    c->present.assign(cfg->max_nodes, 0);
+
+    auto bail = [&](int code, const char *what) {
+        std::string m = std::string("ms_create: ") + what;
+        free_all(c);
+        delete c;
+        return fail(nullptr, code, m);
+    };
+    if (hipSetDevice(cfg->device) != hipSuccess) return bail(MS_E_HIP, "hipSetDevice");
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(MS_E_HIP, "hipStreamCreate");
+    const size_t n = cfg->max_nodes;
+    NodeTable &t = c->t;
+    t.cap = cfg->max_nodes;
+    t.base = cfg->node_base;
+    bool ok = hipMalloc((void **)&t.flags, n) == hipSuccess && hipMalloc((void **)&t.digit, n) == hipSuccess &&
+              hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
+              hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
+              hipMalloc((void **)&t.alloc_cpu, n * 8) == hipSuccess &&
+              hipMalloc((void **)&t.alloc_mem, n * 8) == hipSuccess &&
+              hipMalloc((void **)&t.req_cpu, n * 8) == hipSuccess &&
+              hipMalloc((void **)&t.req_mem, n * 8) == hipSuccess &&
+              hipMalloc((void **)&t.nz_cpu, n * 8) == hipSuccess &&
+              hipMalloc((void **)&t.nz_mem, n * 8) == hipSuccess;
+    if (!ok) return bail(MS_E_OOM, "node table allocation");
+    const size_t b = c->batch_cap;
+    ok = hipHostMalloc((void **)&c->h_pods, b * sizeof(ms_pod_rec)) == hipSuccess &&
+         hipHostMalloc((void **)&c->h_res, b * sizeof(ms_result)) == hipSuccess &&
+         hipMalloc((void **)&c->d_pods, b * sizeof(ms_pod_rec)) == hipSuccess &&
+         hipMalloc((void **)&c->d_res, b * sizeof(ms_result)) == hipSuccess &&
+         hipMalloc((void **)&c->d_keys, b * sizeof(unsigned long long)) == hipSuccess &&
+         hipMalloc((void **)&c->d_flags, b * sizeof(uint32_t)) == hipSuccess &&
+         hipMalloc((void **)&c->d_one, sizeof(ms_pod_rec)) == hipSuccess &&
+         hipMalloc((void **)&c->d_overflow, sizeof(uint32_t)) == hipSuccess;
+    if (!ok) return bail(MS_E_OOM, "staging allocation");
+    if (launch_init_table(t, c->stream) != hipSuccess) return bail(MS_E_HIP, "table init launch");
+    if (hipMemsetAsync(c->d_overflow, 0, 4, c->stream) != hipSuccess) return bail(MS_E_HIP, "memset");
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MS_E_HIP, "table init");
+    *out = c;
+    return MS_OK;
+}
+
+int ms_destroy(ms_ctx *c) {
+    if (!c) return MS_E_INVAL;
+    free_all(c);
+    delete c;
+    return MS_OK;
+}
+
+const char *ms_last_error(const ms_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int ms_get_info(const ms_ctx *c, ms_info *out) {
+    if (!valid_ctx(c) || !out) return MS_E_INVAL;
+    ms_ctx *m = const_cast<ms_ctx *>(c);
+    std::lock_guard<std::mutex> g(m->delta_mu);
+    out->max_nodes = c->cfg.max_nodes;
+    out->node_base = c->cfg.node_base;
+    out->present_nodes = c->present_count;
+    out->pending_deltas = (uint32_t)c->pending.size();
+    out->device = c->cfg.device;
+    out->plugin_set = c->cfg.plugin_set;
+    out->seed = c->cfg.seed;
+    return MS_OK;
+}
+
+int ms_nodes_upsert(ms_ctx *c, uint32_t n, const uint32_t *ord, const ms_node_rec *recs) {
+    if (!valid_ctx(c) || (n && (!ord || !recs))) return MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->delta_mu);
+    for (uint32_t i = 0; i < n; ++i)
+        if (ord[i] < c->cfg.node_base || ord[i] - c->cfg.node_base >= c->cfg.max_nodes)
+            return fail(c, MS_E_CAPACITY, "ms_nodes_upsert: ordinal " + std::to_string(ord[i]) + " outside shard");
+    for (uint32_t i = 0; i < n; ++i) {
+        NodeDelta d;
+        d.local = ord[i] - c->cfg.node_base;
+        d.absent = 0;
+        d.rec = recs[i];
+        c->pending.push_back(d);
+        if (!c->present[d.local]) {
+            c->present[d.local] = 1;
+            ++c->present_count;
+        }
+        c->rows_used = std::max(c->rows_used, d.local + 1);
+    }
+    return MS_OK;
+}
+
+int ms_nodes_delete(ms_ctx *c, uint32_t n, const uint32_t *ord) {
+    if (!valid_ctx(c) || (n && !ord)) return MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->delta_mu);
+    for (uint32_t i = 0; i < n; ++i)
+        if (ord[i] < c->cfg.node_base || ord[i] - c->cfg.node_base >= c->cfg.max_nodes)
+            return fail(c, MS_E_CAPACITY, "ms_nodes_delete: ordinal " + std::to_string(ord[i]) + " outside shard");
+    for (uint32_t i = 0; i < n; ++i) {
+        NodeDelta d{};
+        d.local = ord[i] - c->cfg.node_base;
+        d.absent = 1;
+        c->pending.push_back(d);
+        if (c->present[d.local]) {
+            c->present[d.local] = 0;
+            --c->present_count;
+        }
+    }
+    return MS_OK;
+}
+
+int ms_nodes_flush(ms_ctx *c) {
+    if (!valid_ctx(c)) return MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    MS_HIP(c, hipStreamSynchronize(c->stream));
+    return MS_OK;
+}
+
+int ms_nodes_read(ms_ctx *c, uint32_t first, uint32_t n, ms_node_rec *out) {
+    if (!valid_ctx(c) || (n && !out)) return MS_E_INVAL;
+    if (first < c->cfg.node_base || (uint64_t)first - c->cfg.node_base + n > c->cfg.max_nodes)
+        return fail(c, MS_E_CAPACITY, "ms_nodes_read: range outside shard");
+    if (n == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    ms_node_rec *d = nullptr;
+    MS_HIP(c, hipMalloc((void **)&d, sizeof(ms_node_rec) * n));
+    hipError_t e = launch_read_rows(c->t, first - c->cfg.node_base, n, d, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, d, sizeof(ms_node_rec) * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("ms_nodes_read: ") + hipGetErrorString(e));
+    return MS_OK;
+}
+
+int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode, ms_result *out) {
+    if (!valid_ctx(c) || (n_pods && (!pods || !out))) return MS_E_INVAL;
+    if (mode != MS_MODE_BATCHED && mode != MS_MODE_SEQUENTIAL) return fail(c, MS_E_INVAL, "unknown mode");
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    const hipStream_t s = c->stream;
+    const uint32_t B = c->batch_cap;
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, hipStreamSynchronize(s));  // h_pods / h_res free to reuse
+        std::memcpy(c->h_pods, pods + s0, sizeof(ms_pod_rec) * nb);
+        MS_HIP(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
+        const bool seq_full = (mode == MS_MODE_SEQUENTIAL && c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA);
+        if (seq_full) {
+            rc = run_sequential(c, nb, c->d_pods, c->d_res, s);
+            if (rc) return rc;
+        } else {
+            // NU+NN keys never read mutable node state, so the queue-order
+            // loop equals the batched sweep; binds are committed after it.
+            const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
+            rc = sweep_locked(c, nb, c->d_pods, c->d_keys, want_flags ? c->d_flags : nullptr, s);
+            if (rc) return rc;
+            MS_HIP(c, launch_decode(c->d_pods, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_count,
+                                    c->d_res, s));
+            MS_HIP(c, launch_apply_binds(c->t, c->d_pods, nb, c->d_res, s));
+        }
+        MS_HIP(c, hipMemcpyAsync(c->h_res, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
+        MS_HIP(c, hipStreamSynchronize(s));
+        std::memcpy(out + s0, c->h_res, sizeof(ms_result) * nb);
+    }
+    return MS_OK;
+}
+
+static int bind_common(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod, int sign) {
+    if (!valid_ctx(c) || !pod) return MS_E_INVAL;
+    if (ordinal < c->cfg.node_base || ordinal - c->cfg.node_base >= c->cfg.max_nodes)
+        return fail(c, MS_E_CAPACITY, "bind: ordinal outside shard");
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    MS_HIP(c, hipMemcpyAsync(c->d_one, pod, sizeof(ms_pod_rec), hipMemcpyHostToDevice, c->stream));
+    MS_HIP(c, launch_bind_one(c->t, ordinal - c->cfg.node_base, c->d_one, sign, c->stream));
+    MS_HIP(c, hipStreamSynchronize(c->stream));
+    return MS_OK;
+}
+
+int ms_commit_bind(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod) { return bind_common(c, ordinal, pod, +1); }
+int ms_uncommit_bind(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod) { return bind_common(c, ordinal, pod, -1); }
+
+int ms_sweep_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint64_t *keys_dev, uint32_t *flags_dev,
+                    void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !keys_dev))) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN && n_pods && !flags_dev)
+        return fail(c, MS_E_INVAL, "ms_sweep_device: flags required for the resource-aware plugin set");
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
+    if (rc) return rc;
+    return sweep_locked(c, n_pods, pods_dev, reinterpret_cast<unsigned long long *>(keys_dev), flags_dev, s);
+}
+
+int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, const uint64_t *keys_dev,
+                     const uint32_t *flags_dev, uint32_t present_nodes, ms_result *results_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !keys_dev || !results_dev))) return MS_E_INVAL;
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    MS_HIP(c, launch_decode(pods_dev, n_pods, reinterpret_cast<const unsigned long long *>(keys_dev), flags_dev,
+                            present_nodes, results_dev, pick_stream(c, stream)));
+    return MS_OK;
+}
+
+int ms_apply_binds_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, const ms_result *results_dev,
+                          void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    MS_HIP(c, launch_apply_binds(c->t, pods_dev, n_pods, results_dev, pick_stream(c, stream)));
+    return MS_OK;
+}
+
+int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
+                                  void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
+    if (rc) return rc;
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA) return run_sequential(c, n_pods, pods_dev, results_dev, s);
+    // NU+NN: keys are independent of mutable state -> batched sweep + commit
+    const uint32_t B = c->batch_cap;
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        rc = sweep_locked(c, nb, pods_dev + s0, c->d_keys, nullptr, s);
+        if (rc) return rc;
+        MS_HIP(c, launch_decode(pods_dev + s0, nb, c->d_keys, nullptr, c->present_count, results_dev + s0, s));
+        MS_HIP(c, launch_apply_binds(c->t, pods_dev + s0, nb, results_dev + s0, s));
+    }
+    return MS_OK;
+}
+
+}  // extern "C"

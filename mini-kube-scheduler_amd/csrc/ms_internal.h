@@ -1,0 +1,93 @@
+// ms_internal.h — shared between the HIP kernels and the C-ABI host library.
+// Not part of the public boundary (that is include/minisched_gpu.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "minisched_gpu.h"
+
+namespace msgpu {
+
+// Node flag byte (device column `flags`).
+constexpr uint8_t kNodeUnschedulable = 0x01;  // node.Spec.Unschedulable
+constexpr uint8_t kNodeAbsent = 0x80;         // tombstone / never added: not in Nodes().List
+
+// K1 (NU+NN sweep) geometry: one node per lane-slot, 16 slots per lane.
+constexpr int kNunnThreads = 256;
+constexpr int kNunnSlots = 16;
+constexpr int kNunnTile = kNunnThreads * kNunnSlots;  // nodes per block
+
+// K3 (resource-aware sweep) geometry.
+constexpr int kFullThreads = 256;
+constexpr int kFullSlots = 4;
+constexpr int kFullWaveTile = 64 * kFullSlots;            // nodes per wave  (validator tile)
+constexpr int kFullTile = kFullThreads * kFullSlots;      // nodes per block
+
+constexpr uint32_t kGolden32 = 0x9E3779B1u;
+
+// Device-resident node table, structure of arrays, indexed by LOCAL ordinal.
+struct NodeTable {
+    uint8_t *flags;
+    uint8_t *digit;
+    int32_t *allowed_pods;
+    int32_t *pod_count;
+    int64_t *alloc_cpu, *alloc_mem;
+    int64_t *req_cpu, *req_mem;
+    int64_t *nz_cpu, *nz_mem;
+    uint32_t cap;   // rows allocated
+    uint32_t base;  // global ordinal of row 0
+};
+
+// One queued node delta (upsert or delete) as it travels to the device.
+struct NodeDelta {
+    uint32_t local;   // local row
+    uint32_t absent;  // 1 = delete (tombstone)
+    ms_node_rec rec;
+};
+static_assert(sizeof(ms_node_rec) == 64, "ms_node_rec layout");
+static_assert(sizeof(ms_pod_rec) == 40, "ms_pod_rec layout");
+static_assert(sizeof(ms_result) == 24, "ms_result layout");
+
+__host__ __device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+__host__ __device__ inline uint32_t seed32_of(uint64_t seed) { return (uint32_t)(seed ^ (seed >> 32)); }
+
+// ---- launchers (ms_kernels.hip) -------------------------------------------
+// All return hipError_t of the launch; none synchronises.
+hipError_t launch_apply_deltas(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
+hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
+hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
+                             hipStream_t s);
+hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
+                             hipStream_t s);
+// Per-(pod, wave tile) speculative sweep for the sequential engine:
+// tile_keys[p * n_tiles + t], tile_flags likewise.
+hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
+                                   uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
+                                   uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s);
+// In-order validation of a speculative batch; writes results and commits
+// binds to the table. Single workgroup.
+hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                               uint32_t seed32, const unsigned long long *tile_keys,
+                               const uint32_t *tile_flags, uint32_t n_tiles, ms_result *results,
+                               uint32_t *overflow, hipStream_t s);
+hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
+                         const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s);
+hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32_t n_pods,
+                              const ms_result *res, hipStream_t s);
+hipError_t launch_bind_one(const NodeTable &t, uint32_t local, const ms_pod_rec *pod_dev, int sign,
+                           hipStream_t s);
+hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_node_rec *out, hipStream_t s);
+// Largest speculative batch the sequential validator accepts.
+uint32_t seq_batch_limit();
+
+}  // namespace msgpu

@@ -1,0 +1,647 @@
+// ms_kernels.hip — gfx950 kernels for minisched's scheduling cycle.
+//
+// Reference path (all in /root/reference/minisched/minisched.go):
+//   RunFilterPlugins :115-151 -> NodeUnschedulable.Filter (k8s@v1.22.0, restated)
+//   RunScorePlugins  :164-199 -> NodeNumber.Score (plugins/score/nodenumber/nodenumber.go:73-95)
+//   unweighted sum   :187-196
+//   selectHost       :304-325 (tie-break replaced by the packed key, see minisched_gpu.h)
+//
+// The per-(pod,node) work is integer-only and tiny, so the kernels keep a
+// tile of node columns in registers and stream pods through it: one node per
+// lane-slot, pods wave-uniform (scalar loads), a 64-bit wave max per pod and
+// one coalesced atomicMax wave-instruction per 64 pods.
+#include "ms_internal.h"
+
+namespace msgpu {
+
+namespace {
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ u64 umax64(u64 a, u64 b) { return a > b ? a : b; }
+
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = umax64(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v |= __shfl_xor(v, off, 64);
+    return v;
+}
+
+// packed key (minisched_gpu.h): score<<52 | h<<20 | (0xFFFFF - ordinal)
+__device__ __forceinline__ u64 make_key(uint32_t score, uint32_t h, uint32_t ord) {
+    const uint32_t hi = (score << 20) | (h >> 12);
+    const uint32_t lo = (h << 20) | (0xFFFFFu - ord);
+    return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// ----------------------------------------------------------------------------
+// K1: NodeUnschedulable + NodeNumber, batched (stateless) sweep.
+//   grid.x = node tiles of kNunnTile rows, grid.y = pod chunks (multiple of 64)
+//   Each lane holds kNunnSlots consecutive rows: flags/digits as 16-byte
+//   vectors, the per-row hash term ord*golden, and two 16-bit row masks.
+// ----------------------------------------------------------------------------
+template <bool WANT_FLAGS>
+__global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
+    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
+    uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
+    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
+    const uint32_t lane = lane_id();
+    const uint32_t row0 = blockIdx.x * kNunnTile + threadIdx.x * kNunnSlots;
+
+    uint32_t dw[4];  // 16 digits, 4 per dword
+    uint32_t unsched = 0, absent = 0;
+    if (row0 + kNunnSlots <= n_rows) {
+        const uint4 f4 = *reinterpret_cast<const uint4 *>(nflags + row0);
+        const uint4 d4 = *reinterpret_cast<const uint4 *>(ndigit + row0);
+        const uint32_t fw[4] = {f4.x, f4.y, f4.z, f4.w};
+        dw[0] = d4.x; dw[1] = d4.y; dw[2] = d4.z; dw[3] = d4.w;
+#pragma unroll
+        for (int i = 0; i < kNunnSlots; ++i) {
+            const uint32_t f = (fw[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+            unsched |= (f & kNodeUnschedulable) ? (1u << i) : 0u;
+            absent |= (f & kNodeAbsent) ? (1u << i) : 0u;
+        }
+    } else {
+        dw[0] = dw[1] = dw[2] = dw[3] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 0; i < kNunnSlots; ++i) {
+            const uint32_t r = row0 + i;
+            const uint32_t f = r < n_rows ? nflags[r] : kNodeAbsent;
+            const uint32_t d = r < n_rows ? ndigit[r] : 0xFFu;
+            dw[i >> 2] = (dw[i >> 2] & ~(0xFFu << ((i & 3) * 8))) | (d << ((i & 3) * 8));
+            unsched |= (f & kNodeUnschedulable) ? (1u << i) : 0u;
+            absent |= (f & kNodeAbsent) ? (1u << i) : 0u;
+        }
+    }
+    const uint32_t ord0 = node_base + row0;
+    const uint32_t hterm0 = ord0 * kGolden32;
+    const uint32_t unsched_present = unsched & ~absent;
+
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    u64 mine = 0;
+    uint32_t myflag = 0;
+    for (uint32_t p = pbeg; p < pend; ++p) {
+        const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
+        const uint32_t A = fmix32(seed32 ^ pr.ordinal);
+        const int dig = pr.name_digit;
+        const uint32_t infeas = pr.tolerates_unschedulable ? absent : (absent | unsched);
+        u64 best = 0;
+#pragma unroll
+        for (int i = 0; i < kNunnSlots; ++i) {
+            const int nd = (int)((dw[i >> 2] >> ((i & 3) * 8)) & 0xFFu);
+            const uint32_t score = (nd == dig) ? 10u : 0u;
+            const uint32_t h = fmix32(A ^ (hterm0 + (uint32_t)i * kGolden32));
+            const u64 key = make_key(score, h, ord0 + i);
+            best = ((infeas >> i) & 1u) ? best : umax64(best, key);
+        }
+        best = wave_max_u64(best);
+        const uint32_t slot = (p - pbeg) & 63u;
+        if (lane == slot) mine = best;
+        if (WANT_FLAGS) {
+            const bool nu = !pr.tolerates_unschedulable && unsched_present != 0;
+            const bool any_nu = __ballot(nu) != 0;
+            if (lane == slot) myflag = any_nu ? 1u : 0u;
+        }
+        if (slot == 63u || p + 1 == pend) {
+            const uint32_t pp = p - slot + lane;
+            if (lane <= slot && mine) atomicMax(&keys[pp], mine);
+            if (WANT_FLAGS && lane <= slot && myflag) atomicOr(&pflags[pp], myflag);
+            mine = 0;
+            myflag = 0;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// K3: NodeUnschedulable + NodeResourcesFit filters, NodeNumber + LeastAllocated
+// scores (upstream v1.22 semantics restated in oracle/ms_oracle.c).
+// ----------------------------------------------------------------------------
+struct FullRow {
+    int64_t free_cpu, free_mem;    // Allocatable - Requested
+    int64_t nz_cpu, nz_mem;        // NonZeroRequested
+    int64_t alloc_cpu, alloc_mem;  // Allocatable
+    int32_t room;                  // AllowedPodNumber - len(Pods)
+    uint32_t fd;                   // flags | digit << 8
+};
+
+__device__ __forceinline__ FullRow load_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
+    FullRow x;
+    if (r >= n_rows) {
+        x.free_cpu = x.free_mem = x.nz_cpu = x.nz_mem = x.alloc_cpu = x.alloc_mem = 0;
+        x.room = 0;
+        x.fd = kNodeAbsent | (0xFFu << 8);
+        return x;
+    }
+    x.alloc_cpu = t.alloc_cpu[r];
+    x.alloc_mem = t.alloc_mem[r];
+    x.free_cpu = x.alloc_cpu - t.req_cpu[r];
+    x.free_mem = x.alloc_mem - t.req_mem[r];
+    x.nz_cpu = t.nz_cpu[r];
+    x.nz_mem = t.nz_mem[r];
+    x.room = t.allowed_pods[r] - t.pod_count[r];
+    x.fd = (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8);
+    return x;
+}
+
+// floor(num/den) for num >= 0, den > 0; f64 quotient + one-step integer fix-up
+// (exact while num < 2^53, which holds for cpu millicores and memory bytes
+// times 100 below 90 PB).
+__device__ __forceinline__ int64_t div_floor_pos(int64_t num, int64_t den) {
+    if (num < (1ll << 53) && den < (1ll << 53)) {
+        int64_t q = (int64_t)((double)num / (double)den);
+        const int64_t r = num - q * den;
+        if (r < 0) q -= 1;
+        else if (r >= den) q += 1;
+        return q;
+    }
+    return num / den;
+}
+
+// leastRequestedScore (k8s@v1.22.0 least_allocated.go)
+__device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t capacity) {
+    if (capacity == 0) return 0;
+    if (requested > capacity) return 0;
+    return div_floor_pos((capacity - requested) * 100, capacity);
+}
+
+struct PodFull {
+    int64_t rc, rm, nc, nm;
+    int dig;
+    bool tol;
+    bool zero_req;
+    uint32_t A;
+};
+
+__device__ __forceinline__ PodFull load_pod(const ms_pod_rec &pr, uint32_t seed32) {
+    PodFull q;
+    q.rc = pr.req_milli_cpu;
+    q.rm = pr.req_memory;
+    q.nc = pr.nonzero_milli_cpu;
+    q.nm = pr.nonzero_memory;
+    q.dig = pr.name_digit;
+    q.tol = pr.tolerates_unschedulable != 0;
+    q.zero_req = (q.rc == 0 && q.rm == 0);
+    q.A = fmix32(seed32 ^ pr.ordinal);
+    return q;
+}
+
+// Evaluates one (pod,node) pair: returns the packed key (0 when filtered out)
+// and sets the first-failing filter plugin (minisched.go:130-137 breaks on
+// the first failure, so a node rejected by NU is never charged to NRF).
+__device__ __forceinline__ u64 eval_full(const FullRow &x, uint32_t ord, const PodFull &q,
+                                         uint32_t &nu, uint32_t &nrf) {
+    nu = 0;
+    nrf = 0;
+    const uint32_t fl = x.fd & 0xFFu;
+    if (fl & kNodeAbsent) return 0;
+    if ((fl & kNodeUnschedulable) && !q.tol) { nu = 1; return 0; }
+    bool bad = x.room < 1;  // len(Pods)+1 > AllowedPodNumber
+    if (!q.zero_req) bad = bad || (q.rc > x.free_cpu) || (q.rm > x.free_mem);
+    if (bad) { nrf = 1; return 0; }
+    const int nd = (int)(x.fd >> 8);
+    const uint32_t nn = (nd == q.dig) ? 10u : 0u;
+    const int64_t s_cpu = least_requested(x.nz_cpu + q.nc, x.alloc_cpu);
+    const int64_t s_mem = least_requested(x.nz_mem + q.nm, x.alloc_mem);
+    const uint32_t la = (uint32_t)((s_cpu + s_mem) / 2);
+    const uint32_t h = fmix32(q.A ^ (ord * kGolden32));
+    return make_key(nn + la, h, ord);
+}
+
+// OUT_TILES=false: atomicMax into keys[P] / atomicOr into flags[P].
+// OUT_TILES=true : per (pod, wave tile) key and flags for the sequential validator.
+template <bool OUT_TILES>
+__global__ __launch_bounds__(kFullThreads) void k_sweep_full(
+    NodeTable t, uint32_t n_rows, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
+    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t n_tiles) {
+    const uint32_t lane = lane_id();
+    const uint32_t row0 = blockIdx.x * kFullTile + threadIdx.x * kFullSlots;
+    const uint32_t wave_tile = (blockIdx.x * kFullTile + (threadIdx.x & ~63u) * kFullSlots) / kFullWaveTile;
+    FullRow x[kFullSlots];
+#pragma unroll
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
+    const uint32_t ord0 = t.base + row0;
+
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    u64 mine = 0;
+    uint32_t myflag = 0;
+    for (uint32_t p = pbeg; p < pend; ++p) {
+        const PodFull q = load_pod(pods[p], seed32);
+        u64 best = 0;
+        uint32_t nu_any = 0, nrf_any = 0;
+#pragma unroll
+        for (int s = 0; s < kFullSlots; ++s) {
+            uint32_t nu, nrf;
+            const u64 k = eval_full(x[s], ord0 + s, q, nu, nrf);
+            best = umax64(best, k);
+            nu_any |= nu;
+            nrf_any |= nrf;
+        }
+        best = wave_max_u64(best);
+        const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
+        const uint32_t slot = (p - pbeg) & 63u;
+        if (lane == slot) { mine = best; myflag = f; }
+        if (slot == 63u || p + 1 == pend) {
+            const uint32_t pp = p - slot + lane;
+            if (lane <= slot) {
+                if (OUT_TILES) {
+                    keys[(size_t)pp * n_tiles + wave_tile] = mine;
+                    pflags[(size_t)pp * n_tiles + wave_tile] = myflag;
+                } else {
+                    if (mine) atomicMax(&keys[pp], mine);
+                    if (myflag) atomicOr(&pflags[pp], myflag);
+                }
+            }
+            mine = 0;
+            myflag = 0;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Exact sequential validator (config E). One wave walks the speculative batch
+// in queue order. Speculative per-(pod,tile) maxima were computed against the
+// state at batch start; a bind only lowers keys of the node it lands on
+// (NRF feasibility and LeastAllocated are monotone in Requested/PodCount; NU,
+// NN and the hash do not read them). So a tile whose maximum sits on a node
+// untouched so far in the batch is still exact, and only tiles whose argmax
+// node was modified are re-swept against the current state.
+// ----------------------------------------------------------------------------
+constexpr int kSeqBatch = 1024;
+constexpr int kMapCap = 2048;  // power of two, >= 2 * kSeqBatch
+
+struct SeqShared {
+    uint32_t map_row[kMapCap];  // row + 1, 0 = empty
+    uint16_t map_slot[kMapCap];
+    int64_t req_cpu[kSeqBatch], req_mem[kSeqBatch], nz_cpu[kSeqBatch], nz_mem[kSeqBatch];
+    int32_t cnt[kSeqBatch];
+    uint32_t row[kSeqBatch];
+    uint32_t n_slots;
+};
+
+__device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - 11); }
+static_assert(kMapCap == 1 << 11, "map hash width");
+
+__device__ __forceinline__ int map_find(const SeqShared &S, uint32_t row) {
+    uint32_t h = map_hash(row);
+    for (int i = 0; i < kMapCap; ++i) {
+        const uint32_t k = S.map_row[h];
+        if (k == 0) return -1;
+        if (k == row + 1) return S.map_slot[h];
+        h = (h + 1) & (kMapCap - 1);
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_rows,
+                                                     const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                                                     uint32_t seed32, const u64 *__restrict__ tile_keys,
+                                                     const uint32_t *__restrict__ tile_flags, uint32_t n_tiles,
+                                                     ms_result *__restrict__ results,
+                                                     uint32_t *__restrict__ overflow) {
+    __shared__ SeqShared S;
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map_row[i] = 0;
+    if (lane == 0) S.n_slots = 0;
+    __syncthreads();
+    if (n_pods > (uint32_t)kSeqBatch) {  // host guarantees this; never index past S
+        if (lane == 0) *overflow = 1;
+        return;
+    }
+
+    for (uint32_t p = 0; p < n_pods; ++p) {
+        const ms_pod_rec pr = pods[p];
+        const PodFull q = load_pod(pr, seed32);
+        u64 best = 0;
+        uint32_t fl = 0;
+        for (uint32_t tb = 0; tb < n_tiles; tb += 64) {
+            const uint32_t tt = tb + lane;
+            bool need = false;
+            if (tt < n_tiles) {
+                const u64 k = tile_keys[(size_t)p * n_tiles + tt];
+                if (k) {
+                    const uint32_t row = (0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) - t.base;
+                    if (map_find(S, row) >= 0) need = true;
+                    else best = umax64(best, k);
+                } else {
+                    fl |= tile_flags[(size_t)p * n_tiles + tt];
+                }
+            }
+            u64 m = __ballot(need);
+            while (m) {  // wave-uniform loop over tiles to re-sweep
+                const uint32_t tile = tb + (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+#pragma unroll
+                for (int s = 0; s < kFullSlots; ++s) {
+                    const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + s;
+                    FullRow x = load_row(t, r, n_rows);
+                    if (r < n_rows) {
+                        const int sl = map_find(S, r);
+                        if (sl >= 0) {
+                            x.free_cpu = x.alloc_cpu - S.req_cpu[sl];
+                            x.free_mem = x.alloc_mem - S.req_mem[sl];
+                            x.nz_cpu = S.nz_cpu[sl];
+                            x.nz_mem = S.nz_mem[sl];
+                            x.room = t.allowed_pods[r] - S.cnt[sl];
+                        }
+                    }
+                    uint32_t nu, nrf;
+                    best = umax64(best, eval_full(x, t.base + r, q, nu, nrf));
+                    fl |= (nu ? 1u : 0u) | (nrf ? 0x100u : 0u);
+                }
+            }
+        }
+        best = wave_max_u64(best);
+        fl = wave_or_u32(fl);
+        if (lane == 0) {
+            ms_result res;
+            res._pad = 0;
+            if (best == 0) {
+                res.node = -1;
+                res.code = MS_CODE_UNSCHEDULABLE;
+                res.score = 0;
+                res.plugin_mask = ((fl & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                                  ((fl & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
+            } else if (q.dig < 0) {
+                res.node = -1;
+                res.code = MS_CODE_ERROR;
+                res.score = 0;
+                res.plugin_mask = 0;
+            } else {
+                const uint32_t node = 0xFFFFFu - (uint32_t)(best & 0xFFFFFu);
+                res.node = (int32_t)node;
+                res.code = MS_CODE_SUCCESS;
+                res.score = (int64_t)(best >> 52);
+                res.plugin_mask = 0;
+                // assume-on-select: NodeInfo.AddPod on the winner
+                const uint32_t row = node - t.base;
+                int sl = map_find(S, row);
+                if (sl < 0) {
+                    sl = (int)S.n_slots++;
+                    uint32_t h = map_hash(row);
+                    while (S.map_row[h] != 0) h = (h + 1) & (kMapCap - 1);
+                    S.map_row[h] = row + 1;
+                    S.map_slot[h] = (uint16_t)sl;
+                    S.row[sl] = row;
+                    S.req_cpu[sl] = t.req_cpu[row];
+                    S.req_mem[sl] = t.req_mem[row];
+                    S.nz_cpu[sl] = t.nz_cpu[row];
+                    S.nz_mem[sl] = t.nz_mem[row];
+                    S.cnt[sl] = t.pod_count[row];
+                }
+                S.req_cpu[sl] += q.rc;
+                S.req_mem[sl] += q.rm;
+                S.nz_cpu[sl] += q.nc;
+                S.nz_mem[sl] += q.nm;
+                S.cnt[sl] += 1;
+            }
+            results[p] = res;
+        }
+        __syncthreads();
+    }
+    // commit the batch's modified rows; the next speculative sweep is a new
+    // launch on the same stream, so it observes these stores.
+    for (uint32_t sl = lane; sl < S.n_slots; sl += 64) {
+        const uint32_t r = S.row[sl];
+        t.req_cpu[r] = S.req_cpu[sl];
+        t.req_mem[r] = S.req_mem[sl];
+        t.nz_cpu[r] = S.nz_cpu[sl];
+        t.nz_mem[r] = S.nz_mem[sl];
+        t.pod_count[r] = S.cnt[sl];
+    }
+}
+
+// ----------------------------------------------------------------------------
+// decode / bind commit / deltas
+// ----------------------------------------------------------------------------
+__global__ void k_decode(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const u64 *__restrict__ keys,
+                         const uint32_t *__restrict__ flags, uint32_t present, ms_result *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pods) return;
+    const u64 k = keys[i];
+    ms_result r;
+    r._pad = 0;
+    if (k == 0) {  // FitError: no feasible node anywhere
+        r.node = -1;
+        r.code = MS_CODE_UNSCHEDULABLE;
+        r.score = 0;
+        if (flags) {
+            const uint32_t f = flags[i];
+            r.plugin_mask = ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                            ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
+        } else {
+            // NU+NN: NodeUnschedulable is the only filter, so F == 0 with at
+            // least one node listed means every node was rejected by it.
+            r.plugin_mask = present ? MS_MASK_NODE_UNSCHEDULABLE : 0u;
+        }
+    } else if (pods[i].name_digit < 0) {  // NodeNumber.Score error, F > 0
+        r.node = -1;
+        r.code = MS_CODE_ERROR;
+        r.score = 0;
+        r.plugin_mask = 0;
+    } else {
+        r.node = (int32_t)(0xFFFFFu - (uint32_t)(k & 0xFFFFFu));
+        r.code = MS_CODE_SUCCESS;
+        r.score = (int64_t)(k >> 52);
+        r.plugin_mask = 0;
+    }
+    out[i] = r;
+}
+
+__device__ __forceinline__ void add_pod(const NodeTable &t, uint32_t row, const ms_pod_rec &pr, int sign) {
+    atomicAdd(&t.pod_count[row], sign);
+    atomicAdd(reinterpret_cast<u64 *>(&t.req_cpu[row]), (u64)(sign * pr.req_milli_cpu));
+    atomicAdd(reinterpret_cast<u64 *>(&t.req_mem[row]), (u64)(sign * pr.req_memory));
+    atomicAdd(reinterpret_cast<u64 *>(&t.nz_cpu[row]), (u64)(sign * pr.nonzero_milli_cpu));
+    atomicAdd(reinterpret_cast<u64 *>(&t.nz_mem[row]), (u64)(sign * pr.nonzero_memory));
+}
+
+__global__ void k_apply_binds(NodeTable t, const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                              const ms_result *__restrict__ res) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pods) return;
+    const ms_result r = res[i];
+    if (r.code != MS_CODE_SUCCESS || r.node < 0) return;
+    const uint32_t node = (uint32_t)r.node;
+    if (node < t.base || node - t.base >= t.cap) return;  // another shard owns it
+    add_pod(t, node - t.base, pods[i], +1);
+}
+
+__global__ void k_bind_one(NodeTable t, uint32_t row, const ms_pod_rec *pod, int sign) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) add_pod(t, row, *pod, sign);
+}
+
+__global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeDelta x = d[i];
+    const uint32_t r = x.local;
+    if (x.absent) {
+        t.flags[r] = kNodeAbsent;
+        t.digit[r] = 0xFF;
+        t.allowed_pods[r] = 0;
+        t.pod_count[r] = 0;
+        t.alloc_cpu[r] = t.alloc_mem[r] = 0;
+        t.req_cpu[r] = t.req_mem[r] = 0;
+        t.nz_cpu[r] = t.nz_mem[r] = 0;
+        return;
+    }
+    t.flags[r] = x.rec.unschedulable ? kNodeUnschedulable : 0;
+    t.digit[r] = x.rec.name_digit <= 9 ? x.rec.name_digit : 0xFF;
+    t.allowed_pods[r] = x.rec.allowed_pods;
+    t.pod_count[r] = x.rec.pod_count;
+    t.alloc_cpu[r] = x.rec.alloc_milli_cpu;
+    t.alloc_mem[r] = x.rec.alloc_memory;
+    t.req_cpu[r] = x.rec.req_milli_cpu;
+    t.req_mem[r] = x.rec.req_memory;
+    t.nz_cpu[r] = x.rec.nonzero_milli_cpu;
+    t.nz_mem[r] = x.rec.nonzero_memory;
+}
+
+__global__ void k_init_table(NodeTable t) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= t.cap) return;
+    t.flags[r] = kNodeAbsent;
+    t.digit[r] = 0xFF;
+    t.allowed_pods[r] = 0;
+    t.pod_count[r] = 0;
+    t.alloc_cpu[r] = t.alloc_mem[r] = 0;
+    t.req_cpu[r] = t.req_mem[r] = 0;
+    t.nz_cpu[r] = t.nz_mem[r] = 0;
+}
+
+__global__ void k_read_rows(NodeTable t, uint32_t first, uint32_t n, ms_node_rec *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = first + i;
+    ms_node_rec x = {};
+    const uint8_t f = t.flags[r];
+    x.unschedulable = (f & kNodeUnschedulable) ? 1 : 0;
+    x.name_digit = t.digit[r];
+    x.allowed_pods = (f & kNodeAbsent) ? -1 : t.allowed_pods[r];
+    x.pod_count = t.pod_count[r];
+    x.alloc_milli_cpu = t.alloc_cpu[r];
+    x.alloc_memory = t.alloc_mem[r];
+    x.req_milli_cpu = t.req_cpu[r];
+    x.req_memory = t.req_mem[r];
+    x.nonzero_milli_cpu = t.nz_cpu[r];
+    x.nonzero_memory = t.nz_mem[r];
+    out[i] = x;
+}
+
+inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// pods per chunk: enough blocks to fill the chip twice over, multiple of 64
+inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
+    const uint32_t target = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8u * 2u;
+    uint32_t chunks = cdiv(target, node_blocks > 0 ? node_blocks : 1);
+    chunks = chunks < 1 ? 1 : chunks;
+    const uint32_t max_chunks = cdiv(n_pods, 64);
+    if (chunks > max_chunks) chunks = max_chunks;
+    uint32_t c = cdiv(n_pods, chunks);
+    return cdiv(c, 64) * 64;
+}
+
+}  // namespace
+
+hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
+                             hipStream_t s) {
+    if (n_pods == 0 || n_rows == 0) return hipSuccess;
+    const uint32_t gx = cdiv(n_rows, kNunnTile);
+    const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+    const dim3 grid(gx, cdiv(n_pods, chunk));
+    if (flags)
+        hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows, t.base,
+                           pods, n_pods, chunk, seed32, keys, flags);
+    else
+        hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+                           t.base, pods, n_pods, chunk, seed32, keys, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
+                             hipStream_t s) {
+    if (n_pods == 0 || n_rows == 0) return hipSuccess;
+    const uint32_t gx = cdiv(n_rows, kFullTile);
+    const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+    const dim3 grid(gx, cdiv(n_pods, chunk));
+    hipLaunchKernelGGL(k_sweep_full<false>, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk,
+                       seed32, keys, flags, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
+                                   uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
+                                   uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s) {
+    if (n_pods == 0 || n_rows == 0) return hipSuccess;
+    if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
+    const uint32_t gx = cdiv(n_rows, kFullTile);
+    const uint32_t chunk = 64;  // batch <= kSeqBatch: one wave-slot group per block row
+    const dim3 grid(gx, cdiv(n_pods, chunk));
+    hipLaunchKernelGGL(k_sweep_full<true>, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
+                       tile_keys, tile_flags, n_tiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                               uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
+                               uint32_t n_tiles, ms_result *results, uint32_t *overflow, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    if (n_pods > (uint32_t)kSeqBatch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_validate_seq, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys,
+                       tile_flags, n_tiles, results, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
+                         const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, pods, n_pods, keys, flags,
+                       present_nodes, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32_t n_pods, const ms_result *res,
+                              hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_binds, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, t, pods, n_pods, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_bind_one(const NodeTable &t, uint32_t local, const ms_pod_rec *pod_dev, int sign,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_bind_one, dim3(1), dim3(64), 0, s, t, local, pod_dev, sign);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_deltas(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_apply_deltas, dim3(cdiv(n, 256)), dim3(256), 0, s, t, d_deltas, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_table(const NodeTable &t, hipStream_t s) {
+    if (t.cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_init_table, dim3(cdiv(t.cap, 256)), dim3(256), 0, s, t);
+    return hipGetLastError();
+}
+
+hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_node_rec *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_read_rows, dim3(cdiv(n, 256)), dim3(256), 0, s, t, first, n, out);
+    return hipGetLastError();
+}
+
+uint32_t seq_batch_limit() { return (uint32_t)kSeqBatch; }
+
+}  // namespace msgpu

@@ -1,0 +1,263 @@
+"""ctypes binding of libminisched_gpu.so (include/minisched_gpu.h).
+
+This is the Python twin of the cgo shim described in INTEGRATION.md: plain
+pointers and sizes, numpy structured arrays that match the C structs byte for
+byte. There is no CPU fallback: if the HIP library is missing the import of
+`load()` raises, and every compute call needs a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libminisched_gpu.so")
+
+# ---- constants (minisched_gpu.h) -------------------------------------------
+MS_OK = 0
+MS_E_INVAL, MS_E_HIP, MS_E_RCCL, MS_E_OOM, MS_E_CAPACITY, MS_E_NODEV = -1, -2, -3, -4, -5, -6
+PLUGINS_NU_NN = 0
+PLUGINS_NU_NRF_NN_LA = 1
+MODE_BATCHED = 0
+MODE_SEQUENTIAL = 1
+CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE = 0, 1, 2
+MASK_NODE_UNSCHEDULABLE = 1
+MASK_NODE_RESOURCES_FIT = 2
+MAX_ORDINAL = 0xFFFFE
+
+ERRNAMES = {
+    MS_E_INVAL: "MS_E_INVAL",
+    MS_E_HIP: "MS_E_HIP",
+    MS_E_RCCL: "MS_E_RCCL",
+    MS_E_OOM: "MS_E_OOM",
+    MS_E_CAPACITY: "MS_E_CAPACITY",
+    MS_E_NODEV: "MS_E_NODEV",
+}
+
+# ---- record layouts --------------------------------------------------------
+NODE_REC = np.dtype(
+    [
+        ("unschedulable", "u1"),
+        ("name_digit", "u1"),
+        ("_pad0", "u1", (2,)),
+        ("allowed_pods", "<i4"),
+        ("pod_count", "<i4"),
+        ("_pad1", "<i4"),
+        ("alloc_milli_cpu", "<i8"),
+        ("alloc_memory", "<i8"),
+        ("req_milli_cpu", "<i8"),
+        ("req_memory", "<i8"),
+        ("nonzero_milli_cpu", "<i8"),
+        ("nonzero_memory", "<i8"),
+    ]
+)
+POD_REC = np.dtype(
+    [
+        ("ordinal", "<u4"),
+        ("name_digit", "i1"),
+        ("tolerates_unschedulable", "u1"),
+        ("_pad", "u1", (2,)),
+        ("req_milli_cpu", "<i8"),
+        ("req_memory", "<i8"),
+        ("nonzero_milli_cpu", "<i8"),
+        ("nonzero_memory", "<i8"),
+    ]
+)
+RESULT = np.dtype(
+    [("node", "<i4"), ("code", "<i4"), ("score", "<i8"), ("plugin_mask", "<u4"), ("_pad", "<u4")]
+)
+assert NODE_REC.itemsize == 64 and POD_REC.itemsize == 40 and RESULT.itemsize == 24
+
+
+class ms_config(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("plugin_set", ctypes.c_int32),
+        ("max_nodes", ctypes.c_uint32),
+        ("node_base", ctypes.c_uint32),
+        ("max_batch", ctypes.c_uint32),
+        ("_reserved", ctypes.c_uint32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class ms_info(ctypes.Structure):
+    _fields_ = [
+        ("max_nodes", ctypes.c_uint32),
+        ("node_base", ctypes.c_uint32),
+        ("present_nodes", ctypes.c_uint32),
+        ("pending_deltas", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("plugin_set", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+# Every function the header declares, with its ctypes signature.
+_vp, _u32, _i32, _u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
+SIGNATURES = {
+    "ms_abi_version": (ctypes.c_int, []),
+    "ms_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "ms_create": (ctypes.c_int, [ctypes.POINTER(ms_config), ctypes.POINTER(_vp)]),
+    "ms_destroy": (ctypes.c_int, [_vp]),
+    "ms_last_error": (ctypes.c_char_p, [_vp]),
+    "ms_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(ms_info)]),
+    "ms_nodes_upsert": (ctypes.c_int, [_vp, _u32, _vp, _vp]),
+    "ms_nodes_delete": (ctypes.c_int, [_vp, _u32, _vp]),
+    "ms_nodes_flush": (ctypes.c_int, [_vp]),
+    "ms_nodes_read": (ctypes.c_int, [_vp, _u32, _u32, _vp]),
+    "ms_schedule_batch": (ctypes.c_int, [_vp, _u32, _vp, _i32, _vp]),
+    "ms_commit_bind": (ctypes.c_int, [_vp, _u32, _vp]),
+    "ms_uncommit_bind": (ctypes.c_int, [_vp, _u32, _vp]),
+    "ms_sweep_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp]),
+    "ms_decode_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp]),
+    "ms_apply_binds_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_schedule_sequential_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+}
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads the HIP library (fails loudly when it was not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: build it with `make -C mini-kube-scheduler_amd` "
+            "(there is no CPU fallback for the scheduling path)"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+class MSError(RuntimeError):
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} -> {ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load().ms_device_count(ctypes.byref(n))
+    return n.value
+
+
+class Engine:
+    """One context = one device and one contiguous range of node ordinals."""
+
+    def __init__(
+        self,
+        max_nodes: int,
+        plugin_set: int = PLUGINS_NU_NN,
+        node_base: int = 0,
+        seed: int = 1,
+        device: int = 0,
+        max_batch: int = 1 << 16,
+    ):
+        self.lib = load()
+        cfg = ms_config(device, plugin_set, max_nodes, node_base, max_batch, 0, seed)
+        h = ctypes.c_void_p()
+        rc = self.lib.ms_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != MS_OK:
+            raise MSError("ms_create", rc, self.lib.ms_last_error(None).decode())
+        self.h = h
+        self.max_nodes, self.node_base, self.plugin_set, self.seed = max_nodes, node_base, plugin_set, seed
+
+    def _check(self, fn: str, rc: int):
+        if rc != MS_OK:
+            raise MSError(fn, rc, self.lib.ms_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ms_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def info(self) -> ms_info:
+        out = ms_info()
+        self._check("ms_get_info", self.lib.ms_get_info(self.h, ctypes.byref(out)))
+        return out
+
+    def upsert(self, ordinals: np.ndarray, recs: np.ndarray):
+        o = np.ascontiguousarray(ordinals, dtype=np.uint32)
+        r = np.ascontiguousarray(recs, dtype=NODE_REC)
+        assert len(o) == len(r)
+        self._check("ms_nodes_upsert", self.lib.ms_nodes_upsert(self.h, len(o), _ptr(o), _ptr(r)))
+
+    def delete(self, ordinals: np.ndarray):
+        o = np.ascontiguousarray(ordinals, dtype=np.uint32)
+        self._check("ms_nodes_delete", self.lib.ms_nodes_delete(self.h, len(o), _ptr(o)))
+
+    def flush(self):
+        self._check("ms_nodes_flush", self.lib.ms_nodes_flush(self.h))
+
+    def read(self, first: int, n: int) -> np.ndarray:
+        out = np.zeros(n, dtype=NODE_REC)
+        self._check("ms_nodes_read", self.lib.ms_nodes_read(self.h, first, n, _ptr(out)))
+        return out
+
+    def schedule(self, pods: np.ndarray, mode: int = MODE_BATCHED) -> np.ndarray:
+        p = np.ascontiguousarray(pods, dtype=POD_REC)
+        out = np.zeros(len(p), dtype=RESULT)
+        self._check("ms_schedule_batch", self.lib.ms_schedule_batch(self.h, len(p), _ptr(p), mode, _ptr(out)))
+        return out
+
+    def commit_bind(self, ordinal: int, pod: np.ndarray):
+        p = np.ascontiguousarray(pod, dtype=POD_REC).reshape(1)
+        self._check("ms_commit_bind", self.lib.ms_commit_bind(self.h, ordinal, _ptr(p)))
+
+    def uncommit_bind(self, ordinal: int, pod: np.ndarray):
+        p = np.ascontiguousarray(pod, dtype=POD_REC).reshape(1)
+        self._check("ms_uncommit_bind", self.lib.ms_uncommit_bind(self.h, ordinal, _ptr(p)))
+
+    # ---- device-resident entry points (raw device pointers as ints) --------
+    def sweep_device(self, n_pods: int, pods_dev: int, keys_dev: int, flags_dev: int = 0, stream: int = 0):
+        self._check(
+            "ms_sweep_device",
+            self.lib.ms_sweep_device(self.h, n_pods, pods_dev, keys_dev, flags_dev or None, stream or None),
+        )
+
+    def decode_device(self, n_pods, pods_dev, keys_dev, flags_dev, present_nodes, results_dev, stream=0):
+        self._check(
+            "ms_decode_device",
+            self.lib.ms_decode_device(
+                self.h, n_pods, pods_dev, keys_dev, flags_dev or None, present_nodes, results_dev, stream or None
+            ),
+        )
+
+    def apply_binds_device(self, n_pods, pods_dev, results_dev, stream=0):
+        self._check(
+            "ms_apply_binds_device",
+            self.lib.ms_apply_binds_device(self.h, n_pods, pods_dev, results_dev, stream or None),
+        )
+
+    def schedule_sequential_device(self, n_pods, pods_dev, results_dev, stream=0):
+        self._check(
+            "ms_schedule_sequential_device",
+            self.lib.ms_schedule_sequential_device(self.h, n_pods, pods_dev, results_dev, stream or None),
+        )

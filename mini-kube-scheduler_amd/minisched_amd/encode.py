@@ -1,0 +1,131 @@
+"""v1.Node / v1.Pod -> flat records (what the cgo shim computes per object).
+
+Only the fields the in-scope plugins read cross the boundary:
+  * name_digit  — strconv.Atoi(name[len-1:]) (nodenumber.go:51-52, :81-83):
+                  only '0'..'9' parse; anything else is "not a digit".
+  * tolerates_unschedulable — v1helper.TolerationsTolerateTaint(pod tolerations,
+                  {Key: node.kubernetes.io/unschedulable, Effect: NoSchedule})
+                  (k8s@v1.22.0 nodeunschedulable, restated).
+  * requests    — Fit PreFilter computePodResourceRequest and
+                  NodeInfo.calculateResource / GetNonzeroRequests (k8s@v1.22.0).
+Quantities are already integers here: cpu in millicores, memory in bytes.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ._lib import NODE_REC, POD_REC
+
+TAINT_NODE_UNSCHEDULABLE = "node.kubernetes.io/unschedulable"
+TAINT_EFFECT_NO_SCHEDULE = "NoSchedule"
+DEFAULT_MILLI_CPU_REQUEST = 100
+DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
+
+
+def name_digit(name: str) -> int:
+    """Last character as 0..9, or -1 (strconv.Atoi of a 1-char string)."""
+    if not name:
+        raise ValueError("empty object name (the reference would panic slicing name[-1:])")
+    c = name[-1]
+    return ord(c) - 48 if "0" <= c <= "9" else -1
+
+
+@dataclass
+class Toleration:
+    key: str = ""
+    operator: str = ""  # "" == Equal
+    value: str = ""
+    effect: str = ""
+
+
+def toleration_tolerates(t: Toleration, key: str, value: str, effect: str) -> bool:
+    """k8s.io/api core/v1 Toleration.ToleratesTaint (v0.22.0)."""
+    if t.effect and t.effect != effect:
+        return False
+    if t.key and t.key != key:
+        return False
+    if t.operator in ("", "Equal"):
+        return t.value == value
+    if t.operator == "Exists":
+        return True
+    return False
+
+
+def tolerates_unschedulable(tolerations: List[Toleration]) -> bool:
+    return any(
+        toleration_tolerates(t, TAINT_NODE_UNSCHEDULABLE, "", TAINT_EFFECT_NO_SCHEDULE) for t in tolerations
+    )
+
+
+@dataclass
+class Container:
+    requests: Dict[str, int] = field(default_factory=dict)  # "cpu" (milli), "memory" (bytes)
+
+
+@dataclass
+class Pod:
+    name: str
+    ordinal: int
+    tolerations: List[Toleration] = field(default_factory=list)
+    containers: List[Container] = field(default_factory=list)
+    init_containers: List[Container] = field(default_factory=list)
+    overhead: Optional[Dict[str, int]] = None
+
+
+@dataclass
+class Node:
+    name: str
+    unschedulable: bool = False
+    allocatable: Dict[str, int] = field(default_factory=dict)  # cpu (milli), memory (bytes), pods
+
+
+def pod_requests(p: Pod):
+    """(req_cpu, req_mem, nz_cpu, nz_mem).
+
+    req: Fit.computePodResourceRequest — sum of containers, max with each init
+    container, plus overhead. nz: NodeInfo.calculateResource's non-zero pair —
+    per container GetNonzeroRequests (missing cpu -> 100 m, missing memory ->
+    200 MiB, explicit 0 stays 0), max with init containers, plus overhead.
+    """
+    rc = sum(c.requests.get("cpu", 0) for c in p.containers)
+    rm = sum(c.requests.get("memory", 0) for c in p.containers)
+    nc = sum(c.requests.get("cpu", DEFAULT_MILLI_CPU_REQUEST) for c in p.containers)
+    nm = sum(c.requests.get("memory", DEFAULT_MEMORY_REQUEST) for c in p.containers)
+    for ic in p.init_containers:
+        rc = max(rc, ic.requests.get("cpu", 0))
+        rm = max(rm, ic.requests.get("memory", 0))
+        nc = max(nc, ic.requests.get("cpu", DEFAULT_MILLI_CPU_REQUEST))
+        nm = max(nm, ic.requests.get("memory", DEFAULT_MEMORY_REQUEST))
+    if p.overhead:
+        rc += p.overhead.get("cpu", 0)
+        rm += p.overhead.get("memory", 0)
+        nc += p.overhead.get("cpu", 0)
+        nm += p.overhead.get("memory", 0)
+    return rc, rm, nc, nm
+
+
+def pod_records(pods: List[Pod]) -> np.ndarray:
+    rec = np.zeros(len(pods), dtype=POD_REC)
+    for i, p in enumerate(pods):
+        rc, rm, nc, nm = pod_requests(p)
+        rec[i]["ordinal"] = p.ordinal
+        rec[i]["name_digit"] = name_digit(p.name)
+        rec[i]["tolerates_unschedulable"] = 1 if tolerates_unschedulable(p.tolerations) else 0
+        rec[i]["req_milli_cpu"], rec[i]["req_memory"] = rc, rm
+        rec[i]["nonzero_milli_cpu"], rec[i]["nonzero_memory"] = nc, nm
+    return rec
+
+
+def node_records(nodes: List[Node]) -> np.ndarray:
+    rec = np.zeros(len(nodes), dtype=NODE_REC)
+    for i, n in enumerate(nodes):
+        d = name_digit(n.name)
+        rec[i]["unschedulable"] = 1 if n.unschedulable else 0
+        rec[i]["name_digit"] = d if d >= 0 else 0xFF
+        rec[i]["allowed_pods"] = n.allocatable.get("pods", 110)
+        rec[i]["alloc_milli_cpu"] = n.allocatable.get("cpu", 0)
+        rec[i]["alloc_memory"] = n.allocatable.get("memory", 0)
+    return rec

@@ -1,0 +1,110 @@
+"""Synthetic clusters for BASELINE.json's configs.
+
+All draws come from splitmix64: the k-th output of stream `s` under seed
+`seed` is mix64(state + (k+1) * golden) with state = seed ^ (s * 0xD1B54A32D192ED03),
+i.e. one independent splitmix64 sequence per column. Everything is vectorised
+numpy uint64 arithmetic (wrapping), so any prefix/slice can be generated
+without the rest.
+
+Nodes  : ordinal i, name "node{i}" -> digit i % 10, unschedulable iff u % 1000 < 100.
+Pods   : ordinal j, name "pod{j}"  -> digit j % 10, tolerates iff u % 1000 < 20.
+Config E nodes: alloc cpu {1000,2000,4000,8000} m, memory {2,4,8,16} GiB, 110 pods.
+Config E pods : 10 % have no requests (non-zero defaults 100 m / 200 MiB apply),
+                the rest cpu 100..2000 m step 100, memory 128..2048 MiB step 128.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import NODE_REC, POD_REC
+
+GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+STREAM_SALT = np.uint64(0xD1B54A32D192ED03)
+MiB = 1 << 20
+GiB = 1 << 30
+
+# column streams
+S_NODE_UNSCHED, S_POD_TOL, S_NODE_CPU, S_NODE_MEM, S_POD_NOREQ, S_POD_CPU, S_POD_MEM = 1, 2, 3, 4, 5, 6, 7
+
+DEFAULT_MILLI_CPU_REQUEST = 100  # k8s@v1.22.0 pkg/scheduler/util/non_zero.go
+DEFAULT_MEMORY_REQUEST = 200 * MiB
+
+
+def mix64(z: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def stream_u64(seed: int, stream: int, start: int, n: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        state = np.uint64(seed) ^ (np.uint64(stream) * STREAM_SALT)
+        k = np.arange(start, start + n, dtype=np.uint64) + np.uint64(1)
+        return mix64(state + k * GOLDEN)
+
+
+def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False) -> np.ndarray:
+    """Node records for ordinals [start, start+n)."""
+    rec = np.zeros(n, dtype=NODE_REC)
+    i = np.arange(start, start + n, dtype=np.int64)
+    rec["name_digit"] = (i % 10).astype(np.uint8)
+    rec["unschedulable"] = (stream_u64(seed, S_NODE_UNSCHED, start, n) % np.uint64(1000) < np.uint64(100)).astype(
+        np.uint8
+    )
+    rec["allowed_pods"] = 110
+    if resources:
+        cpu = np.array([1000, 2000, 4000, 8000], dtype=np.int64)
+        mem = np.array([2, 4, 8, 16], dtype=np.int64) * GiB
+        rec["alloc_milli_cpu"] = cpu[(stream_u64(seed, S_NODE_CPU, start, n) % np.uint64(4)).astype(np.int64)]
+        rec["alloc_memory"] = mem[(stream_u64(seed, S_NODE_MEM, start, n) % np.uint64(4)).astype(np.int64)]
+    return rec
+
+
+def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False) -> np.ndarray:
+    """Pod records for ordinals [start, start+n)."""
+    rec = np.zeros(n, dtype=POD_REC)
+    j = np.arange(start, start + n, dtype=np.int64)
+    rec["ordinal"] = j.astype(np.uint32)
+    rec["name_digit"] = (j % 10).astype(np.int8)
+    rec["tolerates_unschedulable"] = (
+        stream_u64(seed, S_POD_TOL, start, n) % np.uint64(1000) < np.uint64(20)
+    ).astype(np.uint8)
+    if resources:
+        noreq = stream_u64(seed, S_POD_NOREQ, start, n) % np.uint64(10) == np.uint64(0)
+        cpu = (np.int64(100) * (np.int64(1) + (stream_u64(seed, S_POD_CPU, start, n) % np.uint64(20)).astype(np.int64)))
+        mem = np.int64(128 * MiB) * (np.int64(1) + (stream_u64(seed, S_POD_MEM, start, n) % np.uint64(16)).astype(np.int64))
+        rec["req_milli_cpu"] = np.where(noreq, 0, cpu)
+        rec["req_memory"] = np.where(noreq, 0, mem)
+        rec["nonzero_milli_cpu"] = np.where(noreq, DEFAULT_MILLI_CPU_REQUEST, cpu)
+        rec["nonzero_memory"] = np.where(noreq, DEFAULT_MEMORY_REQUEST, mem)
+    return rec
+
+
+# BASELINE.md §3
+CONFIGS = {
+    "A": dict(nodes=10, pods=1, plugins="NU+NN", mode="sequential"),
+    "B": dict(nodes=5_000, pods=10_000, plugins="NU+NN", mode="sequential"),
+    "C": dict(nodes=100_000, pods=100_000, plugins="NU+NN", mode="batched-node-sharded"),
+    "D": dict(nodes=50_000, pods=1_000_000, plugins="NU+NN", mode="batched"),
+    "E": dict(nodes=50_000, pods=200_000, plugins="NU+NRF+NN+LA", mode="sequential"),
+}
+
+
+def readme_scenario():
+    """sched.go:70-140: node0..node8 unschedulable, pod1; later node10 (schedulable).
+
+    Returns (first_nodes, node10, pod1) as records; ordinals 0..8 for node0..8
+    and 9 for node10 (ordinal assignment is the caller's, names carry the digit).
+    """
+    first = np.zeros(9, dtype=NODE_REC)
+    first["unschedulable"] = 1
+    first["name_digit"] = np.arange(9, dtype=np.uint8)
+    first["allowed_pods"] = 110
+    node10 = np.zeros(1, dtype=NODE_REC)
+    node10["name_digit"] = 0  # "node10"[-1] == '0'
+    node10["allowed_pods"] = 110
+    pod1 = np.zeros(1, dtype=POD_REC)
+    pod1["ordinal"] = 1
+    pod1["name_digit"] = 1
+    return first, node10, pod1

@@ -1,0 +1,287 @@
+/*
+ * ms_oracle.c — CPU restatement of minisched's scheduling cycle.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ms_oracle.h for the parity status). Each
+ * function names the reference file:line it restates. Citations of the form
+ * k8s@v1.22.0:<path> are upstream Kubernetes sources that are NOT in the
+ * container (the submodule is empty, .gitmodules:1-3); they are restated from
+ * the published v1.22.0 code.
+ */
+#include "ms_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ---- tie-break (replaces minisched.go:316-321 rand.Intn reservoir) -------- */
+
+uint32_t msor_fmix32(uint32_t h) { /* murmur3 finaliser */
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+uint32_t msor_seed32(uint64_t seed) { return (uint32_t)(seed ^ (seed >> 32)); }
+
+uint32_t msor_pod_hash(uint64_t seed, uint32_t pod_ordinal) {
+    return msor_fmix32(msor_seed32(seed) ^ pod_ordinal);
+}
+
+uint32_t msor_h32(uint64_t seed, uint32_t pod, uint32_t node) {
+    return msor_fmix32(msor_pod_hash(seed, pod) ^ (node * 0x9E3779B1u));
+}
+
+/* key = score<<52 | h32<<20 | (0xFFFFF - ordinal); max wins. */
+uint64_t msor_key(int64_t score, uint32_t h, uint32_t node) {
+    return ((uint64_t)score << 52) | ((uint64_t)h << 20) | (uint64_t)(0xFFFFFu - node);
+}
+
+/* ---- upstream LeastAllocated ---------------------------------------------- */
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/noderesources/least_allocated.go
+ * leastRequestedScore: capacity 0 -> 0; requested > capacity -> 0;
+ * else ((capacity - requested) * MaxNodeScore) / capacity (int64 floor). */
+int64_t msor_least_requested(int64_t requested, int64_t capacity) {
+    if (capacity == 0) return 0;
+    if (requested > capacity) return 0;
+    return ((capacity - requested) * 100) / capacity;
+}
+
+/* ---- NodeUnschedulable.Filter -------------------------------------------- */
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/nodeunschedulable/
+ * node_unschedulable.go: Spec.Unschedulable && !TolerationsTolerateTaint(
+ * {node.kubernetes.io/unschedulable, NoSchedule}) -> UnschedulableAndUnresolvable.
+ * The toleration match itself is evaluated once per pod on the host
+ * (pod->tol), exactly as upstream evaluates it once per Filter call. */
+static int nu_rejects(uint8_t flags, uint8_t tol) {
+    return (flags & MSOR_NODE_UNSCHEDULABLE) && !tol;
+}
+
+/* ---- NodeResourcesFit.Filter (fitsRequest) -------------------------------- */
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/noderesources/fit.go fitsRequest:
+ * "Too many pods" when len(Pods)+1 > AllowedPodNumber; if every pod request is
+ * zero only that check applies; else MilliCPU > Allocatable-Requested or
+ * Memory > Allocatable-Requested -> Unschedulable. */
+static int nrf_rejects(const msor_nodes *nd, uint32_t i, const msor_pods *pd, uint32_t j) {
+    int bad = 0;
+    if (nd->pod_count[i] + 1 > nd->allowed_pods[i]) bad = 1;
+    int64_t rc = pd->req_cpu[j], rm = pd->req_mem[j];
+    if (rc == 0 && rm == 0) return bad;
+    if (rc > nd->alloc_cpu[i] - nd->req_cpu[i]) bad = 1;
+    if (rm > nd->alloc_mem[i] - nd->req_mem[i]) bad = 1;
+    return bad;
+}
+
+/* ---- LeastAllocated score (cpu weight 1, memory weight 1) ------------------ */
+/* k8s@v1.22.0:.../noderesources/resource_allocation.go score +
+ * calculateResourceAllocatableRequest: requested = NonZeroRequested + pod
+ * non-zero request; weights pinned at scheduler/plugin/plugins_test.go:839-858. */
+static int64_t la_score(const msor_nodes *nd, uint32_t i, const msor_pods *pd, uint32_t j) {
+    int64_t s_cpu = msor_least_requested(nd->nz_cpu[i] + pd->nz_cpu[j], nd->alloc_cpu[i]);
+    int64_t s_mem = msor_least_requested(nd->nz_mem[i] + pd->nz_mem[j], nd->alloc_mem[i]);
+    return (s_cpu * 1 + s_mem * 1) / 2;
+}
+
+/* ---- NodeNumber.Score ----------------------------------------------------- */
+/* minisched/plugins/score/nodenumber/nodenumber.go:73-95: 10 when the pod's
+ * last-char digit equals the node's, 0 otherwise (0 also for a non-digit node
+ * name). A non-digit POD name makes PreScore skip CycleState.Write
+ * (nodenumber.go:53-56) so Score returns framework.Error (:74-77). */
+static int nn_score(int8_t pod_digit, uint8_t node_digit) {
+    return (node_digit != 0xFF && (int)node_digit == (int)pod_digit) ? 10 : 0;
+}
+
+static int has_resources(const msor_nodes *nd) {
+    return nd->allowed_pods && nd->pod_count && nd->alloc_cpu && nd->alloc_mem && nd->req_cpu &&
+           nd->req_mem && nd->nz_cpu && nd->nz_mem;
+}
+
+/* One scheduling cycle for pod j: minisched.go:32-85 between NewCycleState
+ * (:37) and selectHost (:80), with the deterministic tie-break. */
+static void schedule_one(msor_nodes *nd, const msor_pods *pd, uint32_t j, int plugin_set,
+                         uint64_t seed, uint32_t node_base, int32_t *o_node, int64_t *o_score,
+                         int32_t *o_code, uint32_t *o_mask, uint64_t *o_key) {
+    uint32_t mask = 0, feasible = 0;
+    uint64_t best = 0;
+    const uint32_t ph = msor_pod_hash(seed, pd->ordinal[j]);
+    const int8_t pdig = pd->digit[j];
+    /* RunFilterPlugins (minisched.go:115-151): every node in LIST order, the
+     * first failing plugin of a node is recorded (:130-137). Score plugins
+     * (:164-199) and the unweighted sum (:187-196) are folded into the same
+     * pass: scores of infeasible nodes are never used. */
+    for (uint32_t i = 0; i < nd->n; ++i) {
+        uint8_t f = nd->flags[i];
+        if (f & MSOR_NODE_ABSENT) continue; /* not in Nodes().List (minisched.go:40) */
+        if (nu_rejects(f, pd->tol[j])) { mask |= MSOR_MASK_NU; continue; }
+        if (plugin_set == MSOR_PLUGINS_NU_NRF_NN_LA && nrf_rejects(nd, i, pd, j)) {
+            mask |= MSOR_MASK_NRF;
+            continue;
+        }
+        ++feasible;
+        int64_t score = nn_score(pdig, nd->digit[i]);
+        if (plugin_set == MSOR_PLUGINS_NU_NRF_NN_LA) score += la_score(nd, i, pd, j);
+        uint32_t ord = node_base + i;
+        uint64_t key = msor_key(score, msor_fmix32(ph ^ (ord * 0x9E3779B1u)), ord);
+        if (key > best) best = key; /* selectHost (minisched.go:304-325) */
+    }
+    *o_mask = 0;
+    *o_key = best;
+    if (feasible == 0) { /* FitError (minisched.go:143-148) */
+        *o_code = MSOR_CODE_UNSCHEDULABLE;
+        *o_mask = mask;
+        *o_node = -1;
+        *o_score = 0;
+        return;
+    }
+    if (pdig < 0) { /* NodeNumber.Score error -> RunScorePlugins aborts (:170-172) */
+        *o_code = MSOR_CODE_ERROR;
+        *o_node = -1;
+        *o_score = 0;
+        return;
+    }
+    *o_code = MSOR_CODE_SUCCESS;
+    *o_node = (int32_t)(0xFFFFFu - (uint32_t)(best & 0xFFFFFu));
+    *o_score = (int64_t)(best >> 52);
+}
+
+int msor_schedule(msor_nodes *nd, const msor_pods *pd, int plugin_set, int mode, uint64_t seed,
+                  uint32_t node_base, int32_t *out_node, int64_t *out_score, int32_t *out_code,
+                  uint32_t *out_mask, uint64_t *out_key) {
+    if (!nd || !pd || !nd->flags || !nd->digit || !pd->ordinal || !pd->digit || !pd->tol) return -1;
+    if (plugin_set != MSOR_PLUGINS_NU_NN && plugin_set != MSOR_PLUGINS_NU_NRF_NN_LA) return -1;
+    if (mode != MSOR_MODE_BATCHED && mode != MSOR_MODE_SEQUENTIAL) return -1;
+    const int res = has_resources(nd);
+    if (plugin_set == MSOR_PLUGINS_NU_NRF_NN_LA &&
+        (!res || !pd->req_cpu || !pd->req_mem || !pd->nz_cpu || !pd->nz_mem))
+        return -1;
+    if ((uint64_t)node_base + nd->n >= 0xFFFFFu) return -1;
+    for (uint32_t j = 0; j < pd->n; ++j) {
+        int32_t node, code;
+        int64_t score;
+        uint32_t mask;
+        uint64_t key;
+        schedule_one(nd, pd, j, plugin_set, seed, node_base, &node, &score, &code, &mask, &key);
+        if (out_node) out_node[j] = node;
+        if (out_score) out_score[j] = score;
+        if (out_code) out_code[j] = code;
+        if (out_mask) out_mask[j] = mask;
+        if (out_key) out_key[j] = key;
+        /* assume-on-select: upstream NodeInfo.AddPod / calculateResource
+         * (k8s@v1.22.0:pkg/scheduler/framework/types.go) on the winner only. */
+        if (mode == MSOR_MODE_SEQUENTIAL && code == MSOR_CODE_SUCCESS && res && pd->req_cpu) {
+            uint32_t i = (uint32_t)node - node_base;
+            nd->req_cpu[i] += pd->req_cpu[j];
+            nd->req_mem[i] += pd->req_mem[j];
+            nd->nz_cpu[i] += pd->nz_cpu[j];
+            nd->nz_mem[i] += pd->nz_mem[j];
+            nd->pod_count[i] += 1;
+        } else if (mode == MSOR_MODE_SEQUENTIAL && code == MSOR_CODE_SUCCESS && nd->pod_count) {
+            nd->pod_count[(uint32_t)node - node_base] += 1;
+        }
+    }
+    return 0;
+}
+
+int msor_schedule_nunn_omp(const msor_nodes *nd, const msor_pods *pd, uint64_t seed,
+                           uint32_t node_base, int threads, int32_t *out_node,
+                           int64_t *out_score, int32_t *out_code, uint32_t *out_mask,
+                           uint64_t *out_key) {
+    if (!nd || !pd || !nd->flags || !nd->digit || !pd->ordinal || !pd->digit || !pd->tol) return -1;
+    if ((uint64_t)node_base + nd->n >= 0xFFFFFu) return -1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    const long np = (long)pd->n;
+#pragma omp parallel for schedule(dynamic, 16)
+    for (long j = 0; j < np; ++j) {
+        int32_t node, code;
+        int64_t score;
+        uint32_t mask;
+        uint64_t key;
+        schedule_one((msor_nodes *)nd, pd, (uint32_t)j, MSOR_PLUGINS_NU_NN, seed, node_base,
+                     &node, &score, &code, &mask, &key);
+        if (out_node) out_node[j] = node;
+        if (out_score) out_score[j] = score;
+        if (out_code) out_code[j] = code;
+        if (out_mask) out_mask[j] = mask;
+        if (out_key) out_key[j] = key;
+    }
+    return 0;
+}
+
+/* ---- reference-shaped single-thread form ---------------------------------- */
+
+/* strconv.Atoi of a one-character string: only '0'..'9' parse. */
+static int atoi_last_char(const char *s, int *ok) {
+    size_t n = strlen(s);
+    char c = n ? s[n - 1] : '\0';
+    if (c >= '0' && c <= '9') { *ok = 1; return c - '0'; }
+    *ok = 0;
+    return 0;
+}
+
+typedef struct { const char *name; uint32_t ord; int64_t score; } node_score;
+
+int msor_schedule_nunn_names(const char *const *node_names, const uint8_t *node_flags,
+                             uint32_t n_nodes, const char *const *pod_names,
+                             const uint8_t *pod_tol, const uint32_t *pod_ordinal,
+                             uint32_t n_pods, uint64_t seed, int32_t *out_node,
+                             int64_t *out_score, int32_t *out_code, uint32_t *out_mask) {
+    if (n_nodes >= 0xFFFFFu) return -1;
+    uint32_t *feasible = (uint32_t *)malloc(sizeof(uint32_t) * (n_nodes ? n_nodes : 1));
+    node_score *list = (node_score *)malloc(sizeof(node_score) * (n_nodes ? n_nodes : 1));
+    if (!feasible || !list) { free(feasible); free(list); return -1; }
+    for (uint32_t j = 0; j < n_pods; ++j) {
+        /* RunFilterPlugins (minisched.go:115-151) */
+        uint32_t F = 0, mask = 0;
+        for (uint32_t i = 0; i < n_nodes; ++i) {
+            if (node_flags[i] & MSOR_NODE_ABSENT) continue;
+            if (nu_rejects(node_flags[i], pod_tol[j])) { mask |= MSOR_MASK_NU; continue; }
+            feasible[F++] = i;
+        }
+        out_mask[j] = 0;
+        if (F == 0) {
+            out_code[j] = MSOR_CODE_UNSCHEDULABLE; out_mask[j] = mask;
+            out_node[j] = -1; out_score[j] = 0;
+            continue;
+        }
+        /* RunPreScorePlugins -> NodeNumber.PreScore (nodenumber.go:50-64) */
+        int pod_ok;
+        int podnum = atoi_last_char(pod_names[j], &pod_ok);
+        /* RunScorePlugins (minisched.go:164-199): per node, Score(pod, n.Name) */
+        int err = 0;
+        for (uint32_t k = 0; k < F; ++k) {
+            if (!pod_ok) { err = 1; break; } /* CycleState.Read fails (:74-77) */
+            int node_ok;
+            int nodenum = atoi_last_char(node_names[feasible[k]], &node_ok);
+            list[k].name = node_names[feasible[k]];
+            list[k].ord = feasible[k];
+            list[k].score = (node_ok && podnum == nodenum) ? 10 : 0;
+        }
+        if (err) {
+            out_code[j] = MSOR_CODE_ERROR; out_node[j] = -1; out_score[j] = 0;
+            continue;
+        }
+        /* selectHost (minisched.go:304-325) with the packed-key tie-break */
+        const uint32_t ph = msor_pod_hash(seed, pod_ordinal[j]);
+        uint64_t best = 0;
+        uint32_t best_k = 0;
+        for (uint32_t k = 0; k < F; ++k) {
+            uint64_t key = msor_key(list[k].score, msor_fmix32(ph ^ (list[k].ord * 0x9E3779B1u)),
+                                    list[k].ord);
+            if (key > best) { best = key; best_k = k; }
+        }
+        out_code[j] = MSOR_CODE_SUCCESS;
+        out_node[j] = (int32_t)list[best_k].ord;
+        out_score[j] = list[best_k].score;
+    }
+    free(feasible);
+    free(list);
+    return 0;
+}

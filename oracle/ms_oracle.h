@@ -1,0 +1,103 @@
+/*
+ * ms_oracle.h — CPU restatement of minisched's scheduling cycle.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is the checker, never the product: only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it. The product path (libminisched_gpu.so) never links or calls it.
+ *
+ * Parity status: the Go reference cannot be built or run here (no Go
+ * toolchain, no k8s.io module cache; see DESIGN.md "Oracle"). The
+ * restatement is pinned by the reference's only executable known answer,
+ * the README scenario (sched.go:70-140: node0..node8 unschedulable -> pod1
+ * FitError{NodeUnschedulable}; add node10 -> pod1 bound to node10), plus
+ * hand-derived KATs read off nodenumber.go:50-95 and minisched.go:115-199,
+ * 304-325. Everything beyond those KATs (selectHost tie-break, upstream
+ * NodeResourcesFit/LeastAllocated) is "parity unpinned" by reference
+ * outputs: it is a restatement of published upstream v1.22 semantics.
+ */
+#ifndef MS_ORACLE_H
+#define MS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* plugin sets (same numbering as include/minisched_gpu.h) */
+#define MSOR_PLUGINS_NU_NN 0        /* Filter[NodeUnschedulable], Score[NodeNumber]          */
+#define MSOR_PLUGINS_NU_NRF_NN_LA 1 /* Filter[NU, NodeResourcesFit], Score[NN, LeastAllocated] */
+
+#define MSOR_MODE_BATCHED 0    /* every pod against the same node state          */
+#define MSOR_MODE_SEQUENTIAL 1 /* queue order, assume-on-select NodeInfo.AddPod   */
+
+#define MSOR_CODE_SUCCESS 0
+#define MSOR_CODE_ERROR 1         /* framework.Error from a score plugin (non-FitError) */
+#define MSOR_CODE_UNSCHEDULABLE 2 /* *framework.FitError                               */
+
+#define MSOR_MASK_NU (1u << 0)
+#define MSOR_MASK_NRF (1u << 1)
+
+#define MSOR_NODE_UNSCHEDULABLE 0x01u
+#define MSOR_NODE_ABSENT 0x80u
+
+/* Node table, structure of arrays; resource columns may be NULL for NU_NN. */
+typedef struct {
+    uint32_t n;
+    const uint8_t *flags; /* bit0 Spec.Unschedulable, bit7 tombstone (not in LIST) */
+    const uint8_t *digit; /* last char of node name as 0..9, 0xFF = non-digit      */
+    int32_t *allowed_pods, *pod_count;
+    int64_t *alloc_cpu, *alloc_mem; /* Allocatable.MilliCPU / .Memory              */
+    int64_t *req_cpu, *req_mem;     /* Requested.MilliCPU / .Memory                */
+    int64_t *nz_cpu, *nz_mem;       /* NonZeroRequested.MilliCPU / .Memory         */
+} msor_nodes;
+
+typedef struct {
+    uint32_t n;
+    const uint32_t *ordinal; /* stable pod id fed to the tie-break hash           */
+    const int8_t *digit;     /* last char of pod name as 0..9, -1 = non-digit     */
+    const uint8_t *tol;      /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
+    const int64_t *req_cpu, *req_mem, *nz_cpu, *nz_mem; /* may be NULL for NU_NN */
+} msor_pods;
+
+uint32_t msor_fmix32(uint32_t h);
+uint32_t msor_seed32(uint64_t seed);
+uint32_t msor_pod_hash(uint64_t seed, uint32_t pod_ordinal);
+uint32_t msor_h32(uint64_t seed, uint32_t pod_ordinal, uint32_t node_ordinal);
+uint64_t msor_key(int64_t score, uint32_t h, uint32_t node_ordinal);
+int64_t msor_least_requested(int64_t requested, int64_t capacity);
+
+/* Schedules pods[0..n) in order. node_base = global ordinal of local node 0.
+ * Outputs (each length pods->n, any may be NULL):
+ *   out_node  global ordinal of the selected node or -1
+ *   out_score summed score of the selected node (0 otherwise)
+ *   out_code  MSOR_CODE_*
+ *   out_mask  FitError UnschedulablePlugins as MSOR_MASK_* bits
+ *   out_key   winning packed key (0 when no feasible node)
+ * In MSOR_MODE_SEQUENTIAL the node resource columns are updated in place.
+ * Returns 0, or -1 on invalid arguments. */
+int msor_schedule(msor_nodes *nodes, const msor_pods *pods, int plugin_set, int mode,
+                  uint64_t seed, uint32_t node_base, int32_t *out_node, int64_t *out_score,
+                  int32_t *out_code, uint32_t *out_mask, uint64_t *out_key);
+
+/* Same semantics, NU_NN only, pods evaluated in parallel with OpenMP
+ * (the multi-core CPU baseline). threads <= 0 means all cores. */
+int msor_schedule_nunn_omp(const msor_nodes *nodes, const msor_pods *pods, uint64_t seed,
+                           uint32_t node_base, int threads, int32_t *out_node,
+                           int64_t *out_score, int32_t *out_code, uint32_t *out_mask,
+                           uint64_t *out_key);
+
+/* "Faithful" single-thread form for NU_NN: per (pod, node) it re-parses the
+ * last character of the node NAME (Atoi, nodenumber.go:81-87) and builds the
+ * feasible list and the NodeScoreList like minisched.go:115-199 before
+ * selectHost. names: n_nodes NUL-terminated strings. Used only as the
+ * reference-shaped CPU baseline. */
+int msor_schedule_nunn_names(const char *const *node_names, const uint8_t *node_flags,
+                             uint32_t n_nodes, const char *const *pod_names,
+                             const uint8_t *pod_tol, const uint32_t *pod_ordinal,
+                             uint32_t n_pods, uint64_t seed, int32_t *out_node,
+                             int64_t *out_score, int32_t *out_code, uint32_t *out_mask);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

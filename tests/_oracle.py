@@ -1,0 +1,224 @@
+"""ctypes wrapper of oracle/libmsoracle.so — the CPU restatement (checker only).
+
+Test infrastructure: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "libmsoracle.so")
+
+PLUGINS_NU_NN, PLUGINS_NU_NRF_NN_LA = 0, 1
+MODE_BATCHED, MODE_SEQUENTIAL = 0, 1
+
+
+class msor_nodes(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32)] + [
+        (f, ctypes.c_void_p)
+        for f in (
+            "flags",
+            "digit",
+            "allowed_pods",
+            "pod_count",
+            "alloc_cpu",
+            "alloc_mem",
+            "req_cpu",
+            "req_mem",
+            "nz_cpu",
+            "nz_mem",
+        )
+    ]
+
+
+class msor_pods(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32)] + [
+        (f, ctypes.c_void_p) for f in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem")
+    ]
+
+
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(ORACLE_LIB):
+            build()
+        L = ctypes.CDLL(ORACLE_LIB)
+        L.msor_fmix32.restype = ctypes.c_uint32
+        L.msor_fmix32.argtypes = [ctypes.c_uint32]
+        L.msor_h32.restype = ctypes.c_uint32
+        L.msor_h32.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.msor_key.restype = ctypes.c_uint64
+        L.msor_key.argtypes = [ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint32]
+        L.msor_least_requested.restype = ctypes.c_int64
+        L.msor_least_requested.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.msor_schedule.restype = ctypes.c_int
+        L.msor_schedule.argtypes = [
+            ctypes.POINTER(msor_nodes),
+            ctypes.POINTER(msor_pods),
+            ctypes.c_int,
+            ctypes.c_int,
+            ctypes.c_uint64,
+            ctypes.c_uint32,
+        ] + [ctypes.c_void_p] * 5
+        L.msor_schedule_nunn_omp.restype = ctypes.c_int
+        L.msor_schedule_nunn_omp.argtypes = [
+            ctypes.POINTER(msor_nodes),
+            ctypes.POINTER(msor_pods),
+            ctypes.c_uint64,
+            ctypes.c_uint32,
+            ctypes.c_int,
+        ] + [ctypes.c_void_p] * 5
+        L.msor_schedule_nunn_names.restype = ctypes.c_int
+        L.msor_schedule_nunn_names.argtypes = [
+            ctypes.POINTER(ctypes.c_char_p),
+            ctypes.c_void_p,
+            ctypes.c_uint32,
+            ctypes.POINTER(ctypes.c_char_p),
+            ctypes.c_void_p,
+            ctypes.c_void_p,
+            ctypes.c_uint32,
+            ctypes.c_uint64,
+        ] + [ctypes.c_void_p] * 4
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class NodeCols:
+    """SoA copy of node records (the oracle mutates resource columns in place)."""
+
+    def __init__(self, recs):
+        self.flags = np.ascontiguousarray(
+            np.where(recs["allowed_pods"] < 0, 0x80, 0) | (recs["unschedulable"] & 1), dtype=np.uint8
+        )
+        self.digit = np.ascontiguousarray(np.where(recs["name_digit"] <= 9, recs["name_digit"], 0xFF), dtype=np.uint8)
+        self.allowed_pods = np.ascontiguousarray(recs["allowed_pods"], dtype=np.int32)
+        self.pod_count = np.ascontiguousarray(recs["pod_count"], dtype=np.int32)
+        self.alloc_cpu = np.ascontiguousarray(recs["alloc_milli_cpu"], dtype=np.int64)
+        self.alloc_mem = np.ascontiguousarray(recs["alloc_memory"], dtype=np.int64)
+        self.req_cpu = np.ascontiguousarray(recs["req_milli_cpu"], dtype=np.int64)
+        self.req_mem = np.ascontiguousarray(recs["req_memory"], dtype=np.int64)
+        self.nz_cpu = np.ascontiguousarray(recs["nonzero_milli_cpu"], dtype=np.int64)
+        self.nz_mem = np.ascontiguousarray(recs["nonzero_memory"], dtype=np.int64)
+
+    def struct(self):
+        return msor_nodes(
+            len(self.flags),
+            *[
+                _p(getattr(self, f))
+                for f in (
+                    "flags",
+                    "digit",
+                    "allowed_pods",
+                    "pod_count",
+                    "alloc_cpu",
+                    "alloc_mem",
+                    "req_cpu",
+                    "req_mem",
+                    "nz_cpu",
+                    "nz_mem",
+                )
+            ],
+        )
+
+
+def _pod_cols(pods):
+    cols = dict(
+        ordinal=np.ascontiguousarray(pods["ordinal"], dtype=np.uint32),
+        digit=np.ascontiguousarray(pods["name_digit"], dtype=np.int8),
+        tol=np.ascontiguousarray(pods["tolerates_unschedulable"], dtype=np.uint8),
+        req_cpu=np.ascontiguousarray(pods["req_milli_cpu"], dtype=np.int64),
+        req_mem=np.ascontiguousarray(pods["req_memory"], dtype=np.int64),
+        nz_cpu=np.ascontiguousarray(pods["nonzero_milli_cpu"], dtype=np.int64),
+        nz_mem=np.ascontiguousarray(pods["nonzero_memory"], dtype=np.int64),
+    )
+    st = msor_pods(len(pods), *[_p(cols[k]) for k in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem")])
+    return cols, st
+
+
+def _outs(n):
+    return dict(
+        node=np.empty(n, np.int32),
+        score=np.empty(n, np.int64),
+        code=np.empty(n, np.int32),
+        mask=np.empty(n, np.uint32),
+        key=np.empty(n, np.uint64),
+    )
+
+
+def schedule(node_recs, pods, plugin_set=PLUGINS_NU_NN, mode=MODE_BATCHED, seed=1, node_base=0, cols=None):
+    """Runs the oracle; returns dict of outputs (+ 'cols', the node columns after)."""
+    L = lib()
+    cols = cols if cols is not None else NodeCols(node_recs)
+    nst = cols.struct()
+    pc, pst = _pod_cols(pods)
+    o = _outs(len(pods))
+    rc = L.msor_schedule(
+        ctypes.byref(nst), ctypes.byref(pst), plugin_set, mode, seed, node_base,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),
+    )
+    assert rc == 0, "oracle rejected its arguments"
+    o["cols"] = cols
+    return o
+
+
+def schedule_batched_commit(node_recs, pods, plugin_set, seed=1, node_base=0):
+    """Batched semantics of the engine: decide every pod on the same state,
+    then commit NodeInfo.AddPod for every SUCCESS (minisched_gpu.h MS_MODE_BATCHED)."""
+    o = schedule(node_recs, pods, plugin_set, MODE_BATCHED, seed, node_base)
+    cols = o["cols"]
+    for j in np.nonzero(o["code"] == 0)[0]:
+        i = int(o["node"][j]) - node_base
+        cols.pod_count[i] += 1
+        cols.req_cpu[i] += pods["req_milli_cpu"][j]
+        cols.req_mem[i] += pods["req_memory"][j]
+        cols.nz_cpu[i] += pods["nonzero_milli_cpu"][j]
+        cols.nz_mem[i] += pods["nonzero_memory"][j]
+    return o
+
+
+def schedule_nunn_omp(node_recs, pods, seed=1, node_base=0, threads=0):
+    L = lib()
+    cols = NodeCols(node_recs)
+    nst = cols.struct()
+    pc, pst = _pod_cols(pods)
+    o = _outs(len(pods))
+    rc = L.msor_schedule_nunn_omp(
+        ctypes.byref(nst), ctypes.byref(pst), seed, node_base, threads,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),
+    )
+    assert rc == 0
+    return o
+
+
+def schedule_nunn_names(node_names, node_flags, pod_names, pod_tol, pod_ordinal, seed=1):
+    L = lib()
+    nn = (ctypes.c_char_p * len(node_names))(*[s.encode() for s in node_names])
+    pn = (ctypes.c_char_p * len(pod_names))(*[s.encode() for s in pod_names])
+    nf = np.ascontiguousarray(node_flags, dtype=np.uint8)
+    pt = np.ascontiguousarray(pod_tol, dtype=np.uint8)
+    po = np.ascontiguousarray(pod_ordinal, dtype=np.uint32)
+    n = len(pod_names)
+    o = dict(node=np.empty(n, np.int32), score=np.empty(n, np.int64), code=np.empty(n, np.int32), mask=np.empty(n, np.uint32))
+    rc = L.msor_schedule_nunn_names(
+        nn, _p(nf), len(node_names), pn, _p(pt), _p(po), n, seed,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]),
+    )
+    assert rc == 0
+    return o

@@ -1,0 +1,117 @@
+"""Pure-Python restatement of minisched's cycle on v1-style objects.
+
+Small cases only. It follows minisched.go literally (feasible list, per-plugin
+NodeScoreList, unweighted sum, linear selectHost) on names and tolerations,
+so that it cross-checks both the record encoding and the C oracle.
+Test infrastructure, never product code.
+"""
+from __future__ import annotations
+
+from minisched_amd.encode import name_digit, pod_requests, tolerates_unschedulable
+
+MASK_NU, MASK_NRF = 1, 2
+
+
+def fmix32(h):
+    h &= 0xFFFFFFFF
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return h
+
+
+def seed32(seed):
+    return (seed ^ (seed >> 32)) & 0xFFFFFFFF
+
+
+def h32(seed, pod_ord, node_ord):
+    return fmix32(fmix32(seed32(seed) ^ pod_ord) ^ ((node_ord * 0x9E3779B1) & 0xFFFFFFFF))
+
+
+def key(score, h, node_ord):
+    return (score << 52) | (h << 20) | (0xFFFFF - node_ord)
+
+
+def least_requested(requested, capacity):
+    if capacity == 0:
+        return 0
+    if requested > capacity:
+        return 0
+    return ((capacity - requested) * 100) // capacity
+
+
+class NodeState:
+    """framework.NodeInfo columns for one node (k8s@v1.22.0 types.go)."""
+
+    def __init__(self, node):
+        self.node = node
+        self.req_cpu = self.req_mem = self.nz_cpu = self.nz_mem = 0
+        self.pods = 0
+
+
+def schedule(nodes, pods, resources=False, sequential=False, seed=1):
+    """nodes: list of encode.Node (ordinal = list index); pods: list of encode.Pod.
+    Returns list of (code, node_ordinal, score, mask)."""
+    state = [NodeState(n) for n in nodes]
+    out = []
+    for pod in pods:
+        tol = tolerates_unschedulable(pod.tolerations)
+        rc, rm, nc, nm = pod_requests(pod)
+        # RunFilterPlugins (minisched.go:115-151)
+        feasible, plugins = [], set()
+        for i, st in enumerate(state):
+            n = st.node
+            if n.unschedulable and not tol:  # NodeUnschedulable
+                plugins.add(MASK_NU)
+                continue
+            if resources:  # NodeResourcesFit.fitsRequest
+                bad = st.pods + 1 > n.allocatable.get("pods", 110)
+                if not (rc == 0 and rm == 0):
+                    bad |= rc > n.allocatable.get("cpu", 0) - st.req_cpu
+                    bad |= rm > n.allocatable.get("memory", 0) - st.req_mem
+                if bad:
+                    plugins.add(MASK_NRF)
+                    continue
+            feasible.append(i)
+        if not feasible:
+            m = 0
+            for b in plugins:
+                m |= b
+            out.append((2, -1, 0, m))
+            continue
+        # PreScore: NodeNumber (nodenumber.go:50-64)
+        podnum = name_digit(pod.name)
+        if podnum < 0:  # Score -> CycleState.Read error (nodenumber.go:74-77)
+            out.append((1, -1, 0, 0))
+            continue
+        # RunScorePlugins: per plugin lists, then unweighted sum
+        nn = []
+        for i in feasible:
+            d = name_digit(nodes[i].name)
+            nn.append(10 if (d >= 0 and d == podnum) else 0)
+        total = list(nn)
+        if resources:
+            for k, i in enumerate(feasible):
+                st = state[i]
+                a = nodes[i].allocatable
+                s_cpu = least_requested(st.nz_cpu + nc, a.get("cpu", 0))
+                s_mem = least_requested(st.nz_mem + nm, a.get("memory", 0))
+                total[k] += (s_cpu + s_mem) // 2
+        # selectHost with the deterministic packed key
+        best, best_i = -1, -1
+        for k, i in enumerate(feasible):
+            kk = key(total[k], h32(seed, pod.ordinal, i), i)
+            if kk > best:
+                best, best_i = kk, k
+        w = feasible[best_i]
+        out.append((0, w, total[best_i], 0))
+        if sequential:
+            st = state[w]
+            st.req_cpu += rc
+            st.req_mem += rm
+            st.nz_cpu += nc
+            st.nz_mem += nm
+            st.pods += 1
+    return out

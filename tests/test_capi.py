@@ -1,0 +1,79 @@
+"""The C-ABI library loads and exports exactly what include/minisched_gpu.h declares.
+
+CPU-only: no compute call is made without a GPU.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from minisched_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "minisched_gpu.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(ms_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_and_binding_agree():
+    names = declared_functions()
+    assert len(names) >= 15
+    assert sorted(_lib.SIGNATURES) == names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r" T (ms_\w+)", out.stdout))
+    assert exported == set(declared_functions())
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(
+        ["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
+        capture_output=True,
+        text=True,
+    )
+    text = out.stdout + out.stderr
+    assert "gfx950" in text
+
+
+def test_struct_sizes_match_header():
+    assert _lib.NODE_REC.itemsize == 64
+    assert _lib.POD_REC.itemsize == 40
+    assert _lib.RESULT.itemsize == 24
+    assert ctypes.sizeof(_lib.ms_config) == 32
+
+
+def test_abi_version_and_no_device_error_path():
+    lib = _lib.load()
+    assert lib.ms_abi_version() == 1
+    if _lib.device_count() > 0:
+        pytest.skip("a device is visible; the no-device path is exercised on CPU hosts")
+    cfg = _lib.ms_config(0, 0, 16, 0, 64, 0, 1)
+    h = ctypes.c_void_p()
+    rc = lib.ms_create(ctypes.byref(cfg), ctypes.byref(h))
+    assert rc == _lib.MS_E_NODEV
+    assert b"device" in lib.ms_last_error(None)
+    # argument validation happens before any device work
+    bad = _lib.ms_config(0, 7, 16, 0, 64, 0, 1)
+    assert lib.ms_create(ctypes.byref(bad), ctypes.byref(h)) == _lib.MS_E_INVAL
+    assert lib.ms_create(None, ctypes.byref(h)) == _lib.MS_E_INVAL
+    assert lib.ms_destroy(None) == _lib.MS_E_INVAL
+    assert lib.ms_schedule_batch(None, 0, None, 0, None) == _lib.MS_E_INVAL
+
+
+def test_engine_refuses_without_device():
+    if _lib.device_count() > 0:
+        pytest.skip("device visible")
+    with pytest.raises(_lib.MSError) as e:
+        _lib.Engine(max_nodes=8)
+    assert e.value.code == _lib.MS_E_NODEV
