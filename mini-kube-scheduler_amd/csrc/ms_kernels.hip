@@ -251,7 +251,8 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full(
         if (lane == slot) { mine = best; myflag = f; }
         if (slot == 63u || p + 1 == pend) {
             const uint32_t pp = p - slot + lane;
-            if (lane <= slot) {
+            // a wave entirely past the last row owns no tile and writes nothing
+            if (lane <= slot && (!OUT_TILES || wave_tile < n_tiles)) {
                 if (OUT_TILES) {
                     keys[(size_t)pp * n_tiles + wave_tile] = mine;
                     pflags[(size_t)pp * n_tiles + wave_tile] = myflag;
