@@ -131,6 +131,16 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             f"{path} is missing: build it with `make -C mini-kube-scheduler_amd` "
             "(there is no CPU fallback for the scheduling path)"
         )
+    # One HIP runtime per process. torch bundles its own libamdhip64.so.7 and
+    # links it by a different NEEDED name than ours, so loading our library
+    # first would map /opt/rocm's runtime beside torch's (two HSA runtimes: the
+    # second sees no GPU). Loading torch first makes our NEEDED
+    # libamdhip64.so.7 resolve to the runtime torch already mapped.
+    if os.environ.get("MINISCHED_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -100,22 +100,26 @@ def _p(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _col(a, dtype):
+    # always a private copy: a field view of a 1-row array is already contiguous
+    # and ascontiguousarray would hand the oracle the caller's memory
+    return np.array(a, dtype=dtype, copy=True, order="C")
+
+
 class NodeCols:
     """SoA copy of node records (the oracle mutates resource columns in place)."""
 
     def __init__(self, recs):
-        self.flags = np.ascontiguousarray(
-            np.where(recs["allowed_pods"] < 0, 0x80, 0) | (recs["unschedulable"] & 1), dtype=np.uint8
-        )
-        self.digit = np.ascontiguousarray(np.where(recs["name_digit"] <= 9, recs["name_digit"], 0xFF), dtype=np.uint8)
-        self.allowed_pods = np.ascontiguousarray(recs["allowed_pods"], dtype=np.int32)
-        self.pod_count = np.ascontiguousarray(recs["pod_count"], dtype=np.int32)
-        self.alloc_cpu = np.ascontiguousarray(recs["alloc_milli_cpu"], dtype=np.int64)
-        self.alloc_mem = np.ascontiguousarray(recs["alloc_memory"], dtype=np.int64)
-        self.req_cpu = np.ascontiguousarray(recs["req_milli_cpu"], dtype=np.int64)
-        self.req_mem = np.ascontiguousarray(recs["req_memory"], dtype=np.int64)
-        self.nz_cpu = np.ascontiguousarray(recs["nonzero_milli_cpu"], dtype=np.int64)
-        self.nz_mem = np.ascontiguousarray(recs["nonzero_memory"], dtype=np.int64)
+        self.flags = _col(np.where(recs["allowed_pods"] < 0, 0x80, 0) | (recs["unschedulable"] & 1), np.uint8)
+        self.digit = _col(np.where(recs["name_digit"] <= 9, recs["name_digit"], 0xFF), np.uint8)
+        self.allowed_pods = _col(recs["allowed_pods"], np.int32)
+        self.pod_count = _col(recs["pod_count"], np.int32)
+        self.alloc_cpu = _col(recs["alloc_milli_cpu"], np.int64)
+        self.alloc_mem = _col(recs["alloc_memory"], np.int64)
+        self.req_cpu = _col(recs["req_milli_cpu"], np.int64)
+        self.req_mem = _col(recs["req_memory"], np.int64)
+        self.nz_cpu = _col(recs["nonzero_milli_cpu"], np.int64)
+        self.nz_mem = _col(recs["nonzero_memory"], np.int64)
 
     def struct(self):
         return msor_nodes(
@@ -140,13 +144,13 @@ class NodeCols:
 
 def _pod_cols(pods):
     cols = dict(
-        ordinal=np.ascontiguousarray(pods["ordinal"], dtype=np.uint32),
-        digit=np.ascontiguousarray(pods["name_digit"], dtype=np.int8),
-        tol=np.ascontiguousarray(pods["tolerates_unschedulable"], dtype=np.uint8),
-        req_cpu=np.ascontiguousarray(pods["req_milli_cpu"], dtype=np.int64),
-        req_mem=np.ascontiguousarray(pods["req_memory"], dtype=np.int64),
-        nz_cpu=np.ascontiguousarray(pods["nonzero_milli_cpu"], dtype=np.int64),
-        nz_mem=np.ascontiguousarray(pods["nonzero_memory"], dtype=np.int64),
+        ordinal=_col(pods["ordinal"], np.uint32),
+        digit=_col(pods["name_digit"], np.int8),
+        tol=_col(pods["tolerates_unschedulable"], np.uint8),
+        req_cpu=_col(pods["req_milli_cpu"], np.int64),
+        req_mem=_col(pods["req_memory"], np.int64),
+        nz_cpu=_col(pods["nonzero_milli_cpu"], np.int64),
+        nz_mem=_col(pods["nonzero_memory"], np.int64),
     )
     st = msor_pods(len(pods), *[_p(cols[k]) for k in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem")])
     return cols, st

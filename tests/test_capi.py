@@ -77,3 +77,21 @@ def test_engine_refuses_without_device():
     with pytest.raises(_lib.MSError) as e:
         _lib.Engine(max_nodes=8)
     assert e.value.code == _lib.MS_E_NODEV
+
+
+def hip_runtimes_mapped():
+    libs = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and "libamdhip64" in parts[-1]:
+                libs.add(os.path.realpath(parts[-1]))
+    return libs
+
+
+def test_single_hip_runtime_per_process():
+    # torch and libminisched_gpu.so must share one HIP runtime (see _lib.load)
+    import torch  # noqa: F401
+
+    _lib.load()
+    assert len(hip_runtimes_mapped()) == 1, hip_runtimes_mapped()
