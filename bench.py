@@ -55,11 +55,13 @@ def cpu_baseline(n_nodes, seed, target_s):
 
     threads = min(16, os.cpu_count() or 1)  # the box's CPU share is 16
     nr = synth.nodes(n_nodes, seed=seed)
-    probe = synth.pods(64, seed=seed)
+    n_probe = 1024
+    probe = synth.pods(n_probe, seed=seed)
+    _oracle.schedule_nunn_omp(nr, probe[:64], seed=seed, threads=threads)  # thread pool warm-up
     t0 = time.perf_counter()
     _oracle.schedule_nunn_omp(nr, probe, seed=seed, threads=threads)
     dt = max(time.perf_counter() - t0, 1e-6)
-    n_pods = int(min(200_000, max(64, 64 * target_s / dt)))
+    n_pods = int(min(1_000_000, max(n_probe, n_probe * target_s / dt)))
     pr = synth.pods(n_pods, seed=seed)
     t0 = time.perf_counter()
     _oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=threads)
@@ -106,8 +108,11 @@ def main():
     pods = torch.from_numpy(pods_np.view(np.uint8).copy()).to(dev)
     keys = torch.empty(P, dtype=torch.int64, device=dev)
     results = torch.empty(P * _lib.RESULT.itemsize, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream()
+    # a real (non-null) stream: ms_* treat a NULL stream as the context's own
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp != 0
 
     sweep_events = []
 

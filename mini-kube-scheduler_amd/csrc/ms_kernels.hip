@@ -10,6 +10,9 @@
 // tile of node columns in registers and stream pods through it: one node per
 // lane-slot, pods wave-uniform (scalar loads), a 64-bit wave max per pod and
 // one coalesced atomicMax wave-instruction per 64 pods.
+#include <algorithm>
+#include <cstdlib>
+
 #include "ms_internal.h"
 
 namespace msgpu {
@@ -108,6 +111,135 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
         if (WANT_FLAGS) {
             const bool nu = !pr.tolerates_unschedulable && unsched_present != 0;
             const bool any_nu = __ballot(nu) != 0;
+            if (lane == slot) myflag = any_nu ? 1u : 0u;
+        }
+        if (slot == 63u || p + 1 == pend) {
+            const uint32_t pp = p - slot + lane;
+            if (lane <= slot && mine) atomicMax(&keys[pp], mine);
+            if (WANT_FLAGS && lane <= slot && myflag) atomicOr(&pflags[pp], myflag);
+            mine = 0;
+            myflag = 0;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// K1 (lazy tie-break), the production NU+NN sweep.
+//
+// Every (pod, node) pair is filtered and scored, four nodes per 32-bit op
+// (SWAR over the digit bytes); only pairs that reach the wave's best score
+// pay for the 32-bit tie-break hash. Within a wave the best score is 10 as
+// soon as one lane holds a feasible digit match (NodeNumber's only non-zero
+// score), so lanes hash just their own score-10 candidates in a short
+// divergent loop, then the wave takes the max (hash, -ordinal) pair.
+//
+// Row masks use the SWAR bit layout: bit b <-> slot 4*(b&7) + (b>>3), i.e.
+// byte j of digit dword k sits at bit 8j+k. Ties on the hash are broken
+// towards the lower ordinal explicitly, exactly as the packed key orders them.
+// ----------------------------------------------------------------------------
+constexpr int kLazySlots = 32;
+constexpr int kLazyWaveRows = 64 * kLazySlots;         // 2048 rows per wave
+constexpr int kLazyTile = kNunnThreads * kLazySlots;   // 8192 rows per block
+
+__device__ __forceinline__ uint32_t slot_of_bit(uint32_t b) { return ((b & 7u) << 2) | (b >> 3); }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return v;
+}
+
+// high bit of each zero byte of x (exact, no borrow false positives)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+    return ~t & 0x80808080u;
+}
+
+template <bool WANT_FLAGS>
+__global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn_lazy(
+    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
+    uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
+    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave_row0 = blockIdx.x * kLazyTile + (threadIdx.x >> 6) * kLazyWaveRows;
+    if (wave_row0 >= n_rows) return;  // wave-uniform: no rows, nothing to report
+    const uint32_t row0 = wave_row0 + lane * kLazySlots;
+
+    uint32_t dw[8];
+    uint32_t unsched = 0, absent = 0;  // SWAR bit layout
+    if (row0 + kLazySlots <= n_rows) {
+        const uint4 *dp = reinterpret_cast<const uint4 *>(ndigit + row0);
+        const uint4 *fp = reinterpret_cast<const uint4 *>(nflags + row0);
+        const uint4 d0 = dp[0], d1 = dp[1], f0 = fp[0], f1 = fp[1];
+        dw[0] = d0.x; dw[1] = d0.y; dw[2] = d0.z; dw[3] = d0.w;
+        dw[4] = d1.x; dw[5] = d1.y; dw[6] = d1.z; dw[7] = d1.w;
+        const uint32_t fw[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            absent |= (fw[k] & 0x80808080u) >> (7 - k);
+            unsched |= ((fw[k] & 0x01010101u) << 7) >> (7 - k);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            uint32_t d = 0, f = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t r = row0 + 4 * k + j;
+                const uint32_t dv = r < n_rows ? ndigit[r] : 0xFFu;
+                const uint32_t fv = r < n_rows ? nflags[r] : kNodeAbsent;
+                d |= dv << (8 * j);
+                f |= fv << (8 * j);
+            }
+            dw[k] = d;
+            absent |= (f & 0x80808080u) >> (7 - k);
+            unsched |= ((f & 0x01010101u) << 7) >> (7 - k);
+        }
+    }
+    const uint32_t hterm0 = (node_base + row0) * kGolden32;
+    const uint32_t unsched_present = unsched & ~absent;
+
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    u64 mine = 0;
+    uint32_t myflag = 0;
+    for (uint32_t p = pbeg; p < pend; ++p) {
+        const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
+        const uint32_t A = fmix32(seed32 ^ pr.ordinal);
+        // a non-digit pod name (-1) becomes 0xFE, which matches no node byte
+        const uint32_t pd = pr.name_digit >= 0 ? (uint32_t)pr.name_digit : 0xFEu;
+        const uint32_t rep = pd * 0x01010101u;
+        uint32_t match = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) match |= zero_bytes(dw[k] ^ rep) >> (7 - k);
+        const uint32_t feas = ~(pr.tolerates_unschedulable ? absent : (absent | unsched));
+        const uint32_t c10 = match & feas;
+        const bool any10 = __ballot(c10 != 0) != 0;  // wave-uniform best score
+        uint32_t cand = any10 ? c10 : feas;
+        const bool valid = cand != 0;
+        uint32_t bh = 0, bs = 0xFFFFFFFFu;
+        while (cand) {  // lane-divergent: hash only the wave-best-score candidates
+            const uint32_t b = (uint32_t)__builtin_ctz(cand);
+            cand &= cand - 1;
+            const uint32_t s = slot_of_bit(b);
+            const uint32_t h = fmix32(A ^ (hterm0 + s * kGolden32));
+            if (h > bh || (h == bh && s < bs)) {
+                bh = h;
+                bs = s;
+            }
+        }
+        const uint32_t hmax = wave_max_u32(valid ? bh : 0u);
+        const u64 winners = __ballot(valid && bh == hmax);  // lowest lane = lowest ordinal
+        u64 best = 0;
+        if (winners) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(winners);
+            const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)bs, (int)L);
+            best = make_key(any10 ? 10u : 0u, hmax, node_base + wave_row0 + L * kLazySlots + ws);
+        }
+        const uint32_t slot = (p - pbeg) & 63u;
+        if (lane == slot) mine = best;
+        if (WANT_FLAGS) {
+            const bool any_nu = __ballot(!pr.tolerates_unschedulable && unsched_present != 0) != 0;
             if (lane == slot) myflag = any_nu ? 1u : 0u;
         }
         if (slot == 63u || p + 1 == pend) {
@@ -553,18 +685,42 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 
 }  // namespace
 
+// K1 variant: "lazy" (default) or "v0" (hash every pair; kept for A/B runs
+// inside one process), read from MINISCHED_K1 at each launch.
+static int k1_variant() {
+    const char *e = getenv("MINISCHED_K1");
+    return (e && e[0] == 'v' && e[1] == '0') ? 0 : 1;
+}
+
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s) {
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
-    const uint32_t gx = cdiv(n_rows, kNunnTile);
-    const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+    if (k1_variant() == 0) {
+        const uint32_t gx = cdiv(n_rows, kNunnTile);
+        const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+        const dim3 grid(gx, cdiv(n_pods, chunk));
+        if (flags)
+            hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+                               t.base, pods, n_pods, chunk, seed32, keys, flags);
+        else
+            hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+                               t.base, pods, n_pods, chunk, seed32, keys, flags);
+        return hipGetLastError();
+    }
+    const uint32_t gx = cdiv(n_rows, kLazyTile);
+    // pod chunks so that live waves ~ 8 per SIMD across the chip
+    const uint32_t live_waves = cdiv(n_rows, kLazyWaveRows);
+    const uint32_t target = (uint32_t)(num_cus > 0 ? num_cus : 256) * 32u;
+    uint32_t chunks = cdiv(target, live_waves);
+    chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, cdiv(n_pods, 64)));
+    const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
     const dim3 grid(gx, cdiv(n_pods, chunk));
     if (flags)
-        hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows, t.base,
-                           pods, n_pods, chunk, seed32, keys, flags);
+        hipLaunchKernelGGL(k_sweep_nunn_lazy<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+                           t.base, pods, n_pods, chunk, seed32, keys, flags);
     else
-        hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+        hipLaunchKernelGGL(k_sweep_nunn_lazy<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
                            t.base, pods, n_pods, chunk, seed32, keys, flags);
     return hipGetLastError();
 }

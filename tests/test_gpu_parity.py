@@ -68,9 +68,16 @@ def test_readme_scenario_gpu(oracle):
         assert e.read(9, 1)["pod_count"][0] == 1  # assume-on-select
 
 
-@pytest.mark.parametrize("n_nodes", [1, 15, 16, 17, 1000, 4095, 4096, 4097, 12345])
+@pytest.fixture(params=["lazy", "v0"])
+def k1_variant(request, monkeypatch):
+    # both NU+NN sweep kernels stay bit-exact (v0 is the A/B reference build)
+    monkeypatch.setenv("MINISCHED_K1", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("n_nodes", [1, 15, 16, 17, 1000, 2047, 2048, 2049, 4096, 8193, 12345])
 @pytest.mark.parametrize("n_pods", [1, 63, 64, 65, 700])
-def test_nunn_random_sizes(oracle, n_nodes, n_pods):
+def test_nunn_random_sizes(oracle, k1_variant, n_nodes, n_pods):
     seed = 1000 + n_nodes * 7 + n_pods
     nr = synth.nodes(n_nodes, seed=seed)
     pr = synth.pods(n_pods, seed=seed)
@@ -82,7 +89,7 @@ def test_nunn_random_sizes(oracle, n_nodes, n_pods):
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 
-def test_nunn_edge_cases(oracle):
+def test_nunn_edge_cases(oracle, k1_variant):
     pr = synth.pods(130, seed=4)
     # empty table: FitError with an empty mask
     with Engine(max_nodes=64) as e:
@@ -111,7 +118,7 @@ def test_nunn_edge_cases(oracle):
         assert e.info().present_nodes == 5000
 
 
-def test_config_b_exact_sequential(oracle):
+def test_config_b_exact_sequential(oracle, k1_variant):
     # BASELINE config B: 5k nodes x 10k pods, NU+NN, exact sequential
     nr = synth.nodes(5000, seed=1)
     pr = synth.pods(10000, seed=1)
@@ -122,7 +129,7 @@ def test_config_b_exact_sequential(oracle):
         assert_table_equal(e, o["cols"], 5000)
 
 
-def test_config_c_shape_prefix(oracle):
+def test_config_c_shape_prefix(oracle, k1_variant):
     # config C nodes (100k) against a 1k-pod prefix, plus a 20k-pod run
     # checked on a strided sample
     nr = synth.nodes(100_000, seed=1)
@@ -137,29 +144,29 @@ def test_config_c_shape_prefix(oracle):
 def test_node_sharded_combine_equals_single(oracle):
     # two contexts own disjoint ordinal ranges (what each rank of bench.py does);
     # the element-wise max of their keys decodes to the single-context result
-    import ctypes
-
     import torch
 
     n, p = 20_000, 3000
     nr = synth.nodes(n, seed=8)
     pr = synth.pods(p, seed=8)
     dev = torch.device("cuda:0")
-    pods_d = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
-    keys = []
-    cuts = [0, 7777, n]
+    stream = torch.cuda.Stream(device=dev)  # all work ordered on one real stream
+    sp = stream.cuda_stream
     engines = []
-    for a, b in zip(cuts[:-1], cuts[1:]):
-        e = engine_with(nr[a:b], seed=8, node_base=a)
-        engines.append(e)
-        k = torch.empty(p, dtype=torch.int64, device=dev)
-        e.sweep_device(p, pods_d.data_ptr(), k.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
-        keys.append(k)
-    comb = torch.maximum(keys[0], keys[1])
-    res_d = torch.empty(p * 24, dtype=torch.uint8, device=dev)
-    engines[0].decode_device(p, pods_d.data_ptr(), comb.data_ptr(), 0, n, res_d.data_ptr(),
-                             torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        pods_d = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+        keys = []
+        cuts = [0, 7777, n]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            e = engine_with(nr[a:b], seed=8, node_base=a)
+            engines.append(e)
+            k = torch.empty(p, dtype=torch.int64, device=dev)
+            e.sweep_device(p, pods_d.data_ptr(), k.data_ptr(), 0, sp)
+            keys.append(k)
+        comb = torch.maximum(keys[0], keys[1])
+        res_d = torch.empty(p * 24, dtype=torch.uint8, device=dev)
+        engines[0].decode_device(p, pods_d.data_ptr(), comb.data_ptr(), 0, n, res_d.data_ptr(), sp)
+    stream.synchronize()
     res = res_d.cpu().numpy().view(_lib.RESULT)
     o = oracle.schedule(nr, pr, seed=8)
     assert_same(res, o)
