@@ -191,7 +191,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_sweep_nunn",
+                "kernel": "k_sweep_nunn" if os.environ.get("MINISCHED_K1", "") == "v0" else "k_sweep_nunn_lazy",
                 "kernel_ms": sweep_ms,
                 "algorithmic_bytes_per_launch": local_evals * BYTES_PER_EVAL[plugins],
             },
