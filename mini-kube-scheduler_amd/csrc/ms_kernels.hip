@@ -253,6 +253,181 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn_lazy(
 }
 
 // ----------------------------------------------------------------------------
+// K1 v2 ("bits"): bit-sliced node columns.
+//
+// At tile load each lane turns its SLOTS digit bytes into ten one-hot row
+// masks (bit s of onehot[d] <=> row row0+s has name digit d) and its flag
+// bytes into unschedulable/absent masks. For a pod, digit equality against
+// all SLOTS rows is then one register (a wave-uniform select on the pod's
+// digit) and the NodeUnschedulable filter one and-not: every pair is still
+// filtered and scored, SLOTS pairs per bitwise op. Bits are in row order, so
+// the candidate loop visits rows in ascending ordinal and a strict '>' keeps
+// the lower ordinal on equal hashes, exactly as the packed key orders them.
+// ----------------------------------------------------------------------------
+template <int SLOTS>
+struct RowMask;
+template <>
+struct RowMask<32> {
+    typedef uint32_t T;
+    static __device__ __forceinline__ uint32_t ctz(T m) { return (uint32_t)__builtin_ctz(m); }
+};
+template <>
+struct RowMask<64> {
+    typedef u64 T;
+    static __device__ __forceinline__ uint32_t ctz(T m) { return (uint32_t)__builtin_ctzll(m); }
+};
+
+// Full 64-lane unsigned max; result is wave-uniform (read from lane 63).
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// (base + s * golden) mod 2^32 with full-rate 24-bit multiplies (s < 2^8)
+__device__ __forceinline__ uint32_t hterm_at(uint32_t base, uint32_t s) {
+    return base + __umul24(s, kGolden32 & 0xFFFFFFu) + (__umul24(s, kGolden32 >> 24) << 24);
+}
+
+template <int SLOTS, bool WANT_FLAGS>
+__device__ __forceinline__ void sweep_nunn_bits_body(
+    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
+    uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
+    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
+    typedef typename RowMask<SLOTS>::T M;
+    constexpr uint32_t kWaveRows = 64u * SLOTS;
+    const uint32_t lane = lane_id();
+    const uint32_t wave_row0 = blockIdx.x * (kNunnThreads * SLOTS) + (threadIdx.x >> 6) * kWaveRows;
+    if (wave_row0 >= n_rows) return;  // wave-uniform: no rows, nothing to report
+    const uint32_t row0 = wave_row0 + lane * SLOTS;
+
+    M onehot[10];
+#pragma unroll
+    for (int d = 0; d < 10; ++d) onehot[d] = 0;
+    M unsched = 0, absent = 0;
+    const bool full = row0 + SLOTS <= n_rows;
+#pragma unroll
+    for (int q = 0; q < SLOTS / 16; ++q) {
+        uint32_t dv[4], fv[4];
+        if (full) {
+            const uint4 d4 = reinterpret_cast<const uint4 *>(ndigit + row0)[q];
+            const uint4 f4 = reinterpret_cast<const uint4 *>(nflags + row0)[q];
+            dv[0] = d4.x; dv[1] = d4.y; dv[2] = d4.z; dv[3] = d4.w;
+            fv[0] = f4.x; fv[1] = f4.y; fv[2] = f4.z; fv[3] = f4.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                dv[k] = 0;
+                fv[k] = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t r = row0 + 16 * q + 4 * k + j;
+                    dv[k] |= (r < n_rows ? (uint32_t)ndigit[r] : 0xFFu) << (8 * j);
+                    fv[k] |= (r < n_rows ? (uint32_t)nflags[r] : (uint32_t)kNodeAbsent) << (8 * j);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int s = 16 * q + 4 * k + j;
+                const uint32_t d = (dv[k] >> (8 * j)) & 0xFFu;
+                const uint32_t f = (fv[k] >> (8 * j)) & 0xFFu;
+                const M bit = (M)1 << s;
+#pragma unroll
+                for (int v = 0; v < 10; ++v) onehot[v] |= (d == (uint32_t)v) ? bit : (M)0;
+                unsched |= (f & kNodeUnschedulable) ? bit : (M)0;
+                absent |= (f & kNodeAbsent) ? bit : (M)0;
+            }
+        }
+    }
+    const uint32_t hterm0 = (node_base + row0) * kGolden32;
+    const M unsched_present = unsched & ~absent;
+
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    u64 mine = 0;
+    uint32_t myflag = 0;
+    for (uint32_t p = pbeg; p < pend; ++p) {
+        const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
+        const uint32_t A = fmix32(seed32 ^ pr.ordinal);
+        M match;
+        switch (pr.name_digit) {  // wave-uniform: scalar branch, no VGPR indexing
+            case 0: match = onehot[0]; break;
+            case 1: match = onehot[1]; break;
+            case 2: match = onehot[2]; break;
+            case 3: match = onehot[3]; break;
+            case 4: match = onehot[4]; break;
+            case 5: match = onehot[5]; break;
+            case 6: match = onehot[6]; break;
+            case 7: match = onehot[7]; break;
+            case 8: match = onehot[8]; break;
+            case 9: match = onehot[9]; break;
+            default: match = 0; break;  // non-digit pod name: NodeNumber scores nothing
+        }
+        const M feas = ~(pr.tolerates_unschedulable ? absent : (absent | unsched));
+        const M c10 = match & feas;
+        const bool any10 = __ballot(c10 != 0) != 0;  // wave-uniform best score
+        M cand = any10 ? c10 : feas;
+        const bool valid = cand != 0;
+        uint32_t bh = 0, bs = 0;
+        if (cand) {  // first candidate (lowest row) seeds the lane's best
+            bs = RowMask<SLOTS>::ctz(cand);
+            cand &= cand - 1;
+            bh = fmix32(A ^ hterm_at(hterm0, bs));
+            while (cand) {  // lane-divergent, ascending rows: strict '>' keeps the lower ordinal
+                const uint32_t s = RowMask<SLOTS>::ctz(cand);
+                cand &= cand - 1;
+                const uint32_t h = fmix32(A ^ hterm_at(hterm0, s));
+                if (h > bh) {
+                    bh = h;
+                    bs = s;
+                }
+            }
+        }
+        const uint32_t hmax = wave_max_u32_dpp(valid ? bh : 0u);
+        const u64 winners = __ballot(valid && bh == hmax);  // lowest lane = lowest ordinal
+        u64 best = 0;
+        if (winners) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(winners);
+            const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)bs, (int)L);
+            best = make_key(any10 ? 10u : 0u, hmax, node_base + wave_row0 + L * SLOTS + ws);
+        }
+        const uint32_t slot = (p - pbeg) & 63u;
+        if (lane == slot) mine = best;
+        if (WANT_FLAGS) {
+            const bool any_nu = __ballot(!pr.tolerates_unschedulable && unsched_present != 0) != 0;
+            if (lane == slot) myflag = any_nu ? 1u : 0u;
+        }
+        if (slot == 63u || p + 1 == pend) {
+            const uint32_t pp = p - slot + lane;
+            if (lane <= slot && mine) atomicMax(&keys[pp], mine);
+            if (WANT_FLAGS && lane <= slot && myflag) atomicOr(&pflags[pp], myflag);
+            mine = 0;
+            myflag = 0;
+        }
+    }
+}
+
+#define MS_K1_BITS_KERNEL(NAME, SLOTS)                                                                       \
+    template <bool WANT_FLAGS>                                                                               \
+    __global__ __launch_bounds__(kNunnThreads) void NAME(                                                    \
+        const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,             \
+        uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,            \
+        uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {                            \
+        sweep_nunn_bits_body<SLOTS, WANT_FLAGS>(nflags, ndigit, n_rows, node_base, pods, n_pods, chunk,      \
+                                                seed32, keys, pflags);                                       \
+    }
+MS_K1_BITS_KERNEL(k_sweep_nunn_bits32, 32)
+MS_K1_BITS_KERNEL(k_sweep_nunn_bits64, 64)
+#undef MS_K1_BITS_KERNEL
+
+// ----------------------------------------------------------------------------
 // K3: NodeUnschedulable + NodeResourcesFit filters, NodeNumber + LeastAllocated
 // scores (upstream v1.22 semantics restated in oracle/ms_oracle.c).
 // ----------------------------------------------------------------------------
@@ -685,43 +860,70 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 
 }  // namespace
 
-// K1 variant: "lazy" (default) or "v0" (hash every pair; kept for A/B runs
-// inside one process), read from MINISCHED_K1 at each launch.
+// K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
+// interleave variants inside one process: "v0" (hash every pair), "lazy"
+// (SWAR + lazy hash), "bits32" / "bits64" (bit-sliced columns). Default bits32.
+enum K1Variant { K1_V0 = 0, K1_LAZY = 1, K1_BITS32 = 2, K1_BITS64 = 3 };
 static int k1_variant() {
     const char *e = getenv("MINISCHED_K1");
-    return (e && e[0] == 'v' && e[1] == '0') ? 0 : 1;
+    if (!e || !e[0]) return K1_BITS32;
+    if (e[0] == 'v' && e[1] == '0') return K1_V0;
+    if (e[0] == 'l') return K1_LAZY;
+    if (e[0] == 'b' && e[4] == '6') return K1_BITS64;
+    return K1_BITS32;
 }
+
+// grid for the wave-tiled sweeps: pod chunks so that live waves ~ 8 per SIMD
+static dim3 wave_tiled_grid(uint32_t n_rows, uint32_t n_pods, uint32_t wave_rows, int num_cus, uint32_t &chunk) {
+    const uint32_t block_rows = wave_rows * (kNunnThreads / 64);
+    const uint32_t gx = cdiv(n_rows, block_rows);
+    const uint32_t live_waves = cdiv(n_rows, wave_rows);
+    const uint32_t target = (uint32_t)(num_cus > 0 ? num_cus : 256) * 32u;
+    uint32_t chunks = cdiv(target, live_waves);
+    chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, cdiv(n_pods, 64)));
+    chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
+    return dim3(gx, cdiv(n_pods, chunk));
+}
+
+#define MS_LAUNCH_K1(KERNEL, WAVE_ROWS)                                                                      \
+    do {                                                                                                     \
+        uint32_t chunk_;                                                                                     \
+        const dim3 grid_ = wave_tiled_grid(n_rows, n_pods, (WAVE_ROWS), num_cus, chunk_);                    \
+        if (flags)                                                                                           \
+            hipLaunchKernelGGL(KERNEL<true>, grid_, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows, t.base, \
+                               pods, n_pods, chunk_, seed32, keys, flags);                                   \
+        else                                                                                                 \
+            hipLaunchKernelGGL(KERNEL<false>, grid_, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,       \
+                               t.base, pods, n_pods, chunk_, seed32, keys, flags);                           \
+    } while (0)
 
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s) {
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
-    if (k1_variant() == 0) {
-        const uint32_t gx = cdiv(n_rows, kNunnTile);
-        const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
-        const dim3 grid(gx, cdiv(n_pods, chunk));
-        if (flags)
-            hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
-                               t.base, pods, n_pods, chunk, seed32, keys, flags);
-        else
-            hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
-                               t.base, pods, n_pods, chunk, seed32, keys, flags);
-        return hipGetLastError();
+    switch (k1_variant()) {
+        case K1_V0: {
+            const uint32_t gx = cdiv(n_rows, kNunnTile);
+            const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+            const dim3 grid(gx, cdiv(n_pods, chunk));
+            if (flags)
+                hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+                                   t.base, pods, n_pods, chunk, seed32, keys, flags);
+            else
+                hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit,
+                                   n_rows, t.base, pods, n_pods, chunk, seed32, keys, flags);
+            break;
+        }
+        case K1_LAZY:
+            MS_LAUNCH_K1(k_sweep_nunn_lazy, kLazyWaveRows);
+            break;
+        case K1_BITS64:
+            MS_LAUNCH_K1(k_sweep_nunn_bits64, 64u * 64u);
+            break;
+        default:
+            MS_LAUNCH_K1(k_sweep_nunn_bits32, 64u * 32u);
+            break;
     }
-    const uint32_t gx = cdiv(n_rows, kLazyTile);
-    // pod chunks so that live waves ~ 8 per SIMD across the chip
-    const uint32_t live_waves = cdiv(n_rows, kLazyWaveRows);
-    const uint32_t target = (uint32_t)(num_cus > 0 ? num_cus : 256) * 32u;
-    uint32_t chunks = cdiv(target, live_waves);
-    chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, cdiv(n_pods, 64)));
-    const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
-    const dim3 grid(gx, cdiv(n_pods, chunk));
-    if (flags)
-        hipLaunchKernelGGL(k_sweep_nunn_lazy<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
-                           t.base, pods, n_pods, chunk, seed32, keys, flags);
-    else
-        hipLaunchKernelGGL(k_sweep_nunn_lazy<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
-                           t.base, pods, n_pods, chunk, seed32, keys, flags);
     return hipGetLastError();
 }
 
