@@ -84,25 +84,35 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from minisched_amd import _lib, synth
+    from minisched_amd import _lib, sharded, synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # MINISCHED_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+    # cards round-robin); the driver's real runs use RCCL ("nccl"), one GPU per rank.
+    backend = os.environ.get("MINISCHED_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        local_dev = local
+    else:
+        local_dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     cfg = synth.CONFIGS[args.config]
     N, P = cfg["nodes"], cfg["pods"]
     plugins = cfg["plugins"]
-    lo, hi = rank * N // world, (rank + 1) * N // world  # this rank's node shard
+    lo, hi = sharded.shard_bounds(N, rank, world)  # this rank's node shard
 
     eng = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NN, node_base=lo, seed=args.seed,
-                      device=local)
+                      device=local_dev)
     eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=args.seed, start=lo))
     eng.flush()
 
@@ -127,7 +137,7 @@ def main():
             b.record(stream)
             sweep_events.append((a, b))
         if world > 1:
-            dist.all_reduce(keys, op=dist.ReduceOp.MAX)
+            sharded.combine_(keys)  # RCCL MAX all-reduce of the packed keys over xGMI
         eng.decode_device(P, pods.data_ptr(), keys.data_ptr(), 0, N, results.data_ptr(), sp)
 
     for _ in range(args.warmup):

@@ -1,0 +1,99 @@
+"""N > 1 path on CPU: node-sharded shards combined over torch.distributed (gloo).
+
+Each rank evaluates its own node shard with the oracle (standing in for the
+HIP sweep, which needs a GPU), then the product's combine_ all-reduces the
+packed keys and filter flags; every rank must end with exactly the keys and
+FitError masks of the single-process run over the whole cluster.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from minisched_amd import sharded, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _decode_mask(keys, flags):
+    return np.where(keys == 0, (flags & 0xFF != 0) * 1 | ((flags >> 8) & 0xFF != 0) * 2, 0)
+
+
+def _worker(rank, world, port, n_nodes, n_pods, plugin_set, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "mini-kube-scheduler_amd"))
+    import _oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = plugin_set == 1
+    nr = synth.nodes(n_nodes, seed=11, resources=res)
+    pr = synth.pods(n_pods, seed=11, resources=res)
+    if res:
+        nr["req_milli_cpu"] = nr["alloc_milli_cpu"] * 3 // 4  # make NRF bite
+        nr["pod_count"][::5] = 110
+    lo, hi = sharded.shard_bounds(n_nodes, rank, world)
+    o = _oracle.schedule(nr[lo:hi], pr, plugin_set=plugin_set, seed=11, node_base=lo)
+    keys = torch.from_numpy(o["key"].view(np.int64).copy())
+    # per-shard flags: a shard with no feasible node reports its own FitError mask
+    m = o["mask"].astype(np.uint32)
+    flags = torch.from_numpy(((m & 1) | ((m >> 1) & 1) << 8).astype(np.int32))
+    sharded.combine_(keys, flags if plugin_set == 1 else None)
+    q.put((rank, keys.numpy().view(np.uint64).copy(), flags.numpy().astype(np.uint32).copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("plugin_set", [0, 1])
+def test_node_sharded_combine_gloo(oracle, world, plugin_set):
+    n_nodes, n_pods = 997, 300
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_nodes, n_pods, plugin_set, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = plugin_set == 1
+    nr = synth.nodes(n_nodes, seed=11, resources=res)
+    pr = synth.pods(n_pods, seed=11, resources=res)
+    if res:
+        nr["req_milli_cpu"] = nr["alloc_milli_cpu"] * 3 // 4
+        nr["pod_count"][::5] = 110
+    full = oracle.schedule(nr, pr, plugin_set=plugin_set, seed=11)
+    for rank, keys, flags in got:
+        assert np.array_equal(keys, full["key"]), f"rank {rank}"
+        if plugin_set == 1:
+            assert np.array_equal(_decode_mask(keys, flags), full["mask"]), f"rank {rank}"
+        # decoded winners: the global ordinal sits in the low 20 bits of the key
+        won = full["code"] == 0
+        assert np.array_equal((0xFFFFF - (keys[won] & 0xFFFFF)).astype(np.int64), full["node"][won].astype(np.int64))
+        assert np.array_equal((keys[won] >> 52).astype(np.int64), full["score"][won])
+
+
+def test_shard_bounds_cover_everything():
+    for n in (0, 1, 7, 100_000):
+        for w in (1, 2, 3, 8):
+            spans = [sharded.shard_bounds(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+    with pytest.raises(ValueError):
+        sharded.shard_bounds(10, 3, 3)
