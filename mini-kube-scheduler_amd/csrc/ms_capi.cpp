@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -157,7 +158,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     c->d_tile_flags = nullptr;
     c->tile_cap = 0;
     const size_t n = (size_t)seq_batch_limit() * n_tiles;
-    if (hipMalloc((void **)&c->d_tile_keys, n * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc((void **)&c->d_tile_keys, n * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential tile keys");
     if (hipMalloc((void **)&c->d_tile_flags, n * sizeof(uint32_t)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential tile flags");
@@ -165,8 +166,17 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     return MS_OK;
 }
 
-// Exact sequential engine: speculative per-tile sweep + in-order validation,
-// batch after batch on one stream.
+// Pods per speculative batch: fewer nodes touched per batch keeps the top-K
+// lists valid; more pods amortise the two launches. MINISCHED_SEQ_BATCH
+// overrides (tuning), clamped to the validator's LDS capacity.
+uint32_t seq_batch(const ms_ctx *) {
+    uint32_t b = 256;
+    if (const char *e = getenv("MINISCHED_SEQ_BATCH")) b = (uint32_t)std::max(1, atoi(e));
+    return std::min(b, seq_batch_limit());
+}
+
+// Exact sequential engine: speculative per-tile top-K sweep + in-order
+// validation, batch after batch on one stream.
 int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s) {
     const uint32_t rows = c->rows_used;
     const uint32_t seed32 = seed32_of(c->cfg.seed);
@@ -181,7 +191,7 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
     int rc = ensure_tiles(c, n_tiles);
     if (rc) return rc;
-    const uint32_t B = seq_batch_limit();
+    const uint32_t B = seq_batch(c);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,

@@ -69,8 +69,9 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s);
-// Per-(pod, wave tile) speculative sweep for the sequential engine:
-// tile_keys[p * n_tiles + t], tile_flags likewise.
+// Per-(pod, wave tile) speculative sweep for the sequential engine: the
+// tile's top-K keys at tile_keys[(p * n_tiles + t) * K + j], 0-terminated,
+// and its filter flags at tile_flags[p * n_tiles + t].
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
                                    uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s);
@@ -89,5 +90,7 @@ hipError_t launch_bind_one(const NodeTable &t, uint32_t local, const ms_pod_rec 
 hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_node_rec *out, hipStream_t s);
 // Largest speculative batch the sequential validator accepts.
 uint32_t seq_batch_limit();
+// Entries per (pod, tile) speculative list: tile_keys has n_pods * n_tiles * seq_topk() u64.
+uint32_t seq_topk();
 
 }  // namespace msgpu

@@ -522,15 +522,13 @@ __device__ __forceinline__ u64 eval_full(const FullRow &x, uint32_t ord, const P
     return make_key(nn + la, h, ord);
 }
 
-// OUT_TILES=false: atomicMax into keys[P] / atomicOr into flags[P].
-// OUT_TILES=true : per (pod, wave tile) key and flags for the sequential validator.
-template <bool OUT_TILES>
-__global__ __launch_bounds__(kFullThreads) void k_sweep_full(
-    NodeTable t, uint32_t n_rows, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
-    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t n_tiles) {
+// Batched resource-aware sweep: atomicMax into keys[P] / atomicOr into flags[P].
+__global__ __launch_bounds__(kFullThreads) void k_sweep_full(NodeTable t, uint32_t n_rows,
+                                                             const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                                                             uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
+                                                             uint32_t *__restrict__ pflags) {
     const uint32_t lane = lane_id();
     const uint32_t row0 = blockIdx.x * kFullTile + threadIdx.x * kFullSlots;
-    const uint32_t wave_tile = (blockIdx.x * kFullTile + (threadIdx.x & ~63u) * kFullSlots) / kFullWaveTile;
     FullRow x[kFullSlots];
 #pragma unroll
     for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
@@ -558,15 +556,9 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full(
         if (lane == slot) { mine = best; myflag = f; }
         if (slot == 63u || p + 1 == pend) {
             const uint32_t pp = p - slot + lane;
-            // a wave entirely past the last row owns no tile and writes nothing
-            if (lane <= slot && (!OUT_TILES || wave_tile < n_tiles)) {
-                if (OUT_TILES) {
-                    keys[(size_t)pp * n_tiles + wave_tile] = mine;
-                    pflags[(size_t)pp * n_tiles + wave_tile] = myflag;
-                } else {
-                    if (mine) atomicMax(&keys[pp], mine);
-                    if (myflag) atomicOr(&pflags[pp], myflag);
-                }
+            if (lane <= slot) {
+                if (mine) atomicMax(&keys[pp], mine);
+                if (myflag) atomicOr(&pflags[pp], myflag);
             }
             mine = 0;
             myflag = 0;
@@ -574,29 +566,112 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full(
     }
 }
 
+// 64-bit unsigned wave max from two DPP u32 reductions; wave-uniform result.
+__device__ __forceinline__ u64 wave_max_u64_dpp(u64 v) {
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    const uint32_t hmax = wave_max_u32_dpp(hi);
+    const uint32_t lmax = wave_max_u32_dpp(hi == hmax ? lo : 0u);
+    return ((u64)hmax << 32) | lmax;
+}
+
+__device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
+    const u64 hi = umax64(a, b), lo = a > b ? b : a;
+    a = hi;
+    b = lo;
+}
+
 // ----------------------------------------------------------------------------
-// Exact sequential validator (config E). One wave walks the speculative batch
-// in queue order. Speculative per-(pod,tile) maxima were computed against the
-// state at batch start; a bind only lowers keys of the node it lands on
-// (NRF feasibility and LeastAllocated are monotone in Requested/PodCount; NU,
-// NN and the hash do not read them). So a tile whose maximum sits on a node
-// untouched so far in the batch is still exact, and only tiles whose argmax
-// node was modified are re-swept against the current state.
+// Exact sequential engine, speculative half (config E).
+// For each pod of a batch and each 256-row wave tile: the tile's top-K packed
+// keys against the batch-start state (0-terminated when the tile has fewer
+// than K feasible rows) and the tile's filter flags.
+// ----------------------------------------------------------------------------
+constexpr int kTopK = 4;
+static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
+
+__global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, uint32_t n_rows,
+                                                                  const ms_pod_rec *__restrict__ pods,
+                                                                  uint32_t n_pods, uint32_t chunk, uint32_t seed32,
+                                                                  u64 *__restrict__ tile_keys,
+                                                                  uint32_t *__restrict__ tile_flags,
+                                                                  uint32_t n_tiles) {
+    const uint32_t lane = lane_id();
+    const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
+    if (tile >= n_tiles) return;  // wave-uniform; no block barriers in this kernel
+    const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
+    FullRow x[kFullSlots];
+#pragma unroll
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
+    const uint32_t ord0 = t.base + row0;
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    for (uint32_t p = pbeg; p < pend; ++p) {
+        const PodFull q = load_pod(pods[p], seed32);
+        u64 k[kFullSlots];
+        uint32_t nu_any = 0, nrf_any = 0;
+#pragma unroll
+        for (int s = 0; s < kFullSlots; ++s) {
+            uint32_t nu, nrf;
+            k[s] = eval_full(x[s], ord0 + s, q, nu, nrf);
+            nu_any |= nu;
+            nrf_any |= nrf;
+        }
+        // descending sort of the lane's 4 keys (keys are unique unless 0)
+        cswap_desc(k[0], k[1]);
+        cswap_desc(k[2], k[3]);
+        cswap_desc(k[0], k[2]);
+        cswap_desc(k[1], k[3]);
+        cswap_desc(k[1], k[2]);
+        u64 out = 0;
+#pragma unroll
+        for (int j = 0; j < kTopK; ++j) {
+            const u64 m = wave_max_u64_dpp(k[0]);
+            if (lane == (uint32_t)j) out = m;
+            if (m != 0 && k[0] == m) {  // the owning lane pops its head
+                k[0] = k[1];
+                k[1] = k[2];
+                k[2] = k[3];
+                k[3] = 0;
+            }
+        }
+        const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
+        const size_t cell = (size_t)p * n_tiles + tile;
+        if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out;
+        if (lane == 0) tile_flags[cell] = f;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Exact sequential engine, in-order half. One 1024-thread workgroup walks the
+// batch in queue order. A bind only lowers keys of the node it lands on (NRF
+// feasibility and LeastAllocated are monotone in Requested/pod_count; NU, NN
+// and the hash do not read them), so for each tile the first top-K entry whose
+// node is untouched so far in the batch is still that tile's best among
+// untouched nodes; entries above it (touched nodes) are re-evaluated from the
+// LDS copy of their current record. Only a tile whose K entries are all
+// touched (and whose list is not complete) is re-swept against current state.
 // ----------------------------------------------------------------------------
 constexpr int kSeqBatch = 1024;
-constexpr int kMapCap = 2048;  // power of two, >= 2 * kSeqBatch
+constexpr int kMapBits = 12;
+constexpr int kMapCap = 1 << kMapBits;  // >= 4 * kSeqBatch
+constexpr int kValThreads = 1024;
+constexpr int kValWaves = kValThreads / 64;
 
 struct SeqShared {
     uint32_t map_row[kMapCap];  // row + 1, 0 = empty
     uint16_t map_slot[kMapCap];
+    // full current record of each node bound in this batch
     int64_t req_cpu[kSeqBatch], req_mem[kSeqBatch], nz_cpu[kSeqBatch], nz_mem[kSeqBatch];
-    int32_t cnt[kSeqBatch];
-    uint32_t row[kSeqBatch];
-    uint32_t n_slots;
+    int64_t alloc_cpu[kSeqBatch], alloc_mem[kSeqBatch];
+    int32_t cnt[kSeqBatch], allowed[kSeqBatch];
+    uint32_t fd[kSeqBatch], row[kSeqBatch];
+    u64 wave_best[kValWaves];
+    uint32_t wave_fl[kValWaves];
+    uint32_t need[kSeqBatch];  // tiles to re-sweep for the current pod (bounded below)
+    uint32_t n_need, n_slots;
 };
 
-__device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - 11); }
-static_assert(kMapCap == 1 << 11, "map hash width");
+__device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
 
 __device__ __forceinline__ int map_find(const SeqShared &S, uint32_t row) {
     uint32_t h = map_hash(row);
@@ -609,85 +684,132 @@ __device__ __forceinline__ int map_find(const SeqShared &S, uint32_t row) {
     return -1;
 }
 
-__global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_rows,
-                                                     const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
-                                                     uint32_t seed32, const u64 *__restrict__ tile_keys,
-                                                     const uint32_t *__restrict__ tile_flags, uint32_t n_tiles,
-                                                     ms_result *__restrict__ results,
-                                                     uint32_t *__restrict__ overflow) {
+__device__ __forceinline__ FullRow slot_row(const SeqShared &S, int sl) {
+    FullRow x;
+    x.alloc_cpu = S.alloc_cpu[sl];
+    x.alloc_mem = S.alloc_mem[sl];
+    x.free_cpu = x.alloc_cpu - S.req_cpu[sl];
+    x.free_mem = x.alloc_mem - S.req_mem[sl];
+    x.nz_cpu = S.nz_cpu[sl];
+    x.nz_mem = S.nz_mem[sl];
+    x.room = S.allowed[sl] - S.cnt[sl];
+    x.fd = S.fd[sl];
+    return x;
+}
+
+__global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint32_t n_rows,
+                                                              const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                                                              uint32_t seed32, const u64 *__restrict__ tile_keys,
+                                                              const uint32_t *__restrict__ tile_flags,
+                                                              uint32_t n_tiles, ms_result *__restrict__ results,
+                                                              uint32_t *__restrict__ overflow) {
     __shared__ SeqShared S;
-    const uint32_t lane = threadIdx.x;
-    for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map_row[i] = 0;
-    if (lane == 0) S.n_slots = 0;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint32_t i = tid; i < (uint32_t)kMapCap; i += kValThreads) S.map_row[i] = 0;
+    if (tid == 0) {
+        S.n_slots = 0;
+        S.n_need = 0;
+    }
     __syncthreads();
     if (n_pods > (uint32_t)kSeqBatch) {  // host guarantees this; never index past S
-        if (lane == 0) *overflow = 1;
+        if (tid == 0) *overflow = 1;
         return;
     }
 
     for (uint32_t p = 0; p < n_pods; ++p) {
-        const ms_pod_rec pr = pods[p];
-        const PodFull q = load_pod(pr, seed32);
+        const PodFull q = load_pod(pods[p], seed32);
+        // ---- phase A: every tile's best from its speculative top-K list
         u64 best = 0;
         uint32_t fl = 0;
-        for (uint32_t tb = 0; tb < n_tiles; tb += 64) {
-            const uint32_t tt = tb + lane;
-            bool need = false;
-            if (tt < n_tiles) {
-                const u64 k = tile_keys[(size_t)p * n_tiles + tt];
-                if (k) {
-                    const uint32_t row = (0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) - t.base;
-                    if (map_find(S, row) >= 0) need = true;
-                    else best = umax64(best, k);
-                } else {
-                    fl |= tile_flags[(size_t)p * n_tiles + tt];
-                }
+        for (uint32_t tt = tid; tt < n_tiles; tt += kValThreads) {
+            const size_t cell = (size_t)p * n_tiles + tt;
+            const u64 *e = tile_keys + cell * kTopK;
+            const uint32_t sf = tile_flags[cell];
+            u64 c = 0, r = 0;
+            bool found = false, ended = false;
+#pragma unroll
+            for (int j = 0; j < kTopK; ++j) {
+                const u64 ej = e[j];
+                if (ej == 0) { ended = true; break; }
+                const uint32_t row = (0xFFFFFu - (uint32_t)(ej & 0xFFFFFu)) - t.base;
+                const int sl = map_find(S, row);
+                if (sl < 0) { c = ej; found = true; break; }
+                uint32_t nu, nrf;
+                r = umax64(r, eval_full(slot_row(S, sl), t.base + row, q, nu, nrf));
             }
-            u64 m = __ballot(need);
-            while (m) {  // wave-uniform loop over tiles to re-sweep
-                const uint32_t tile = tb + (uint32_t)__builtin_ctzll(m);
-                m &= m - 1;
+            if (!found && !ended) {
+                const uint32_t i = atomicAdd(&S.n_need, 1u);
+                if (i < (uint32_t)kSeqBatch) S.need[i] = tt;
+                else atomicOr(overflow, 2u);  // unreachable: each such tile holds K distinct touched rows, so n_need <= n_slots / K
+            } else {
+                const u64 tb = umax64(c, r);
+                best = umax64(best, tb);
+                // no feasible row left in this tile: its rejections are the
+                // speculative ones plus NRF for every row a bind made infeasible
+                if (tb == 0) fl |= sf | (e[0] != 0 ? 0x100u : 0u);
+            }
+        }
+        best = wave_max_u64_dpp(best);
+        const uint32_t wfl = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+        if (lane == 0) {
+            S.wave_best[wave] = best;
+            S.wave_fl[wave] = wfl;
+        }
+        __syncthreads();
+        // ---- phase B: re-sweep tiles whose K listed nodes were all touched
+        const uint32_t n_need = min(S.n_need, (uint32_t)kSeqBatch);
+        if (n_need) {
+            u64 rb = 0;
+            uint32_t rfl = 0;
+            for (uint32_t i = wave; i < n_need; i += kValWaves) {
+                const uint32_t tile = S.need[i];
 #pragma unroll
                 for (int s = 0; s < kFullSlots; ++s) {
                     const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + s;
                     FullRow x = load_row(t, r, n_rows);
                     if (r < n_rows) {
                         const int sl = map_find(S, r);
-                        if (sl >= 0) {
-                            x.free_cpu = x.alloc_cpu - S.req_cpu[sl];
-                            x.free_mem = x.alloc_mem - S.req_mem[sl];
-                            x.nz_cpu = S.nz_cpu[sl];
-                            x.nz_mem = S.nz_mem[sl];
-                            x.room = t.allowed_pods[r] - S.cnt[sl];
-                        }
+                        if (sl >= 0) x = slot_row(S, sl);
                     }
                     uint32_t nu, nrf;
-                    best = umax64(best, eval_full(x, t.base + r, q, nu, nrf));
-                    fl |= (nu ? 1u : 0u) | (nrf ? 0x100u : 0u);
+                    rb = umax64(rb, eval_full(x, t.base + r, q, nu, nrf));
+                    rfl |= (nu ? 1u : 0u) | (nrf ? 0x100u : 0u);
                 }
             }
+            rb = wave_max_u64_dpp(rb);
+            const uint32_t rw = (__ballot((rfl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((rfl & 0xFF00u) != 0) ? 0x100u : 0u);
+            if (lane == 0) {
+                S.wave_best[wave] = umax64(S.wave_best[wave], rb);
+                S.wave_fl[wave] |= rw;
+            }
+            __syncthreads();
         }
-        best = wave_max_u64(best);
-        fl = wave_or_u32(fl);
-        if (lane == 0) {
+        // ---- phase C: decide, commit the bind, publish the result
+        if (tid == 0) {
+            u64 b = 0;
+            uint32_t f = 0;
+            for (int w = 0; w < kValWaves; ++w) {
+                b = umax64(b, S.wave_best[w]);
+                f |= S.wave_fl[w];
+            }
             ms_result res;
             res._pad = 0;
-            if (best == 0) {
+            if (b == 0) {
                 res.node = -1;
                 res.code = MS_CODE_UNSCHEDULABLE;
                 res.score = 0;
-                res.plugin_mask = ((fl & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
-                                  ((fl & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
+                res.plugin_mask = ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                                  ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
             } else if (q.dig < 0) {
                 res.node = -1;
                 res.code = MS_CODE_ERROR;
                 res.score = 0;
                 res.plugin_mask = 0;
             } else {
-                const uint32_t node = 0xFFFFFu - (uint32_t)(best & 0xFFFFFu);
+                const uint32_t node = 0xFFFFFu - (uint32_t)(b & 0xFFFFFu);
                 res.node = (int32_t)node;
                 res.code = MS_CODE_SUCCESS;
-                res.score = (int64_t)(best >> 52);
+                res.score = (int64_t)(b >> 52);
                 res.plugin_mask = 0;
                 // assume-on-select: NodeInfo.AddPod on the winner
                 const uint32_t row = node - t.base;
@@ -704,6 +826,10 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                     S.nz_cpu[sl] = t.nz_cpu[row];
                     S.nz_mem[sl] = t.nz_mem[row];
                     S.cnt[sl] = t.pod_count[row];
+                    S.alloc_cpu[sl] = t.alloc_cpu[row];
+                    S.alloc_mem[sl] = t.alloc_mem[row];
+                    S.allowed[sl] = t.allowed_pods[row];
+                    S.fd[sl] = (uint32_t)t.flags[row] | ((uint32_t)t.digit[row] << 8);
                 }
                 S.req_cpu[sl] += q.rc;
                 S.req_mem[sl] += q.rm;
@@ -712,12 +838,13 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                 S.cnt[sl] += 1;
             }
             results[p] = res;
+            S.n_need = 0;
         }
         __syncthreads();
     }
     // commit the batch's modified rows; the next speculative sweep is a new
     // launch on the same stream, so it observes these stores.
-    for (uint32_t sl = lane; sl < S.n_slots; sl += 64) {
+    for (uint32_t sl = tid; sl < S.n_slots; sl += kValThreads) {
         const uint32_t r = S.row[sl];
         t.req_cpu[r] = S.req_cpu[sl];
         t.req_mem[r] = S.req_mem[sl];
@@ -934,8 +1061,8 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
     const uint32_t gx = cdiv(n_rows, kFullTile);
     const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
     const dim3 grid(gx, cdiv(n_pods, chunk));
-    hipLaunchKernelGGL(k_sweep_full<false>, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk,
-                       seed32, keys, flags, 0u);
+    hipLaunchKernelGGL(k_sweep_full, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32, keys,
+                       flags);
     return hipGetLastError();
 }
 
@@ -944,10 +1071,10 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
                                    uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s) {
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
     if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
-    const uint32_t gx = cdiv(n_rows, kFullTile);
-    const uint32_t chunk = 64;  // batch <= kSeqBatch: one wave-slot group per block row
+    const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
+    const uint32_t chunk = 16;  // pods per wave: node rows amortised, >= 16 x n_tiles waves
     const dim3 grid(gx, cdiv(n_pods, chunk));
-    hipLaunchKernelGGL(k_sweep_full<true>, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
+    hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
                        tile_keys, tile_flags, n_tiles);
     return hipGetLastError();
 }
@@ -957,8 +1084,8 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
                                uint32_t n_tiles, ms_result *results, uint32_t *overflow, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_validate_seq, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys,
-                       tile_flags, n_tiles, results, overflow);
+    hipLaunchKernelGGL(k_validate_seq, dim3(1), dim3(kValThreads), 0, s, t, n_rows, pods, n_pods, seed32,
+                       tile_keys, tile_flags, n_tiles, results, overflow);
     return hipGetLastError();
 }
 
@@ -1002,5 +1129,6 @@ hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_n
 }
 
 uint32_t seq_batch_limit() { return (uint32_t)kSeqBatch; }
+uint32_t seq_topk() { return (uint32_t)kTopK; }
 
 }  // namespace msgpu
