@@ -118,13 +118,14 @@ def main():
 
     pods_np = synth.pods(P, seed=args.seed)
     pods = torch.from_numpy(pods_np.view(np.uint8).copy()).to(dev)
-    keys = torch.empty(P, dtype=torch.int64, device=dev)
-    results = torch.empty(P * _lib.RESULT.itemsize, dtype=torch.uint8, device=dev)
     # a real (non-null) stream: ms_* treat a NULL stream as the context's own
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
-    assert sp != 0
+    assert stream.cuda_stream != 0
+    # N > 1: pod chunks so each chunk's RCCL all-reduce overlaps the next sweep
+    chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
+    cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks)
+    results = cyc.results
 
     sweep_events = []
 
@@ -132,13 +133,11 @@ def main():
         if timed:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
-        eng.sweep_device(P, pods.data_ptr(), keys.data_ptr(), 0, sp)
-        if timed:
+            cyc.step(world)
             b.record(stream)
             sweep_events.append((a, b))
-        if world > 1:
-            sharded.combine_(keys)  # RCCL MAX all-reduce of the packed keys over xGMI
-        eng.decode_device(P, pods.data_ptr(), keys.data_ptr(), 0, N, results.data_ptr(), sp)
+        else:
+            cyc.step(world)
 
     for _ in range(args.warmup):
         step(False)
@@ -158,7 +157,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in sweep_events]))
+    step_dev_ms = float(np.mean([a.elapsed_time(b) for a, b in sweep_events]))
+    # kernel-only timing on the sweep's stream: separate timed launches after the run
+    kev = []
+    for _ in range(max(3, min(args.steps, 10))):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        cyc.sweep(0, P)
+        b.record(stream)
+        kev.append((a, b))
+    torch.cuda.synchronize()
+    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     res = results.cpu().numpy().view(_lib.RESULT)
     ok = int((res["code"] == _lib.CODE_SUCCESS).sum())
 
@@ -195,6 +204,8 @@ def main():
                 "parallelism": f"node-shard{world}",
             },
             "pods_per_s": P * args.steps / elapsed,
+            "device_ms_per_step": step_dev_ms,
+            "pod_chunks": len(cyc.chunks),
             "pods_scheduled": ok,
             "roofline": {
                 "bound": "hbm",

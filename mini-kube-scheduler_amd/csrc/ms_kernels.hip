@@ -772,18 +772,15 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     }
 
     // Software pipeline: while pod p is decided, thread tid's first tile list
-    // for pod p+1 (and the record of its head node, the likely winner) are
-    // already in flight. Lists and records of untouched nodes cannot change
-    // within the batch except through binds, which land in the LDS map.
+    // for pod p+1 is already in flight (lists were written by the previous
+    // launch and do not change during this one).
     const bool has_tile = tid < n_tiles;
     u64 nx_e[kTopK] = {0, 0, 0, 0};
     uint32_t nx_sf = 0;
-    NodeRecRegs nx_rec = {};
     if (has_tile) {
 #pragma unroll
         for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[(size_t)tid * kTopK + j];
         nx_sf = tile_flags[tid];
-        if (nx_e[0]) nx_rec = load_rec(t, row_of_key(nx_e[0], t.base));
     }
 
     for (uint32_t p = 0; p < n_pods; ++p) {
@@ -792,7 +789,6 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
 #pragma unroll
         for (int j = 0; j < kTopK; ++j) e[j] = nx_e[j];
         const uint32_t sf0 = nx_sf;
-        const NodeRecRegs head_rec = nx_rec;
         if (has_tile && p + 1 < n_pods) {
             const size_t cell = (size_t)(p + 1) * n_tiles + tid;
 #pragma unroll
@@ -802,7 +798,6 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         // ---- phase A: every tile's best from its speculative top-K list
         u64 best = 0, tbest = 0, own_key = 0;  // own_key: untouched candidate this thread may commit
         uint32_t own_row = 0, fl = 0;
-        int own_j = -1;
         for (uint32_t tt = tid; tt < n_tiles; tt += kValThreads) {
             const size_t cell = (size_t)p * n_tiles + tt;
             u64 ee[kTopK];
@@ -849,14 +844,12 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 if (c != 0 && c > own_key) {
                     own_key = c;
                     own_row = row_of_key(c, t.base);
-                    own_j = (tt == tid) ? cj : kTopK;  // kTopK: record not prefetched
                 }
                 // no feasible row left in this tile: its rejections are the
                 // speculative ones plus NRF for every row a bind made infeasible
                 if (tb == 0) fl |= sf | (ee[0] != 0 ? 0x100u : 0u);
             }
         }
-        if (has_tile && p + 1 < n_pods && nx_e[0]) nx_rec = load_rec(t, row_of_key(nx_e[0], t.base));
         {
             const u64 wb = wave_max_u64_dpp(best);
             const u64 wt = wave_max_u64_dpp(tbest);
@@ -950,7 +943,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             S.n_need = 0;
         }
         if (bind && !winner_touched && own_key == b) {  // untouched winner from this thread's lists
-            slot_insert(S, own_row, own_j == 0 ? head_rec : load_rec(t, own_row), q);
+            slot_insert(S, own_row, load_rec(t, own_row), q);
         } else if (bind && !winner_touched && rs_key == b) {  // untouched winner found by a re-sweep
             slot_insert(S, rs_row, load_rec(t, rs_row), q);
         }

@@ -29,7 +29,7 @@ def _decode_mask(keys, flags):
     return np.where(keys == 0, (flags & 0xFF != 0) * 1 | ((flags >> 8) & 0xFF != 0) * 2, 0)
 
 
-def _worker(rank, world, port, n_nodes, n_pods, plugin_set, q):
+def _worker(rank, world, port, n_nodes, n_pods, plugin_set, q, chunks=1):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -52,19 +52,29 @@ def _worker(rank, world, port, n_nodes, n_pods, plugin_set, q):
     # per-shard flags: a shard with no feasible node reports its own FitError mask
     m = o["mask"].astype(np.uint32)
     flags = torch.from_numpy(((m & 1) | ((m >> 1) & 1) << 8).astype(np.int32))
-    sharded.combine_(keys, flags if plugin_set == 1 else None)
+    if chunks == 1:
+        sharded.combine_(keys, flags if plugin_set == 1 else None)
+    else:  # pipelined form used by ShardedCycle.step: async per chunk, wait at the end
+        works = []
+        for a, b in sharded.chunk_bounds(n_pods, chunks):
+            works += sharded.combine_(keys[a:b], flags[a:b] if plugin_set == 1 else None, async_op=True)
+        for w in works:
+            w.wait()
     q.put((rank, keys.numpy().view(np.uint64).copy(), flags.numpy().astype(np.uint32).copy()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 1), (2, 3)])
 @pytest.mark.parametrize("plugin_set", [0, 1])
-def test_node_sharded_combine_gloo(oracle, world, plugin_set):
+def test_node_sharded_combine_gloo(oracle, world, chunks, plugin_set):
     n_nodes, n_pods = 997, 300
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_nodes, n_pods, plugin_set, q)) for r in range(world)]
+    procs = [
+        ctx.Process(target=_worker, args=(r, world, port, n_nodes, n_pods, plugin_set, q, chunks))
+        for r in range(world)
+    ]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
@@ -97,3 +107,13 @@ def test_shard_bounds_cover_everything():
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
     with pytest.raises(ValueError):
         sharded.shard_bounds(10, 3, 3)
+
+
+def test_chunk_bounds():
+    for n in (1, 63, 64, 65, 1000, 100_000):
+        for c in (1, 2, 4, 7):
+            spans = sharded.chunk_bounds(n, c)
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert all(a % 64 == 0 for a, _ in spans)
+            assert len(spans) <= c
