@@ -119,6 +119,9 @@ typedef struct ms_info {
     uint32_t pending_deltas; /* queued upserts/deletes not yet on the device   */
     int32_t device, plugin_set;
     uint64_t seed;
+    /* exact sequential engine counters since ms_create (diagnostics):
+     * pods validated, tiles re-swept, speculative entries re-evaluated */
+    uint32_t seq_pods, seq_resweep_tiles, seq_recomputes, _pad;
 } ms_info;
 
 typedef struct ms_ctx ms_ctx;

@@ -286,10 +286,10 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
          hipMalloc((void **)&c->d_keys, b * sizeof(unsigned long long)) == hipSuccess &&
          hipMalloc((void **)&c->d_flags, b * sizeof(uint32_t)) == hipSuccess &&
          hipMalloc((void **)&c->d_one, sizeof(ms_pod_rec)) == hipSuccess &&
-         hipMalloc((void **)&c->d_overflow, sizeof(uint32_t)) == hipSuccess;
+         hipMalloc((void **)&c->d_overflow, 4 * sizeof(uint32_t)) == hipSuccess;
     if (!ok) return bail(MS_E_OOM, "staging allocation");
     if (launch_init_table(t, c->stream) != hipSuccess) return bail(MS_E_HIP, "table init launch");
-    if (hipMemsetAsync(c->d_overflow, 0, 4, c->stream) != hipSuccess) return bail(MS_E_HIP, "memset");
+    if (hipMemsetAsync(c->d_overflow, 0, 4 * sizeof(uint32_t), c->stream) != hipSuccess) return bail(MS_E_HIP, "memset");
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MS_E_HIP, "table init");
     *out = c;
     return MS_OK;
@@ -315,6 +315,15 @@ int ms_get_info(const ms_ctx *c, ms_info *out) {
     out->device = c->cfg.device;
     out->plugin_set = c->cfg.plugin_set;
     out->seed = c->cfg.seed;
+    uint32_t st[4] = {0, 0, 0, 0};
+    // counters are written on the (non-blocking) context stream
+    if (hipSetDevice(c->cfg.device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(st, c->d_overflow, sizeof(st), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(m, MS_E_HIP, "ms_get_info: counter read-back");
+    out->seq_pods = st[3];
+    out->seq_resweep_tiles = st[1];
+    out->seq_recomputes = st[2];
+    out->_pad = st[0];  // non-zero would mean a validator capacity violation
     return MS_OK;
 }
 

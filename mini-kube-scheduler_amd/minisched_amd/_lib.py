@@ -93,6 +93,10 @@ class ms_info(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("plugin_set", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("seq_pods", ctypes.c_uint32),
+        ("seq_resweep_tiles", ctypes.c_uint32),
+        ("seq_recomputes", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32),
     ]
 
 

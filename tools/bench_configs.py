@@ -82,6 +82,9 @@ def main():
             med, mn = float(np.median(ts)), float(np.min(ts))
             r = results.cpu().numpy().view(_lib.RESULT)
             extra["codes"] = {k: int((r["code"] == v).sum()) for k, v in (("success", 0), ("error", 1), ("fit_error", 2))}
+            inf = eng.info()
+            extra["seq_counters_all_reps"] = dict(pods=inf.seq_pods, resweep_tiles=inf.seq_resweep_tiles,
+                                                  recomputes=inf.seq_recomputes, overflow=inf._pad)
             mode = "exact sequential (device-resident)"
         elif c == "C":
             eng.upsert(np.arange(N), nr)
