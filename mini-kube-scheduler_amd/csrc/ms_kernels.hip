@@ -772,137 +772,200 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         return;
     }
 
+    // Software pipeline over pods for this thread's first tile (tt == tid):
+    //   cur_*  list of pod p (arrived), cur_rec = record of its head node
+    //          (issued one pod earlier, used only if that node wins untouched)
+    //   nx_*   list of pod p+1, in flight.
+    // Lists were written by the previous launch and records of nodes not yet
+    // bound in this batch are unchanged, so early loads are always valid.
+    const bool has_tile = tid < n_tiles;
+    u64 cur_e[kTopK] = {0, 0, 0, 0}, nx_e[kTopK] = {0, 0, 0, 0};
+    uint32_t cur_sf = 0, nx_sf = 0;
+    NodeRecRegs cur_rec = {};
+    if (has_tile) {
+#pragma unroll
+        for (int j = 0; j < kTopK; ++j) cur_e[j] = tile_keys[(size_t)tid * kTopK + j];
+        cur_sf = tile_flags[tid];
+        if (cur_e[0]) cur_rec = load_rec(t, row_of_key(cur_e[0], t.base));
+        if (n_pods > 1) {
+            const size_t cell = (size_t)n_tiles + tid;
+#pragma unroll
+            for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[cell * kTopK + j];
+            nx_sf = tile_flags[cell];
+        }
+    }
+
     for (uint32_t p = 0; p < n_pods; ++p) {
         const PodFull q = load_pod(pods[p], seed32);
         // ---- phase A: every tile's best from its speculative top-K list
-        u64 best = 0;
-        uint32_t fl = 0;
-        uint32_t n_recompute = 0;
+        u64 best = 0, tbest = 0, own_key = 0;
+        uint32_t own_row = 0, fl = 0, n_recompute = 0;
+        bool own_head = false;  // own_key is cur_e[0] of tile tid: record prefetched
         for (uint32_t tt = tid; tt < n_tiles; tt += kValThreads) {
-            const size_t cell = (size_t)p * n_tiles + tt;
-            const u64 *e = tile_keys + cell * kTopK;
-            const uint32_t sf = tile_flags[cell];
+            u64 ee[kTopK];
+            uint32_t sf;
+            if (tt == tid) {
+#pragma unroll
+                for (int j = 0; j < kTopK; ++j) ee[j] = cur_e[j];
+                sf = cur_sf;
+            } else {
+                const size_t cell = (size_t)p * n_tiles + tt;
+#pragma unroll
+                for (int j = 0; j < kTopK; ++j) ee[j] = tile_keys[cell * kTopK + j];
+                sf = tile_flags[cell];
+            }
             u64 c = 0, r = 0;
-            bool found = false, ended = false;
+            int cj = -1;
+            bool ended = false;
 #pragma unroll
             for (int j = 0; j < kTopK; ++j) {
-                const u64 ej = e[j];
-                if (ej == 0) { ended = true; break; }
-                const uint32_t row = (0xFFFFFu - (uint32_t)(ej & 0xFFFFFu)) - t.base;
-                const int sl = map_find(S, row);
-                if (sl < 0) { c = ej; found = true; break; }
-                uint32_t nu, nrf;
-                r = umax64(r, eval_full(slot_row(S, sl), t.base + row, q, nu, nrf));
-                ++n_recompute;
+                if (cj < 0 && !ended) {
+                    const u64 ej = ee[j];
+                    if (ej == 0) {
+                        ended = true;
+                    } else {
+                        const uint32_t row = row_of_key(ej, t.base);
+                        const int sl = map_find(S, row);
+                        if (sl < 0) {
+                            c = ej;
+                            cj = j;
+                        } else {
+                            uint32_t nu, nrf;
+                            r = umax64(r, eval_full(slot_row(S, sl), t.base + row, q, nu, nrf));
+                            ++n_recompute;
+                        }
+                    }
+                }
             }
-            if (!found && !ended) {
+            if (cj < 0 && !ended) {
                 const uint32_t i = atomicAdd(&S.n_need, 1u);
                 if (i < (uint32_t)kSeqBatch) S.need[i] = tt;
-                else atomicOr(overflow, 2u);  // unreachable: each such tile holds K distinct touched rows, so n_need <= n_slots / K
+                else atomicOr(overflow, 2u);  // unreachable: each such tile holds K distinct touched rows
             } else {
                 const u64 tb = umax64(c, r);
                 best = umax64(best, tb);
+                tbest = umax64(tbest, r);
+                if (c > own_key) {
+                    own_key = c;
+                    own_row = row_of_key(c, t.base);
+                    own_head = (tt == tid) && cj == 0;
+                }
                 // no feasible row left in this tile: its rejections are the
                 // speculative ones plus NRF for every row a bind made infeasible
-                if (tb == 0) fl |= sf | (e[0] != 0 ? 0x100u : 0u);
+                if (tb == 0) fl |= sf | (ee[0] != 0 ? 0x100u : 0u);
             }
         }
         if (n_recompute) atomicAdd(&stats[2], n_recompute);
-        best = wave_max_u64_dpp(best);
-        const uint32_t wfl = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
-        if (lane == 0) {
-            S.wave_best[wave] = best;
-            S.wave_fl[wave] = wfl;
+        {
+            const u64 wb = wave_max_u64_dpp(best);
+            const u64 wt = wave_max_u64_dpp(tbest);
+            const uint32_t wfl =
+                (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+            if (lane == 0) {
+                S.wave_best[wave] = wb;
+                S.wave_touched[wave] = wt;
+                S.wave_fl[wave] = wfl;
+            }
         }
         __syncthreads();
         // ---- phase B: re-sweep tiles whose K listed nodes were all touched
         const uint32_t n_need = min(S.n_need, (uint32_t)kSeqBatch);
+        u64 rs_key = 0;  // this lane's best re-swept untouched row
+        uint32_t rs_row = 0;
         if (n_need) {
-            u64 rb = 0;
+            u64 rb = 0, rt = 0;
             uint32_t rfl = 0;
             for (uint32_t i = wave; i < n_need; i += kValWaves) {
                 const uint32_t tile = S.need[i];
 #pragma unroll
-                for (int s = 0; s < kFullSlots; ++s) {
-                    const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + s;
+                for (int sidx = 0; sidx < kFullSlots; ++sidx) {
+                    const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + sidx;
                     FullRow x = load_row(t, r, n_rows);
+                    bool touched = false;
                     if (r < n_rows) {
                         const int sl = map_find(S, r);
-                        if (sl >= 0) x = slot_row(S, sl);
+                        if (sl >= 0) {
+                            x = slot_row(S, sl);
+                            touched = true;
+                        }
                     }
                     uint32_t nu, nrf;
-                    rb = umax64(rb, eval_full(x, t.base + r, q, nu, nrf));
+                    const u64 k = eval_full(x, t.base + r, q, nu, nrf);
+                    rb = umax64(rb, k);
+                    if (touched) rt = umax64(rt, k);
+                    else if (k > rs_key) {
+                        rs_key = k;
+                        rs_row = r;
+                    }
                     rfl |= (nu ? 1u : 0u) | (nrf ? 0x100u : 0u);
                 }
             }
             rb = wave_max_u64_dpp(rb);
-            const uint32_t rw = (__ballot((rfl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((rfl & 0xFF00u) != 0) ? 0x100u : 0u);
+            rt = wave_max_u64_dpp(rt);
+            const uint32_t rw =
+                (__ballot((rfl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((rfl & 0xFF00u) != 0) ? 0x100u : 0u);
             if (lane == 0) {
                 S.wave_best[wave] = umax64(S.wave_best[wave], rb);
+                S.wave_touched[wave] = umax64(S.wave_touched[wave], rt);
                 S.wave_fl[wave] |= rw;
             }
             __syncthreads();
         }
-        // ---- phase C: decide, commit the bind, publish the result
+        // ---- phase C: each wave reduces the 16 partials (one per lane, DPP),
+        // so every thread knows the winner without another barrier. Keys are
+        // unique per node: the winner is either already bound in this batch
+        // (thread 0 updates its LDS record) or untouched and held by exactly
+        // one thread (that thread inserts it); the cases never race.
+        const bool lane_part = lane < (uint32_t)kValWaves;
+        const u64 b = wave_max_u64_dpp(lane_part ? S.wave_best[lane] : 0ull);
+        const u64 bt = wave_max_u64_dpp(lane_part ? S.wave_touched[lane] : 0ull);
+        const uint32_t pf = lane_part ? S.wave_fl[lane] : 0u;
+        const uint32_t f = (__ballot((pf & 0xFFu) != 0) ? 1u : 0u) | (__ballot((pf & 0xFF00u) != 0) ? 0x100u : 0u);
+        const bool bind = b != 0 && q.dig >= 0;
+        const bool winner_touched = bind && bt == b;
         if (tid == 0) {
-            u64 b = 0;
-            uint32_t f = 0;
-            for (int w = 0; w < kValWaves; ++w) {
-                b = umax64(b, S.wave_best[w]);
-                f |= S.wave_fl[w];
-            }
             ms_result res;
             res._pad = 0;
+            res.plugin_mask = 0;
+            res.node = -1;
+            res.score = 0;
             if (b == 0) {
-                res.node = -1;
                 res.code = MS_CODE_UNSCHEDULABLE;
-                res.score = 0;
                 res.plugin_mask = ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
                                   ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
             } else if (q.dig < 0) {
-                res.node = -1;
                 res.code = MS_CODE_ERROR;
-                res.score = 0;
-                res.plugin_mask = 0;
             } else {
-                const uint32_t node = 0xFFFFFu - (uint32_t)(b & 0xFFFFFu);
-                res.node = (int32_t)node;
+                res.node = (int32_t)(0xFFFFFu - (uint32_t)(b & 0xFFFFFu));
                 res.code = MS_CODE_SUCCESS;
                 res.score = (int64_t)(b >> 52);
-                res.plugin_mask = 0;
-                // assume-on-select: NodeInfo.AddPod on the winner
-                const uint32_t row = node - t.base;
-                int sl = map_find(S, row);
-                if (sl < 0) {
-                    sl = (int)S.n_slots++;
-                    uint32_t h = map_hash(row);
-                    while (S.map_row[h] != 0) h = (h + 1) & (kMapCap - 1);
-                    S.map_row[h] = row + 1;
-                    S.map_slot[h] = (uint16_t)sl;
-                    S.row[sl] = row;
-                    S.req_cpu[sl] = t.req_cpu[row];
-                    S.req_mem[sl] = t.req_mem[row];
-                    S.nz_cpu[sl] = t.nz_cpu[row];
-                    S.nz_mem[sl] = t.nz_mem[row];
-                    S.cnt[sl] = t.pod_count[row];
-                    S.alloc_cpu[sl] = t.alloc_cpu[row];
-                    S.alloc_mem[sl] = t.alloc_mem[row];
-                    S.allowed[sl] = t.allowed_pods[row];
-                    S.fd[sl] = (uint32_t)t.flags[row] | ((uint32_t)t.digit[row] << 8);
-                }
-                S.req_cpu[sl] += q.rc;
-                S.req_mem[sl] += q.rm;
-                S.nz_cpu[sl] += q.nc;
-                S.nz_mem[sl] += q.nm;
-                S.cnt[sl] += 1;
             }
             results[p] = res;
-            atomicAdd(&stats[1], S.n_need);
-            atomicAdd(&stats[3], 1u);
+            if (winner_touched) slot_add_pod(S, map_find(S, row_of_key(b, t.base)), q);
+            if (n_need) atomicAdd(&stats[1], n_need);
             S.n_need = 0;
+        }
+        if (bind && !winner_touched && own_key == b) {  // untouched winner from this thread's lists
+            slot_insert(S, own_row, own_head ? cur_rec : load_rec(t, own_row), q);
+        } else if (bind && !winner_touched && rs_key == b) {  // untouched winner found by a re-sweep
+            slot_insert(S, rs_row, load_rec(t, rs_row), q);
+        }
+        // rotate the pipeline: pod p+1's list has had a whole pod to land
+        if (has_tile && p + 1 < n_pods) {
+#pragma unroll
+            for (int j = 0; j < kTopK; ++j) cur_e[j] = nx_e[j];
+            cur_sf = nx_sf;
+            if (cur_e[0]) cur_rec = load_rec(t, row_of_key(cur_e[0], t.base));
+            if (p + 2 < n_pods) {
+                const size_t cell = (size_t)(p + 2) * n_tiles + tid;
+#pragma unroll
+                for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[cell * kTopK + j];
+                nx_sf = tile_flags[cell];
+            }
         }
         __syncthreads();
     }
+    if (tid == 0) atomicAdd(&stats[3], n_pods);
     // commit the batch's modified rows; the next speculative sweep is a new
     // launch on the same stream, so it observes these stores.
     for (uint32_t sl = tid; sl < S.n_slots; sl += kValThreads) {
