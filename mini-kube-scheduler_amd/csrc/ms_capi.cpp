@@ -62,6 +62,10 @@ namespace {
 
 thread_local std::string g_create_err;
 
+// validator counters: u32[4] (overflow, re-swept tiles, recomputes, pods),
+// then u64[5] per-phase cycle sums in the MS_STAMPS diagnostic build
+constexpr size_t kStatsBytes = 16 + 5 * 8;
+
 int fail(ms_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
     else g_create_err = msg;
@@ -286,10 +290,10 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
          hipMalloc((void **)&c->d_keys, b * sizeof(unsigned long long)) == hipSuccess &&
          hipMalloc((void **)&c->d_flags, b * sizeof(uint32_t)) == hipSuccess &&
          hipMalloc((void **)&c->d_one, sizeof(ms_pod_rec)) == hipSuccess &&
-         hipMalloc((void **)&c->d_overflow, 4 * sizeof(uint32_t)) == hipSuccess;
+         hipMalloc((void **)&c->d_overflow, kStatsBytes) == hipSuccess;
     if (!ok) return bail(MS_E_OOM, "staging allocation");
     if (launch_init_table(t, c->stream) != hipSuccess) return bail(MS_E_HIP, "table init launch");
-    if (hipMemsetAsync(c->d_overflow, 0, 4 * sizeof(uint32_t), c->stream) != hipSuccess) return bail(MS_E_HIP, "memset");
+    if (hipMemsetAsync(c->d_overflow, 0, kStatsBytes, c->stream) != hipSuccess) return bail(MS_E_HIP, "memset");
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MS_E_HIP, "table init");
     *out = c;
     return MS_OK;
@@ -297,6 +301,21 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
 
 int ms_destroy(ms_ctx *c) {
     if (!c) return MS_E_INVAL;
+#ifdef MS_STAMPS
+    {
+        uint64_t st[2 + 5] = {};
+        (void)hipSetDevice(c->cfg.device);
+        (void)hipStreamSynchronize(c->stream);
+        if (hipMemcpy(st, c->d_overflow, kStatsBytes, hipMemcpyDeviceToHost) == hipSuccess) {
+            const uint32_t *u = reinterpret_cast<const uint32_t *>(st);
+            std::fprintf(stderr,
+                         "MS_STAMPS pods=%u recomputes=%u resweeps=%u cycles: A=%llu A_reduce_barrier=%llu B=%llu "
+                         "C=%llu C_barrier=%llu\n",
+                         u[3], u[2], u[1], (unsigned long long)st[2], (unsigned long long)st[3],
+                         (unsigned long long)st[4], (unsigned long long)st[5], (unsigned long long)st[6]);
+        }
+    }
+#endif
     free_all(c);
     delete c;
     return MS_OK;

@@ -761,6 +761,24 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     uint32_t *stats = overflow;  // [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods
     __shared__ SeqShared S;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+#ifdef MS_STAMPS
+    // diagnostic build only: wave 0's cycles per phase, summed over pods
+    u64 st_prev = 0, st_acc[5] = {0, 0, 0, 0, 0};
+#define MS_STAMP(i)                                                  \
+    do {                                                             \
+        __builtin_amdgcn_sched_barrier(0);                           \
+        if (tid == 0) {                                              \
+            const u64 now_ = __builtin_amdgcn_s_memtime();           \
+            if ((i) >= 0) st_acc[(i) < 0 ? 0 : (i)] += now_ - st_prev; \
+            st_prev = now_;                                          \
+        }                                                            \
+        __builtin_amdgcn_sched_barrier(0);                           \
+    } while (0)
+#else
+#define MS_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
     for (uint32_t i = tid; i < (uint32_t)kMapCap; i += kValThreads) S.map_row[i] = 0;
     if (tid == 0) {
         S.n_slots = 0;
@@ -795,6 +813,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         }
     }
 
+    MS_STAMP(-1);
     for (uint32_t p = 0; p < n_pods; ++p) {
         const PodFull q = load_pod(pods[p], seed32);
         // ---- phase A: every tile's best from its speculative top-K list
@@ -856,6 +875,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             }
         }
         if (n_recompute) atomicAdd(&stats[2], n_recompute);
+        MS_STAMP(0);
         {
             const u64 wb = wave_max_u64_dpp(best);
             const u64 wt = wave_max_u64_dpp(tbest);
@@ -868,6 +888,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             }
         }
         __syncthreads();
+        MS_STAMP(1);
         // ---- phase B: re-sweep tiles whose K listed nodes were all touched
         const uint32_t n_need = min(S.n_need, (uint32_t)kSeqBatch);
         u64 rs_key = 0;  // this lane's best re-swept untouched row
@@ -911,6 +932,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             }
             __syncthreads();
         }
+        MS_STAMP(2);
         // ---- phase C: each wave reduces the 16 partials (one per lane, DPP),
         // so every thread knows the winner without another barrier. Keys are
         // unique per node: the winner is either already bound in this batch
@@ -963,8 +985,17 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 nx_sf = tile_flags[cell];
             }
         }
+        MS_STAMP(3);
         __syncthreads();
+        MS_STAMP(4);
     }
+#ifdef MS_STAMPS
+    if (tid == 0) {
+        u64 *acc = reinterpret_cast<u64 *>(stats + 4);
+        for (int i = 0; i < 5; ++i) atomicAdd(&acc[i], st_acc[i]);
+    }
+#endif
+#undef MS_STAMP
     if (tid == 0) atomicAdd(&stats[3], n_pods);
     // commit the batch's modified rows; the next speculative sweep is a new
     // launch on the same stream, so it observes these stores.

@@ -14,7 +14,9 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libminisched_gpu.so")
+# MINISCHED_LIB selects another build of the same ABI (e.g. the MS_STAMPS
+# diagnostic library); the default is the production library.
+LIB_PATH = os.environ.get("MINISCHED_LIB") or os.path.join(HERE, "libminisched_gpu.so")
 
 # ---- constants (minisched_gpu.h) -------------------------------------------
 MS_OK = 0
