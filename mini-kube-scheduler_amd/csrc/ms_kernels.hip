@@ -670,6 +670,11 @@ struct SeqShared {
     uint32_t wave_fl[kValWaves];
     uint32_t need[kSeqBatch];  // tiles to re-sweep for the current pod (bounded below)
     uint32_t n_need, n_slots;
+    // results and counters stay in LDS until the batch ends: a global store or
+    // atomic inside the pod loop would be waited on (vmcnt counts stores) at
+    // the next control-flow join, a memory round trip per pod
+    ms_result res[kSeqBatch];
+    uint32_t n_recompute, n_resweep;
 };
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
@@ -783,6 +788,8 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     if (tid == 0) {
         S.n_slots = 0;
         S.n_need = 0;
+        S.n_recompute = 0;
+        S.n_resweep = 0;
     }
     __syncthreads();
     if (n_pods > (uint32_t)kSeqBatch) {  // host guarantees this; never index past S
@@ -859,7 +866,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             if (cj < 0 && !ended) {
                 const uint32_t i = atomicAdd(&S.n_need, 1u);
                 if (i < (uint32_t)kSeqBatch) S.need[i] = tt;
-                else atomicOr(overflow, 2u);  // unreachable: each such tile holds K distinct touched rows
+                else S.n_resweep |= 0x80000000u;  // unreachable: each such tile holds K distinct touched rows
             } else {
                 const u64 tb = umax64(c, r);
                 best = umax64(best, tb);
@@ -874,7 +881,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 if (tb == 0) fl |= sf | (ee[0] != 0 ? 0x100u : 0u);
             }
         }
-        if (n_recompute) atomicAdd(&stats[2], n_recompute);
+        if (n_recompute) atomicAdd(&S.n_recompute, n_recompute);
         MS_STAMP(0);
         {
             const u64 wb = wave_max_u64_dpp(best);
@@ -962,9 +969,9 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 res.code = MS_CODE_SUCCESS;
                 res.score = (int64_t)(b >> 52);
             }
-            results[p] = res;
+            S.res[p] = res;
             if (winner_touched) slot_add_pod(S, map_find(S, row_of_key(b, t.base)), q);
-            if (n_need) atomicAdd(&stats[1], n_need);
+            S.n_resweep += n_need;
             S.n_need = 0;
         }
         if (bind && !winner_touched && own_key == b) {  // untouched winner from this thread's lists
@@ -996,7 +1003,13 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     }
 #endif
 #undef MS_STAMP
-    if (tid == 0) atomicAdd(&stats[3], n_pods);
+    if (tid == 0) {
+        atomicAdd(&stats[1], S.n_resweep & 0x7FFFFFFFu);
+        atomicAdd(&stats[2], S.n_recompute);
+        atomicAdd(&stats[3], n_pods);
+        if (S.n_resweep & 0x80000000u) atomicOr(overflow, 2u);
+    }
+    for (uint32_t i = tid; i < n_pods; i += kValThreads) results[i] = S.res[i];
     // commit the batch's modified rows; the next speculative sweep is a new
     // launch on the same stream, so it observes these stores.
     for (uint32_t sl = tid; sl < S.n_slots; sl += kValThreads) {
