@@ -674,7 +674,8 @@ struct SeqShared {
     // atomic inside the pod loop would be waited on (vmcnt counts stores) at
     // the next control-flow join, a memory round trip per pod
     ms_result res[kSeqBatch];
-    uint32_t n_recompute, n_resweep;
+    uint32_t spec_row[kSeqBatch];  // speculative global winner row per pod (0xFFFFFFFF: none)
+    uint32_t n_recompute, n_resweep, n_pref_hit, n_pref_miss;
 };
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
@@ -769,15 +770,15 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
 #ifdef MS_STAMPS
     // diagnostic build only: wave 0's cycles per phase, summed over pods
     u64 st_prev = 0, st_acc[5] = {0, 0, 0, 0, 0};
-#define MS_STAMP(i)                                                  \
-    do {                                                             \
-        __builtin_amdgcn_sched_barrier(0);                           \
-        if (tid == 0) {                                              \
-            const u64 now_ = __builtin_amdgcn_s_memtime();           \
+#define MS_STAMP(i)                                                    \
+    do {                                                               \
+        __builtin_amdgcn_sched_barrier(0);                             \
+        if (tid == 0) {                                                \
+            const u64 now_ = __builtin_amdgcn_s_memtime();             \
             if ((i) >= 0) st_acc[(i) < 0 ? 0 : (i)] += now_ - st_prev; \
-            st_prev = now_;                                          \
-        }                                                            \
-        __builtin_amdgcn_sched_barrier(0);                           \
+            st_prev = now_;                                            \
+        }                                                              \
+        __builtin_amdgcn_sched_barrier(0);                             \
     } while (0)
 #else
 #define MS_STAMP(i) \
@@ -790,28 +791,33 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         S.n_need = 0;
         S.n_recompute = 0;
         S.n_resweep = 0;
+        S.n_pref_hit = 0;
+        S.n_pref_miss = 0;
     }
-    __syncthreads();
     if (n_pods > (uint32_t)kSeqBatch) {  // host guarantees this; never index past S
         if (tid == 0) *overflow = 1;
         return;
     }
+    // Prologue: each pod's speculative global winner (max tile head). Thread 0
+    // prefetches the next pod's winner record during the current pod, so the
+    // common bind (winner untouched and as speculated) never waits on memory.
+    for (uint32_t p = wave; p < n_pods; p += kValWaves) {
+        u64 m = 0;
+        for (uint32_t tt = lane; tt < n_tiles; tt += 64) m = umax64(m, tile_keys[((size_t)p * n_tiles + tt) * kTopK]);
+        m = wave_max_u64_dpp(m);
+        if (lane == 0) S.spec_row[p] = m ? row_of_key(m, t.base) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
 
-    // Software pipeline over pods for this thread's first tile (tt == tid):
-    //   cur_*  list of pod p (arrived), cur_rec = record of its head node
-    //          (issued one pod earlier, used only if that node wins untouched)
-    //   nx_*   list of pod p+1, in flight.
-    // Lists were written by the previous launch and records of nodes not yet
-    // bound in this batch are unchanged, so early loads are always valid.
+    // Each thread's first tile list for pod p+1 is in flight while pod p is
+    // decided (coalesced: consecutive threads read consecutive cells).
     const bool has_tile = tid < n_tiles;
     u64 cur_e[kTopK] = {0, 0, 0, 0}, nx_e[kTopK] = {0, 0, 0, 0};
     uint32_t cur_sf = 0, nx_sf = 0;
-    NodeRecRegs cur_rec = {};
     if (has_tile) {
 #pragma unroll
         for (int j = 0; j < kTopK; ++j) cur_e[j] = tile_keys[(size_t)tid * kTopK + j];
         cur_sf = tile_flags[tid];
-        if (cur_e[0]) cur_rec = load_rec(t, row_of_key(cur_e[0], t.base));
         if (n_pods > 1) {
             const size_t cell = (size_t)n_tiles + tid;
 #pragma unroll
@@ -819,14 +825,19 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             nx_sf = tile_flags[cell];
         }
     }
+    uint32_t pref_row = 0xFFFFFFFFu;  // thread 0 only
+    NodeRecRegs pref_rec = {};
+    if (tid == 0 && S.spec_row[0] != 0xFFFFFFFFu) {
+        pref_row = S.spec_row[0];
+        pref_rec = load_rec(t, pref_row);
+    }
 
     MS_STAMP(-1);
     for (uint32_t p = 0; p < n_pods; ++p) {
         const PodFull q = load_pod(pods[p], seed32);
         // ---- phase A: every tile's best from its speculative top-K list
-        u64 best = 0, tbest = 0, own_key = 0;
-        uint32_t own_row = 0, fl = 0, n_recompute = 0;
-        bool own_head = false;  // own_key is cur_e[0] of tile tid: record prefetched
+        u64 best = 0;
+        uint32_t fl = 0, n_recompute = 0;
         for (uint32_t tt = tid; tt < n_tiles; tt += kValThreads) {
             u64 ee[kTopK];
             uint32_t sf;
@@ -841,11 +852,10 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 sf = tile_flags[cell];
             }
             u64 c = 0, r = 0;
-            int cj = -1;
-            bool ended = false;
+            bool found = false, ended = false;
 #pragma unroll
             for (int j = 0; j < kTopK; ++j) {
-                if (cj < 0 && !ended) {
+                if (!found && !ended) {
                     const u64 ej = ee[j];
                     if (ej == 0) {
                         ended = true;
@@ -854,7 +864,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                         const int sl = map_find(S, row);
                         if (sl < 0) {
                             c = ej;
-                            cj = j;
+                            found = true;
                         } else {
                             uint32_t nu, nrf;
                             r = umax64(r, eval_full(slot_row(S, sl), t.base + row, q, nu, nrf));
@@ -863,19 +873,13 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                     }
                 }
             }
-            if (cj < 0 && !ended) {
+            if (!found && !ended) {
                 const uint32_t i = atomicAdd(&S.n_need, 1u);
                 if (i < (uint32_t)kSeqBatch) S.need[i] = tt;
                 else S.n_resweep |= 0x80000000u;  // unreachable: each such tile holds K distinct touched rows
             } else {
                 const u64 tb = umax64(c, r);
                 best = umax64(best, tb);
-                tbest = umax64(tbest, r);
-                if (c > own_key) {
-                    own_key = c;
-                    own_row = row_of_key(c, t.base);
-                    own_head = (tt == tid) && cj == 0;
-                }
                 // no feasible row left in this tile: its rejections are the
                 // speculative ones plus NRF for every row a bind made infeasible
                 if (tb == 0) fl |= sf | (ee[0] != 0 ? 0x100u : 0u);
@@ -885,12 +889,10 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         MS_STAMP(0);
         {
             const u64 wb = wave_max_u64_dpp(best);
-            const u64 wt = wave_max_u64_dpp(tbest);
             const uint32_t wfl =
                 (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
             if (lane == 0) {
                 S.wave_best[wave] = wb;
-                S.wave_touched[wave] = wt;
                 S.wave_fl[wave] = wfl;
             }
         }
@@ -898,10 +900,8 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         MS_STAMP(1);
         // ---- phase B: re-sweep tiles whose K listed nodes were all touched
         const uint32_t n_need = min(S.n_need, (uint32_t)kSeqBatch);
-        u64 rs_key = 0;  // this lane's best re-swept untouched row
-        uint32_t rs_row = 0;
         if (n_need) {
-            u64 rb = 0, rt = 0;
+            u64 rb = 0;
             uint32_t rfl = 0;
             for (uint32_t i = wave; i < n_need; i += kValWaves) {
                 const uint32_t tile = S.need[i];
@@ -909,82 +909,77 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 for (int sidx = 0; sidx < kFullSlots; ++sidx) {
                     const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + sidx;
                     FullRow x = load_row(t, r, n_rows);
-                    bool touched = false;
                     if (r < n_rows) {
                         const int sl = map_find(S, r);
-                        if (sl >= 0) {
-                            x = slot_row(S, sl);
-                            touched = true;
-                        }
+                        if (sl >= 0) x = slot_row(S, sl);
                     }
                     uint32_t nu, nrf;
-                    const u64 k = eval_full(x, t.base + r, q, nu, nrf);
-                    rb = umax64(rb, k);
-                    if (touched) rt = umax64(rt, k);
-                    else if (k > rs_key) {
-                        rs_key = k;
-                        rs_row = r;
-                    }
+                    rb = umax64(rb, eval_full(x, t.base + r, q, nu, nrf));
                     rfl |= (nu ? 1u : 0u) | (nrf ? 0x100u : 0u);
                 }
             }
             rb = wave_max_u64_dpp(rb);
-            rt = wave_max_u64_dpp(rt);
             const uint32_t rw =
                 (__ballot((rfl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((rfl & 0xFF00u) != 0) ? 0x100u : 0u);
             if (lane == 0) {
                 S.wave_best[wave] = umax64(S.wave_best[wave], rb);
-                S.wave_touched[wave] = umax64(S.wave_touched[wave], rt);
                 S.wave_fl[wave] |= rw;
             }
             __syncthreads();
         }
         MS_STAMP(2);
-        // ---- phase C: each wave reduces the 16 partials (one per lane, DPP),
-        // so every thread knows the winner without another barrier. Keys are
-        // unique per node: the winner is either already bound in this batch
-        // (thread 0 updates its LDS record) or untouched and held by exactly
-        // one thread (that thread inserts it); the cases never race.
-        const bool lane_part = lane < (uint32_t)kValWaves;
-        const u64 b = wave_max_u64_dpp(lane_part ? S.wave_best[lane] : 0ull);
-        const u64 bt = wave_max_u64_dpp(lane_part ? S.wave_touched[lane] : 0ull);
-        const uint32_t pf = lane_part ? S.wave_fl[lane] : 0u;
-        const uint32_t f = (__ballot((pf & 0xFFu) != 0) ? 1u : 0u) | (__ballot((pf & 0xFF00u) != 0) ? 0x100u : 0u);
-        const bool bind = b != 0 && q.dig >= 0;
-        const bool winner_touched = bind && bt == b;
-        if (tid == 0) {
-            ms_result res;
-            res._pad = 0;
-            res.plugin_mask = 0;
-            res.node = -1;
-            res.score = 0;
-            if (b == 0) {
-                res.code = MS_CODE_UNSCHEDULABLE;
-                res.plugin_mask = ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
-                                  ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
-            } else if (q.dig < 0) {
-                res.code = MS_CODE_ERROR;
-            } else {
-                res.node = (int32_t)(0xFFFFFu - (uint32_t)(b & 0xFFFFFu));
-                res.code = MS_CODE_SUCCESS;
-                res.score = (int64_t)(b >> 52);
+        // ---- phase C (wave 0): reduce the 16 partials, decide, commit
+        if (wave == 0) {
+            const bool lane_part = lane < (uint32_t)kValWaves;
+            const u64 b = wave_max_u64_dpp(lane_part ? S.wave_best[lane] : 0ull);
+            const uint32_t pf = lane_part ? S.wave_fl[lane] : 0u;
+            const uint32_t f =
+                (__ballot((pf & 0xFFu) != 0) ? 1u : 0u) | (__ballot((pf & 0xFF00u) != 0) ? 0x100u : 0u);
+            if (lane == 0) {
+                ms_result res;
+                res._pad = 0;
+                res.plugin_mask = 0;
+                res.node = -1;
+                res.score = 0;
+                if (b == 0) {
+                    res.code = MS_CODE_UNSCHEDULABLE;
+                    res.plugin_mask = ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                                      ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
+                } else if (q.dig < 0) {
+                    res.code = MS_CODE_ERROR;
+                } else {
+                    const uint32_t node = 0xFFFFFu - (uint32_t)(b & 0xFFFFFu);
+                    res.node = (int32_t)node;
+                    res.code = MS_CODE_SUCCESS;
+                    res.score = (int64_t)(b >> 52);
+                    // assume-on-select: NodeInfo.AddPod on the winner
+                    const uint32_t row = node - t.base;
+                    const int sl = map_find(S, row);
+                    if (sl >= 0) {
+                        slot_add_pod(S, sl, q);
+                    } else if (row == pref_row) {
+                        slot_insert(S, row, pref_rec, q);
+                        ++S.n_pref_hit;
+                    } else {
+                        slot_insert(S, row, load_rec(t, row), q);
+                        ++S.n_pref_miss;
+                    }
+                }
+                S.res[p] = res;
+                S.n_resweep += n_need;
+                S.n_need = 0;
+                // prefetch the next pod's speculative winner record
+                if (p + 1 < n_pods && S.spec_row[p + 1] != 0xFFFFFFFFu && S.spec_row[p + 1] != pref_row) {
+                    pref_row = S.spec_row[p + 1];
+                    pref_rec = load_rec(t, pref_row);
+                }
             }
-            S.res[p] = res;
-            if (winner_touched) slot_add_pod(S, map_find(S, row_of_key(b, t.base)), q);
-            S.n_resweep += n_need;
-            S.n_need = 0;
         }
-        if (bind && !winner_touched && own_key == b) {  // untouched winner from this thread's lists
-            slot_insert(S, own_row, own_head ? cur_rec : load_rec(t, own_row), q);
-        } else if (bind && !winner_touched && rs_key == b) {  // untouched winner found by a re-sweep
-            slot_insert(S, rs_row, load_rec(t, rs_row), q);
-        }
-        // rotate the pipeline: pod p+1's list has had a whole pod to land
+        // rotate the list pipeline: pod p+1's lists have had a whole pod to land
         if (has_tile && p + 1 < n_pods) {
 #pragma unroll
             for (int j = 0; j < kTopK; ++j) cur_e[j] = nx_e[j];
             cur_sf = nx_sf;
-            if (cur_e[0]) cur_rec = load_rec(t, row_of_key(cur_e[0], t.base));
             if (p + 2 < n_pods) {
                 const size_t cell = (size_t)(p + 2) * n_tiles + tid;
 #pragma unroll
@@ -996,19 +991,19 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         __syncthreads();
         MS_STAMP(4);
     }
-#ifdef MS_STAMPS
-    if (tid == 0) {
-        u64 *acc = reinterpret_cast<u64 *>(stats + 4);
-        for (int i = 0; i < 5; ++i) atomicAdd(&acc[i], st_acc[i]);
-    }
-#endif
-#undef MS_STAMP
     if (tid == 0) {
         atomicAdd(&stats[1], S.n_resweep & 0x7FFFFFFFu);
         atomicAdd(&stats[2], S.n_recompute);
         atomicAdd(&stats[3], n_pods);
         if (S.n_resweep & 0x80000000u) atomicOr(overflow, 2u);
+#ifdef MS_STAMPS
+        u64 *acc = reinterpret_cast<u64 *>(stats + 4);
+        for (int i = 0; i < 5; ++i) atomicAdd(&acc[i], st_acc[i]);
+        atomicAdd(&stats[14], S.n_pref_hit);
+        atomicAdd(&stats[15], S.n_pref_miss);
+#endif
     }
+#undef MS_STAMP
     for (uint32_t i = tid; i < n_pods; i += kValThreads) results[i] = S.res[i];
     // commit the batch's modified rows; the next speculative sweep is a new
     // launch on the same stream, so it observes these stores.
