@@ -651,8 +651,8 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
 // LDS copy of their current record. Only a tile whose K entries are all
 // touched (and whose list is not complete) is re-swept against current state.
 // ----------------------------------------------------------------------------
-constexpr int kSeqBatch = 1024;
-constexpr int kMapBits = 12;
+constexpr int kSeqBatch = 512;
+constexpr int kMapBits = 11;
 constexpr int kMapCap = 1 << kMapBits;  // >= 4 * kSeqBatch
 constexpr int kValThreads = 1024;
 constexpr int kValWaves = kValThreads / 64;
@@ -675,6 +675,7 @@ struct SeqShared {
     // the next control-flow join, a memory round trip per pod
     ms_result res[kSeqBatch];
     uint32_t spec_row[kSeqBatch];  // speculative global winner row per pod (0xFFFFFFFF: none)
+    ms_pod_rec pods[kSeqBatch];    // the batch's pod records (no scalar-cache miss per pod)
     uint32_t n_recompute, n_resweep, n_pref_hit, n_pref_miss;
 };
 
@@ -801,6 +802,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     // Prologue: each pod's speculative global winner (max tile head). Thread 0
     // prefetches the next pod's winner record during the current pod, so the
     // common bind (winner untouched and as speculated) never waits on memory.
+    for (uint32_t i = tid; i < n_pods; i += kValThreads) S.pods[i] = pods[i];
     for (uint32_t p = wave; p < n_pods; p += kValWaves) {
         u64 m = 0;
         for (uint32_t tt = lane; tt < n_tiles; tt += 64) m = umax64(m, tile_keys[((size_t)p * n_tiles + tt) * kTopK]);
@@ -834,7 +836,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
 
     MS_STAMP(-1);
     for (uint32_t p = 0; p < n_pods; ++p) {
-        const PodFull q = load_pod(pods[p], seed32);
+        const PodFull q = load_pod(S.pods[p], seed32);
         // ---- phase A: every tile's best from its speculative top-K list
         u64 best = 0;
         uint32_t fl = 0, n_recompute = 0;
