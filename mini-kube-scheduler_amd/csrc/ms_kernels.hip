@@ -676,6 +676,8 @@ struct SeqShared {
     ms_result res[kSeqBatch];
     uint32_t spec_row[kSeqBatch];  // speculative global winner row per pod (0xFFFFFFFF: none)
     ms_pod_rec pods[kSeqBatch];    // the batch's pod records (no scalar-cache miss per pod)
+    u64 lst[2][kValThreads][kTopK];  // two-slot buffer of the first kValThreads tiles' lists
+    uint32_t lsf[2][kValThreads];
     uint32_t n_recompute, n_resweep, n_pref_hit, n_pref_miss;
 };
 
@@ -811,22 +813,16 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     }
     __syncthreads();
 
-    // Each thread's first tile list for pod p+1 is in flight while pod p is
-    // decided (coalesced: consecutive threads read consecutive cells).
+    // Lists of the first kValThreads tiles go through a two-slot LDS buffer:
+    // pod p+1's are loaded right after pod p's list walk and parked in LDS just
+    // before the pod's closing barrier, so phase A only ever reads LDS.
     const bool has_tile = tid < n_tiles;
-    u64 cur_e[kTopK] = {0, 0, 0, 0}, nx_e[kTopK] = {0, 0, 0, 0};
-    uint32_t cur_sf = 0, nx_sf = 0;
     if (has_tile) {
 #pragma unroll
-        for (int j = 0; j < kTopK; ++j) cur_e[j] = tile_keys[(size_t)tid * kTopK + j];
-        cur_sf = tile_flags[tid];
-        if (n_pods > 1) {
-            const size_t cell = (size_t)n_tiles + tid;
-#pragma unroll
-            for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[cell * kTopK + j];
-            nx_sf = tile_flags[cell];
-        }
+        for (int j = 0; j < kTopK; ++j) S.lst[0][tid][j] = tile_keys[(size_t)tid * kTopK + j];
+        S.lsf[0][tid] = tile_flags[tid];
     }
+    __syncthreads();
     uint32_t pref_row = 0xFFFFFFFFu;  // thread 0 only
     NodeRecRegs pref_rec = {};
     if (tid == 0 && S.spec_row[0] != 0xFFFFFFFFu) {
@@ -845,8 +841,8 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             uint32_t sf;
             if (tt == tid) {
 #pragma unroll
-                for (int j = 0; j < kTopK; ++j) ee[j] = cur_e[j];
-                sf = cur_sf;
+                for (int j = 0; j < kTopK; ++j) ee[j] = S.lst[p & 1][tid][j];
+                sf = S.lsf[p & 1][tid];
             } else {
                 const size_t cell = (size_t)p * n_tiles + tt;
 #pragma unroll
@@ -888,6 +884,14 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
             }
         }
         if (n_recompute) atomicAdd(&S.n_recompute, n_recompute);
+        u64 nx_e[kTopK] = {0, 0, 0, 0};  // pod p+1's list, landing during phases B/C
+        uint32_t nx_sf = 0;
+        if (has_tile && p + 1 < n_pods) {
+            const size_t cell = (size_t)(p + 1) * n_tiles + tid;
+#pragma unroll
+            for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[cell * kTopK + j];
+            nx_sf = tile_flags[cell];
+        }
         MS_STAMP(0);
         {
             const u64 wb = wave_max_u64_dpp(best);
@@ -977,17 +981,11 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 }
             }
         }
-        // rotate the list pipeline: pod p+1's lists have had a whole pod to land
+        // park pod p+1's list in the other LDS slot (read after the barrier)
         if (has_tile && p + 1 < n_pods) {
 #pragma unroll
-            for (int j = 0; j < kTopK; ++j) cur_e[j] = nx_e[j];
-            cur_sf = nx_sf;
-            if (p + 2 < n_pods) {
-                const size_t cell = (size_t)(p + 2) * n_tiles + tid;
-#pragma unroll
-                for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[cell * kTopK + j];
-                nx_sf = tile_flags[cell];
-            }
+            for (int j = 0; j < kTopK; ++j) S.lst[(p + 1) & 1][tid][j] = nx_e[j];
+            S.lsf[(p + 1) & 1][tid] = nx_sf;
         }
         MS_STAMP(3);
         __syncthreads();
