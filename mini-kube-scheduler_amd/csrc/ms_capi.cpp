@@ -64,7 +64,7 @@ thread_local std::string g_create_err;
 
 // validator counters: u32[4] (overflow, re-swept tiles, recomputes, pods),
 // then u64[5] per-phase cycle sums in the MS_STAMPS diagnostic build
-constexpr size_t kStatsBytes = 16 + 5 * 8 + 8;  // + u32 prefetch hit/miss (stamps build)
+constexpr size_t kStatsBytes = 16 + 8 * 8 + 8;  // + u32 prefetch hit/miss (stamps build)
 
 int fail(ms_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -303,16 +303,17 @@ int ms_destroy(ms_ctx *c) {
     if (!c) return MS_E_INVAL;
 #ifdef MS_STAMPS
     {
-        uint64_t st[2 + 5 + 1] = {};
+        uint64_t st[2 + 8 + 1] = {};
         (void)hipSetDevice(c->cfg.device);
         (void)hipStreamSynchronize(c->stream);
         if (hipMemcpy(st, c->d_overflow, kStatsBytes, hipMemcpyDeviceToHost) == hipSuccess) {
             const uint32_t *u = reinterpret_cast<const uint32_t *>(st);
             std::fprintf(stderr,
-                         "MS_STAMPS pods=%u recomputes=%u resweeps=%u pref_hit=%u pref_miss=%u cycles: A=%llu "
-                         "A_reduce_barrier=%llu B=%llu C=%llu C_barrier=%llu\n",
-                         u[3], u[2], u[1], u[14], u[15], (unsigned long long)st[2], (unsigned long long)st[3],
-                         (unsigned long long)st[4], (unsigned long long)st[5], (unsigned long long)st[6]);
+                         "MS_STAMPS pods=%u recomputes=%u resweeps=%u pref_hit=%u pref_miss=%u cycles: A_tail=%llu "
+                         "A_reduce_barrier=%llu B=%llu C=%llu C_barrier=%llu pod_load=%llu list_walk=%llu\n",
+                         u[3], u[2], u[1], u[20], u[21], (unsigned long long)st[2], (unsigned long long)st[3],
+                         (unsigned long long)st[4], (unsigned long long)st[5], (unsigned long long)st[6],
+                         (unsigned long long)st[7], (unsigned long long)st[8]);
         }
     }
 #endif

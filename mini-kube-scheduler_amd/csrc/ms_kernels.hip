@@ -772,7 +772,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
 #ifdef MS_STAMPS
     // diagnostic build only: wave 0's cycles per phase, summed over pods
-    u64 st_prev = 0, st_acc[5] = {0, 0, 0, 0, 0};
+    u64 st_prev = 0, st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define MS_STAMP(i)                                                    \
     do {                                                               \
         __builtin_amdgcn_sched_barrier(0);                             \
@@ -833,6 +833,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
     MS_STAMP(-1);
     for (uint32_t p = 0; p < n_pods; ++p) {
         const PodFull q = load_pod(S.pods[p], seed32);
+        MS_STAMP(5);
         // ---- phase A: every tile's best from its speculative top-K list
         u64 best = 0;
         uint32_t fl = 0, n_recompute = 0;
@@ -883,6 +884,7 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
                 if (tb == 0) fl |= sf | (ee[0] != 0 ? 0x100u : 0u);
             }
         }
+        MS_STAMP(6);
         if (n_recompute) atomicAdd(&S.n_recompute, n_recompute);
         u64 nx_e[kTopK] = {0, 0, 0, 0};  // pod p+1's list, landing during phases B/C
         uint32_t nx_sf = 0;
@@ -998,9 +1000,9 @@ __global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint3
         if (S.n_resweep & 0x80000000u) atomicOr(overflow, 2u);
 #ifdef MS_STAMPS
         u64 *acc = reinterpret_cast<u64 *>(stats + 4);
-        for (int i = 0; i < 5; ++i) atomicAdd(&acc[i], st_acc[i]);
-        atomicAdd(&stats[14], S.n_pref_hit);
-        atomicAdd(&stats[15], S.n_pref_miss);
+        for (int i = 0; i < 8; ++i) atomicAdd(&acc[i], st_acc[i]);
+        atomicAdd(&stats[20], S.n_pref_hit);
+        atomicAdd(&stats[21], S.n_pref_miss);
 #endif
     }
 #undef MS_STAMP
