@@ -293,7 +293,7 @@ __device__ __forceinline__ uint32_t hterm_at(uint32_t base, uint32_t s) {
     return base + __umul24(s, kGolden32 & 0xFFFFFFu) + (__umul24(s, kGolden32 >> 24) << 24);
 }
 
-template <int SLOTS, bool WANT_FLAGS>
+template <int SLOTS, bool WANT_FLAGS, bool LDS_ONEHOT>
 __device__ __forceinline__ void sweep_nunn_bits_body(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
@@ -348,6 +348,18 @@ __device__ __forceinline__ void sweep_nunn_bits_body(
     }
     const uint32_t hterm0 = (node_base + row0) * kGolden32;
     const M unsched_present = unsched & ~absent;
+    // LDS_ONEHOT: the ten masks (plus an all-zero row for non-digit pods) go
+    // to LDS so a pod's digit select is one read at a wave-uniform offset
+    // instead of a scalar branch tree.
+    __shared__ M onehot_lds[LDS_ONEHOT ? 11 : 1][LDS_ONEHOT ? kNunnThreads : 1];
+    if (LDS_ONEHOT) {
+#pragma unroll
+        for (int d = 0; d < 10; ++d) onehot_lds[d][threadIdx.x] = onehot[d];
+        onehot_lds[10][threadIdx.x] = 0;
+        // each wave reads only its own lanes' entries: no workgroup barrier needed
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
 
     const uint32_t pbeg = blockIdx.y * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
@@ -357,6 +369,10 @@ __device__ __forceinline__ void sweep_nunn_bits_body(
         const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
         const uint32_t A = fmix32(seed32 ^ pr.ordinal);
         M match;
+        if (LDS_ONEHOT) {
+            const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
+            match = onehot_lds[d][threadIdx.x];
+        } else
         switch (pr.name_digit) {  // wave-uniform: scalar branch, no VGPR indexing
             case 0: match = onehot[0]; break;
             case 1: match = onehot[1]; break;
@@ -414,17 +430,18 @@ __device__ __forceinline__ void sweep_nunn_bits_body(
     }
 }
 
-#define MS_K1_BITS_KERNEL(NAME, SLOTS)                                                                       \
+#define MS_K1_BITS_KERNEL(NAME, SLOTS, LDS)                                                                  \
     template <bool WANT_FLAGS>                                                                               \
     __global__ __launch_bounds__(kNunnThreads) void NAME(                                                    \
         const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,             \
         uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,            \
         uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {                            \
-        sweep_nunn_bits_body<SLOTS, WANT_FLAGS>(nflags, ndigit, n_rows, node_base, pods, n_pods, chunk,      \
-                                                seed32, keys, pflags);                                       \
+        sweep_nunn_bits_body<SLOTS, WANT_FLAGS, LDS>(nflags, ndigit, n_rows, node_base, pods, n_pods, chunk, \
+                                                     seed32, keys, pflags);                                  \
     }
-MS_K1_BITS_KERNEL(k_sweep_nunn_bits32, 32)
-MS_K1_BITS_KERNEL(k_sweep_nunn_bits64, 64)
+MS_K1_BITS_KERNEL(k_sweep_nunn_bits32, 32, false)
+MS_K1_BITS_KERNEL(k_sweep_nunn_bits64, 64, false)
+MS_K1_BITS_KERNEL(k_sweep_nunn_bits32l, 32, true)
 #undef MS_K1_BITS_KERNEL
 
 // ----------------------------------------------------------------------------
@@ -1155,13 +1172,14 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 // K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
 // interleave variants inside one process: "v0" (hash every pair), "lazy"
 // (SWAR + lazy hash), "bits32" / "bits64" (bit-sliced columns). Default bits32.
-enum K1Variant { K1_V0 = 0, K1_LAZY = 1, K1_BITS32 = 2, K1_BITS64 = 3 };
+enum K1Variant { K1_V0 = 0, K1_LAZY = 1, K1_BITS32 = 2, K1_BITS64 = 3, K1_BITS32L = 4 };
 static int k1_variant() {
     const char *e = getenv("MINISCHED_K1");
     if (!e || !e[0]) return K1_BITS32;
     if (e[0] == 'v' && e[1] == '0') return K1_V0;
     if (e[0] == 'l') return K1_LAZY;
     if (e[0] == 'b' && e[4] == '6') return K1_BITS64;
+    if (e[0] == 'b' && e[6] == 'l') return K1_BITS32L;
     return K1_BITS32;
 }
 
@@ -1211,6 +1229,9 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
             break;
         case K1_BITS64:
             MS_LAUNCH_K1(k_sweep_nunn_bits64, 64u * 64u);
+            break;
+        case K1_BITS32L:
+            MS_LAUNCH_K1(k_sweep_nunn_bits32l, 64u * 32u);
             break;
         default:
             MS_LAUNCH_K1(k_sweep_nunn_bits32, 64u * 32u);
