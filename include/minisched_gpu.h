@@ -22,10 +22,13 @@
  * split across GPUs. The tie-break that replaces rand.Intn
  * (minisched.go:316-321) is the packed key
  *     key = score<<52 | h32(seed,pod,node)<<20 | (0xFFFFF - node),
- *     h32 = fmix32(fmix32(seed32 ^ pod_ordinal) ^ (node * 0x9E3779B1)),
+ *     h32 = mix32(fmix32(seed32 ^ pod_ordinal) + node * 0x9E3779) & ~31,
  *     seed32 = (uint32)(seed ^ seed>>32),
- * maximum wins; it is a pure function of (seed, pod, node) so the result does
- * not depend on scan order, sharding or reduction tree.
+ * (rule "r2"; fmix32 = murmur3 finaliser, mix32 = fmix32 without its last
+ * xor-shift; all arithmetic mod 2^32). Maximum wins: the highest hash, then
+ * the lowest ordinal. It is a pure function of (seed, pod, node) so the
+ * result does not depend on scan order, sharding or reduction tree
+ * (DESIGN.md §2).
  */
 #ifndef MINISCHED_GPU_H
 #define MINISCHED_GPU_H

@@ -55,6 +55,13 @@ struct ms_ctx {
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
 
+    // NU+NN pod stream (k_pod_prep output), reused call after call; a call on
+    // another stream first waits for the previous user (pstream_ev)
+    uint2 *d_pstream = nullptr;
+    uint32_t pstream_cap = 0;
+    hipStream_t pstream_last = nullptr;
+    hipEvent_t pstream_ev = nullptr;
+
     std::string err;
 };
 
@@ -88,12 +95,13 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_overflow};
+                   c->d_tile_keys, c->d_tile_flags, c->d_overflow, c->d_pstream};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
+    if (c->pstream_ev) (void)hipEventDestroy(c->pstream_ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -206,15 +214,38 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     return MS_OK;
 }
 
+// The NU+NN pod stream scratch: grown on demand (hipFree synchronises the
+// device, so no in-flight sweep still reads the old buffer).
+int ensure_pstream(ms_ctx *c, uint32_t n_pods) {
+    const uint32_t need = n_pods + kPodStreamPad;
+    if (need <= c->pstream_cap) return MS_OK;
+    const uint32_t cap = std::max<uint32_t>(need, std::max<uint32_t>(4096, c->pstream_cap * 2));
+    if (c->d_pstream) (void)hipFree(c->d_pstream);
+    c->d_pstream = nullptr;
+    c->pstream_cap = 0;
+    if (hipMalloc((void **)&c->d_pstream, sizeof(uint2) * cap) != hipSuccess)
+        return fail(c, MS_E_OOM, "pod stream");
+    c->pstream_cap = cap;
+    return MS_OK;
+}
+
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
                  hipStream_t s) {
-    MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
-    if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
     const uint32_t seed32 = seed32_of(c->cfg.seed);
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN)
-        MS_HIP(c, launch_sweep_nunn(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
-    else
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN) {
+        int rc = ensure_pstream(c, n_pods);
+        if (rc) return rc;
+        if (!c->pstream_ev) MS_HIP(c, hipEventCreateWithFlags(&c->pstream_ev, hipEventDisableTiming));
+        if (c->pstream_last && c->pstream_last != s) MS_HIP(c, hipStreamWaitEvent(s, c->pstream_ev, 0));
+        MS_HIP(c, launch_sweep_nunn(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->d_pstream,
+                                    c->num_cus, s));
+        MS_HIP(c, hipEventRecord(c->pstream_ev, s));
+        c->pstream_last = s;
+    } else {
+        MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
+        if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
         MS_HIP(c, launch_sweep_full(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
+    }
     return MS_OK;
 }
 

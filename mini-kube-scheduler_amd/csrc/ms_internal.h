@@ -24,7 +24,12 @@ constexpr int kFullSlots = 4;
 constexpr int kFullWaveTile = 64 * kFullSlots;            // nodes per wave  (validator tile)
 constexpr int kFullTile = kFullThreads * kFullSlots;      // nodes per block
 
-constexpr uint32_t kGolden32 = 0x9E3779B1u;
+constexpr uint32_t kGolden32 = 0x9E3779B1u;  // LDS map hashing in the validator
+
+// K1 v5 geometry: a wave owns 64 lanes x 32 rows; the pod stream is padded
+// so the sweep's one-step-ahead prefetch of a pod pair stays in bounds.
+constexpr uint32_t kK1WaveRows = 64u * 32u;
+constexpr uint32_t kPodStreamPad = 4;
 
 // Device-resident node table, structure of arrays, indexed by LOCAL ordinal.
 struct NodeTable {
@@ -59,13 +64,35 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
 }
 __host__ __device__ inline uint32_t seed32_of(uint64_t seed) { return (uint32_t)(seed ^ (seed >> 32)); }
 
+// Tie-break hash (minisched_gpu.h, rule "r2"; oracle/ms_oracle.c msor_tb_hash):
+//   A = fmix32(seed32 ^ pod_ordinal); h = mix32(A + node_ordinal * kG24) & ~31
+// mix32 is fmix32 without its final xor-shift. node_ordinal < 2^20, so the
+// product is one v_mad_u32_u24, and the dropped low 5 bits leave room for a
+// lane's row slot in the sweep's 32-bit lane keys.
+constexpr uint32_t kG24 = 0x9E3779u;  // odd, 24-bit
+__host__ __device__ inline uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85ebca6bu;
+    x ^= x >> 13;
+    x *= 0xc2b2ae35u;
+    return x;
+}
+__host__ __device__ inline uint32_t tb_pod(uint32_t seed32, uint32_t pod_ordinal) {
+    return fmix32(seed32 ^ pod_ordinal);
+}
+__host__ __device__ inline uint32_t tb_hash(uint32_t A, uint32_t node_ordinal) {
+    return mix32(A + node_ordinal * kG24) & ~31u;
+}
+
 // ---- launchers (ms_kernels.hip) -------------------------------------------
 // All return hipError_t of the launch; none synchronises.
 hipError_t launch_apply_deltas(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
 hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
+// NU+NN sweep: k_pod_prep (pod stream, zeroes keys/flags) then the K1 sweep.
+// pstream holds >= n_pods + kPodStreamPad entries.
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
-                             hipStream_t s);
+                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
+                             int num_cus, hipStream_t s);
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s);

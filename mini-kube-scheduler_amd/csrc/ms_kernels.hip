@@ -44,11 +44,23 @@ __device__ __forceinline__ u64 make_key(uint32_t score, uint32_t h, uint32_t ord
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// Full 64-lane unsigned max; result is wave-uniform (read from lane 63).
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // ----------------------------------------------------------------------------
-// K1: NodeUnschedulable + NodeNumber, batched (stateless) sweep.
+// K1 v0: NodeUnschedulable + NodeNumber, batched (stateless) sweep, the plain
+// form: every (pod, node) pair is filtered, scored and hashed, one 64-bit key
+// max per pair. Kept as an independent GPU cross-check of the production
+// kernel (MINISCHED_K1=v0).
 //   grid.x = node tiles of kNunnTile rows, grid.y = pod chunks (multiple of 64)
-//   Each lane holds kNunnSlots consecutive rows: flags/digits as 16-byte
-//   vectors, the per-row hash term ord*golden, and two 16-bit row masks.
 // ----------------------------------------------------------------------------
 template <bool WANT_FLAGS>
 __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
@@ -84,7 +96,6 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
         }
     }
     const uint32_t ord0 = node_base + row0;
-    const uint32_t hterm0 = ord0 * kGolden32;
     const uint32_t unsched_present = unsched & ~absent;
 
     const uint32_t pbeg = blockIdx.y * chunk;
@@ -92,8 +103,8 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
     u64 mine = 0;
     uint32_t myflag = 0;
     for (uint32_t p = pbeg; p < pend; ++p) {
-        const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
-        const uint32_t A = fmix32(seed32 ^ pr.ordinal);
+        const ms_pod_rec pr = pods[p];  // wave-uniform
+        const uint32_t A = tb_pod(seed32, pr.ordinal);
         const int dig = pr.name_digit;
         const uint32_t infeas = pr.tolerates_unschedulable ? absent : (absent | unsched);
         u64 best = 0;
@@ -101,8 +112,7 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
         for (int i = 0; i < kNunnSlots; ++i) {
             const int nd = (int)((dw[i >> 2] >> ((i & 3) * 8)) & 0xFFu);
             const uint32_t score = (nd == dig) ? 10u : 0u;
-            const uint32_t h = fmix32(A ^ (hterm0 + (uint32_t)i * kGolden32));
-            const u64 key = make_key(score, h, ord0 + i);
+            const u64 key = make_key(score, tb_hash(A, ord0 + i), ord0 + i);
             best = ((infeas >> i) & 1u) ? best : umax64(best, key);
         }
         best = wave_max_u64(best);
@@ -124,325 +134,253 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
 }
 
 // ----------------------------------------------------------------------------
-// K1 (lazy tie-break), the production NU+NN sweep.
-//
-// Every (pod, node) pair is filtered and scored, four nodes per 32-bit op
-// (SWAR over the digit bytes); only pairs that reach the wave's best score
-// pay for the 32-bit tie-break hash. Within a wave the best score is 10 as
-// soon as one lane holds a feasible digit match (NodeNumber's only non-zero
-// score), so lanes hash just their own score-10 candidates in a short
-// divergent loop, then the wave takes the max (hash, -ordinal) pair.
-//
-// Row masks use the SWAR bit layout: bit b <-> slot 4*(b&7) + (b>>3), i.e.
-// byte j of digit dword k sits at bit 8j+k. Ties on the hash are broken
-// towards the lower ordinal explicitly, exactly as the packed key orders them.
+// Pod stream: one 8-byte entry per pod, built once per batch by k_pod_prep
+// (which also zeroes the batch's keys/flags, replacing two memsets):
+//   .x = A = tb_pod(seed32, ordinal)   (the pod half of the tie-break hash)
+//   .y = class = digit (0..9, 10 = name does not end in a digit) + 11 * tolerates
+// Every node wave reads it through the scalar cache, two pods per 16-byte load.
+// The buffer carries kPodStreamPad padding entries so the one-step-ahead
+// prefetch never needs a bounds check.
 // ----------------------------------------------------------------------------
-constexpr int kLazySlots = 32;
-constexpr int kLazyWaveRows = 64 * kLazySlots;         // 2048 rows per wave
-constexpr int kLazyTile = kNunnThreads * kLazySlots;   // 8192 rows per block
-
-__device__ __forceinline__ uint32_t slot_of_bit(uint32_t b) { return ((b & 7u) << 2) | (b >> 3); }
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
-    return v;
+__global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t seed32,
+                           uint2 *__restrict__ ps, u64 *__restrict__ keys, uint32_t *__restrict__ flags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const ms_pod_rec pr = pods[i];
+        const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
+        ps[i] = make_uint2(tb_pod(seed32, pr.ordinal), d + (pr.tolerates_unschedulable ? 11u : 0u));
+        keys[i] = 0;
+        if (flags) flags[i] = 0;
+    } else if (i < n + kPodStreamPad) {
+        ps[i] = make_uint2(0u, 10u);
+    }
 }
 
-// high bit of each zero byte of x (exact, no borrow false positives)
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
-    const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
-    return ~t & 0x80808080u;
+// ----------------------------------------------------------------------------
+// K1 v5, the production NU+NN sweep: bit-sliced node columns, pod classes.
+//
+// Layout: a wave owns 2048 consecutive rows, 32 per lane, for its whole
+// lifetime, and streams a chunk of pods through them. At load each lane turns
+// its 32 digit bytes into four bit planes and then ten one-hot masks (bit s
+// <=> row row0+s has name digit d), and its flag bytes into unschedulable /
+// absent masks. The 22-entry class table tab[digit + 11*tolerates] holds, per
+// pod class, the rows that pass NodeUnschedulable AND score 10 under
+// NodeNumber. A pod's filter+score over its 32 rows is then one register
+// read at a wave-uniform index (v_movrels): every pair is still evaluated
+// from that node's own columns, 32 pairs per register, and nothing is shared
+// between pods except the node columns.
+//
+// Argmax: NodeNumber's only non-zero score is 10, so a wave's best score is
+// 10 as soon as any lane has a candidate (ballot). Each lane then scores its
+// own candidates by the tie-break hash, one v_mad_u32_u24 + mix32 each, into
+// the u32 lane key h27<<5 | (31-slot) (max = highest hash, then lowest row);
+// a DPP max + ballot finds the wave's winner (lowest lane = lowest ordinal on
+// equal hashes). Pods go in pairs: their candidate loops share one
+// lane-divergent loop and their DPP reductions interleave. Wave results land
+// in one lane each (v_writelane) and every 64 pods leave as one coalesced
+// 64-bit atomicMax wave-instruction.
+//
+// Grid: one block = one wave; grid.x = node waves, grid.y = pod chunks sized
+// so that all waves are resident at once (launch_one_round).
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void wave_max_u32_dpp2(uint32_t &a, uint32_t &b) {
+#define MS_DPP2(CTRL, RM)                                                                       \
+    a = max(a, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, CTRL, RM, 0xF, false));        \
+    b = max(b, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, CTRL, RM, 0xF, false));
+    MS_DPP2(0x111, 0xF)  // row_shr:1
+    MS_DPP2(0x112, 0xF)  // row_shr:2
+    MS_DPP2(0x114, 0xF)  // row_shr:4
+    MS_DPP2(0x118, 0xF)  // row_shr:8
+    MS_DPP2(0x142, 0xA)  // row_bcast:15
+    MS_DPP2(0x143, 0xC)  // row_bcast:31
+#undef MS_DPP2
+    a = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+    b = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
 }
 
-template <bool WANT_FLAGS>
-__global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn_lazy(
-    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
-    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
-    const uint32_t lane = lane_id();
-    const uint32_t wave_row0 = blockIdx.x * kLazyTile + (threadIdx.x >> 6) * kLazyWaveRows;
-    if (wave_row0 >= n_rows) return;  // wave-uniform: no rows, nothing to report
-    const uint32_t row0 = wave_row0 + lane * kLazySlots;
+struct Bits32Cols {
+    uint32_t onehot[10];
+    uint32_t unsched, absent;
+};
 
-    uint32_t dw[8];
-    uint32_t unsched = 0, absent = 0;  // SWAR bit layout
-    if (row0 + kLazySlots <= n_rows) {
+// bit `bit` of each byte of x -> 4 bits (byte 0 lowest)
+__device__ __forceinline__ uint32_t gather4(uint32_t x, int bit) {
+    return ((((x >> bit) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
+}
+
+// Bit planes of the 32 digit bytes (bit i of every byte in one register, four
+// rows per multiply), then onehot[v] = AND of the four planes or their
+// complements; 0xFF ("no digit") is 15 in the low nibble and matches nothing.
+__device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ nflags,
+                                                   const uint8_t *__restrict__ ndigit, uint32_t n_rows,
+                                                   uint32_t row0, Bits32Cols &c) {
+    uint32_t dv[8], fv[8];
+    if (row0 + 32 <= n_rows) {
         const uint4 *dp = reinterpret_cast<const uint4 *>(ndigit + row0);
         const uint4 *fp = reinterpret_cast<const uint4 *>(nflags + row0);
         const uint4 d0 = dp[0], d1 = dp[1], f0 = fp[0], f1 = fp[1];
-        dw[0] = d0.x; dw[1] = d0.y; dw[2] = d0.z; dw[3] = d0.w;
-        dw[4] = d1.x; dw[5] = d1.y; dw[6] = d1.z; dw[7] = d1.w;
-        const uint32_t fw[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            absent |= (fw[k] & 0x80808080u) >> (7 - k);
-            unsched |= ((fw[k] & 0x01010101u) << 7) >> (7 - k);
-        }
+        dv[0] = d0.x; dv[1] = d0.y; dv[2] = d0.z; dv[3] = d0.w;
+        dv[4] = d1.x; dv[5] = d1.y; dv[6] = d1.z; dv[7] = d1.w;
+        fv[0] = f0.x; fv[1] = f0.y; fv[2] = f0.z; fv[3] = f0.w;
+        fv[4] = f1.x; fv[5] = f1.y; fv[6] = f1.z; fv[7] = f1.w;
     } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            uint32_t d = 0, f = 0;
+            dv[k] = 0;
+            fv[k] = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t r = row0 + 4 * k + j;
-                const uint32_t dv = r < n_rows ? ndigit[r] : 0xFFu;
-                const uint32_t fv = r < n_rows ? nflags[r] : kNodeAbsent;
-                d |= dv << (8 * j);
-                f |= fv << (8 * j);
+                dv[k] |= (r < n_rows ? (uint32_t)ndigit[r] : 0xFFu) << (8 * j);
+                fv[k] |= (r < n_rows ? (uint32_t)nflags[r] : (uint32_t)kNodeAbsent) << (8 * j);
             }
-            dw[k] = d;
-            absent |= (f & 0x80808080u) >> (7 - k);
-            unsched |= ((f & 0x01010101u) << 7) >> (7 - k);
         }
     }
-    const uint32_t hterm0 = (node_base + row0) * kGolden32;
-    const uint32_t unsched_present = unsched & ~absent;
-
-    const uint32_t pbeg = blockIdx.y * chunk;
-    const uint32_t pend = min(n_pods, pbeg + chunk);
-    u64 mine = 0;
-    uint32_t myflag = 0;
-    for (uint32_t p = pbeg; p < pend; ++p) {
-        const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
-        const uint32_t A = fmix32(seed32 ^ pr.ordinal);
-        // a non-digit pod name (-1) becomes 0xFE, which matches no node byte
-        const uint32_t pd = pr.name_digit >= 0 ? (uint32_t)pr.name_digit : 0xFEu;
-        const uint32_t rep = pd * 0x01010101u;
-        uint32_t match = 0;
+    uint32_t pl[4] = {0, 0, 0, 0};
+    c.unsched = c.absent = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) match |= zero_bytes(dw[k] ^ rep) >> (7 - k);
-        const uint32_t feas = ~(pr.tolerates_unschedulable ? absent : (absent | unsched));
-        const uint32_t c10 = match & feas;
-        const bool any10 = __ballot(c10 != 0) != 0;  // wave-uniform best score
-        uint32_t cand = any10 ? c10 : feas;
-        const bool valid = cand != 0;
-        uint32_t bh = 0, bs = 0xFFFFFFFFu;
-        while (cand) {  // lane-divergent: hash only the wave-best-score candidates
-            const uint32_t b = (uint32_t)__builtin_ctz(cand);
-            cand &= cand - 1;
-            const uint32_t s = slot_of_bit(b);
-            const uint32_t h = fmix32(A ^ (hterm0 + s * kGolden32));
-            if (h > bh || (h == bh && s < bs)) {
-                bh = h;
-                bs = s;
-            }
-        }
-        const uint32_t hmax = wave_max_u32(valid ? bh : 0u);
-        const u64 winners = __ballot(valid && bh == hmax);  // lowest lane = lowest ordinal
-        u64 best = 0;
-        if (winners) {
-            const uint32_t L = (uint32_t)__builtin_ctzll(winners);
-            const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)bs, (int)L);
-            best = make_key(any10 ? 10u : 0u, hmax, node_base + wave_row0 + L * kLazySlots + ws);
-        }
-        const uint32_t slot = (p - pbeg) & 63u;
-        if (lane == slot) mine = best;
-        if (WANT_FLAGS) {
-            const bool any_nu = __ballot(!pr.tolerates_unschedulable && unsched_present != 0) != 0;
-            if (lane == slot) myflag = any_nu ? 1u : 0u;
-        }
-        if (slot == 63u || p + 1 == pend) {
-            const uint32_t pp = p - slot + lane;
-            if (lane <= slot && mine) atomicMax(&keys[pp], mine);
-            if (WANT_FLAGS && lane <= slot && myflag) atomicOr(&pflags[pp], myflag);
-            mine = 0;
-            myflag = 0;
-        }
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pl[i] |= gather4(dv[k], i) << (4 * k);
+        c.unsched |= gather4(fv[k], 0) << (4 * k);  // kNodeUnschedulable = bit 0
+        c.absent |= gather4(fv[k], 7) << (4 * k);   // kNodeAbsent = bit 7
     }
+#pragma unroll
+    for (int v = 0; v < 10; ++v)
+        c.onehot[v] = ((v & 1) ? pl[0] : ~pl[0]) & ((v & 2) ? pl[1] : ~pl[1]) & ((v & 4) ? pl[2] : ~pl[2]) &
+                      ((v & 8) ? pl[3] : ~pl[3]);
 }
 
-// ----------------------------------------------------------------------------
-// K1 v2 ("bits"): bit-sliced node columns.
-//
-// At tile load each lane turns its SLOTS digit bytes into ten one-hot row
-// masks (bit s of onehot[d] <=> row row0+s has name digit d) and its flag
-// bytes into unschedulable/absent masks. For a pod, digit equality against
-// all SLOTS rows is then one register (a wave-uniform select on the pod's
-// digit) and the NodeUnschedulable filter one and-not: every pair is still
-// filtered and scored, SLOTS pairs per bitwise op. Bits are in row order, so
-// the candidate loop visits rows in ascending ordinal and a strict '>' keeps
-// the lower ordinal on equal hashes, exactly as the packed key orders them.
-// ----------------------------------------------------------------------------
-template <int SLOTS>
-struct RowMask;
-template <>
-struct RowMask<32> {
-    typedef uint32_t T;
-    static __device__ __forceinline__ uint32_t ctz(T m) { return (uint32_t)__builtin_ctz(m); }
+// v_writelane_b32: lane `lane` of v takes the wave-uniform value x.
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t lane) {
+    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
+                 : "+v"(v)
+                 : "s"(__builtin_amdgcn_readfirstlane(x)), "s"(__builtin_amdgcn_readfirstlane(lane))
+                 : "m0");
+    return v;
+}
+
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// Row slot of the lowest candidate (v_ffbl; 0xFFFFFFFF for an empty mask).
+__device__ __forceinline__ uint32_t first_slot(uint32_t m) {
+    uint32_t s;
+    asm("v_ffbl_b32 %0, %1" : "=v"(s) : "v"(m));
+    return s;
+}
+
+// Lane key of slot s: (tb_hash & ~31) | (31 - s). AH = A + (ordinal of row0) * kG24.
+__device__ __forceinline__ uint32_t lane_key(uint32_t AH, uint32_t s) {
+    const uint32_t h = mix32(AH + __umul24(s, kG24));  // s < 32: v_mad_u32_u24
+    uint32_t k;  // bit i = ((31 >> i) & 1) ? ~s : h
+    asm("v_bitop3_b32 %0, %1, 31, %2 bitop3:0x74" : "=v"(k) : "v"(h), "v"(s));
+    return k;
+}
+
+struct PodLane {
+    uint32_t AH;    // A + hterm0
+    uint32_t cand;  // candidates not yet hashed (bit s <-> row row0 + s)
+    uint32_t kb;    // lane best key (0 while the lane has no candidate)
+    bool valid, any10;
 };
-template <>
-struct RowMask<64> {
-    typedef u64 T;
-    static __device__ __forceinline__ uint32_t ctz(T m) { return (uint32_t)__builtin_ctzll(m); }
-};
 
-// Full 64-lane unsigned max; result is wave-uniform (read from lane 63).
-__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+__device__ __forceinline__ void pod_begin(const u32x16 &onehot, uint32_t feasN, uint32_t feasT, uint32_t A,
+                                          uint32_t cls, uint32_t hterm0, PodLane &q) {
+    // filter + score of 32 pairs: the digit's one-hot row mask (wave-uniform
+    // index, v_movrels) AND the NodeUnschedulable-feasible rows for the class
+    const bool tol = cls >= 11;
+    uint32_t cand = onehot[tol ? cls - 11 : cls] & (tol ? feasT : feasN);
+    q.any10 = __ballot(cand != 0) != 0;      // wave-uniform best score
+    if (!q.any10) cand = cls >= 11 ? feasT : feasN;  // no digit match in this wave: score-0 candidates
+    q.valid = cand != 0;
+    q.AH = A + hterm0;
+    q.kb = 0;
+    if (cand) q.kb = lane_key(q.AH, first_slot(cand));  // lowest candidate seeds the lane best
+    q.cand = cand & (cand - 1);
 }
 
-// (base + s * golden) mod 2^32 with full-rate 24-bit multiplies (s < 2^8)
-__device__ __forceinline__ uint32_t hterm_at(uint32_t base, uint32_t s) {
-    return base + __umul24(s, kGolden32 & 0xFFFFFFu) + (__umul24(s, kGolden32 >> 24) << 24);
+__device__ __forceinline__ void pod_step(PodLane &q) {
+    const uint32_t s = first_slot(q.cand);
+    const bool live = q.cand != 0;
+    q.cand &= q.cand - 1;  // stays 0 once empty
+    if (live) q.kb = max(q.kb, lane_key(q.AH, s));
 }
 
-template <int SLOTS, bool WANT_FLAGS, bool LDS_ONEHOT>
-__device__ __forceinline__ void sweep_nunn_bits_body(
+// Wave winner as a packed key (0 when the wave has no feasible row).
+__device__ __forceinline__ u64 pod_key(const PodLane &q, uint32_t kmax, uint32_t ord_wave0) {
+    const u64 winners = __ballot(q.valid && (q.kb ^ kmax) < 32u);  // same hash; lowest lane = lowest ordinal
+    if (!winners) return 0;
+    const uint32_t L = (uint32_t)__builtin_ctzll(winners);
+    const uint32_t kL = (uint32_t)__builtin_amdgcn_readlane((int)q.kb, (int)L);
+    return make_key(q.any10 ? 10u : 0u, kL & ~31u, ord_wave0 + L * 32u + (31u - (kL & 31u)));
+}
+
+template <bool WANT_FLAGS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v5(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
-    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
-    typedef typename RowMask<SLOTS>::T M;
-    constexpr uint32_t kWaveRows = 64u * SLOTS;
+    uint32_t node_base, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk, u64 *__restrict__ keys,
+    uint32_t *__restrict__ pflags) {
     const uint32_t lane = lane_id();
-    const uint32_t wave_row0 = blockIdx.x * (kNunnThreads * SLOTS) + (threadIdx.x >> 6) * kWaveRows;
-    if (wave_row0 >= n_rows) return;  // wave-uniform: no rows, nothing to report
-    const uint32_t row0 = wave_row0 + lane * SLOTS;
-
-    M onehot[10];
-#pragma unroll
-    for (int d = 0; d < 10; ++d) onehot[d] = 0;
-    M unsched = 0, absent = 0;
-    const bool full = row0 + SLOTS <= n_rows;
-#pragma unroll
-    for (int q = 0; q < SLOTS / 16; ++q) {
-        uint32_t dv[4], fv[4];
-        if (full) {
-            const uint4 d4 = reinterpret_cast<const uint4 *>(ndigit + row0)[q];
-            const uint4 f4 = reinterpret_cast<const uint4 *>(nflags + row0)[q];
-            dv[0] = d4.x; dv[1] = d4.y; dv[2] = d4.z; dv[3] = d4.w;
-            fv[0] = f4.x; fv[1] = f4.y; fv[2] = f4.z; fv[3] = f4.w;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                dv[k] = 0;
-                fv[k] = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t r = row0 + 16 * q + 4 * k + j;
-                    dv[k] |= (r < n_rows ? (uint32_t)ndigit[r] : 0xFFu) << (8 * j);
-                    fv[k] |= (r < n_rows ? (uint32_t)nflags[r] : (uint32_t)kNodeAbsent) << (8 * j);
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int s = 16 * q + 4 * k + j;
-                const uint32_t d = (dv[k] >> (8 * j)) & 0xFFu;
-                const uint32_t f = (fv[k] >> (8 * j)) & 0xFFu;
-                const M bit = (M)1 << s;
-#pragma unroll
-                for (int v = 0; v < 10; ++v) onehot[v] |= (d == (uint32_t)v) ? bit : (M)0;
-                unsched |= (f & kNodeUnschedulable) ? bit : (M)0;
-                absent |= (f & kNodeAbsent) ? bit : (M)0;
-            }
-        }
-    }
-    const uint32_t hterm0 = (node_base + row0) * kGolden32;
-    const M unsched_present = unsched & ~absent;
-    // LDS_ONEHOT: the ten masks (plus an all-zero row for non-digit pods) go
-    // to LDS so a pod's digit select is one read at a wave-uniform offset
-    // instead of a scalar branch tree.
-    __shared__ M onehot_lds[LDS_ONEHOT ? 11 : 1][LDS_ONEHOT ? kNunnThreads : 1];
-    if (LDS_ONEHOT) {
-#pragma unroll
-        for (int d = 0; d < 10; ++d) onehot_lds[d][threadIdx.x] = onehot[d];
-        onehot_lds[10][threadIdx.x] = 0;
-        // each wave reads only its own lanes' entries: no workgroup barrier needed
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-
+    const uint32_t wave_row0 = blockIdx.x * kK1WaveRows;
     const uint32_t pbeg = blockIdx.y * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
-    u64 mine = 0;
-    uint32_t myflag = 0;
-    for (uint32_t p = pbeg; p < pend; ++p) {
-        const ms_pod_rec pr = pods[p];  // wave-uniform -> scalar loads
-        const uint32_t A = fmix32(seed32 ^ pr.ordinal);
-        M match;
-        if (LDS_ONEHOT) {
-            const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
-            match = onehot_lds[d][threadIdx.x];
-        } else
-        switch (pr.name_digit) {  // wave-uniform: scalar branch, no VGPR indexing
-            case 0: match = onehot[0]; break;
-            case 1: match = onehot[1]; break;
-            case 2: match = onehot[2]; break;
-            case 3: match = onehot[3]; break;
-            case 4: match = onehot[4]; break;
-            case 5: match = onehot[5]; break;
-            case 6: match = onehot[6]; break;
-            case 7: match = onehot[7]; break;
-            case 8: match = onehot[8]; break;
-            case 9: match = onehot[9]; break;
-            default: match = 0; break;  // non-digit pod name: NodeNumber scores nothing
+    if (wave_row0 >= n_rows || pbeg >= pend) return;  // wave-uniform
+    const uint32_t row0 = wave_row0 + lane * 32u;
+
+    u32x16 onehot;  // [10..15] = 0: a non-digit pod name scores 0 everywhere
+    uint32_t feasN, feasT;
+    bool wave_unsched;
+    {
+        Bits32Cols c;
+        load_bits32_planes(nflags, ndigit, n_rows, row0, c);
+        feasN = ~(c.absent | c.unsched);
+        feasT = ~c.absent;
+        onehot = (u32x16)(0u);
+#pragma unroll
+        for (int d = 0; d < 10; ++d) onehot[d] = c.onehot[d];
+        wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
+    }
+    const uint32_t hterm0 = (node_base + row0) * kG24;
+    const uint32_t ord_wave0 = node_base + wave_row0;
+
+    // pbeg is a multiple of 64, so pod pairs are 16-byte aligned
+    const uint4 *__restrict__ ps4 = reinterpret_cast<const uint4 *>(ps);
+    uint4 nx = ps4[pbeg >> 1];
+    uint32_t mine_lo = 0, mine_hi = 0, myflag = 0;
+    for (uint32_t p = pbeg; p < pend; p += 2) {
+        const uint4 w = nx;                 // pods p, p+1: {A, class} x 2
+        nx = ps4[(p >> 1) + 1];             // prefetch; the stream is padded past n_pods
+        const bool hasB = p + 1 < pend;
+        PodLane a, b;
+        pod_begin(onehot, feasN, feasT, w.x, w.y, hterm0, a);
+        pod_begin(onehot, feasN, feasT, w.z, w.w, hterm0, b);  // beyond pend: padding, never recorded
+        while (a.cand | b.cand) {  // lane-divergent; one loop for both pods
+            pod_step(a);
+            pod_step(b);
         }
-        const M feas = ~(pr.tolerates_unschedulable ? absent : (absent | unsched));
-        const M c10 = match & feas;
-        const bool any10 = __ballot(c10 != 0) != 0;  // wave-uniform best score
-        M cand = any10 ? c10 : feas;
-        const bool valid = cand != 0;
-        uint32_t bh = 0, bs = 0;
-        if (cand) {  // first candidate (lowest row) seeds the lane's best
-            bs = RowMask<SLOTS>::ctz(cand);
-            cand &= cand - 1;
-            bh = fmix32(A ^ hterm_at(hterm0, bs));
-            while (cand) {  // lane-divergent, ascending rows: strict '>' keeps the lower ordinal
-                const uint32_t s = RowMask<SLOTS>::ctz(cand);
-                cand &= cand - 1;
-                const uint32_t h = fmix32(A ^ hterm_at(hterm0, s));
-                if (h > bh) {
-                    bh = h;
-                    bs = s;
-                }
-            }
+        uint32_t ka = a.kb, kb = b.kb;
+        wave_max_u32_dpp2(ka, kb);
+        const u64 keya = pod_key(a, ka, ord_wave0);
+        const u64 keyb = pod_key(b, kb, ord_wave0);
+        const uint32_t slot = (p - pbeg) & 63u;  // even
+        mine_lo = writelane(mine_lo, (uint32_t)keya, slot);
+        mine_hi = writelane(mine_hi, (uint32_t)(keya >> 32), slot);
+        mine_lo = writelane(mine_lo, (uint32_t)keyb, slot + 1);
+        mine_hi = writelane(mine_hi, (uint32_t)(keyb >> 32), slot + 1);
+        if (WANT_FLAGS) {  // NodeUnschedulable rejected >= 1 row of this wave for the pod
+            myflag = writelane(myflag, (w.y < 11 && wave_unsched) ? 1u : 0u, slot);
+            myflag = writelane(myflag, (w.w < 11 && wave_unsched) ? 1u : 0u, slot + 1);
         }
-        const uint32_t hmax = wave_max_u32_dpp(valid ? bh : 0u);
-        const u64 winners = __ballot(valid && bh == hmax);  // lowest lane = lowest ordinal
-        u64 best = 0;
-        if (winners) {
-            const uint32_t L = (uint32_t)__builtin_ctzll(winners);
-            const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)bs, (int)L);
-            best = make_key(any10 ? 10u : 0u, hmax, node_base + wave_row0 + L * SLOTS + ws);
-        }
-        const uint32_t slot = (p - pbeg) & 63u;
-        if (lane == slot) mine = best;
-        if (WANT_FLAGS) {
-            const bool any_nu = __ballot(!pr.tolerates_unschedulable && unsched_present != 0) != 0;
-            if (lane == slot) myflag = any_nu ? 1u : 0u;
-        }
-        if (slot == 63u || p + 1 == pend) {
+        const uint32_t last = hasB ? slot + 1 : slot;
+        if (last == 63u || p + 2 >= pend) {
             const uint32_t pp = p - slot + lane;
-            if (lane <= slot && mine) atomicMax(&keys[pp], mine);
-            if (WANT_FLAGS && lane <= slot && myflag) atomicOr(&pflags[pp], myflag);
-            mine = 0;
-            myflag = 0;
+            const u64 mine = ((u64)mine_hi << 32) | mine_lo;
+            if (lane <= last && mine) atomicMax(&keys[pp], mine);
+            if (WANT_FLAGS && lane <= last && myflag) atomicOr(&pflags[pp], myflag);
+            mine_lo = mine_hi = myflag = 0;
         }
     }
 }
-
-#define MS_K1_BITS_KERNEL(NAME, SLOTS, LDS)                                                                  \
-    template <bool WANT_FLAGS>                                                                               \
-    __global__ __launch_bounds__(kNunnThreads) void NAME(                                                    \
-        const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,             \
-        uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,            \
-        uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {                            \
-        sweep_nunn_bits_body<SLOTS, WANT_FLAGS, LDS>(nflags, ndigit, n_rows, node_base, pods, n_pods, chunk, \
-                                                     seed32, keys, pflags);                                  \
-    }
-MS_K1_BITS_KERNEL(k_sweep_nunn_bits32, 32, false)
-MS_K1_BITS_KERNEL(k_sweep_nunn_bits64, 64, false)
-MS_K1_BITS_KERNEL(k_sweep_nunn_bits32l, 32, true)
-#undef MS_K1_BITS_KERNEL
 
 // ----------------------------------------------------------------------------
 // K3: NodeUnschedulable + NodeResourcesFit filters, NodeNumber + LeastAllocated
@@ -513,7 +451,7 @@ __device__ __forceinline__ PodFull load_pod(const ms_pod_rec &pr, uint32_t seed3
     q.dig = pr.name_digit;
     q.tol = pr.tolerates_unschedulable != 0;
     q.zero_req = (q.rc == 0 && q.rm == 0);
-    q.A = fmix32(seed32 ^ pr.ordinal);
+    q.A = tb_pod(seed32, pr.ordinal);
     return q;
 }
 
@@ -535,8 +473,7 @@ __device__ __forceinline__ u64 eval_full(const FullRow &x, uint32_t ord, const P
     const int64_t s_cpu = least_requested(x.nz_cpu + q.nc, x.alloc_cpu);
     const int64_t s_mem = least_requested(x.nz_mem + q.nm, x.alloc_mem);
     const uint32_t la = (uint32_t)((s_cpu + s_mem) / 2);
-    const uint32_t h = fmix32(q.A ^ (ord * kGolden32));
-    return make_key(nn + la, h, ord);
+    return make_key(nn + la, tb_hash(q.A, ord), ord);
 }
 
 // Batched resource-aware sweep: atomicMax into keys[P] / atomicOr into flags[P].
@@ -1170,74 +1107,65 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 }  // namespace
 
 // K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
-// interleave variants inside one process: "v0" (hash every pair), "lazy"
-// (SWAR + lazy hash), "bits32" / "bits64" (bit-sliced columns). Default bits32.
-enum K1Variant { K1_V0 = 0, K1_LAZY = 1, K1_BITS32 = 2, K1_BITS64 = 3, K1_BITS32L = 4 };
+// interleave variants inside one process: "v0" (hash every pair, the plain
+// cross-check) or the default v5.
+enum K1Variant { K1_V0 = 0, K1_V5 = 5 };
 static int k1_variant() {
     const char *e = getenv("MINISCHED_K1");
-    if (!e || !e[0]) return K1_BITS32;
-    if (e[0] == 'v' && e[1] == '0') return K1_V0;
-    if (e[0] == 'l') return K1_LAZY;
-    if (e[0] == 'b' && e[4] == '6') return K1_BITS64;
-    if (e[0] == 'b' && e[6] == 'l') return K1_BITS32L;
-    return K1_BITS32;
+    if (e && e[0] == 'v' && e[1] == '0') return K1_V0;
+    return K1_V5;
 }
 
-// grid for the wave-tiled sweeps: pod chunks so that live waves ~ 8 per SIMD
-static dim3 wave_tiled_grid(uint32_t n_rows, uint32_t n_pods, uint32_t wave_rows, int num_cus, uint32_t &chunk) {
-    const uint32_t block_rows = wave_rows * (kNunnThreads / 64);
-    const uint32_t gx = cdiv(n_rows, block_rows);
-    const uint32_t live_waves = cdiv(n_rows, wave_rows);
-    const uint32_t target = (uint32_t)(num_cus > 0 ? num_cus : 256) * 32u;
-    uint32_t chunks = cdiv(target, live_waves);
-    chunks = std::max<uint32_t>(1, std::min<uint32_t>(chunks, cdiv(n_pods, 64)));
-    chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
-    return dim3(gx, cdiv(n_pods, chunk));
+// One-round grid (v5): as many pod chunks as resident waves allow, so every
+// wave sweeps the same pod count in a single round. MINISCHED_K1_ROUNDS
+// (default 1) multiplies the pod chunks for experiments.
+template <bool WANT_FLAGS>
+static hipError_t launch_v5(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
+                            unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
+    static int blocks_per_cu = 0;
+    if (!blocks_per_cu) {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void *>(k_sweep_nunn_v5<WANT_FLAGS>), 64, 0);
+        if (e != hipSuccess) return e;
+        blocks_per_cu = nb > 0 ? nb : 1;
+    }
+    uint32_t rounds = 1;
+    if (const char *r = getenv("MINISCHED_K1_ROUNDS")) rounds = (uint32_t)std::max(1, atoi(r));
+    const uint32_t gx = cdiv(n_rows, kK1WaveRows);
+    const uint32_t resident = (uint32_t)blocks_per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
+    uint32_t chunks = std::max<uint32_t>(1, resident / gx) * rounds;
+    chunks = std::min<uint32_t>(chunks, cdiv(n_pods, 64));
+    const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
+    hipLaunchKernelGGL(k_sweep_nunn_v5<WANT_FLAGS>, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags,
+                       t.digit, n_rows, t.base, ps, n_pods, chunk, keys, flags);
+    return hipGetLastError();
 }
-
-#define MS_LAUNCH_K1(KERNEL, WAVE_ROWS)                                                                      \
-    do {                                                                                                     \
-        uint32_t chunk_;                                                                                     \
-        const dim3 grid_ = wave_tiled_grid(n_rows, n_pods, (WAVE_ROWS), num_cus, chunk_);                    \
-        if (flags)                                                                                           \
-            hipLaunchKernelGGL(KERNEL<true>, grid_, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows, t.base, \
-                               pods, n_pods, chunk_, seed32, keys, flags);                                   \
-        else                                                                                                 \
-            hipLaunchKernelGGL(KERNEL<false>, grid_, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,       \
-                               t.base, pods, n_pods, chunk_, seed32, keys, flags);                           \
-    } while (0)
 
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
-                             hipStream_t s) {
-    if (n_pods == 0 || n_rows == 0) return hipSuccess;
-    switch (k1_variant()) {
-        case K1_V0: {
-            const uint32_t gx = cdiv(n_rows, kNunnTile);
-            const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
-            const dim3 grid(gx, cdiv(n_pods, chunk));
-            if (flags)
-                hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
-                                   t.base, pods, n_pods, chunk, seed32, keys, flags);
-            else
-                hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit,
-                                   n_rows, t.base, pods, n_pods, chunk, seed32, keys, flags);
-            break;
-        }
-        case K1_LAZY:
-            MS_LAUNCH_K1(k_sweep_nunn_lazy, kLazyWaveRows);
-            break;
-        case K1_BITS64:
-            MS_LAUNCH_K1(k_sweep_nunn_bits64, 64u * 64u);
-            break;
-        case K1_BITS32L:
-            MS_LAUNCH_K1(k_sweep_nunn_bits32l, 64u * 32u);
-            break;
-        default:
-            MS_LAUNCH_K1(k_sweep_nunn_bits32, 64u * 32u);
-            break;
+                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
+                             int num_cus, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    // pod stream + zeroed keys/flags (the sweep's atomicMax/atomicOr targets)
+    const uint32_t n_prep = n_pods + kPodStreamPad;
+    hipLaunchKernelGGL(k_pod_prep, dim3(cdiv(n_prep, 256)), dim3(256), 0, s, pods, n_pods, seed32, pstream, keys,
+                       flags);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || n_rows == 0) return e;
+    if (k1_variant() == K1_V0) {
+        const uint32_t gx = cdiv(n_rows, kNunnTile);
+        const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+        const dim3 grid(gx, cdiv(n_pods, chunk));
+        if (flags)
+            hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows, t.base,
+                               pods, n_pods, chunk, seed32, keys, flags);
+        else
+            hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
+                               t.base, pods, n_pods, chunk, seed32, keys, flags);
+        return hipGetLastError();
     }
-    return hipGetLastError();
+    return flags ? launch_v5<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
+                 : launch_v5<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
 }
 
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,

@@ -32,8 +32,24 @@ uint32_t msor_pod_hash(uint64_t seed, uint32_t pod_ordinal) {
     return msor_fmix32(msor_seed32(seed) ^ pod_ordinal);
 }
 
+/* murmur3 finaliser without its last xor-shift */
+uint32_t msor_mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x85ebca6bu;
+    x ^= x >> 13;
+    x *= 0xc2b2ae35u;
+    return x;
+}
+
+/* Tie-break hash, rule "r2" (include/minisched_gpu.h): the pod half A is
+ * msor_pod_hash, the node enters additively as ordinal * 0x9E3779 (a 24-bit
+ * odd constant), and the low 5 bits of the result are dropped. */
+uint32_t msor_tb_hash(uint32_t pod_hash, uint32_t node) {
+    return msor_mix32(pod_hash + node * 0x9E3779u) & ~31u;
+}
+
 uint32_t msor_h32(uint64_t seed, uint32_t pod, uint32_t node) {
-    return msor_fmix32(msor_pod_hash(seed, pod) ^ (node * 0x9E3779B1u));
+    return msor_tb_hash(msor_pod_hash(seed, pod), node);
 }
 
 /* key = score<<52 | h32<<20 | (0xFFFFF - ordinal); max wins. */
@@ -125,7 +141,7 @@ static void schedule_one(msor_nodes *nd, const msor_pods *pd, uint32_t j, int pl
         int64_t score = nn_score(pdig, nd->digit[i]);
         if (plugin_set == MSOR_PLUGINS_NU_NRF_NN_LA) score += la_score(nd, i, pd, j);
         uint32_t ord = node_base + i;
-        uint64_t key = msor_key(score, msor_fmix32(ph ^ (ord * 0x9E3779B1u)), ord);
+        uint64_t key = msor_key(score, msor_tb_hash(ph, ord), ord);
         if (key > best) best = key; /* selectHost (minisched.go:304-325) */
     }
     *o_mask = 0;
@@ -273,7 +289,7 @@ int msor_schedule_nunn_names(const char *const *node_names, const uint8_t *node_
         uint64_t best = 0;
         uint32_t best_k = 0;
         for (uint32_t k = 0; k < F; ++k) {
-            uint64_t key = msor_key(list[k].score, msor_fmix32(ph ^ (list[k].ord * 0x9E3779B1u)),
+            uint64_t key = msor_key(list[k].score, msor_tb_hash(ph, list[k].ord),
                                     list[k].ord);
             if (key > best) { best = key; best_k = k; }
         }

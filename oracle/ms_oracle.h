@@ -62,6 +62,8 @@ typedef struct {
 uint32_t msor_fmix32(uint32_t h);
 uint32_t msor_seed32(uint64_t seed);
 uint32_t msor_pod_hash(uint64_t seed, uint32_t pod_ordinal);
+uint32_t msor_mix32(uint32_t x);
+uint32_t msor_tb_hash(uint32_t pod_hash, uint32_t node_ordinal);
 uint32_t msor_h32(uint64_t seed, uint32_t pod_ordinal, uint32_t node_ordinal);
 uint64_t msor_key(int64_t score, uint32_t h, uint32_t node_ordinal);
 int64_t msor_least_requested(int64_t requested, int64_t capacity);

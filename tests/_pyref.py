@@ -26,8 +26,20 @@ def seed32(seed):
     return (seed ^ (seed >> 32)) & 0xFFFFFFFF
 
 
+def mix32(x):
+    """fmix32 without its final xor-shift."""
+    x &= 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
+    return x
+
+
 def h32(seed, pod_ord, node_ord):
-    return fmix32(fmix32(seed32(seed) ^ pod_ord) ^ ((node_ord * 0x9E3779B1) & 0xFFFFFFFF))
+    """Tie-break hash, rule r2 (include/minisched_gpu.h)."""
+    a = fmix32(seed32(seed) ^ pod_ord)
+    return mix32(a + node_ord * 0x9E3779) & 0xFFFFFFE0
 
 
 def key(score, h, node_ord):

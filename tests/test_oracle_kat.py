@@ -226,3 +226,22 @@ def test_sequential_equals_batched_for_nunn(oracle):
     b = oracle.schedule(nr, pr, mode=1, seed=3)
     for k in ("node", "score", "code", "mask"):
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("T,stride", [(2, 1), (3, 1), (10, 1), (64, 1), (16, 10), (32, 1000)])
+def test_tiebreak_uniform_over_tied_nodes(T, stride):
+    # Rule r2 (minisched_gpu.h) stands in for selectHost's reservoir choice
+    # (minisched.go:316-321): over many pods each of T tied nodes must win
+    # about 1/T of the time, also for consecutive ordinals (the additive
+    # node term's weakest case). Chi-square against uniform, 5-sigma bound.
+    P = 20000
+    ords = np.arange(T, dtype=np.uint64) * stride
+    wins = np.zeros(T, dtype=np.int64)
+    for seed in (1, 7):
+        for j in range(seed * 1000003, seed * 1000003 + P // 2):  # disjoint pod ordinals per seed
+            hs = [_pyref.key(10, _pyref.h32(seed, j, int(o)), int(o)) for o in ords]
+            wins[int(np.argmax(hs))] += 1
+    exp = P / T
+    chi2 = float(((wins - exp) ** 2 / exp).sum())
+    dof = T - 1
+    assert chi2 < dof + 5 * np.sqrt(2 * dof), (chi2, wins.tolist())
