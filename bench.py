@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
 METRIC = "pod×node filter+score evals/sec and pods scheduled/sec at 100k nodes, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_EVAL = {"NU+NN": 2, "NU+NRF+NN+LA": 58}
-K1_KERNELS = {"v0": "k_sweep_nunn", "v5": "k_sweep_nunn_v5"}
+K1_KERNELS = {"v0": "k_sweep_nunn", "v6": "k_sweep_nunn_v6"}
 
 
 def parse():
@@ -213,7 +213,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v5"), "k_sweep_nunn_v5"),
+                "kernel": K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v6"), "k_sweep_nunn_v6"),
                 "kernel_ms": sweep_ms,
                 "algorithmic_bytes_per_launch": local_evals * BYTES_PER_EVAL[plugins],
             },

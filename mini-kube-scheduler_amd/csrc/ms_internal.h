@@ -66,14 +66,15 @@ __host__ __device__ inline uint32_t seed32_of(uint64_t seed) { return (uint32_t)
 
 // Tie-break hash (minisched_gpu.h, rule "r2"; oracle/ms_oracle.c msor_tb_hash):
 //   A = fmix32(seed32 ^ pod_ordinal); h = mix32(A + node_ordinal * kG24) & ~31
-// mix32 is fmix32 without its final xor-shift. node_ordinal < 2^20, so the
+// mix32(x): x ^= x>>16; x *= 0x85ebca6b; x ^= x>>16; x *= 0xc2b2ae35 (both
+// xor-shifts by 16, one SDWA v_xor each). node_ordinal < 2^20, so the
 // product is one v_mad_u32_u24, and the dropped low 5 bits leave room for a
 // lane's row slot in the sweep's 32-bit lane keys.
 constexpr uint32_t kG24 = 0x9E3779u;  // odd, 24-bit
 __host__ __device__ inline uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x85ebca6bu;
-    x ^= x >> 13;
+    x ^= x >> 16;
     x *= 0xc2b2ae35u;
     return x;
 }

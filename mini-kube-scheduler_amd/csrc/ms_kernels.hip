@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
 // Pod stream: one 8-byte entry per pod, built once per batch by k_pod_prep
 // (which also zeroes the batch's keys/flags, replacing two memsets):
 //   .x = A = tb_pod(seed32, ordinal)   (the pod half of the tie-break hash)
-//   .y = class = digit (0..9, 10 = name does not end in a digit) + 11 * tolerates
+//   .y = class = digit (0..9, 10 = name does not end in a digit) | tolerates << 4
 // Every node wave reads it through the scalar cache, two pods per 16-byte load.
 // The buffer carries kPodStreamPad padding entries so the one-step-ahead
 // prefetch never needs a bounds check.
@@ -148,7 +148,7 @@ __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint
     if (i < n) {
         const ms_pod_rec pr = pods[i];
         const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
-        ps[i] = make_uint2(tb_pod(seed32, pr.ordinal), d + (pr.tolerates_unschedulable ? 11u : 0u));
+        ps[i] = make_uint2(tb_pod(seed32, pr.ordinal), d | (pr.tolerates_unschedulable ? 16u : 0u));
         keys[i] = 0;
         if (flags) flags[i] = 0;
     } else if (i < n + kPodStreamPad) {
@@ -157,18 +157,18 @@ __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint
 }
 
 // ----------------------------------------------------------------------------
-// K1 v5, the production NU+NN sweep: bit-sliced node columns, pod classes.
+// K1 v6, the production NU+NN sweep: bit-sliced node columns, pod classes.
 //
 // Layout: a wave owns 2048 consecutive rows, 32 per lane, for its whole
 // lifetime, and streams a chunk of pods through them. At load each lane turns
 // its 32 digit bytes into four bit planes and then ten one-hot masks (bit s
 // <=> row row0+s has name digit d), and its flag bytes into unschedulable /
-// absent masks. The 22-entry class table tab[digit + 11*tolerates] holds, per
-// pod class, the rows that pass NodeUnschedulable AND score 10 under
-// NodeNumber. A pod's filter+score over its 32 rows is then one register
-// read at a wave-uniform index (v_movrels): every pair is still evaluated
-// from that node's own columns, 32 pairs per register, and nothing is shared
-// between pods except the node columns.
+// absent masks. tabN[d] = onehot[d] & (rows passing NodeUnschedulable for a
+// non-tolerating pod) lives in registers; a pod's filter+score over its 32
+// rows is one register read at a wave-uniform index (v_movrels). Tolerating
+// pods (rare) read the raw one-hot masks from LDS behind a wave-uniform
+// branch. Every pair is still evaluated from that node's own columns, 32
+// pairs per register; nothing is shared between pods but the node columns.
 //
 // Argmax: NodeNumber's only non-zero score is 10, so a wave's best score is
 // 10 as soon as any lane has a candidate (ballot). Each lane then scores its
@@ -176,12 +176,15 @@ __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint
 // the u32 lane key h27<<5 | (31-slot) (max = highest hash, then lowest row);
 // a DPP max + ballot finds the wave's winner (lowest lane = lowest ordinal on
 // equal hashes). Pods go in pairs: their candidate loops share one
-// lane-divergent loop and their DPP reductions interleave. Wave results land
-// in one lane each (v_writelane) and every 64 pods leave as one coalesced
-// 64-bit atomicMax wave-instruction.
+// lane-divergent, branch-free loop (the carry of cand-1 is the "live"
+// predicate of a v_cndmask, no exec-mask SALU per candidate) and their DPP
+// reductions interleave. A pod's wave result (lane key, winner lane | score
+// flag) lands in one lane of two registers (v_writelane); every 64 pods the
+// lanes assemble the 64-bit packed keys and leave as one coalesced atomicMax
+// wave-instruction.
 //
 // Grid: one block = one wave; grid.x = node waves, grid.y = pod chunks sized
-// so that all waves are resident at once (launch_one_round).
+// so that all waves are resident at once (launch_v6).
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void wave_max_u32_dpp2(uint32_t &a, uint32_t &b) {
 #define MS_DPP2(CTRL, RM)                                                                       \
@@ -251,7 +254,12 @@ __device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ n
                       ((v & 8) ? pl[3] : ~pl[3]);
 }
 
-// v_writelane_b32: lane `lane` of v takes the wave-uniform value x.
+// v_writelane_b32: lane `lane` of v takes the wave-uniform value x. gfx950
+// VOP3 reads one SGPR per instruction, so a dynamic lane index goes through
+// m0; the asm sets m0 itself right before the write, and the kernels using it
+// keep nothing of their own in m0 (checked in `make asm`), hence the pragma.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t lane) {
     asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
                  : "+v"(v)
@@ -259,6 +267,7 @@ __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t l
                  : "m0");
     return v;
 }
+#pragma clang diagnostic pop
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
@@ -277,49 +286,53 @@ __device__ __forceinline__ uint32_t lane_key(uint32_t AH, uint32_t s) {
     return k;
 }
 
-struct PodLane {
+struct PodLane6 {
     uint32_t AH;    // A + hterm0
-    uint32_t cand;  // candidates not yet hashed (bit s <-> row row0 + s)
-    uint32_t kb;    // lane best key (0 while the lane has no candidate)
-    bool valid, any10;
+    uint32_t cand;  // candidates not yet hashed
+    uint32_t kb;    // lane best key
 };
 
-__device__ __forceinline__ void pod_begin(const u32x16 &onehot, uint32_t feasN, uint32_t feasT, uint32_t A,
-                                          uint32_t cls, uint32_t hterm0, PodLane &q) {
-    // filter + score of 32 pairs: the digit's one-hot row mask (wave-uniform
-    // index, v_movrels) AND the NodeUnschedulable-feasible rows for the class
-    const bool tol = cls >= 11;
-    uint32_t cand = onehot[tol ? cls - 11 : cls] & (tol ? feasT : feasN);
-    q.any10 = __ballot(cand != 0) != 0;      // wave-uniform best score
-    if (!q.any10) cand = cls >= 11 ? feasT : feasN;  // no digit match in this wave: score-0 candidates
-    q.valid = cand != 0;
-    q.AH = A + hterm0;
-    q.kb = 0;
-    if (cand) q.kb = lane_key(q.AH, first_slot(cand));  // lowest candidate seeds the lane best
-    q.cand = cand & (cand - 1);
-}
-
-__device__ __forceinline__ void pod_step(PodLane &q) {
+// one candidate step without exec masking: dead lanes (cand == 0) keep kb
+__device__ __forceinline__ void pod_step6(PodLane6 &q) {
     const uint32_t s = first_slot(q.cand);
-    const bool live = q.cand != 0;
-    q.cand &= q.cand - 1;  // stays 0 once empty
-    if (live) q.kb = max(q.kb, lane_key(q.AH, s));
+    const bool live = q.cand != 0;  // = carry of cand + 0xFFFFFFFF
+    q.cand &= q.cand - 1;
+    const uint32_t k = lane_key(q.AH, s);
+    q.kb = live ? max(q.kb, k) : q.kb;
 }
 
-// Wave winner as a packed key (0 when the wave has no feasible row).
-__device__ __forceinline__ u64 pod_key(const PodLane &q, uint32_t kmax, uint32_t ord_wave0) {
-    const u64 winners = __ballot(q.valid && (q.kb ^ kmax) < 32u);  // same hash; lowest lane = lowest ordinal
-    if (!winners) return 0;
-    const uint32_t L = (uint32_t)__builtin_ctzll(winners);
-    const uint32_t kL = (uint32_t)__builtin_amdgcn_readlane((int)q.kb, (int)L);
-    return make_key(q.any10 ? 10u : 0u, kL & ~31u, ord_wave0 + L * 32u + (31u - (kL & 31u)));
+// Wave winners of two pods: candidate rows ca/cb (lanes with any: va/vb),
+// AH = A + hterm0. L = winner lane (64: no feasible row), kL = its lane key.
+__device__ __forceinline__ void pair_winners(uint32_t ca, uint32_t cb, u64 va, u64 vb, uint32_t AHa, uint32_t AHb,
+                                             uint32_t &La, uint32_t &kLa, uint32_t &Lb, uint32_t &kLb) {
+    PodLane6 a, b;
+    a.AH = AHa;
+    b.AH = AHb;
+    a.kb = lane_key(a.AH, first_slot(ca));  // lowest candidate; garbage on empty lanes, masked below
+    b.kb = lane_key(b.AH, first_slot(cb));
+    a.cand = ca & (ca - 1);
+    b.cand = cb & (cb - 1);
+    while (a.cand | b.cand) {  // lane-divergent trip count, branch-free body
+        pod_step6(a);
+        pod_step6(b);
+    }
+    uint32_t ka = ca != 0 ? a.kb : 0u, kbm = cb != 0 ? b.kb : 0u;
+    wave_max_u32_dpp2(ka, kbm);
+    // same 27-bit hash as the max (lane keys never exceed it): lowest lane wins
+    const u64 wa = __ballot(a.kb >= (ka & ~31u)) & va;
+    const u64 wb = __ballot(b.kb >= (kbm & ~31u)) & vb;
+    La = wa ? (uint32_t)__builtin_ctzll(wa) : 64u;
+    Lb = wb ? (uint32_t)__builtin_ctzll(wb) : 64u;
+    kLa = (uint32_t)__builtin_amdgcn_readlane((int)a.kb, (int)(La & 63u));
+    kLb = (uint32_t)__builtin_amdgcn_readlane((int)b.kb, (int)(Lb & 63u));
 }
 
 template <bool WANT_FLAGS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v5(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v6(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk, u64 *__restrict__ keys,
     uint32_t *__restrict__ pflags) {
+    __shared__ uint32_t raw[10][64];  // one-hot masks for tolerating pods
     const uint32_t lane = lane_id();
     const uint32_t wave_row0 = blockIdx.x * kK1WaveRows;
     const uint32_t pbeg = blockIdx.y * chunk;
@@ -327,7 +340,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
     if (wave_row0 >= n_rows || pbeg >= pend) return;  // wave-uniform
     const uint32_t row0 = wave_row0 + lane * 32u;
 
-    u32x16 onehot;  // [10..15] = 0: a non-digit pod name scores 0 everywhere
+    u32x16 tabN;  // [d] = rows with digit d passing NodeUnschedulable for a non-tolerating pod
     uint32_t feasN, feasT;
     bool wave_unsched;
     {
@@ -335,50 +348,68 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
         load_bits32_planes(nflags, ndigit, n_rows, row0, c);
         feasN = ~(c.absent | c.unsched);
         feasT = ~c.absent;
-        onehot = (u32x16)(0u);
+        tabN = (u32x16)(0u);
 #pragma unroll
-        for (int d = 0; d < 10; ++d) onehot[d] = c.onehot[d];
+        for (int d = 0; d < 10; ++d) {
+            tabN[d] = c.onehot[d] & feasN;
+            raw[d][lane] = c.onehot[d];
+        }
         wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
+        // each wave reads only its own lanes' entries: no workgroup barrier needed
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
     const uint32_t hterm0 = (node_base + row0) * kG24;
-    const uint32_t ord_wave0 = node_base + wave_row0;
 
-    // pbeg is a multiple of 64, so pod pairs are 16-byte aligned
-    const uint4 *__restrict__ ps4 = reinterpret_cast<const uint4 *>(ps);
-    uint4 nx = ps4[pbeg >> 1];
-    uint32_t mine_lo = 0, mine_hi = 0, myflag = 0;
-    for (uint32_t p = pbeg; p < pend; p += 2) {
-        const uint4 w = nx;                 // pods p, p+1: {A, class} x 2
-        nx = ps4[(p >> 1) + 1];             // prefetch; the stream is padded past n_pods
-        const bool hasB = p + 1 < pend;
-        PodLane a, b;
-        pod_begin(onehot, feasN, feasT, w.x, w.y, hterm0, a);
-        pod_begin(onehot, feasN, feasT, w.z, w.w, hterm0, b);  // beyond pend: padding, never recorded
-        while (a.cand | b.cand) {  // lane-divergent; one loop for both pods
-            pod_step(a);
-            pod_step(b);
+    const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
+    uint4 nx = q4[0];
+    for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod groups: one flush each
+        const uint32_t gn = min(64u, pend - g);
+        uint32_t m_key = 0, m_info = 0xFFFFFFFFu, myflag = 0;  // info: winner lane (64: none) | score10 << 7
+        for (uint32_t i = 0; i < gn; i += 2) {
+            const uint4 w = nx;
+            ++q4;
+            nx = q4[0];  // prefetch; the stream is padded past n_pods
+            uint32_t ca, cb;
+            {
+                const uint32_t da = w.y & 15u, db = w.w & 15u;
+                ca = (w.y >= 16) ? (da < 10 ? raw[da][lane] & feasT : 0u) : tabN[da];
+                cb = (w.w >= 16) ? (db < 10 ? raw[db][lane] & feasT : 0u) : tabN[db];
+            }
+            u64 va = __ballot(ca != 0), vb = __ballot(cb != 0);  // lanes holding candidates
+            const bool a10 = va != 0, b10 = vb != 0;               // wave-uniform best score 10
+            uint32_t La, kLa, Lb, kLb;
+            if (a10 && b10) {
+                pair_winners(ca, cb, va, vb, w.x + hterm0, w.z + hterm0, La, kLa, Lb, kLb);
+            } else {  // rare: no digit match in this wave, the pod's feasible rows all score 0
+                if (!a10) {
+                    ca = (w.y >= 16) ? feasT : feasN;
+                    va = __ballot(ca != 0);
+                }
+                if (!b10) {
+                    cb = (w.w >= 16) ? feasT : feasN;
+                    vb = __ballot(cb != 0);
+                }
+                pair_winners(ca, cb, va, vb, w.x + hterm0, w.z + hterm0, La, kLa, Lb, kLb);
+            }
+            m_key = writelane(m_key, kLa, i);
+            m_info = writelane(m_info, La | (a10 ? 128u : 0u), i);
+            if (i + 1 < gn) {
+                m_key = writelane(m_key, kLb, i + 1);
+                m_info = writelane(m_info, Lb | (b10 ? 128u : 0u), i + 1);
+            }
+            if (WANT_FLAGS) {  // NodeUnschedulable rejected >= 1 row of this wave for the pod
+                myflag = writelane(myflag, (w.y < 16 && wave_unsched) ? 1u : 0u, i);
+                myflag = writelane(myflag, (w.w < 16 && wave_unsched) ? 1u : 0u, i + 1);
+            }
         }
-        uint32_t ka = a.kb, kb = b.kb;
-        wave_max_u32_dpp2(ka, kb);
-        const u64 keya = pod_key(a, ka, ord_wave0);
-        const u64 keyb = pod_key(b, kb, ord_wave0);
-        const uint32_t slot = (p - pbeg) & 63u;  // even
-        mine_lo = writelane(mine_lo, (uint32_t)keya, slot);
-        mine_hi = writelane(mine_hi, (uint32_t)(keya >> 32), slot);
-        mine_lo = writelane(mine_lo, (uint32_t)keyb, slot + 1);
-        mine_hi = writelane(mine_hi, (uint32_t)(keyb >> 32), slot + 1);
-        if (WANT_FLAGS) {  // NodeUnschedulable rejected >= 1 row of this wave for the pod
-            myflag = writelane(myflag, (w.y < 11 && wave_unsched) ? 1u : 0u, slot);
-            myflag = writelane(myflag, (w.w < 11 && wave_unsched) ? 1u : 0u, slot + 1);
+        // flush: lane j holds pod g+j's wave winner -> packed key (minisched_gpu.h)
+        const uint32_t L = m_info & 127u;
+        if (lane < gn && L < 64u) {
+            const uint32_t ord = node_base + wave_row0 + L * 32u + (31u - (m_key & 31u));
+            atomicMax(&keys[g + lane], make_key((m_info & 128u) ? 10u : 0u, m_key & ~31u, ord));
         }
-        const uint32_t last = hasB ? slot + 1 : slot;
-        if (last == 63u || p + 2 >= pend) {
-            const uint32_t pp = p - slot + lane;
-            const u64 mine = ((u64)mine_hi << 32) | mine_lo;
-            if (lane <= last && mine) atomicMax(&keys[pp], mine);
-            if (WANT_FLAGS && lane <= last && myflag) atomicOr(&pflags[pp], myflag);
-            mine_lo = mine_hi = myflag = 0;
-        }
+        if (WANT_FLAGS && lane < gn && myflag) atomicOr(&pflags[g + lane], myflag);
     }
 }
 
@@ -1108,25 +1139,28 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 
 // K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
 // interleave variants inside one process: "v0" (hash every pair, the plain
-// cross-check) or the default v5.
-enum K1Variant { K1_V0 = 0, K1_V5 = 5 };
+// cross-check) or the default v6.
+enum K1Variant { K1_V0 = 0, K1_V6 = 6 };
 static int k1_variant() {
     const char *e = getenv("MINISCHED_K1");
     if (e && e[0] == 'v' && e[1] == '0') return K1_V0;
-    return K1_V5;
+    return K1_V6;
 }
 
-// One-round grid (v5): as many pod chunks as resident waves allow, so every
+// One-round grid: as many pod chunks as resident waves allow, so every
 // wave sweeps the same pod count in a single round. MINISCHED_K1_ROUNDS
 // (default 1) multiplies the pod chunks for experiments.
+typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, const uint2 *, uint32_t, uint32_t,
+                         unsigned long long *, uint32_t *);
+
 template <bool WANT_FLAGS>
-static hipError_t launch_v5(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
+static hipError_t launch_v6(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
                             unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
+    const K1Kernel kern = k_sweep_nunn_v6<WANT_FLAGS>;
     static int blocks_per_cu = 0;
     if (!blocks_per_cu) {
         int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, reinterpret_cast<const void *>(k_sweep_nunn_v5<WANT_FLAGS>), 64, 0);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64, 0);
         if (e != hipSuccess) return e;
         blocks_per_cu = nb > 0 ? nb : 1;
     }
@@ -1137,8 +1171,8 @@ static hipError_t launch_v5(const NodeTable &t, uint32_t n_rows, const uint2 *ps
     uint32_t chunks = std::max<uint32_t>(1, resident / gx) * rounds;
     chunks = std::min<uint32_t>(chunks, cdiv(n_pods, 64));
     const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
-    hipLaunchKernelGGL(k_sweep_nunn_v5<WANT_FLAGS>, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags,
-                       t.digit, n_rows, t.base, ps, n_pods, chunk, keys, flags);
+    hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags, t.digit, n_rows, t.base, ps,
+                       n_pods, chunk, keys, flags);
     return hipGetLastError();
 }
 
@@ -1164,8 +1198,8 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
                                t.base, pods, n_pods, chunk, seed32, keys, flags);
         return hipGetLastError();
     }
-    return flags ? launch_v5<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
-                 : launch_v5<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
+    return flags ? launch_v6<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
+                 : launch_v6<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
 }
 
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,

@@ -32,11 +32,11 @@ uint32_t msor_pod_hash(uint64_t seed, uint32_t pod_ordinal) {
     return msor_fmix32(msor_seed32(seed) ^ pod_ordinal);
 }
 
-/* murmur3 finaliser without its last xor-shift */
+/* murmur3-style mixer: two xor-shifts by 16 around the fmix32 multipliers */
 uint32_t msor_mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x85ebca6bu;
-    x ^= x >> 13;
+    x ^= x >> 16;
     x *= 0xc2b2ae35u;
     return x;
 }

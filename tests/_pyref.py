@@ -27,11 +27,11 @@ def seed32(seed):
 
 
 def mix32(x):
-    """fmix32 without its final xor-shift."""
+    """Mixer of rule r2: xor-shift 16, multiply, xor-shift 16, multiply."""
     x &= 0xFFFFFFFF
     x ^= x >> 16
     x = (x * 0x85EBCA6B) & 0xFFFFFFFF
-    x ^= x >> 13
+    x ^= x >> 16
     x = (x * 0xC2B2AE35) & 0xFFFFFFFF
     return x
 
