@@ -176,12 +176,18 @@ def main():
         value = evals * args.steps / elapsed
         local_evals = float(P) * float(hi - lo)
         achieved = local_evals * BYTES_PER_EVAL[plugins] / (sweep_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, limiter = None, None
         if os.path.exists(args.traffic_json) and world == 1:
             try:
-                traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+                tj = json.load(open(args.traffic_json))
+                if tj.get("kernel") == K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v6")):
+                    traffic = tj.get("hbm_bytes_per_launch")
+                    # the sweep keeps node columns in registers, so issue, not HBM, binds it
+                    limiter = {"kind": "VALU issue", "valu_busy_frac": tj.get("valu_busy_frac"),
+                               "valu_insts_per_launch": tj.get("valu_insts_per_launch"),
+                               "source": os.path.relpath(args.traffic_json, ROOT)}
             except Exception:
-                traffic = None
+                traffic, limiter = None, None
         line = {
             "metric": METRIC,
             "value": value,
@@ -216,6 +222,7 @@ def main():
                 "kernel": K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v6"), "k_sweep_nunn_v6"),
                 "kernel_ms": sweep_ms,
                 "algorithmic_bytes_per_launch": local_evals * BYTES_PER_EVAL[plugins],
+                "limiter": limiter,
             },
             "cpu_baseline": None,
         }
