@@ -52,6 +52,8 @@ struct ms_ctx {
     // sequential engine scratch
     unsigned long long *d_tile_keys = nullptr;
     uint32_t *d_tile_flags = nullptr;
+    unsigned long long *d_spec = nullptr;  // per-pod speculative winner key (atomicMax target)
+    uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
 
@@ -69,9 +71,8 @@ namespace {
 
 thread_local std::string g_create_err;
 
-// validator counters: u32[4] (overflow, re-swept tiles, recomputes, pods),
-// then u64[5] per-phase cycle sums in the MS_STAMPS diagnostic build
-constexpr size_t kStatsBytes = 16 + 8 * 8 + 8;  // + u32 prefetch hit/miss (stamps build)
+// validator counters: u32[5] (overflow, re-swept tiles, recomputes, pods, record prefetch misses)
+constexpr size_t kStatsBytes = 32;
 
 int fail(ms_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -95,7 +96,7 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_overflow, c->d_pstream};
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_overflow, c->d_pstream};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -166,14 +167,25 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (n_tiles <= c->tile_cap) return MS_OK;
     if (c->d_tile_keys) (void)hipFree(c->d_tile_keys);
     if (c->d_tile_flags) (void)hipFree(c->d_tile_flags);
+    if (c->d_spec) (void)hipFree(c->d_spec);
+    if (c->d_spec_flags) (void)hipFree(c->d_spec_flags);
     c->d_tile_keys = nullptr;
     c->d_tile_flags = nullptr;
+    c->d_spec = nullptr;
+    c->d_spec_flags = nullptr;
     c->tile_cap = 0;
     const size_t n = (size_t)seq_batch_limit() * n_tiles;
     if (hipMalloc((void **)&c->d_tile_keys, n * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential tile keys");
     if (hipMalloc((void **)&c->d_tile_flags, n * sizeof(uint32_t)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential tile flags");
+    if (hipMalloc((void **)&c->d_spec, seq_batch_limit() * sizeof(unsigned long long)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sequential spec keys");
+    if (hipMalloc((void **)&c->d_spec_flags, seq_batch_limit() * sizeof(uint32_t)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sequential spec flags");
+    MS_HIP(c, hipMemsetAsync(c->d_spec, 0, seq_batch_limit() * sizeof(unsigned long long), c->stream));
+    MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, seq_batch_limit() * sizeof(uint32_t), c->stream));
+    MS_HIP(c, hipStreamSynchronize(c->stream));
     c->tile_cap = n_tiles;
     return MS_OK;
 }
@@ -200,16 +212,22 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         }
         return MS_OK;
     }
+    if (rows > seq_max_rows())
+        return fail(c, MS_E_CAPACITY, "resource-aware sequential mode supports at most " +
+                                          std::to_string(seq_max_rows()) + " rows per context (shard the nodes)");
     const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
     int rc = ensure_tiles(c, n_tiles);
+    if (rc) return rc;
+    // the sequential scratch (tile lists, spec keys) was last used on the context stream
+    rc = order_after_ctx_stream(c, s);
     if (rc) return rc;
     const uint32_t B = seq_batch(c);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
-                                          n_tiles, s));
+                                          c->d_spec, c->d_spec_flags, n_tiles, s));
         MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
-                                      n_tiles, d_res + s0, c->d_overflow, s));
+                                      c->d_spec, c->d_spec_flags, n_tiles, d_res + s0, c->d_overflow, s));
     }
     return MS_OK;
 }
@@ -332,22 +350,6 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
 
 int ms_destroy(ms_ctx *c) {
     if (!c) return MS_E_INVAL;
-#ifdef MS_STAMPS
-    {
-        uint64_t st[2 + 8 + 1] = {};
-        (void)hipSetDevice(c->cfg.device);
-        (void)hipStreamSynchronize(c->stream);
-        if (hipMemcpy(st, c->d_overflow, kStatsBytes, hipMemcpyDeviceToHost) == hipSuccess) {
-            const uint32_t *u = reinterpret_cast<const uint32_t *>(st);
-            std::fprintf(stderr,
-                         "MS_STAMPS pods=%u recomputes=%u resweeps=%u pref_hit=%u pref_miss=%u cycles: A_tail=%llu "
-                         "A_reduce_barrier=%llu B=%llu C=%llu C_barrier=%llu pod_load=%llu list_walk=%llu\n",
-                         u[3], u[2], u[1], u[20], u[21], (unsigned long long)st[2], (unsigned long long)st[3],
-                         (unsigned long long)st[4], (unsigned long long)st[5], (unsigned long long)st[6],
-                         (unsigned long long)st[7], (unsigned long long)st[8]);
-        }
-    }
-#endif
     free_all(c);
     delete c;
     return MS_OK;

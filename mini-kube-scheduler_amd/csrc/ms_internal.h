@@ -100,15 +100,23 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 // Per-(pod, wave tile) speculative sweep for the sequential engine: the
 // tile's top-K keys at tile_keys[(p * n_tiles + t) * K + j], 0-terminated,
 // and its filter flags at tile_flags[p * n_tiles + t].
+// spec[p] accumulates (atomicMax) pod p's speculative global winner key and
+// spec_flags[p] the filter flags of tiles without a feasible row; both must be
+// zero on entry (k_validate_seq zeroes the entries it consumed).
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
-                                   uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s);
+                                   uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
+                                   uint32_t n_tiles, hipStream_t s);
 // In-order validation of a speculative batch; writes results and commits
 // binds to the table. Single workgroup.
+// stats: u32[6] = overflow flags, re-swept tiles, recomputed entries, pods,
+// speculation misses, pods that needed the tile-list scan.
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys,
-                               const uint32_t *tile_flags, uint32_t n_tiles, ms_result *results,
-                               uint32_t *overflow, hipStream_t s);
+                               const uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
+                               uint32_t n_tiles, ms_result *results, uint32_t *stats, hipStream_t s);
+// Rows the sequential engine's validator supports (tile lists held in registers).
+uint32_t seq_max_rows();
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
                          const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s);
 hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32_t n_pods,

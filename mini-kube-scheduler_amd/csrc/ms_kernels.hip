@@ -421,20 +421,26 @@ struct FullRow {
     int64_t free_cpu, free_mem;    // Allocatable - Requested
     int64_t nz_cpu, nz_mem;        // NonZeroRequested
     int64_t alloc_cpu, alloc_mem;  // Allocatable
+    double inv_cpu, inv_mem;       // 1/Allocatable (f64), for the LeastAllocated quotient
     int32_t room;                  // AllowedPodNumber - len(Pods)
     uint32_t fd;                   // flags | digit << 8
 };
+
+__device__ __forceinline__ double recip(int64_t c) { return c > 0 ? 1.0 / (double)c : 0.0; }
 
 __device__ __forceinline__ FullRow load_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
     FullRow x;
     if (r >= n_rows) {
         x.free_cpu = x.free_mem = x.nz_cpu = x.nz_mem = x.alloc_cpu = x.alloc_mem = 0;
+        x.inv_cpu = x.inv_mem = 0.0;
         x.room = 0;
         x.fd = kNodeAbsent | (0xFFu << 8);
         return x;
     }
     x.alloc_cpu = t.alloc_cpu[r];
     x.alloc_mem = t.alloc_mem[r];
+    x.inv_cpu = recip(x.alloc_cpu);
+    x.inv_mem = recip(x.alloc_mem);
     x.free_cpu = x.alloc_cpu - t.req_cpu[r];
     x.free_mem = x.alloc_mem - t.req_mem[r];
     x.nz_cpu = t.nz_cpu[r];
@@ -444,12 +450,13 @@ __device__ __forceinline__ FullRow load_row(const NodeTable &t, uint32_t r, uint
     return x;
 }
 
-// floor(num/den) for num >= 0, den > 0; f64 quotient + one-step integer fix-up
-// (exact while num < 2^53, which holds for cpu millicores and memory bytes
-// times 100 below 90 PB).
-__device__ __forceinline__ int64_t div_floor_pos(int64_t num, int64_t den) {
-    if (num < (1ll << 53) && den < (1ll << 53)) {
-        int64_t q = (int64_t)((double)num / (double)den);
+// floor(num/den) for 0 <= num <= 100*den, den > 0, given inv = RN(1/den): the
+// f64 product is within a few ulps of the quotient (<= 100), so it is off by at
+// most one and one integer fix-up makes it exact. num >= 2^53 (beyond any cpu
+// millicores or memory bytes x 100 below 90 PB) takes the integer division.
+__device__ __forceinline__ int64_t div_floor_recip(int64_t num, int64_t den, double inv) {
+    if (num < (1ll << 53)) {
+        int64_t q = (int64_t)((double)num * inv);
         const int64_t r = num - q * den;
         if (r < 0) q -= 1;
         else if (r >= den) q += 1;
@@ -459,10 +466,10 @@ __device__ __forceinline__ int64_t div_floor_pos(int64_t num, int64_t den) {
 }
 
 // leastRequestedScore (k8s@v1.22.0 least_allocated.go)
-__device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t capacity) {
+__device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t capacity, double inv) {
     if (capacity == 0) return 0;
     if (requested > capacity) return 0;
-    return div_floor_pos((capacity - requested) * 100, capacity);
+    return div_floor_recip((capacity - requested) * 100, capacity, inv);
 }
 
 struct PodFull {
@@ -501,8 +508,8 @@ __device__ __forceinline__ u64 eval_full(const FullRow &x, uint32_t ord, const P
     if (bad) { nrf = 1; return 0; }
     const int nd = (int)(x.fd >> 8);
     const uint32_t nn = (nd == q.dig) ? 10u : 0u;
-    const int64_t s_cpu = least_requested(x.nz_cpu + q.nc, x.alloc_cpu);
-    const int64_t s_mem = least_requested(x.nz_mem + q.nm, x.alloc_mem);
+    const int64_t s_cpu = least_requested(x.nz_cpu + q.nc, x.alloc_cpu, x.inv_cpu);
+    const int64_t s_mem = least_requested(x.nz_mem + q.nm, x.alloc_mem, x.inv_mem);
     const uint32_t la = (uint32_t)((s_cpu + s_mem) / 2);
     return make_key(nn + la, tb_hash(q.A, ord), ord);
 }
@@ -579,7 +586,8 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
                                                                   uint32_t n_pods, uint32_t chunk, uint32_t seed32,
                                                                   u64 *__restrict__ tile_keys,
                                                                   uint32_t *__restrict__ tile_flags,
-                                                                  uint32_t n_tiles) {
+                                                                  u64 *__restrict__ spec,
+                                                                  uint32_t *__restrict__ spec_flags, uint32_t n_tiles) {
     const uint32_t lane = lane_id();
     const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
     if (tile >= n_tiles) return;  // wave-uniform; no block barriers in this kernel
@@ -622,385 +630,407 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
         const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
         const size_t cell = (size_t)p * n_tiles + tile;
         if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out;
-        if (lane == 0) tile_flags[cell] = f;
+        if (lane == 0) {
+            tile_flags[cell] = f;
+            if (out) atomicMax(&spec[p], out);  // speculative global winner (zeroed by the validator)
+            else if (f) atomicOr(&spec_flags[p], f);  // filters of tiles with no feasible row
+        }
     }
 }
 
 // ----------------------------------------------------------------------------
-// Exact sequential engine, in-order half. One 1024-thread workgroup walks the
-// batch in queue order. A bind only lowers keys of the node it lands on (NRF
-// feasibility and LeastAllocated are monotone in Requested/pod_count; NU, NN
-// and the hash do not read them), so for each tile the first top-K entry whose
-// node is untouched so far in the batch is still that tile's best among
-// untouched nodes; entries above it (touched nodes) are re-evaluated from the
-// LDS copy of their current record. Only a tile whose K entries are all
-// touched (and whose list is not complete) is re-swept against current state.
+// Exact sequential engine, in-order half: ONE wave walks the batch in queue
+// order, with no barriers. A bind only lowers keys of the node it lands on
+// (NRF feasibility and LeastAllocated are monotone in Requested/pod_count; NU,
+// NN and the hash do not read them), so for each tile the first top-K entry
+// whose node is untouched so far in the batch is still that tile's best among
+// untouched nodes; touched entries above it are re-evaluated from the LDS copy
+// of their current record. Only a tile whose K entries are all touched (and
+// whose list is full) is re-swept against current state.
+//
+// Latency layout (one wave has nothing to hide latency behind):
+//  - prologue: the batch's pod records, speculative winner rows (the sweep's
+//    per-pod atomicMax) and those rows' batch-start records go to LDS;
+//  - a lane owns tiles lane, lane+64, ...; their lists and flags are loaded
+//    two pods ahead into one of two register buffers (the pod loop is
+//    unrolled by two, so no buffer rotation forces a vmcnt wait);
+//  - every head's touched-map probe is issued before any is tested;
+//  - a 64-bit DPP max picks the winner; the lane that produced it knows
+//    whether it is a touched node's LDS slot;
+//  - the bind (NodeInfo.AddPod) updates that LDS record, one field per lane.
+// Results and records stay in LDS until the batch ends.
 // ----------------------------------------------------------------------------
-constexpr int kSeqBatch = 512;
-constexpr int kMapBits = 11;
-constexpr int kMapCap = 1 << kMapBits;  // >= 4 * kSeqBatch
-constexpr int kValThreads = 1024;
-constexpr int kValWaves = kValThreads / 64;
+constexpr int kSeqBatch = 256;  // pods per speculative batch (host clamps)
+constexpr int kMapBits = 10;
+constexpr int kMapCap = 1 << kMapBits;  // 4 x slots: the first probe nearly always decides
+constexpr int kSeqMaxJ = 16;            // tile lists per lane in registers: n_tiles <= 1024 (262k rows)
+constexpr int kRecF = 12;               // record fields per slot (see RecField)
+constexpr int kSpecF = 9;               // fields loaded from the node table (F_REQ_CPU .. F_FD)
 
+// LDS record of a touched node, one i64 (or f64 bit pattern) per field
+enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALLOC_MEM, F_CNT, F_ALLOWED, F_FD,
+                F_ROW, F_INV_CPU, F_INV_MEM };
+
+// Slots: rec[p] for p < kSeqBatch is pod p's speculative winner's record,
+// loaded at batch start (it becomes that node's live record when pod p binds
+// there first); rec[kSeqBatch + i] are records loaded on a speculation miss.
 struct SeqShared {
-    uint32_t map_row[kMapCap];  // row + 1, 0 = empty
-    uint16_t map_slot[kMapCap];
-    // full current record of each node bound in this batch
-    int64_t req_cpu[kSeqBatch], req_mem[kSeqBatch], nz_cpu[kSeqBatch], nz_mem[kSeqBatch];
-    int64_t alloc_cpu[kSeqBatch], alloc_mem[kSeqBatch];
-    int32_t cnt[kSeqBatch], allowed[kSeqBatch];
-    uint32_t fd[kSeqBatch], row[kSeqBatch];
-    u64 wave_best[kValWaves];
-    u64 wave_touched[kValWaves];  // best key among nodes already bound in this batch
-    uint32_t wave_fl[kValWaves];
-    uint32_t need[kSeqBatch];  // tiles to re-sweep for the current pod (bounded below)
-    uint32_t n_need, n_slots;
-    // results and counters stay in LDS until the batch ends: a global store or
-    // atomic inside the pod loop would be waited on (vmcnt counts stores) at
-    // the next control-flow join, a memory round trip per pod
+    uint32_t map[kMapCap];  // ((row + 1) << 9) | slot; 0 = empty
+    int64_t rec[2 * kSeqBatch][kRecF];
     ms_result res[kSeqBatch];
-    uint32_t spec_row[kSeqBatch];  // speculative global winner row per pod (0xFFFFFFFF: none)
-    ms_pod_rec pods[kSeqBatch];    // the batch's pod records (no scalar-cache miss per pod)
-    u64 lst[2][kValThreads][kTopK];  // two-slot buffer of the first kValThreads tiles' lists
-    uint32_t lsf[2][kValThreads];
-    uint32_t n_recompute, n_resweep, n_pref_hit, n_pref_miss;
+    ms_pod_rec pods[kSeqBatch];
+    u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
+    uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
 };
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
 
-__device__ __forceinline__ int map_find(const SeqShared &S, uint32_t row) {
+// slot of row in the touched-node map, -1 if untouched, continuing a probe
+// whose first read returned v (load factor <= 1/4)
+__device__ __forceinline__ int map_resolve(const SeqShared &S, uint32_t row, uint32_t v) {
     uint32_t h = map_hash(row);
-    for (int i = 0; i < kMapCap; ++i) {
-        const uint32_t k = S.map_row[h];
-        if (k == 0) return -1;
-        if (k == row + 1) return S.map_slot[h];
+    const uint32_t key = row + 1;
+    for (;;) {
+        if (v == 0) return -1;
+        if ((v >> 9) == key) return (int)(v & 511u);
         h = (h + 1) & (kMapCap - 1);
+        v = S.map[h];
     }
-    return -1;
+}
+
+__device__ __forceinline__ int map_find(const SeqShared &S, uint32_t row) {
+    return map_resolve(S, row, S.map[map_hash(row)]);
 }
 
 __device__ __forceinline__ FullRow slot_row(const SeqShared &S, int sl) {
+    const int64_t *r = S.rec[sl];
     FullRow x;
-    x.alloc_cpu = S.alloc_cpu[sl];
-    x.alloc_mem = S.alloc_mem[sl];
-    x.free_cpu = x.alloc_cpu - S.req_cpu[sl];
-    x.free_mem = x.alloc_mem - S.req_mem[sl];
-    x.nz_cpu = S.nz_cpu[sl];
-    x.nz_mem = S.nz_mem[sl];
-    x.room = S.allowed[sl] - S.cnt[sl];
-    x.fd = S.fd[sl];
+    x.alloc_cpu = r[F_ALLOC_CPU];
+    x.alloc_mem = r[F_ALLOC_MEM];
+    x.free_cpu = x.alloc_cpu - r[F_REQ_CPU];
+    x.free_mem = x.alloc_mem - r[F_REQ_MEM];
+    x.nz_cpu = r[F_NZ_CPU];
+    x.nz_mem = r[F_NZ_MEM];
+    x.inv_cpu = __longlong_as_double(r[F_INV_CPU]);
+    x.inv_mem = __longlong_as_double(r[F_INV_MEM]);
+    x.room = (int32_t)(r[F_ALLOWED] - r[F_CNT]);
+    x.fd = (uint32_t)r[F_FD];
     return x;
 }
 
-// Current record of one node as the validator needs it (a map slot's payload).
-struct NodeRecRegs {
-    int64_t req_cpu, req_mem, nz_cpu, nz_mem, alloc_cpu, alloc_mem;
-    int32_t cnt, allowed;
-    uint32_t fd;
-};
-
-__device__ __forceinline__ NodeRecRegs load_rec(const NodeTable &t, uint32_t r) {
-    NodeRecRegs x;
-    x.req_cpu = t.req_cpu[r];
-    x.req_mem = t.req_mem[r];
-    x.nz_cpu = t.nz_cpu[r];
-    x.nz_mem = t.nz_mem[r];
-    x.alloc_cpu = t.alloc_cpu[r];
-    x.alloc_mem = t.alloc_mem[r];
-    x.cnt = t.pod_count[r];
-    x.allowed = t.allowed_pods[r];
-    x.fd = (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8);
-    return x;
+// Field f (< kSpecF) of node row r's current device record.
+__device__ __forceinline__ int64_t rec_field(const NodeTable &t, uint32_t r, uint32_t f) {
+    switch (f) {
+        case F_REQ_CPU: return t.req_cpu[r];
+        case F_REQ_MEM: return t.req_mem[r];
+        case F_NZ_CPU: return t.nz_cpu[r];
+        case F_NZ_MEM: return t.nz_mem[r];
+        case F_ALLOC_CPU: return t.alloc_cpu[r];
+        case F_ALLOC_MEM: return t.alloc_mem[r];
+        case F_CNT: return t.pod_count[r];
+        case F_ALLOWED: return t.allowed_pods[r];
+        default: return (int64_t)((uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8));  // F_FD
+    }
 }
 
 __device__ __forceinline__ uint32_t row_of_key(u64 k, uint32_t base) {
     return (0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) - base;
 }
 
-// Adds pod q to map slot sl (NodeInfo.AddPod on the LDS copy).
-__device__ __forceinline__ void slot_add_pod(SeqShared &S, int sl, const PodFull &q) {
-    S.req_cpu[sl] += q.rc;
-    S.req_mem[sl] += q.rm;
-    S.nz_cpu[sl] += q.nc;
-    S.nz_mem[sl] += q.nm;
-    S.cnt[sl] += 1;
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// Inserts row (not yet in the map) with its current record, then adds pod q.
-__device__ __forceinline__ void slot_insert(SeqShared &S, uint32_t row, const NodeRecRegs &x, const PodFull &q) {
-    const int sl = (int)S.n_slots++;
-    uint32_t h = map_hash(row);
-    while (S.map_row[h] != 0) h = (h + 1) & (kMapCap - 1);
-    S.map_row[h] = row + 1;
-    S.map_slot[h] = (uint16_t)sl;
-    S.row[sl] = row;
-    S.req_cpu[sl] = x.req_cpu;
-    S.req_mem[sl] = x.req_mem;
-    S.nz_cpu[sl] = x.nz_cpu;
-    S.nz_mem[sl] = x.nz_mem;
-    S.cnt[sl] = x.cnt;
-    S.alloc_cpu[sl] = x.alloc_cpu;
-    S.alloc_mem[sl] = x.alloc_mem;
-    S.allowed[sl] = x.allowed;
-    S.fd[sl] = x.fd;
-    slot_add_pod(S, sl, q);
-}
+template <int J>
+struct TileLists {
+    u64 e[J][kTopK];
+    uint32_t f[J];
+};
 
-__global__ __launch_bounds__(kValThreads) void k_validate_seq(NodeTable t, uint32_t n_rows,
-                                                              const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
-                                                              uint32_t seed32, const u64 *__restrict__ tile_keys,
-                                                              const uint32_t *__restrict__ tile_flags,
-                                                              uint32_t n_tiles, ms_result *__restrict__ results,
-                                                              uint32_t *__restrict__ overflow) {
-    uint32_t *stats = overflow;  // [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods
-    __shared__ SeqShared S;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-#ifdef MS_STAMPS
-    // diagnostic build only: wave 0's cycles per phase, summed over pods
-    u64 st_prev = 0, st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define MS_STAMP(i)                                                    \
-    do {                                                               \
-        __builtin_amdgcn_sched_barrier(0);                             \
-        if (tid == 0) {                                                \
-            const u64 now_ = __builtin_amdgcn_s_memtime();             \
-            if ((i) >= 0) st_acc[(i) < 0 ? 0 : (i)] += now_ - st_prev; \
-            st_prev = now_;                                            \
-        }                                                              \
-        __builtin_amdgcn_sched_barrier(0);                             \
-    } while (0)
-#else
-#define MS_STAMP(i) \
-    do {            \
-    } while (0)
-#endif
-    for (uint32_t i = tid; i < (uint32_t)kMapCap; i += kValThreads) S.map_row[i] = 0;
-    if (tid == 0) {
-        S.n_slots = 0;
-        S.n_need = 0;
-        S.n_recompute = 0;
-        S.n_resweep = 0;
-        S.n_pref_hit = 0;
-        S.n_pref_miss = 0;
+// Pod p's lists and flags for this lane's tiles (zeros past the batch / tiles).
+template <int J>
+__device__ __forceinline__ void load_lists(TileLists<J> &B, const u64 *__restrict__ tile_keys,
+                                           const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_pods,
+                                           uint32_t n_tiles, uint32_t lane) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const uint32_t tt = lane + 64u * j;
+        if (p < n_pods && tt < n_tiles) {
+            const size_t cell = (size_t)p * n_tiles + tt;
+            const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
+            const uint4 a = q[0], b = q[1];
+            B.e[j][0] = ((u64)a.y << 32) | a.x;
+            B.e[j][1] = ((u64)a.w << 32) | a.z;
+            B.e[j][2] = ((u64)b.y << 32) | b.x;
+            B.e[j][3] = ((u64)b.w << 32) | b.z;
+            B.f[j] = tile_flags[cell];
+        } else {
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) B.e[j][k] = 0;
+            B.f[j] = 0;
+        }
     }
-    if (n_pods > (uint32_t)kSeqBatch) {  // host guarantees this; never index past S
-        if (tid == 0) *overflow = 1;
+}
+
+struct SeqCounters {
+    uint32_t recompute, resweep, miss, slow;
+};
+
+constexpr int kFreshSlot = 0x10000;  // wslot flag: pod's own speculative slot, not yet in the map
+
+// Full scan of pod p's tile lists (the speculative winner was touched, or
+// the pod had no feasible row at speculation): b = winner key, wslot = its
+// LDS slot if it is a touched node.
+template <int J>
+__device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, uint32_t n_rows, const PodFull &q,
+                                              const TileLists<J> &B, uint32_t lane, SeqCounters &ctr, u64 &b_out,
+                                              int &wslot_out) {
+    // ---- every head's first map probe, issued together
+    uint32_t hrow[J], hv[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        hrow[j] = row_of_key(B.e[j][0], t.base);
+        hv[j] = B.e[j][0] ? S.map[map_hash(hrow[j])] : 0u;
+    }
+    // ---- every tile's best: first untouched list entry, touched ones re-evaluated
+    u64 best = 0;
+    int best_slot = -1;  // map slot of the lane's best when it came from a touched node
+    uint32_t need = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        if (B.e[j][0] == 0) continue;  // no feasible row in this tile at speculation (or no tile)
+        int sl = map_resolve(S, hrow[j], hv[j]);
+        if (sl < 0) {  // untouched head: exact, and the tile's best
+            if (B.e[j][0] > best) {
+                best = B.e[j][0];
+                best_slot = -1;
+            }
+            continue;
+        }
+        // walk the list: touched entries are re-evaluated, the first untouched one ends it
+        for (int k = 0;;) {
+            const uint32_t row = row_of_key(B.e[j][k], t.base);
+            uint32_t nu, nrf;
+            const u64 r = eval_full(slot_row(S, sl), t.base + row, q, nu, nrf);
+            ++ctr.recompute;
+            if (r > best) {
+                best = r;
+                best_slot = sl;
+            }
+            if (++k == kTopK) {
+                need |= 1u << j;  // K touched entries: the tile's next row is unknown, re-sweep it
+                break;
+            }
+            const u64 e2 = B.e[j][k];
+            if (e2 == 0) break;  // list ended: the remaining rows were infeasible and stay so
+            sl = map_find(S, row_of_key(e2, t.base));
+            if (sl < 0) {
+                if (e2 > best) {
+                    best = e2;
+                    best_slot = -1;
+                }
+                break;
+            }
+        }
+    }
+    // ---- rare: tiles to re-sweep against current state, cooperatively (4 rows per lane)
+    u64 need_any = __ballot(need != 0);
+    while (need_any) {
+        const uint32_t src = (uint32_t)__builtin_ctzll(need_any);
+        const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)need, (int)src);
+        const uint32_t tile = src + 64u * (uint32_t)__builtin_ctz(bits);
+        if (lane == src) need &= need - 1;
+        need_any = __ballot(need != 0);
+        ++ctr.resweep;
+#pragma unroll
+        for (int sidx = 0; sidx < kFullSlots; ++sidx) {
+            const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + sidx;
+            FullRow x = load_row(t, r, n_rows);
+            int sl = -1;
+            if (r < n_rows) {
+                sl = map_find(S, r);
+                if (sl >= 0) x = slot_row(S, sl);
+            }
+            uint32_t nu, nrf;
+            const u64 k = eval_full(x, t.base + r, q, nu, nrf);
+            if (k > best) {
+                best = k;
+                best_slot = sl;
+            }
+        }
+    }
+    // ---- decide: 64-bit wave max; the owning lane knows the winner's slot
+    const u64 b = wave_max_u64_dpp(best);
+    const u64 own = __ballot(b != 0 && best == b);
+    b_out = b;
+    wslot_out = own ? __builtin_amdgcn_readlane(best_slot, (int)__builtin_ctzll(own)) : -1;
+}
+
+// Result of pod p from its winner key b (0: FitError), and the bind.
+template <int J>
+__device__ __forceinline__ void commit_pod(SeqShared &S, const NodeTable &t, const PodFull &q, uint32_t p,
+                                           const TileLists<J> &B, uint32_t lane, uint32_t &n_misses, SeqCounters &ctr,
+                                           u64 b, int wslot) {
+    ms_result res;
+    res._pad = 0;
+    res.plugin_mask = 0;
+    res.node = -1;
+    res.score = 0;
+    if (b == 0) {  // FitError
+        uint32_t f;
+        if (S.spec_key[p] == 0) {
+            f = S.spec_flags[p];  // every tile was infeasible at speculation: their flags, OR-ed by the sweep
+        } else {  // per tile: speculative flags, + NRF if its feasible rows were all bound away
+            uint32_t fl = 0;
+#pragma unroll
+            for (int j = 0; j < J; ++j) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
+            f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+        }
+        res.code = MS_CODE_UNSCHEDULABLE;
+        res.plugin_mask =
+            ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) | ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
+    } else if (q.dig < 0) {
+        res.code = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
+    } else {
+        const uint32_t node = 0xFFFFFu - (uint32_t)(b & 0xFFFFFu);
+        res.node = (int32_t)node;
+        res.code = MS_CODE_SUCCESS;
+        res.score = (int64_t)(b >> 52);
+        // assume-on-select: NodeInfo.AddPod on the winner's LDS record
+        const uint32_t row = node - t.base;
+        int sl = wslot;
+        if (sl < 0) {  // untouched winner other than the speculative one: load its record
+            sl = kSeqBatch + (int)n_misses++;
+            ++ctr.miss;
+            int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
+            const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
+            if (lane == (uint32_t)F_ROW) v = row;
+            if (lane == (uint32_t)F_INV_CPU) v = __double_as_longlong(recip(capc));
+            if (lane == (uint32_t)F_INV_MEM) v = __double_as_longlong(recip(capm));
+            if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
+            sl |= kFreshSlot;
+        }
+        if (sl & kFreshSlot) {  // first bind on this node in the batch: map it
+            sl &= ~kFreshSlot;
+            if (lane == 0) {
+                uint32_t h = map_hash(row);
+                while (S.map[h] != 0) h = (h + 1) & (kMapCap - 1);
+                S.map[h] = ((row + 1) << 9) | (uint32_t)sl;
+            }
+        }
+        int64_t add = 0;
+        switch (lane) {
+            case F_REQ_CPU: add = q.rc; break;
+            case F_REQ_MEM: add = q.rm; break;
+            case F_NZ_CPU: add = q.nc; break;
+            case F_NZ_MEM: add = q.nm; break;
+            case F_CNT: add = 1; break;
+            default: break;
+        }
+        if (add) atomicAdd(reinterpret_cast<unsigned long long *>(&S.rec[sl][lane]), (unsigned long long)add);
+    }
+    if (lane == 0) S.res[p] = res;
+}
+
+// One pod of the in-order walk (all 64 lanes).
+template <int J>
+__device__ __forceinline__ void validate_pod(SeqShared &S, const NodeTable &t, uint32_t n_rows, uint32_t seed32,
+                                             uint32_t p, const TileLists<J> &B, uint32_t lane, uint32_t &n_misses,
+                                             SeqCounters &ctr) {
+    const PodFull q = load_pod(S.pods[p], seed32);
+    // ---- fast path: every current key is <= its speculative key, so an
+    // untouched speculative winner is still the exact winner
+    // (slot p holds that node's batch-start record, so it becomes its slot)
+    const u64 sk = S.spec_key[p];
+    u64 b;
+    int wslot;
+    if (sk == 0) {  // no feasible row at speculation: none now either (FitError)
+        b = 0;
+        wslot = -1;
+    } else if (map_find(S, row_of_key(sk, t.base)) < 0) {
+        b = sk;
+        wslot = (int)p | kFreshSlot;
+    } else {
+        ++ctr.slow;
+        validate_scan<J>(S, t, n_rows, q, B, lane, ctr, b, wslot);
+    }
+    commit_pod<J>(S, t, q, p, B, lane, n_misses, ctr, b, wslot);
+}
+
+template <int J>  // tile lists per lane: n_tiles <= 64 * J
+__global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_rows,
+                                                     const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                                                     uint32_t seed32, const u64 *__restrict__ tile_keys,
+                                                     const uint32_t *__restrict__ tile_flags, u64 *__restrict__ spec,
+                                                     uint32_t *__restrict__ spec_flags, uint32_t n_tiles,
+                                                     ms_result *__restrict__ results, uint32_t *__restrict__ stats) {
+    // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
+    //        [4] speculation misses (records loaded), [5] pods that needed the list scan
+    __shared__ SeqShared S;
+    const uint32_t lane = threadIdx.x;
+    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
+        if (lane == 0) atomicOr(&stats[0], 1u);
         return;
     }
-    // Prologue: each pod's speculative global winner (max tile head). Thread 0
-    // prefetches the next pod's winner record during the current pod, so the
-    // common bind (winner untouched and as speculated) never waits on memory.
-    for (uint32_t i = tid; i < n_pods; i += kValThreads) S.pods[i] = pods[i];
-    for (uint32_t p = wave; p < n_pods; p += kValWaves) {
-        u64 m = 0;
-        for (uint32_t tt = lane; tt < n_tiles; tt += 64) m = umax64(m, tile_keys[((size_t)p * n_tiles + tt) * kTopK]);
-        m = wave_max_u64_dpp(m);
-        if (lane == 0) S.spec_row[p] = m ? row_of_key(m, t.base) : 0xFFFFFFFFu;
+    // the first two pods' lists are in flight while the prologue runs
+    TileLists<J> LA, LB;
+    load_lists(LA, tile_keys, tile_flags, 0, n_pods, n_tiles, lane);
+    load_lists(LB, tile_keys, tile_flags, 1, n_pods, n_tiles, lane);
+    // prologue: touched map, pods, speculative winners and their batch-start records (slot p)
+    for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map[i] = 0;
+    for (uint32_t i = lane; i < n_pods; i += 64) {
+        S.pods[i] = pods[i];
+        const u64 sk = spec[i];
+        S.spec_key[i] = sk;
+        S.spec_flags[i] = spec_flags[i];
+        spec[i] = 0;  // the next batch's sweep accumulates here again
+        spec_flags[i] = 0;
+        if (sk) {
+            const uint32_t r = row_of_key(sk, t.base);
+            int64_t *rec = S.rec[i];
+#pragma unroll
+            for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
+            rec[F_ROW] = r;
+            rec[F_INV_CPU] = __double_as_longlong(recip(rec[F_ALLOC_CPU]));
+            rec[F_INV_MEM] = __double_as_longlong(recip(rec[F_ALLOC_MEM]));
+        }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 
-    // Lists of the first kValThreads tiles go through a two-slot LDS buffer:
-    // pod p+1's are loaded right after pod p's list walk and parked in LDS just
-    // before the pod's closing barrier, so phase A only ever reads LDS.
-    const bool has_tile = tid < n_tiles;
-    if (has_tile) {
-#pragma unroll
-        for (int j = 0; j < kTopK; ++j) S.lst[0][tid][j] = tile_keys[(size_t)tid * kTopK + j];
-        S.lsf[0][tid] = tile_flags[tid];
+    uint32_t n_misses = 0;
+    SeqCounters ctr = {0, 0, 0, 0};
+    for (uint32_t p = 0; p < n_pods; p += 2) {  // unrolled by two: the buffers never rotate
+        validate_pod<J>(S, t, n_rows, seed32, p, LA, lane, n_misses, ctr);
+        load_lists(LA, tile_keys, tile_flags, p + 2, n_pods, n_tiles, lane);
+        if (p + 1 < n_pods) {
+            validate_pod<J>(S, t, n_rows, seed32, p + 1, LB, lane, n_misses, ctr);
+            load_lists(LB, tile_keys, tile_flags, p + 3, n_pods, n_tiles, lane);
+        }
     }
-    __syncthreads();
-    uint32_t pref_row = 0xFFFFFFFFu;  // thread 0 only
-    NodeRecRegs pref_rec = {};
-    if (tid == 0 && S.spec_row[0] != 0xFFFFFFFFu) {
-        pref_row = S.spec_row[0];
-        pref_rec = load_rec(t, pref_row);
-    }
-
-    MS_STAMP(-1);
-    for (uint32_t p = 0; p < n_pods; ++p) {
-        const PodFull q = load_pod(S.pods[p], seed32);
-        MS_STAMP(5);
-        // ---- phase A: every tile's best from its speculative top-K list
-        u64 best = 0;
-        uint32_t fl = 0, n_recompute = 0;
-        for (uint32_t tt = tid; tt < n_tiles; tt += kValThreads) {
-            u64 ee[kTopK];
-            uint32_t sf;
-            if (tt == tid) {
-#pragma unroll
-                for (int j = 0; j < kTopK; ++j) ee[j] = S.lst[p & 1][tid][j];
-                sf = S.lsf[p & 1][tid];
-            } else {
-                const size_t cell = (size_t)p * n_tiles + tt;
-#pragma unroll
-                for (int j = 0; j < kTopK; ++j) ee[j] = tile_keys[cell * kTopK + j];
-                sf = tile_flags[cell];
-            }
-            u64 c = 0, r = 0;
-            bool found = false, ended = false;
-#pragma unroll
-            for (int j = 0; j < kTopK; ++j) {
-                if (!found && !ended) {
-                    const u64 ej = ee[j];
-                    if (ej == 0) {
-                        ended = true;
-                    } else {
-                        const uint32_t row = row_of_key(ej, t.base);
-                        const int sl = map_find(S, row);
-                        if (sl < 0) {
-                            c = ej;
-                            found = true;
-                        } else {
-                            uint32_t nu, nrf;
-                            r = umax64(r, eval_full(slot_row(S, sl), t.base + row, q, nu, nrf));
-                            ++n_recompute;
-                        }
-                    }
-                }
-            }
-            if (!found && !ended) {
-                const uint32_t i = atomicAdd(&S.n_need, 1u);
-                if (i < (uint32_t)kSeqBatch) S.need[i] = tt;
-                else S.n_resweep |= 0x80000000u;  // unreachable: each such tile holds K distinct touched rows
-            } else {
-                const u64 tb = umax64(c, r);
-                best = umax64(best, tb);
-                // no feasible row left in this tile: its rejections are the
-                // speculative ones plus NRF for every row a bind made infeasible
-                if (tb == 0) fl |= sf | (ee[0] != 0 ? 0x100u : 0u);
-            }
-        }
-        MS_STAMP(6);
-        if (n_recompute) atomicAdd(&S.n_recompute, n_recompute);
-        u64 nx_e[kTopK] = {0, 0, 0, 0};  // pod p+1's list, landing during phases B/C
-        uint32_t nx_sf = 0;
-        if (has_tile && p + 1 < n_pods) {
-            const size_t cell = (size_t)(p + 1) * n_tiles + tid;
-#pragma unroll
-            for (int j = 0; j < kTopK; ++j) nx_e[j] = tile_keys[cell * kTopK + j];
-            nx_sf = tile_flags[cell];
-        }
-        MS_STAMP(0);
-        {
-            const u64 wb = wave_max_u64_dpp(best);
-            const uint32_t wfl =
-                (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
-            if (lane == 0) {
-                S.wave_best[wave] = wb;
-                S.wave_fl[wave] = wfl;
-            }
-        }
-        __syncthreads();
-        MS_STAMP(1);
-        // ---- phase B: re-sweep tiles whose K listed nodes were all touched
-        const uint32_t n_need = min(S.n_need, (uint32_t)kSeqBatch);
-        if (n_need) {
-            u64 rb = 0;
-            uint32_t rfl = 0;
-            for (uint32_t i = wave; i < n_need; i += kValWaves) {
-                const uint32_t tile = S.need[i];
-#pragma unroll
-                for (int sidx = 0; sidx < kFullSlots; ++sidx) {
-                    const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + sidx;
-                    FullRow x = load_row(t, r, n_rows);
-                    if (r < n_rows) {
-                        const int sl = map_find(S, r);
-                        if (sl >= 0) x = slot_row(S, sl);
-                    }
-                    uint32_t nu, nrf;
-                    rb = umax64(rb, eval_full(x, t.base + r, q, nu, nrf));
-                    rfl |= (nu ? 1u : 0u) | (nrf ? 0x100u : 0u);
-                }
-            }
-            rb = wave_max_u64_dpp(rb);
-            const uint32_t rw =
-                (__ballot((rfl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((rfl & 0xFF00u) != 0) ? 0x100u : 0u);
-            if (lane == 0) {
-                S.wave_best[wave] = umax64(S.wave_best[wave], rb);
-                S.wave_fl[wave] |= rw;
-            }
-            __syncthreads();
-        }
-        MS_STAMP(2);
-        // ---- phase C (wave 0): reduce the 16 partials, decide, commit
-        if (wave == 0) {
-            const bool lane_part = lane < (uint32_t)kValWaves;
-            const u64 b = wave_max_u64_dpp(lane_part ? S.wave_best[lane] : 0ull);
-            const uint32_t pf = lane_part ? S.wave_fl[lane] : 0u;
-            const uint32_t f =
-                (__ballot((pf & 0xFFu) != 0) ? 1u : 0u) | (__ballot((pf & 0xFF00u) != 0) ? 0x100u : 0u);
-            if (lane == 0) {
-                ms_result res;
-                res._pad = 0;
-                res.plugin_mask = 0;
-                res.node = -1;
-                res.score = 0;
-                if (b == 0) {
-                    res.code = MS_CODE_UNSCHEDULABLE;
-                    res.plugin_mask = ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
-                                      ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
-                } else if (q.dig < 0) {
-                    res.code = MS_CODE_ERROR;
-                } else {
-                    const uint32_t node = 0xFFFFFu - (uint32_t)(b & 0xFFFFFu);
-                    res.node = (int32_t)node;
-                    res.code = MS_CODE_SUCCESS;
-                    res.score = (int64_t)(b >> 52);
-                    // assume-on-select: NodeInfo.AddPod on the winner
-                    const uint32_t row = node - t.base;
-                    const int sl = map_find(S, row);
-                    if (sl >= 0) {
-                        slot_add_pod(S, sl, q);
-                    } else if (row == pref_row) {
-                        slot_insert(S, row, pref_rec, q);
-                        ++S.n_pref_hit;
-                    } else {
-                        slot_insert(S, row, load_rec(t, row), q);
-                        ++S.n_pref_miss;
-                    }
-                }
-                S.res[p] = res;
-                S.n_resweep += n_need;
-                S.n_need = 0;
-                // prefetch the next pod's speculative winner record
-                if (p + 1 < n_pods && S.spec_row[p + 1] != 0xFFFFFFFFu && S.spec_row[p + 1] != pref_row) {
-                    pref_row = S.spec_row[p + 1];
-                    pref_rec = load_rec(t, pref_row);
-                }
-            }
-        }
-        // park pod p+1's list in the other LDS slot (read after the barrier)
-        if (has_tile && p + 1 < n_pods) {
-#pragma unroll
-            for (int j = 0; j < kTopK; ++j) S.lst[(p + 1) & 1][tid][j] = nx_e[j];
-            S.lsf[(p + 1) & 1][tid] = nx_sf;
-        }
-        MS_STAMP(3);
-        __syncthreads();
-        MS_STAMP(4);
-    }
-    if (tid == 0) {
-        atomicAdd(&stats[1], S.n_resweep & 0x7FFFFFFFu);
-        atomicAdd(&stats[2], S.n_recompute);
+    // counters, results, then the batch's modified rows
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (ctr.recompute) atomicAdd(&stats[2], ctr.recompute);
+    if (lane == 0) {
+        atomicAdd(&stats[1], ctr.resweep);
         atomicAdd(&stats[3], n_pods);
-        if (S.n_resweep & 0x80000000u) atomicOr(overflow, 2u);
-#ifdef MS_STAMPS
-        u64 *acc = reinterpret_cast<u64 *>(stats + 4);
-        for (int i = 0; i < 8; ++i) atomicAdd(&acc[i], st_acc[i]);
-        atomicAdd(&stats[20], S.n_pref_hit);
-        atomicAdd(&stats[21], S.n_pref_miss);
-#endif
+        atomicAdd(&stats[4], ctr.miss);
+        atomicAdd(&stats[5], ctr.slow);
     }
-#undef MS_STAMP
-    for (uint32_t i = tid; i < n_pods; i += kValThreads) results[i] = S.res[i];
-    // commit the batch's modified rows; the next speculative sweep is a new
-    // launch on the same stream, so it observes these stores.
-    for (uint32_t sl = tid; sl < S.n_slots; sl += kValThreads) {
-        const uint32_t r = S.row[sl];
-        t.req_cpu[r] = S.req_cpu[sl];
-        t.req_mem[r] = S.req_mem[sl];
-        t.nz_cpu[r] = S.nz_cpu[sl];
-        t.nz_mem[r] = S.nz_mem[sl];
-        t.pod_count[r] = S.cnt[sl];
+    for (uint32_t i = lane; i < n_pods; i += 64) results[i] = S.res[i];
+    for (uint32_t h = lane; h < (uint32_t)kMapCap; h += 64) {  // every touched node's record
+        const uint32_t v = S.map[h];
+        if (v == 0) continue;
+        const int64_t *r = S.rec[v & 511u];
+        const uint32_t row = (uint32_t)r[F_ROW];
+        t.req_cpu[row] = r[F_REQ_CPU];
+        t.req_mem[row] = r[F_REQ_MEM];
+        t.nz_cpu[row] = r[F_NZ_CPU];
+        t.nz_mem[row] = r[F_NZ_MEM];
+        t.pod_count[row] = (int32_t)r[F_CNT];
     }
 }
 
@@ -1216,26 +1246,37 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
-                                   uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s) {
+                                   uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
+                                   uint32_t n_tiles, hipStream_t s) {
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
     if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
     const uint32_t chunk = 16;  // pods per wave: node rows amortised, >= 16 x n_tiles waves
     const dim3 grid(gx, cdiv(n_pods, chunk));
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
-                       tile_keys, tile_flags, n_tiles);
+                       tile_keys, tile_flags, spec, spec_flags, n_tiles);
     return hipGetLastError();
 }
 
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
-                               uint32_t n_tiles, ms_result *results, uint32_t *overflow, hipStream_t s) {
+                               unsigned long long *spec, uint32_t *spec_flags, uint32_t n_tiles,
+                               ms_result *results, uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
-    if (n_pods > (uint32_t)kSeqBatch) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_validate_seq, dim3(1), dim3(kValThreads), 0, s, t, n_rows, pods, n_pods, seed32,
-                       tile_keys, tile_flags, n_tiles, results, overflow);
+    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
+#define MS_VAL(J)                                                                                          \
+    hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys, \
+                       tile_flags, spec, spec_flags, n_tiles, results, stats)
+    if (n_tiles <= 64) MS_VAL(1);
+    else if (n_tiles <= 128) MS_VAL(2);
+    else if (n_tiles <= 256) MS_VAL(4);
+    else if (n_tiles <= 512) MS_VAL(8);
+    else MS_VAL(16);
+#undef MS_VAL
     return hipGetLastError();
 }
+
+uint32_t seq_max_rows() { return 64u * kSeqMaxJ * kFullWaveTile; }
 
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
                          const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s) {

@@ -236,3 +236,29 @@ def test_chunked_batches(oracle):
     o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=6)
     with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=6, max_batch=700) as e:
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
+
+
+@pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
+def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch):
+    # speculative batch boundaries must not change placements: 50 nodes (one
+    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted)
+    monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
+    for n_nodes, n_pods in ((50, 600), (2500, 3000)):
+        seed = 11 * n_nodes + int(batch)
+        nr = synth.nodes(n_nodes, seed=seed, resources=True)
+        pr = synth.pods(n_pods, seed=seed, resources=True)
+        o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed)
+        with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed) as e:
+            assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
+            assert_table_equal(e, o["cols"], n_nodes)
+
+
+@pytest.mark.parametrize("n_nodes", [20_000, 100_000, 140_000])
+def test_resource_sequential_tile_counts(oracle, n_nodes):
+    # validator register layouts for 79, 391 and 547 tiles (2, 8 and 16 lists per lane)
+    nr = synth.nodes(n_nodes, seed=5, resources=True)
+    pr = synth.pods(1500, seed=5, resources=True)
+    o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=5)
+    with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=5) as e:
+        assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
+        assert_table_equal(e, o["cols"], n_nodes)
