@@ -54,6 +54,7 @@ struct ms_ctx {
     uint32_t *d_tile_flags = nullptr;
     unsigned long long *d_spec = nullptr;  // per-pod speculative winner key (atomicMax target)
     uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
+    unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
 
@@ -71,8 +72,9 @@ namespace {
 
 thread_local std::string g_create_err;
 
-// validator counters: u32[5] (overflow, re-swept tiles, recomputes, pods, record prefetch misses)
-constexpr size_t kStatsBytes = 32;
+// validator counters: u32[6] (overflow, re-swept tiles, recomputes, pods, speculation misses,
+// list scans), then u64[4] phase cycles in the MS_VSTAMPS diagnostic build
+constexpr size_t kStatsBytes = 96;
 
 int fail(ms_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -96,7 +98,7 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_overflow, c->d_pstream};
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_overflow, c->d_pstream};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -169,6 +171,8 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (c->d_tile_flags) (void)hipFree(c->d_tile_flags);
     if (c->d_spec) (void)hipFree(c->d_spec);
     if (c->d_spec_flags) (void)hipFree(c->d_spec_flags);
+    if (c->d_top4) (void)hipFree(c->d_top4);
+    c->d_top4 = nullptr;
     c->d_tile_keys = nullptr;
     c->d_tile_flags = nullptr;
     c->d_spec = nullptr;
@@ -183,6 +187,8 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
         return fail(c, MS_E_OOM, "sequential spec keys");
     if (hipMalloc((void **)&c->d_spec_flags, seq_batch_limit() * sizeof(uint32_t)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential spec flags");
+    if (hipMalloc((void **)&c->d_top4, seq_batch_limit() * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sequential top-4 keys");
     MS_HIP(c, hipMemsetAsync(c->d_spec, 0, seq_batch_limit() * sizeof(unsigned long long), c->stream));
     MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, seq_batch_limit() * sizeof(uint32_t), c->stream));
     MS_HIP(c, hipStreamSynchronize(c->stream));
@@ -226,8 +232,10 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
                                           c->d_spec, c->d_spec_flags, n_tiles, s));
+        MS_HIP(c, launch_topk_merge(c->d_tile_keys, nb, n_tiles, c->d_top4, s));
         MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
-                                      c->d_spec, c->d_spec_flags, n_tiles, d_res + s0, c->d_overflow, s));
+                                      c->d_spec, c->d_spec_flags, c->d_top4, n_tiles, d_res + s0, c->d_overflow,
+                                      s));
     }
     return MS_OK;
 }
@@ -350,6 +358,22 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
 
 int ms_destroy(ms_ctx *c) {
     if (!c) return MS_E_INVAL;
+#ifdef MS_VSTAMPS
+    {
+        uint32_t st[24] = {};
+        (void)hipSetDevice(c->cfg.device);
+        (void)hipStreamSynchronize(c->stream);
+        if (hipMemcpy(st, c->d_overflow, kStatsBytes, hipMemcpyDeviceToHost) == hipSuccess) {
+            const uint64_t *cy = reinterpret_cast<const uint64_t *>(st + 8);
+            std::fprintf(stderr,
+                         "MS_VSTAMPS pods=%u scans=%u misses=%u recomputes=%u resweeps=%u cycles: prologue=%llu "
+                         "fast_check=%llu scan=%llu commit=%llu loop=%llu epilogue=%llu\n",
+                         st[3], st[5], st[4], st[2], st[1], (unsigned long long)cy[0], (unsigned long long)cy[1],
+                         (unsigned long long)cy[2], (unsigned long long)cy[3], (unsigned long long)cy[4],
+                         (unsigned long long)cy[5]);
+        }
+    }
+#endif
     free_all(c);
     delete c;
     return MS_OK;

@@ -639,6 +639,52 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
 }
 
 // ----------------------------------------------------------------------------
+// Global speculative top-4 per pod, merged from the per-tile top-4 lists (one
+// wave per pod). Exact: the global rank-r entry (r < 4) is within its tile's
+// top r+1, so it is in its tile's list.
+// ----------------------------------------------------------------------------
+template <int J>
+__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys, uint32_t n_pods,
+                                                   uint32_t n_tiles, u64 *__restrict__ top) {
+    const uint32_t p = blockIdx.x, lane = threadIdx.x;
+    if (p >= n_pods) return;
+    u64 e[J][kTopK];
+    uint32_t pos[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const uint32_t tt = lane + 64u * j;
+        pos[j] = tt < n_tiles ? 0u : (uint32_t)kTopK;
+        const uint32_t tc = min(tt, n_tiles - 1);
+        const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + ((size_t)p * n_tiles + tc) * kTopK);
+        const uint4 a = q[0], b = q[1];
+        e[j][0] = ((u64)a.y << 32) | a.x;
+        e[j][1] = ((u64)a.w << 32) | a.z;
+        e[j][2] = ((u64)b.y << 32) | b.x;
+        e[j][3] = ((u64)b.w << 32) | b.z;
+    }
+    u64 out = 0;
+#pragma unroll
+    for (int r = 0; r < kTopK; ++r) {
+        u64 head = 0;  // this lane's best list head
+        int hj = -1;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            u64 h = 0;
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) h = pos[j] == (uint32_t)k ? e[j][k] : h;
+            if (h > head) {
+                head = h;
+                hj = j;
+            }
+        }
+        const u64 m = wave_max_u64_dpp(head);
+        if (lane == (uint32_t)r) out = m;
+        if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
+    }
+    if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
+}
+
+// ----------------------------------------------------------------------------
 // Exact sequential engine, in-order half: ONE wave walks the batch in queue
 // order, with no barriers. A bind only lowers keys of the node it lands on
 // (NRF feasibility and LeastAllocated are monotone in Requested/pod_count; NU,
@@ -677,10 +723,10 @@ enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALL
 struct SeqShared {
     uint32_t map[kMapCap];  // ((row + 1) << 9) | slot; 0 = empty
     int64_t rec[2 * kSeqBatch][kRecF];
-    ms_result res[kSeqBatch];
     ms_pod_rec pods[kSeqBatch];
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
     uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
+    u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
 };
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
@@ -749,28 +795,27 @@ struct TileLists {
     uint32_t f[J];
 };
 
-// Pod p's lists and flags for this lane's tiles (zeros past the batch / tiles).
+// Pod p's lists and flags for this lane's tiles. The loads are unconditional
+// from clamped (always valid) cells: a zero-fill branch for the out-of-range
+// lanes would write the load's destination registers and force the wave to
+// wait for the loads right here. Consumers skip tiles outside the lane's
+// `tiles` mask; lists of pods past the batch are never consumed.
 template <int J>
 __device__ __forceinline__ void load_lists(TileLists<J> &B, const u64 *__restrict__ tile_keys,
                                            const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_pods,
                                            uint32_t n_tiles, uint32_t lane) {
+    const uint32_t pc = min(p, n_pods - 1);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        const uint32_t tt = lane + 64u * j;
-        if (p < n_pods && tt < n_tiles) {
-            const size_t cell = (size_t)p * n_tiles + tt;
-            const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
-            const uint4 a = q[0], b = q[1];
-            B.e[j][0] = ((u64)a.y << 32) | a.x;
-            B.e[j][1] = ((u64)a.w << 32) | a.z;
-            B.e[j][2] = ((u64)b.y << 32) | b.x;
-            B.e[j][3] = ((u64)b.w << 32) | b.z;
-            B.f[j] = tile_flags[cell];
-        } else {
-#pragma unroll
-            for (int k = 0; k < kTopK; ++k) B.e[j][k] = 0;
-            B.f[j] = 0;
-        }
+        const uint32_t tt = min(lane + 64u * j, n_tiles - 1);
+        const size_t cell = (size_t)pc * n_tiles + tt;
+        const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
+        const uint4 a = q[0], b = q[1];
+        B.e[j][0] = ((u64)a.y << 32) | a.x;
+        B.e[j][1] = ((u64)a.w << 32) | a.z;
+        B.e[j][2] = ((u64)b.y << 32) | b.x;
+        B.e[j][3] = ((u64)b.w << 32) | b.z;
+        B.f[j] = tile_flags[cell];
     }
 }
 
@@ -785,14 +830,15 @@ constexpr int kFreshSlot = 0x10000;  // wslot flag: pod's own speculative slot, 
 // LDS slot if it is a touched node.
 template <int J>
 __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, uint32_t n_rows, const PodFull &q,
-                                              const TileLists<J> &B, uint32_t lane, SeqCounters &ctr, u64 &b_out,
-                                              int &wslot_out) {
+                                              const TileLists<J> &B, uint32_t tiles, uint32_t lane, SeqCounters &ctr,
+                                              u64 &b_out, int &wslot_out) {
+    // (B was loaded on entry to the slow path: ~6% of config E's pods need it)
     // ---- every head's first map probe, issued together
     uint32_t hrow[J], hv[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         hrow[j] = row_of_key(B.e[j][0], t.base);
-        hv[j] = B.e[j][0] ? S.map[map_hash(hrow[j])] : 0u;
+        hv[j] = (((tiles >> j) & 1u) && B.e[j][0]) ? S.map[map_hash(hrow[j])] : 0u;
     }
     // ---- every tile's best: first untouched list entry, touched ones re-evaluated
     u64 best = 0;
@@ -800,7 +846,7 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
     uint32_t need = 0;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-        if (B.e[j][0] == 0) continue;  // no feasible row in this tile at speculation (or no tile)
+        if (!((tiles >> j) & 1u) || B.e[j][0] == 0) continue;  // no tile, or no feasible row at speculation
         int sl = map_resolve(S, hrow[j], hv[j]);
         if (sl < 0) {  // untouched head: exact, and the tile's best
             if (B.e[j][0] > best) {
@@ -868,104 +914,68 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
     wslot_out = own ? __builtin_amdgcn_readlane(best_slot, (int)__builtin_ctzll(own)) : -1;
 }
 
-// Result of pod p from its winner key b (0: FitError), and the bind.
-template <int J>
-__device__ __forceinline__ void commit_pod(SeqShared &S, const NodeTable &t, const PodFull &q, uint32_t p,
-                                           const TileLists<J> &B, uint32_t lane, uint32_t &n_misses, SeqCounters &ctr,
-                                           u64 b, int wslot) {
-    ms_result res;
-    res._pad = 0;
-    res.plugin_mask = 0;
-    res.node = -1;
-    res.score = 0;
-    if (b == 0) {  // FitError
-        uint32_t f;
-        if (S.spec_key[p] == 0) {
-            f = S.spec_flags[p];  // every tile was infeasible at speculation: their flags, OR-ed by the sweep
-        } else {  // per tile: speculative flags, + NRF if its feasible rows were all bound away
-            uint32_t fl = 0;
-#pragma unroll
-            for (int j = 0; j < J; ++j) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
-            f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
-        }
-        res.code = MS_CODE_UNSCHEDULABLE;
-        res.plugin_mask =
-            ((f & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) | ((f & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
-    } else if (q.dig < 0) {
-        res.code = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
-    } else {
-        const uint32_t node = 0xFFFFFu - (uint32_t)(b & 0xFFFFFu);
-        res.node = (int32_t)node;
-        res.code = MS_CODE_SUCCESS;
-        res.score = (int64_t)(b >> 52);
-        // assume-on-select: NodeInfo.AddPod on the winner's LDS record
-        const uint32_t row = node - t.base;
-        int sl = wslot;
-        if (sl < 0) {  // untouched winner other than the speculative one: load its record
-            sl = kSeqBatch + (int)n_misses++;
-            ++ctr.miss;
-            int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
-            const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
-            if (lane == (uint32_t)F_ROW) v = row;
-            if (lane == (uint32_t)F_INV_CPU) v = __double_as_longlong(recip(capc));
-            if (lane == (uint32_t)F_INV_MEM) v = __double_as_longlong(recip(capm));
-            if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
-            sl |= kFreshSlot;
-        }
-        if (sl & kFreshSlot) {  // first bind on this node in the batch: map it
-            sl &= ~kFreshSlot;
-            if (lane == 0) {
-                uint32_t h = map_hash(row);
-                while (S.map[h] != 0) h = (h + 1) & (kMapCap - 1);
-                S.map[h] = ((row + 1) << 9) | (uint32_t)sl;
-            }
-        }
-        int64_t add = 0;
-        switch (lane) {
-            case F_REQ_CPU: add = q.rc; break;
-            case F_REQ_MEM: add = q.rm; break;
-            case F_NZ_CPU: add = q.nc; break;
-            case F_NZ_MEM: add = q.nm; break;
-            case F_CNT: add = 1; break;
-            default: break;
-        }
-        if (add) atomicAdd(reinterpret_cast<unsigned long long *>(&S.rec[sl][lane]), (unsigned long long)add);
+// Deferred bind effects of a 64-pod group, lane i <-> pod i of the group:
+//  prow/pslot: the (row, slot) map entry of a node pod i bound first in the batch;
+//  padd: the slot pod i bound to, whose record still lacks pod i's NodeInfo.AddPod.
+// Applied (all lanes at once) before anything reads the map or the records: a
+// list scan, the next group's touched check, the write-back.
+__device__ __forceinline__ void flush_pending(SeqShared &S, uint32_t &prow, uint32_t pslot, int &padd,
+                                              const ms_pod_rec &mypod) {
+    if (prow != 0xFFFFFFFFu) {
+        uint32_t h = map_hash(prow);
+        const uint32_t v = ((prow + 1) << 9) | pslot;
+        while (atomicCAS(&S.map[h], 0u, v) != 0u) h = (h + 1) & (kMapCap - 1);
+        prow = 0xFFFFFFFFu;
     }
-    if (lane == 0) S.res[p] = res;
+    if (padd >= 0) {  // Requested += req, NonZeroRequested += nz, pod_count += 1
+        unsigned long long *r = reinterpret_cast<unsigned long long *>(S.rec[padd]);
+        atomicAdd(&r[F_REQ_CPU], (unsigned long long)mypod.req_milli_cpu);
+        atomicAdd(&r[F_REQ_MEM], (unsigned long long)mypod.req_memory);
+        atomicAdd(&r[F_NZ_CPU], (unsigned long long)mypod.nonzero_milli_cpu);
+        atomicAdd(&r[F_NZ_MEM], (unsigned long long)mypod.nonzero_memory);
+        atomicAdd(&r[F_CNT], 1ull);
+        padd = -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 }
 
-// One pod of the in-order walk (all 64 lanes).
-template <int J>
-__device__ __forceinline__ void validate_pod(SeqShared &S, const NodeTable &t, uint32_t n_rows, uint32_t seed32,
-                                             uint32_t p, const TileLists<J> &B, uint32_t lane, uint32_t &n_misses,
-                                             SeqCounters &ctr) {
-    const PodFull q = load_pod(S.pods[p], seed32);
-    // ---- fast path: every current key is <= its speculative key, so an
-    // untouched speculative winner is still the exact winner
-    // (slot p holds that node's batch-start record, so it becomes its slot)
-    const u64 sk = S.spec_key[p];
-    u64 b;
-    int wslot;
-    if (sk == 0) {  // no feasible row at speculation: none now either (FitError)
-        b = 0;
-        wslot = -1;
-    } else if (map_find(S, row_of_key(sk, t.base)) < 0) {
-        b = sk;
-        wslot = (int)p | kFreshSlot;
-    } else {
-        ++ctr.slow;
-        validate_scan<J>(S, t, n_rows, q, B, lane, ctr, b, wslot);
-    }
-    commit_pod<J>(S, t, q, p, B, lane, n_misses, ctr, b, wslot);
+__device__ __forceinline__ u64 readlane_u64(u64 v, uint32_t l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+    return ((u64)hi << 32) | lo;
 }
+
+// Diagnostic build only (make vstamps): cycles per validator phase, summed
+// over the batch, land in stats[8..] (u64), printed at ms_destroy.
+#ifdef MS_VSTAMPS
+struct VStamps {
+    u64 prev, acc[6];
+};
+#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0}};
+#define MS_VST(i)                                               \
+    do {                                                        \
+        __builtin_amdgcn_sched_barrier(0);                      \
+        const u64 vst_now = __builtin_amdgcn_s_memtime();       \
+        vst.acc[i] += vst_now - vst.prev;                       \
+        vst.prev = vst_now;                                     \
+        __builtin_amdgcn_sched_barrier(0);                      \
+    } while (0)
+#else
+#define MS_VST_DECL
+#define MS_VST(i) \
+    do {          \
+    } while (0)
+#endif
 
 template <int J>  // tile lists per lane: n_tiles <= 64 * J
 __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_rows,
                                                      const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
                                                      uint32_t seed32, const u64 *__restrict__ tile_keys,
                                                      const uint32_t *__restrict__ tile_flags, u64 *__restrict__ spec,
-                                                     uint32_t *__restrict__ spec_flags, uint32_t n_tiles,
-                                                     ms_result *__restrict__ results, uint32_t *__restrict__ stats) {
+                                                     uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
+                                                     uint32_t n_tiles, ms_result *__restrict__ results,
+                                                     uint32_t *__restrict__ stats) {
     // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
     //        [4] speculation misses (records loaded), [5] pods that needed the list scan
     __shared__ SeqShared S;
@@ -974,10 +984,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         if (lane == 0) atomicOr(&stats[0], 1u);
         return;
     }
-    // the first two pods' lists are in flight while the prologue runs
-    TileLists<J> LA, LB;
-    load_lists(LA, tile_keys, tile_flags, 0, n_pods, n_tiles, lane);
-    load_lists(LB, tile_keys, tile_flags, 1, n_pods, n_tiles, lane);
+    MS_VST_DECL
     // prologue: touched map, pods, speculative winners and their batch-start records (slot p)
     for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map[i] = 0;
     for (uint32_t i = lane; i < n_pods; i += 64) {
@@ -985,6 +992,8 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         const u64 sk = spec[i];
         S.spec_key[i] = sk;
         S.spec_flags[i] = spec_flags[i];
+#pragma unroll
+        for (int k = 0; k < kTopK; ++k) S.top4[i][k] = top4[(size_t)i * kTopK + k];
         spec[i] = 0;  // the next batch's sweep accumulates here again
         spec_flags[i] = 0;
         if (sk) {
@@ -999,20 +1008,140 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-
-    uint32_t n_misses = 0;
+    uint32_t n_misses = 0, tiles = 0;  // tiles: bit j <=> this lane owns tile lane + 64 j
+#pragma unroll
+    for (int j = 0; j < J; ++j) tiles |= (lane + 64u * j < n_tiles) ? 1u << j : 0u;
     SeqCounters ctr = {0, 0, 0, 0};
-    for (uint32_t p = 0; p < n_pods; p += 2) {  // unrolled by two: the buffers never rotate
-        validate_pod<J>(S, t, n_rows, seed32, p, LA, lane, n_misses, ctr);
-        load_lists(LA, tile_keys, tile_flags, p + 2, n_pods, n_tiles, lane);
-        if (p + 1 < n_pods) {
-            validate_pod<J>(S, t, n_rows, seed32, p + 1, LB, lane, n_misses, ctr);
-            load_lists(LB, tile_keys, tile_flags, p + 3, n_pods, n_tiles, lane);
+    MS_VST(0);
+
+    // Pods go in groups of 64, lane i <-> pod g+i. A pod whose speculative
+    // winner is untouched binds there (exact: current keys never exceed their
+    // speculative ones); `touched` marks the group's pods whose speculative
+    // winner row was bound earlier in the batch: by an earlier group (map
+    // probe at group start) or earlier in this group (ballot at each bind).
+    for (uint32_t g = 0; g < n_pods; g += 64) {
+        const uint32_t gn = min(64u, n_pods - g);
+        const bool mine = lane < gn;
+        const uint32_t pl = g + (mine ? lane : 0u);
+        const u64 sk_l = mine ? S.spec_key[pl] : 0ull;
+        const uint32_t srow_l = sk_l ? row_of_key(sk_l, t.base) : 0xFFFFFFFEu;  // ~1: matches no row
+        const int dig_l = mine ? (int)S.pods[pl].name_digit : 0;
+        u64 touched = __ballot(sk_l != 0 && map_find(S, srow_l) >= 0);
+        uint32_t prow = 0xFFFFFFFFu, pslot = 0;  // this lane's pending map insert
+        int padd = -1;                           // and pending AddPod (flush_pending)
+        const ms_pod_rec &mypod = S.pods[pl];
+        uint32_t rk_lo = 0, rk_hi = 0, rinfo = 0;  // this lane's pod: winner key, code | plugin mask << 8
+        MS_VST(1);
+        for (uint32_t i = 0; i < gn; ++i) {
+            const uint32_t p = g + i;
+            const u64 sk = readlane_u64(sk_l, i);
+            u64 b = 0;
+            int wslot = -1;
+            uint32_t fmask = 0;  // filter flags for a FitError
+            if (sk == 0) {  // no feasible row at speculation: none now either
+                fmask = S.spec_flags[p];
+            } else if (!((touched >> i) & 1u)) {
+                b = sk;
+                wslot = (int)p | kFreshSlot;
+            } else {  // the speculative winner was bound earlier in the batch
+                ++ctr.slow;
+                MS_VST(2);
+                flush_pending(S, prow, pslot, padd, mypod);
+                const PodFull q = load_pod(S.pods[p], seed32);
+                // global top-4 (lanes 0-3): touched entries are re-evaluated, the first
+                // untouched one is exact and bounds every row below it
+                const u64 e = lane < (uint32_t)kTopK ? S.top4[p][lane] : 0ull;
+                const int esl = e ? map_find(S, row_of_key(e, t.base)) : -1;
+                const u64 untouched = __ballot(e != 0 && esl < 0);
+                const u64 present = __ballot(e != 0);
+                bool scan = false;
+                if (untouched || __builtin_popcountll(present) < kTopK) {
+                    const uint32_t f = untouched ? (uint32_t)__builtin_ctzll(untouched) : (uint32_t)kTopK;
+                    u64 v = 0;
+                    int vs = -1;
+                    if (lane < f && e != 0) {
+                        uint32_t nu, nrf;
+                        v = eval_full(slot_row(S, esl), row_of_key(e, t.base) + t.base, q, nu, nrf);
+                        vs = esl;
+                        ++ctr.recompute;
+                    } else if (lane == f) {
+                        v = e;
+                    }
+                    b = wave_max_u64_dpp(v);
+                    const u64 own = __ballot(b != 0 && v == b);
+                    wslot = own ? __builtin_amdgcn_readlane(vs, (int)__builtin_ctzll(own)) : -1;
+                    scan = b == 0;  // FitError: its plugin mask needs the tiles' flags
+                } else {
+                    scan = true;  // all four touched: rows below them are unknown
+                }
+                TileLists<J> B;
+                if (scan) {
+                    load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
+                    validate_scan<J>(S, t, n_rows, q, B, tiles, lane, ctr, b, wslot);
+                }
+                if (b == 0) {  // per tile: speculative flags, + NRF if its feasible rows were all bound away
+                    uint32_t fl = 0;
+#pragma unroll
+                    for (int j = 0; j < J; ++j)
+                        if ((tiles >> j) & 1u) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
+                    fmask = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+                }
+                MS_VST(3);
+            }
+            uint32_t info;
+            if (b == 0) {
+                info = MS_CODE_UNSCHEDULABLE | ((((fmask & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                                                 ((fmask & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u))
+                                                << 8);
+            } else if (__builtin_amdgcn_readlane(dig_l, (int)i) < 0) {
+                info = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
+            } else {
+                info = MS_CODE_SUCCESS;
+                // assume-on-select: NodeInfo.AddPod on the winner's LDS record
+                const uint32_t row = row_of_key(b, t.base);
+                int sl = wslot;
+                if (sl < 0) {  // untouched winner other than the speculative one: load its record
+                    sl = kSeqBatch + (int)n_misses++;
+                    ++ctr.miss;
+                    int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
+                    const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
+                    if (lane == (uint32_t)F_ROW) v = row;
+                    if (lane == (uint32_t)F_INV_CPU) v = __double_as_longlong(recip(capc));
+                    if (lane == (uint32_t)F_INV_MEM) v = __double_as_longlong(recip(capm));
+                    if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
+                    sl |= kFreshSlot;
+                }
+                const bool fresh = (sl & kFreshSlot) != 0;  // first bind on this node in the batch
+                sl &= ~kFreshSlot;
+                if (lane == i) {  // map entry (if fresh) and AddPod, both deferred
+                    if (fresh) {
+                        prow = row;
+                        pslot = (uint32_t)sl;
+                    }
+                    padd = sl;
+                }
+                touched |= __ballot(srow_l == row);  // later pods of the group that speculated on it
+            }
+            rk_lo = writelane(rk_lo, (uint32_t)b, i);
+            rk_hi = writelane(rk_hi, (uint32_t)(b >> 32), i);
+            rinfo = writelane(rinfo, info, i);
+            MS_VST(4);
         }
+        flush_pending(S, prow, pslot, padd, mypod);
+        if (mine) {  // this lane's pod result
+            const u64 k = ((u64)rk_hi << 32) | rk_lo;
+            ms_result r;
+            r._pad = 0;
+            r.code = (int32_t)(rinfo & 0xFFu);
+            r.plugin_mask = rinfo >> 8;
+            const bool ok = r.code == MS_CODE_SUCCESS;
+            r.node = ok ? (int32_t)(0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) : -1;
+            r.score = ok ? (int64_t)(k >> 52) : 0;
+            results[pl] = r;
+        }
+        MS_VST(1);
     }
-    // counters, results, then the batch's modified rows
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    // counters, then every touched node's record goes back to the table
     if (ctr.recompute) atomicAdd(&stats[2], ctr.recompute);
     if (lane == 0) {
         atomicAdd(&stats[1], ctr.resweep);
@@ -1020,8 +1149,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         atomicAdd(&stats[4], ctr.miss);
         atomicAdd(&stats[5], ctr.slow);
     }
-    for (uint32_t i = lane; i < n_pods; i += 64) results[i] = S.res[i];
-    for (uint32_t h = lane; h < (uint32_t)kMapCap; h += 64) {  // every touched node's record
+    for (uint32_t h = lane; h < (uint32_t)kMapCap; h += 64) {
         const uint32_t v = S.map[h];
         if (v == 0) continue;
         const int64_t *r = S.rec[v & 511u];
@@ -1032,6 +1160,11 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         t.nz_mem[row] = r[F_NZ_MEM];
         t.pod_count[row] = (int32_t)r[F_CNT];
     }
+#ifdef MS_VSTAMPS
+    MS_VST(5);
+    if (lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i, vst.acc[i]);
+#endif
 }
 
 // ----------------------------------------------------------------------------
@@ -1260,19 +1393,33 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
-                               unsigned long long *spec, uint32_t *spec_flags, uint32_t n_tiles,
-                               ms_result *results, uint32_t *stats, hipStream_t s) {
+                               unsigned long long *spec, uint32_t *spec_flags, const unsigned long long *top4,
+                               uint32_t n_tiles, ms_result *results, uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
 #define MS_VAL(J)                                                                                          \
     hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys, \
-                       tile_flags, spec, spec_flags, n_tiles, results, stats)
+                       tile_flags, spec, spec_flags, top4, n_tiles, results, stats)
     if (n_tiles <= 64) MS_VAL(1);
     else if (n_tiles <= 128) MS_VAL(2);
     else if (n_tiles <= 256) MS_VAL(4);
     else if (n_tiles <= 512) MS_VAL(8);
     else MS_VAL(16);
 #undef MS_VAL
+    return hipGetLastError();
+}
+
+hipError_t launch_topk_merge(const unsigned long long *tile_keys, uint32_t n_pods, uint32_t n_tiles,
+                             unsigned long long *top, hipStream_t s) {
+    if (n_pods == 0 || n_tiles == 0) return hipSuccess;
+    if (n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
+#define MS_MERGE(J) hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, n_pods, n_tiles, top)
+    if (n_tiles <= 64) MS_MERGE(1);
+    else if (n_tiles <= 128) MS_MERGE(2);
+    else if (n_tiles <= 256) MS_MERGE(4);
+    else if (n_tiles <= 512) MS_MERGE(8);
+    else MS_MERGE(16);
+#undef MS_MERGE
     return hipGetLastError();
 }
 
