@@ -55,6 +55,12 @@ struct ms_ctx {
     unsigned long long *d_spec = nullptr;  // per-pod speculative winner key (atomicMax target)
     uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
     unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
+    uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
+    // pipelined sequential engine: batch k+1's speculation (seq_stream) runs
+    // while batch k validates (caller stream); every buffer above is double-
+    // buffered by batch parity
+    hipStream_t seq_stream = nullptr;
+    hipEvent_t ev_swept[2] = {nullptr, nullptr}, ev_valid[2] = {nullptr, nullptr}, ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
 
@@ -98,13 +104,22 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_overflow, c->d_pstream};
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
     if (c->pstream_ev) (void)hipEventDestroy(c->pstream_ev);
+    for (int i = 0; i < 2; ++i) {
+        if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
+        if (c->ev_valid[i]) (void)hipEventDestroy(c->ev_valid[i]);
+    }
+    if (c->ev_seq) (void)hipEventDestroy(c->ev_seq);
+    if (c->seq_stream) {
+        (void)hipStreamSynchronize(c->seq_stream);
+        (void)hipStreamDestroy(c->seq_stream);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -165,32 +180,38 @@ int order_after_ctx_stream(ms_ctx *c, hipStream_t s) {
     return MS_OK;
 }
 
+// Sequential-engine scratch for n_tiles tiles, two batches deep (pipelining).
 int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
+    if (!c->seq_stream) {
+        MS_HIP(c, hipStreamCreateWithFlags(&c->seq_stream, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i) {
+            MS_HIP(c, hipEventCreateWithFlags(&c->ev_swept[i], hipEventDisableTiming));
+            MS_HIP(c, hipEventCreateWithFlags(&c->ev_valid[i], hipEventDisableTiming));
+        }
+        MS_HIP(c, hipEventCreateWithFlags(&c->ev_seq, hipEventDisableTiming));
+    }
     if (n_tiles <= c->tile_cap) return MS_OK;
-    if (c->d_tile_keys) (void)hipFree(c->d_tile_keys);
-    if (c->d_tile_flags) (void)hipFree(c->d_tile_flags);
-    if (c->d_spec) (void)hipFree(c->d_spec);
-    if (c->d_spec_flags) (void)hipFree(c->d_spec_flags);
-    if (c->d_top4) (void)hipFree(c->d_top4);
-    c->d_top4 = nullptr;
+    MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
+    void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev};
+    for (void *q : old)
+        if (q) (void)hipFree(q);
     c->d_tile_keys = nullptr;
     c->d_tile_flags = nullptr;
     c->d_spec = nullptr;
     c->d_spec_flags = nullptr;
+    c->d_top4 = nullptr;
+    c->d_prev = nullptr;
     c->tile_cap = 0;
-    const size_t n = (size_t)seq_batch_limit() * n_tiles;
-    if (hipMalloc((void **)&c->d_tile_keys, n * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
-        return fail(c, MS_E_OOM, "sequential tile keys");
-    if (hipMalloc((void **)&c->d_tile_flags, n * sizeof(uint32_t)) != hipSuccess)
-        return fail(c, MS_E_OOM, "sequential tile flags");
-    if (hipMalloc((void **)&c->d_spec, seq_batch_limit() * sizeof(unsigned long long)) != hipSuccess)
-        return fail(c, MS_E_OOM, "sequential spec keys");
-    if (hipMalloc((void **)&c->d_spec_flags, seq_batch_limit() * sizeof(uint32_t)) != hipSuccess)
-        return fail(c, MS_E_OOM, "sequential spec flags");
-    if (hipMalloc((void **)&c->d_top4, seq_batch_limit() * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
-        return fail(c, MS_E_OOM, "sequential top-4 keys");
-    MS_HIP(c, hipMemsetAsync(c->d_spec, 0, seq_batch_limit() * sizeof(unsigned long long), c->stream));
-    MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, seq_batch_limit() * sizeof(uint32_t), c->stream));
+    const size_t B = seq_batch_limit(), n = 2 * B * n_tiles;
+    if (hipMalloc((void **)&c->d_tile_keys, n * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&c->d_tile_flags, n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_spec, 2 * B * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&c->d_spec_flags, 2 * B * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_top4, 2 * B * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&c->d_prev, 2 * (B + 1) * sizeof(uint32_t)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sequential-engine scratch");
+    MS_HIP(c, hipMemsetAsync(c->d_spec, 0, 2 * B * sizeof(unsigned long long), c->stream));
+    MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, 2 * B * sizeof(uint32_t), c->stream));
     MS_HIP(c, hipStreamSynchronize(c->stream));
     c->tile_cap = n_tiles;
     return MS_OK;
@@ -224,18 +245,41 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
     int rc = ensure_tiles(c, n_tiles);
     if (rc) return rc;
-    // the sequential scratch (tile lists, spec keys) was last used on the context stream
-    rc = order_after_ctx_stream(c, s);
-    if (rc) return rc;
-    const uint32_t B = seq_batch(c);
-    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
-        const uint32_t nb = std::min(B, n_pods - s0);
-        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
-                                          c->d_spec, c->d_spec_flags, n_tiles, s));
-        MS_HIP(c, launch_topk_merge(c->d_tile_keys, nb, n_tiles, c->d_top4, s));
-        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, c->d_tile_keys, c->d_tile_flags,
-                                      c->d_spec, c->d_spec_flags, c->d_top4, n_tiles, d_res + s0, c->d_overflow,
-                                      s));
+    // Batch k: speculative sweep + top-4 merge on seq_stream into buffer k&1, after
+    // validation k-2 (which last read that buffer, and whose binds the sweep must
+    // see); validation k on s after sweep k. Validation k marks the nodes batch k-1
+    // bound as touched (prev rows): sweep k may have run concurrently with it.
+    MS_HIP(c, hipEventRecord(c->ev_seq, s));
+    MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_seq, 0));
+    const uint32_t B = seq_batch(c), SB = seq_batch_limit();
+    static const bool pipe = [] {
+        const char *e = getenv("MINISCHED_SEQ_PIPE");
+        return !e || atoi(e) != 0;
+    }();
+    uint32_t k = 0;
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
+        const uint32_t nb = std::min(B, n_pods - s0), par = k & 1u;
+        const size_t cells = (size_t)SB * n_tiles * par;
+        unsigned long long *tk = c->d_tile_keys + cells * seq_topk();
+        uint32_t *tf = c->d_tile_flags + cells;
+        unsigned long long *sp = c->d_spec + SB * par, *top = c->d_top4 + (size_t)SB * seq_topk() * par;
+        uint32_t *sf = c->d_spec_flags + SB * par;
+        if (k >= (pipe ? 2u : 1u)) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[pipe ? par : par ^ 1u], 0));
+        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, n_tiles,
+                                          c->seq_stream));
+        MS_HIP(c, launch_topk_merge(tk, nb, n_tiles, top, c->seq_stream));
+        MS_HIP(c, hipEventRecord(c->ev_swept[par], c->seq_stream));
+        MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[par], 0));
+        const uint32_t *prev_in = (pipe && k) ? c->d_prev + (SB + 1) * (par ^ 1u) : nullptr;
+        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, n_tiles, prev_in,
+                                      c->d_prev + (SB + 1) * par, d_res + s0, c->d_overflow, s));
+        MS_HIP(c, hipEventRecord(c->ev_valid[par], s));
+    }
+    // later deltas and calls (on any stream) order after the context stream:
+    // chain it after this call's last validation
+    if (s != c->stream) {
+        MS_HIP(c, hipEventRecord(c->ev_seq, s));
+        MS_HIP(c, hipStreamWaitEvent(c->stream, c->ev_seq, 0));
     }
     return MS_OK;
 }

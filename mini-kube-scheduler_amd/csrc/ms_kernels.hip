@@ -707,11 +707,13 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
 // Results and records stay in LDS until the batch ends.
 // ----------------------------------------------------------------------------
 constexpr int kSeqBatch = 256;  // pods per speculative batch (host clamps)
-constexpr int kMapBits = 10;
-constexpr int kMapCap = 1 << kMapBits;  // 4 x slots: the first probe nearly always decides
+constexpr int kMapBits = 11;
+constexpr int kMapCap = 1 << kMapBits;  // >= 4 x the nodes a batch and its predecessor bind
 constexpr int kSeqMaxJ = 16;            // tile lists per lane in registers: n_tiles <= 1024 (262k rows)
 constexpr int kRecF = 12;               // record fields per slot (see RecField)
 constexpr int kSpecF = 9;               // fields loaded from the node table (F_REQ_CPU .. F_FD)
+constexpr int kClaimBits = 12;          // claim table: 64 lanes in 4096 buckets, ~0.8% false conflicts
+constexpr int kClaimCap = 1 << kClaimBits;
 
 // LDS record of a touched node, one i64 (or f64 bit pattern) per field
 enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALLOC_MEM, F_CNT, F_ALLOWED, F_FD,
@@ -719,17 +721,24 @@ enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALL
 
 // Slots: rec[p] for p < kSeqBatch is pod p's speculative winner's record,
 // loaded at batch start (it becomes that node's live record when pod p binds
-// there first); rec[kSeqBatch + i] are records loaded on a speculation miss.
+// there first); rec[kSeqBatch + i] are records loaded on a speculation miss;
+// rec[2*kSeqBatch + i] are the nodes the previous batch bound (pipelined
+// mode: this batch's speculation may predate those binds).
 struct SeqShared {
-    uint32_t map[kMapCap];  // ((row + 1) << 9) | slot; 0 = empty
-    int64_t rec[2 * kSeqBatch][kRecF];
+    uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
+    int64_t rec[3 * kSeqBatch][kRecF];
+    uint8_t bound[3 * kSeqBatch];  // slot was bound in this batch
+    uint32_t n_out;
     ms_pod_rec pods[kSeqBatch];
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
     uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
     u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
+    uint32_t claim[kClaimCap];       // per round: lowest lane whose speculative winner hashes here
 };
+static_assert(sizeof(SeqShared) <= 160 * 1024, "validator LDS");
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
+__device__ __forceinline__ uint32_t claim_hash(uint32_t row) { return (row * 0x85EBCA6Bu) >> (32 - kClaimBits); }
 
 // slot of row in the touched-node map, -1 if untouched, continuing a probe
 // whose first read returned v (load factor <= 1/4)
@@ -738,7 +747,7 @@ __device__ __forceinline__ int map_resolve(const SeqShared &S, uint32_t row, uin
     const uint32_t key = row + 1;
     for (;;) {
         if (v == 0) return -1;
-        if ((v >> 9) == key) return (int)(v & 511u);
+        if ((v >> 10) == key) return (int)(v & 1023u);
         h = (h + 1) & (kMapCap - 1);
         v = S.map[h];
     }
@@ -823,7 +832,6 @@ struct SeqCounters {
     uint32_t recompute, resweep, miss, slow;
 };
 
-constexpr int kFreshSlot = 0x10000;  // wslot flag: pod's own speculative slot, not yet in the map
 
 // Full scan of pod p's tile lists (the speculative winner was touched, or
 // the pod had no feasible row at speculation): b = winner key, wslot = its
@@ -923,7 +931,7 @@ __device__ __forceinline__ void flush_pending(SeqShared &S, uint32_t &prow, uint
                                               const ms_pod_rec &mypod) {
     if (prow != 0xFFFFFFFFu) {
         uint32_t h = map_hash(prow);
-        const uint32_t v = ((prow + 1) << 9) | pslot;
+        const uint32_t v = ((prow + 1) << 10) | pslot;
         while (atomicCAS(&S.map[h], 0u, v) != 0u) h = (h + 1) & (kMapCap - 1);
         prow = 0xFFFFFFFFu;
     }
@@ -934,6 +942,7 @@ __device__ __forceinline__ void flush_pending(SeqShared &S, uint32_t &prow, uint
         atomicAdd(&r[F_NZ_CPU], (unsigned long long)mypod.nonzero_milli_cpu);
         atomicAdd(&r[F_NZ_MEM], (unsigned long long)mypod.nonzero_memory);
         atomicAdd(&r[F_CNT], 1ull);
+        S.bound[padd] = 1;
         padd = -1;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -974,10 +983,13 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                                                      uint32_t seed32, const u64 *__restrict__ tile_keys,
                                                      const uint32_t *__restrict__ tile_flags, u64 *__restrict__ spec,
                                                      uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
-                                                     uint32_t n_tiles, ms_result *__restrict__ results,
+                                                     uint32_t n_tiles, const uint32_t *__restrict__ prev_in,
+                                                     uint32_t *__restrict__ prev_out, ms_result *__restrict__ results,
                                                      uint32_t *__restrict__ stats) {
     // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
-    //        [4] speculation misses (records loaded), [5] pods that needed the list scan
+    //        [4] speculation misses (records loaded), [5] pods whose speculative winner was touched
+    // prev_in/prev_out: {count, rows...} of the nodes the previous / this batch bound
+    // (prev_in null when the sweep of this batch saw every earlier bind).
     __shared__ SeqShared S;
     const uint32_t lane = threadIdx.x;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
@@ -987,6 +999,26 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     MS_VST_DECL
     // prologue: touched map, pods, speculative winners and their batch-start records (slot p)
     for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map[i] = 0;
+    for (uint32_t i = lane; i < 3u * kSeqBatch; i += 64) S.bound[i] = 0;
+    for (uint32_t i = lane; i < (uint32_t)kClaimCap; i += 64) S.claim[i] = ~0u;
+    if (lane == 0) S.n_out = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // nodes the previous batch bound are "touched" here: this batch's speculation
+    // may have read them before or during that batch's write-back
+    const uint32_t n_prev = prev_in ? min(prev_in[0], (uint32_t)kSeqBatch) : 0u;
+    for (uint32_t i = lane; i < n_prev; i += 64) {
+        const uint32_t r = prev_in[1 + i];
+        const uint32_t sl = 2u * kSeqBatch + i;
+        int64_t *rec = S.rec[sl];
+#pragma unroll
+        for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
+        rec[F_ROW] = r;
+        rec[F_INV_CPU] = __double_as_longlong(recip(rec[F_ALLOC_CPU]));
+        rec[F_INV_MEM] = __double_as_longlong(recip(rec[F_ALLOC_MEM]));
+        uint32_t h = map_hash(r);
+        while (atomicCAS(&S.map[h], 0u, ((r + 1) << 10) | sl) != 0u) h = (h + 1) & (kMapCap - 1);
+    }
     for (uint32_t i = lane; i < n_pods; i += 64) {
         S.pods[i] = pods[i];
         const u64 sk = spec[i];
@@ -1014,93 +1046,118 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     SeqCounters ctr = {0, 0, 0, 0};
     MS_VST(0);
 
-    // Pods go in groups of 64, lane i <-> pod g+i. A pod whose speculative
-    // winner is untouched binds there (exact: current keys never exceed their
-    // speculative ones); `touched` marks the group's pods whose speculative
-    // winner row was bound earlier in the batch: by an earlier group (map
-    // probe at group start) or earlier in this group (ballot at each bind).
+    // Pods go in groups of 64, lane i <-> pod g+i, decided in rounds. A round
+    // takes the group's undecided pods i0.. in parallel: the first one whose
+    // speculative winner is touched (in the map: bound earlier in the batch) or
+    // is claimed by an earlier undecided pod (hash claim; collisions only make
+    // false conflicts) is the round's slow pod s. Pods i0..s-1 take their
+    // speculative outcome, exact (current keys never exceed speculative ones and
+    // their winners are distinct and untouched) and bind at once; pod s is
+    // resolved alone against current state; the next round starts at s+1.
     for (uint32_t g = 0; g < n_pods; g += 64) {
         const uint32_t gn = min(64u, n_pods - g);
         const bool mine = lane < gn;
         const uint32_t pl = g + (mine ? lane : 0u);
         const u64 sk_l = mine ? S.spec_key[pl] : 0ull;
-        const uint32_t srow_l = sk_l ? row_of_key(sk_l, t.base) : 0xFFFFFFFEu;  // ~1: matches no row
+        const uint32_t srow_l = sk_l ? row_of_key(sk_l, t.base) : 0xFFFFFFFEu;
         const int dig_l = mine ? (int)S.pods[pl].name_digit : 0;
-        u64 touched = __ballot(sk_l != 0 && map_find(S, srow_l) >= 0);
+        const bool binds_l = sk_l != 0 && dig_l >= 0;  // binds at its speculative winner if that is exact
+        const uint32_t ch = claim_hash(srow_l);
+        const ms_pod_rec &mypod = S.pods[pl];
         uint32_t prow = 0xFFFFFFFFu, pslot = 0;  // this lane's pending map insert
         int padd = -1;                           // and pending AddPod (flush_pending)
-        const ms_pod_rec &mypod = S.pods[pl];
-        uint32_t rk_lo = 0, rk_hi = 0, rinfo = 0;  // this lane's pod: winner key, code | plugin mask << 8
+        u64 rk = 0;                              // this lane's pod: winner key
+        uint32_t rinfo = 0;                      // and code | plugin mask << 8
         MS_VST(1);
-        for (uint32_t i = 0; i < gn; ++i) {
-            const uint32_t p = g + i;
-            const u64 sk = readlane_u64(sk_l, i);
+        for (uint32_t i0 = 0; i0 < gn;) {
+            const bool act = mine && lane >= i0 && sk_l != 0;
+            bool conflict = false;
+            if (act) {
+                conflict = map_find(S, srow_l) >= 0;
+                if (binds_l) atomicMin(&S.claim[ch], lane);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (act) conflict = conflict || S.claim[ch] < lane;
+            const u64 bad = __ballot(act && conflict);
+            const uint32_t s = bad ? (uint32_t)__builtin_ctzll(bad) : gn;
+            __builtin_amdgcn_wave_barrier();
+            if (act && binds_l) S.claim[ch] = ~0u;  // (every lane read its bucket above)
+            if (mine && lane >= i0 && lane < s) {  // speculative outcome, exact
+                rk = sk_l;
+                if (sk_l == 0) {  // no feasible row at speculation: none now either
+                    const uint32_t fm = S.spec_flags[pl];
+                    rinfo = MS_CODE_UNSCHEDULABLE | ((((fm & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                                                      ((fm & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u))
+                                                     << 8);
+                } else if (dig_l < 0) {
+                    rinfo = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
+                } else {
+                    rinfo = MS_CODE_SUCCESS;
+                    prow = srow_l;  // first bind on this node in the batch: its record is slot pl
+                    pslot = pl;
+                    padd = (int)pl;
+                }
+            }
+            flush_pending(S, prow, pslot, padd, mypod);
+            MS_VST(4);
+            if (s == gn) break;
+            // ---- slow pod p: resolved against current state
+            const uint32_t p = g + s;
+            ++ctr.slow;
+            const PodFull q = load_pod(S.pods[p], seed32);
             u64 b = 0;
             int wslot = -1;
-            uint32_t fmask = 0;  // filter flags for a FitError
-            if (sk == 0) {  // no feasible row at speculation: none now either
-                fmask = S.spec_flags[p];
-            } else if (!((touched >> i) & 1u)) {
-                b = sk;
-                wslot = (int)p | kFreshSlot;
-            } else {  // the speculative winner was bound earlier in the batch
-                ++ctr.slow;
-                MS_VST(2);
-                flush_pending(S, prow, pslot, padd, mypod);
-                const PodFull q = load_pod(S.pods[p], seed32);
-                // global top-4 (lanes 0-3): touched entries are re-evaluated, the first
-                // untouched one is exact and bounds every row below it
-                const u64 e = lane < (uint32_t)kTopK ? S.top4[p][lane] : 0ull;
-                const int esl = e ? map_find(S, row_of_key(e, t.base)) : -1;
-                const u64 untouched = __ballot(e != 0 && esl < 0);
-                const u64 present = __ballot(e != 0);
-                bool scan = false;
-                if (untouched || __builtin_popcountll(present) < kTopK) {
-                    const uint32_t f = untouched ? (uint32_t)__builtin_ctzll(untouched) : (uint32_t)kTopK;
-                    u64 v = 0;
-                    int vs = -1;
-                    if (lane < f && e != 0) {
-                        uint32_t nu, nrf;
-                        v = eval_full(slot_row(S, esl), row_of_key(e, t.base) + t.base, q, nu, nrf);
-                        vs = esl;
-                        ++ctr.recompute;
-                    } else if (lane == f) {
-                        v = e;
-                    }
-                    b = wave_max_u64_dpp(v);
-                    const u64 own = __ballot(b != 0 && v == b);
-                    wslot = own ? __builtin_amdgcn_readlane(vs, (int)__builtin_ctzll(own)) : -1;
-                    scan = b == 0;  // FitError: its plugin mask needs the tiles' flags
-                } else {
-                    scan = true;  // all four touched: rows below them are unknown
+            uint32_t fmask = 0;
+            // global top-4 (lanes 0-3): touched entries are re-evaluated, the first
+            // untouched one is exact and bounds every row below it
+            const u64 e = lane < (uint32_t)kTopK ? S.top4[p][lane] : 0ull;
+            const int esl = e ? map_find(S, row_of_key(e, t.base)) : -1;
+            const u64 untouched = __ballot(e != 0 && esl < 0);
+            const u64 present = __ballot(e != 0);
+            bool scan = false;
+            if (untouched || __builtin_popcountll(present) < kTopK) {
+                const uint32_t f = untouched ? (uint32_t)__builtin_ctzll(untouched) : (uint32_t)kTopK;
+                u64 v = 0;
+                int vs = -1;
+                if (lane < f && e != 0) {
+                    uint32_t nu, nrf;
+                    v = eval_full(slot_row(S, esl), row_of_key(e, t.base) + t.base, q, nu, nrf);
+                    vs = esl;
+                    ++ctr.recompute;
+                } else if (lane == f) {
+                    v = e;
                 }
-                TileLists<J> B;
-                if (scan) {
-                    load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
-                    validate_scan<J>(S, t, n_rows, q, B, tiles, lane, ctr, b, wslot);
-                }
-                if (b == 0) {  // per tile: speculative flags, + NRF if its feasible rows were all bound away
-                    uint32_t fl = 0;
-#pragma unroll
-                    for (int j = 0; j < J; ++j)
-                        if ((tiles >> j) & 1u) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
-                    fmask = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
-                }
-                MS_VST(3);
+                b = wave_max_u64_dpp(v);
+                const u64 own = __ballot(b != 0 && v == b);
+                wslot = own ? __builtin_amdgcn_readlane(vs, (int)__builtin_ctzll(own)) : -1;
+                scan = b == 0;  // FitError: its plugin mask needs the tiles' flags
+            } else {
+                scan = true;  // all four touched: rows below them are unknown
+            }
+            TileLists<J> B;
+            if (scan) {
+                load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
+                validate_scan<J>(S, t, n_rows, q, B, tiles, lane, ctr, b, wslot);
             }
             uint32_t info;
-            if (b == 0) {
+            if (b == 0) {  // per tile: speculative flags, + NRF if its feasible rows were all bound away
+                uint32_t fl = 0;
+#pragma unroll
+                for (int j = 0; j < J; ++j)
+                    if ((tiles >> j) & 1u) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
+                fmask = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
                 info = MS_CODE_UNSCHEDULABLE | ((((fmask & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
                                                  ((fmask & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u))
                                                 << 8);
-            } else if (__builtin_amdgcn_readlane(dig_l, (int)i) < 0) {
-                info = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
+            } else if (__builtin_amdgcn_readlane(dig_l, (int)s) < 0) {
+                info = MS_CODE_ERROR;
             } else {
                 info = MS_CODE_SUCCESS;
                 // assume-on-select: NodeInfo.AddPod on the winner's LDS record
                 const uint32_t row = row_of_key(b, t.base);
                 int sl = wslot;
-                if (sl < 0) {  // untouched winner other than the speculative one: load its record
+                if (sl < 0) {  // untouched winner: load its record (the table holds its batch-start state)
                     sl = kSeqBatch + (int)n_misses++;
                     ++ctr.miss;
                     int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
@@ -1109,34 +1166,29 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                     if (lane == (uint32_t)F_INV_CPU) v = __double_as_longlong(recip(capc));
                     if (lane == (uint32_t)F_INV_MEM) v = __double_as_longlong(recip(capm));
                     if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
-                    sl |= kFreshSlot;
-                }
-                const bool fresh = (sl & kFreshSlot) != 0;  // first bind on this node in the batch
-                sl &= ~kFreshSlot;
-                if (lane == i) {  // map entry (if fresh) and AddPod, both deferred
-                    if (fresh) {
+                    if (lane == s) {
                         prow = row;
                         pslot = (uint32_t)sl;
                     }
-                    padd = sl;
                 }
-                touched |= __ballot(srow_l == row);  // later pods of the group that speculated on it
+                if (lane == s) padd = sl;
             }
-            rk_lo = writelane(rk_lo, (uint32_t)b, i);
-            rk_hi = writelane(rk_hi, (uint32_t)(b >> 32), i);
-            rinfo = writelane(rinfo, info, i);
-            MS_VST(4);
+            if (lane == s) {
+                rk = b;
+                rinfo = info;
+            }
+            flush_pending(S, prow, pslot, padd, mypod);
+            MS_VST(3);
+            i0 = s + 1;
         }
-        flush_pending(S, prow, pslot, padd, mypod);
         if (mine) {  // this lane's pod result
-            const u64 k = ((u64)rk_hi << 32) | rk_lo;
             ms_result r;
             r._pad = 0;
             r.code = (int32_t)(rinfo & 0xFFu);
             r.plugin_mask = rinfo >> 8;
             const bool ok = r.code == MS_CODE_SUCCESS;
-            r.node = ok ? (int32_t)(0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) : -1;
-            r.score = ok ? (int64_t)(k >> 52) : 0;
+            r.node = ok ? (int32_t)(0xFFFFFu - (uint32_t)(rk & 0xFFFFFu)) : -1;
+            r.score = ok ? (int64_t)(rk >> 52) : 0;
             results[pl] = r;
         }
         MS_VST(1);
@@ -1151,15 +1203,19 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     }
     for (uint32_t h = lane; h < (uint32_t)kMapCap; h += 64) {
         const uint32_t v = S.map[h];
-        if (v == 0) continue;
-        const int64_t *r = S.rec[v & 511u];
+        if (v == 0 || !S.bound[v & 1023u]) continue;  // a previous batch's node not bound again
+        const int64_t *r = S.rec[v & 1023u];
         const uint32_t row = (uint32_t)r[F_ROW];
         t.req_cpu[row] = r[F_REQ_CPU];
         t.req_mem[row] = r[F_REQ_MEM];
         t.nz_cpu[row] = r[F_NZ_CPU];
         t.nz_mem[row] = r[F_NZ_MEM];
         t.pod_count[row] = (int32_t)r[F_CNT];
+        if (prev_out) prev_out[1 + atomicAdd(&S.n_out, 1u)] = row;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (prev_out && lane == 0) prev_out[0] = S.n_out;
 #ifdef MS_VSTAMPS
     MS_VST(5);
     if (lane == 0)
@@ -1384,7 +1440,8 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
     if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
-    const uint32_t chunk = 16;  // pods per wave: node rows amortised, >= 16 x n_tiles waves
+    uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
+    if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::max(1, atoi(e));
     const dim3 grid(gx, cdiv(n_pods, chunk));
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
                        tile_keys, tile_flags, spec, spec_flags, n_tiles);
@@ -1394,12 +1451,13 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
                                unsigned long long *spec, uint32_t *spec_flags, const unsigned long long *top4,
-                               uint32_t n_tiles, ms_result *results, uint32_t *stats, hipStream_t s) {
+                               uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out, ms_result *results,
+                               uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
 #define MS_VAL(J)                                                                                          \
     hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys, \
-                       tile_flags, spec, spec_flags, top4, n_tiles, results, stats)
+                       tile_flags, spec, spec_flags, top4, n_tiles, prev_in, prev_out, results, stats)
     if (n_tiles <= 64) MS_VAL(1);
     else if (n_tiles <= 128) MS_VAL(2);
     else if (n_tiles <= 256) MS_VAL(4);
