@@ -410,9 +410,9 @@ int ms_destroy(ms_ctx *c) {
         if (hipMemcpy(st, c->d_overflow, kStatsBytes, hipMemcpyDeviceToHost) == hipSuccess) {
             const uint64_t *cy = reinterpret_cast<const uint64_t *>(st + 8);
             std::fprintf(stderr,
-                         "MS_VSTAMPS pods=%u scans=%u misses=%u recomputes=%u resweeps=%u cycles: prologue=%llu "
+                         "MS_VSTAMPS pods=%u slow=%u tile_scans=%u misses=%u recomputes=%u resweeps=%u cycles: prologue=%llu "
                          "fast_check=%llu scan=%llu commit=%llu loop=%llu epilogue=%llu\n",
-                         st[3], st[5], st[4], st[2], st[1], (unsigned long long)cy[0], (unsigned long long)cy[1],
+                         st[3], st[5], st[6], st[4], st[2], st[1], (unsigned long long)cy[0], (unsigned long long)cy[1],
                          (unsigned long long)cy[2], (unsigned long long)cy[3], (unsigned long long)cy[4],
                          (unsigned long long)cy[5]);
         }

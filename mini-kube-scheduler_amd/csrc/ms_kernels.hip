@@ -714,6 +714,7 @@ constexpr int kRecF = 12;               // record fields per slot (see RecField)
 constexpr int kSpecF = 9;               // fields loaded from the node table (F_REQ_CPU .. F_FD)
 constexpr int kClaimBits = 12;          // claim table: 64 lanes in 4096 buckets, ~0.8% false conflicts
 constexpr int kClaimCap = 1 << kClaimBits;
+constexpr uint32_t kForceSlow = 0xFFFFu;  // spec_slot: speculation could not be re-resolved
 
 // LDS record of a touched node, one i64 (or f64 bit pattern) per field
 enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALLOC_MEM, F_CNT, F_ALLOWED, F_FD,
@@ -721,9 +722,11 @@ enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALL
 
 // Slots: rec[p] for p < kSeqBatch is pod p's speculative winner's record,
 // loaded at batch start (it becomes that node's live record when pod p binds
-// there first); rec[kSeqBatch + i] are records loaded on a speculation miss;
+// there first); rec[kSeqBatch + p] is pod p's next candidate (prefetched at
+// batch start; reloaded if pod p binds elsewhere off its speculation);
 // rec[2*kSeqBatch + i] are the nodes the previous batch bound (pipelined
-// mode: this batch's speculation may predate those binds).
+// mode: this batch's speculation may predate those binds). A node has at most
+// one live slot: the map's.
 struct SeqShared {
     uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
     int64_t rec[3 * kSeqBatch][kRecF];
@@ -734,6 +737,7 @@ struct SeqShared {
     uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
     u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
     uint32_t claim[kClaimCap];       // per round: lowest lane whose speculative winner hashes here
+    uint16_t spec_slot[kSeqBatch];   // slot of the speculative winner's record (kForceSlow: unresolved)
 };
 static_assert(sizeof(SeqShared) <= 160 * 1024, "validator LDS");
 
@@ -788,6 +792,16 @@ __device__ __forceinline__ int64_t rec_field(const NodeTable &t, uint32_t r, uin
     }
 }
 
+// Node row r's current device record into LDS slot sl (one lane).
+__device__ __forceinline__ void load_rec(SeqShared &S, const NodeTable &t, uint32_t sl, uint32_t r) {
+    int64_t *rec = S.rec[sl];
+#pragma unroll
+    for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
+    rec[F_ROW] = r;
+    rec[F_INV_CPU] = __double_as_longlong(recip(rec[F_ALLOC_CPU]));
+    rec[F_INV_MEM] = __double_as_longlong(recip(rec[F_ALLOC_MEM]));
+}
+
 __device__ __forceinline__ uint32_t row_of_key(u64 k, uint32_t base) {
     return (0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) - base;
 }
@@ -829,7 +843,7 @@ __device__ __forceinline__ void load_lists(TileLists<J> &B, const u64 *__restric
 }
 
 struct SeqCounters {
-    uint32_t recompute, resweep, miss, slow;
+    uint32_t recompute, resweep, miss, slow, scan;
 };
 
 
@@ -987,7 +1001,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                                                      uint32_t *__restrict__ prev_out, ms_result *__restrict__ results,
                                                      uint32_t *__restrict__ stats) {
     // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
-    //        [4] speculation misses (records loaded), [5] pods whose speculative winner was touched
+    //        [4] speculation misses (records loaded), [5] slow pods, [6] slow pods that scanned the tile lists
     // prev_in/prev_out: {count, rows...} of the nodes the previous / this batch bound
     // (prev_in null when the sweep of this batch saw every earlier bind).
     __shared__ SeqShared S;
@@ -1010,40 +1024,87 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     for (uint32_t i = lane; i < n_prev; i += 64) {
         const uint32_t r = prev_in[1 + i];
         const uint32_t sl = 2u * kSeqBatch + i;
-        int64_t *rec = S.rec[sl];
-#pragma unroll
-        for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
-        rec[F_ROW] = r;
-        rec[F_INV_CPU] = __double_as_longlong(recip(rec[F_ALLOC_CPU]));
-        rec[F_INV_MEM] = __double_as_longlong(recip(rec[F_ALLOC_MEM]));
+        load_rec(S, t, sl, r);
         uint32_t h = map_hash(r);
         while (atomicCAS(&S.map[h], 0u, ((r + 1) << 10) | sl) != 0u) h = (h + 1) & (kMapCap - 1);
     }
     for (uint32_t i = lane; i < n_pods; i += 64) {
         S.pods[i] = pods[i];
-        const u64 sk = spec[i];
-        S.spec_key[i] = sk;
+        S.spec_key[i] = spec[i];
         S.spec_flags[i] = spec_flags[i];
 #pragma unroll
         for (int k = 0; k < kTopK; ++k) S.top4[i][k] = top4[(size_t)i * kTopK + k];
         spec[i] = 0;  // the next batch's sweep accumulates here again
         spec_flags[i] = 0;
-        if (sk) {
-            const uint32_t r = row_of_key(sk, t.base);
-            int64_t *rec = S.rec[i];
-#pragma unroll
-            for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
-            rec[F_ROW] = r;
-            rec[F_INV_CPU] = __double_as_longlong(recip(rec[F_ALLOC_CPU]));
-            rec[F_INV_MEM] = __double_as_longlong(recip(rec[F_ALLOC_MEM]));
-        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    uint32_t n_misses = 0, tiles = 0;  // tiles: bit j <=> this lane owns tile lane + 64 j
+    for (uint32_t i = lane; i < n_pods; i += 64) {
+        u64 sk = S.spec_key[i];
+        uint32_t sslot = i;
+        if (sk && n_prev && map_find(S, row_of_key(sk, t.base)) >= 0) {
+            // Pipelined: the winner is a node the previous batch bound, so its key
+            // is stale. Re-resolve against the current state (nothing of this
+            // batch is bound yet) from the top-4: previous-batch entries are
+            // re-evaluated from their records, the first other entry is exact
+            // and bounds every row below it.
+            const PodFull q = load_pod(S.pods[i], seed32);
+            u64 best = 0;
+            int bslot = -1;
+            bool done = false;
+            for (int k = 0; k < kTopK && !done; ++k) {
+                const u64 e = S.top4[i][k];
+                if (e == 0) {  // list ended: every feasible row was listed
+                    done = true;
+                    break;
+                }
+                const int es = map_find(S, row_of_key(e, t.base));
+                if (es < 0) {
+                    if (e > best) {
+                        best = e;
+                        bslot = -1;
+                    }
+                    done = true;
+                    break;
+                }
+                uint32_t nu, nrf;
+                const u64 v = eval_full(slot_row(S, es), row_of_key(e, t.base) + t.base, q, nu, nrf);
+                if (v > best) {
+                    best = v;
+                    bslot = es;
+                }
+            }
+            if (done && best != 0) {
+                sk = best;
+                sslot = bslot >= 0 ? (uint32_t)bslot : i;
+                S.spec_key[i] = sk;
+            } else {
+                sslot = kForceSlow;  // all four stale (or none feasible now): resolved in order
+            }
+        }
+        S.spec_slot[i] = (uint16_t)sslot;
+        const uint32_t wrow = sk ? row_of_key(sk, t.base) : 0xFFFFFFFFu;
+        if (sk && sslot == i) load_rec(S, t, i, wrow);
+        // the pod's next candidate: first other top-4 entry on a node without a live record
+        uint32_t prow = 0xFFFFFFFFu;
+        for (int k = 0; k < kTopK; ++k) {
+            const u64 e = S.top4[i][k];
+            if (e == 0) break;
+            const uint32_t r = row_of_key(e, t.base);
+            if (r != wrow && map_find(S, r) < 0) {
+                prow = r;
+                break;
+            }
+        }
+        if (prow != 0xFFFFFFFFu) load_rec(S, t, kSeqBatch + i, prow);
+        else S.rec[kSeqBatch + i][F_ROW] = -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    uint32_t tiles = 0;  // tiles: bit j <=> this lane owns tile lane + 64 j
 #pragma unroll
     for (int j = 0; j < J; ++j) tiles |= (lane + 64u * j < n_tiles) ? 1u << j : 0u;
-    SeqCounters ctr = {0, 0, 0, 0};
+    SeqCounters ctr = {0, 0, 0, 0, 0};
     MS_VST(0);
 
     // Pods go in groups of 64, lane i <-> pod g+i, decided in rounds. A round
@@ -1062,6 +1123,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         const uint32_t srow_l = sk_l ? row_of_key(sk_l, t.base) : 0xFFFFFFFEu;
         const int dig_l = mine ? (int)S.pods[pl].name_digit : 0;
         const bool binds_l = sk_l != 0 && dig_l >= 0;  // binds at its speculative winner if that is exact
+        const uint32_t ss_l = mine ? (uint32_t)S.spec_slot[pl] : 0u;
         const uint32_t ch = claim_hash(srow_l);
         const ms_pod_rec &mypod = S.pods[pl];
         uint32_t prow = 0xFFFFFFFFu, pslot = 0;  // this lane's pending map insert
@@ -1073,7 +1135,10 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
             const bool act = mine && lane >= i0 && sk_l != 0;
             bool conflict = false;
             if (act) {
-                conflict = map_find(S, srow_l) >= 0;
+                // touched: bound earlier in the batch (a previous batch's node
+                // whose record is in the map is touched only once bound again)
+                const int sl = map_find(S, srow_l);
+                conflict = ss_l == kForceSlow || (sl >= 0 && (sl < 2 * kSeqBatch || S.bound[sl]));
                 if (binds_l) atomicMin(&S.claim[ch], lane);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1094,9 +1159,11 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                     rinfo = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
                 } else {
                     rinfo = MS_CODE_SUCCESS;
-                    prow = srow_l;  // first bind on this node in the batch: its record is slot pl
-                    pslot = pl;
-                    padd = (int)pl;
+                    if (ss_l == pl) {  // first bind on this node in the batch: its record is slot pl
+                        prow = srow_l;
+                        pslot = pl;
+                    }
+                    padd = (int)ss_l;
                 }
             }
             flush_pending(S, prow, pslot, padd, mypod);
@@ -1137,6 +1204,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
             }
             TileLists<J> B;
             if (scan) {
+                ++ctr.scan;
                 load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
                 validate_scan<J>(S, t, n_rows, q, B, tiles, lane, ctr, b, wslot);
             }
@@ -1157,8 +1225,9 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                 // assume-on-select: NodeInfo.AddPod on the winner's LDS record
                 const uint32_t row = row_of_key(b, t.base);
                 int sl = wslot;
-                if (sl < 0) {  // untouched winner: load its record (the table holds its batch-start state)
-                    sl = kSeqBatch + (int)n_misses++;
+                if (sl < 0) {  // untouched winner: its batch-start record (prefetched, or from the table)
+                    sl = kSeqBatch + (int)p;
+                    if ((uint32_t)S.rec[sl][F_ROW] != row) {
                     ++ctr.miss;
                     int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
                     const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
@@ -1166,6 +1235,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                     if (lane == (uint32_t)F_INV_CPU) v = __double_as_longlong(recip(capc));
                     if (lane == (uint32_t)F_INV_MEM) v = __double_as_longlong(recip(capm));
                     if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
+                    }
                     if (lane == s) {
                         prow = row;
                         pslot = (uint32_t)sl;
@@ -1200,11 +1270,11 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         atomicAdd(&stats[3], n_pods);
         atomicAdd(&stats[4], ctr.miss);
         atomicAdd(&stats[5], ctr.slow);
+        atomicAdd(&stats[6], ctr.scan);
     }
-    for (uint32_t h = lane; h < (uint32_t)kMapCap; h += 64) {
-        const uint32_t v = S.map[h];
-        if (v == 0 || !S.bound[v & 1023u]) continue;  // a previous batch's node not bound again
-        const int64_t *r = S.rec[v & 1023u];
+    for (uint32_t sl = lane; sl < 3u * kSeqBatch; sl += 64) {
+        if (!S.bound[sl]) continue;  // not bound in this batch (a prefetch, a previous batch's node)
+        const int64_t *r = S.rec[sl];
         const uint32_t row = (uint32_t)r[F_ROW];
         t.req_cpu[row] = r[F_REQ_CPU];
         t.req_mem[row] = r[F_REQ_MEM];
