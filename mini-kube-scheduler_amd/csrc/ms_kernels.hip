@@ -645,7 +645,8 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
 // ----------------------------------------------------------------------------
 template <int J>
 __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys, uint32_t n_pods,
-                                                   uint32_t n_tiles, u64 *__restrict__ top) {
+                                                   uint32_t n_tiles, u64 *__restrict__ top,
+                                                   uint32_t *__restrict__ ready) {
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_pods) return;
     u64 e[J][kTopK];
@@ -682,6 +683,10 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
+    // publish: the validator of this batch (already running on another stream)
+    // waits for n_pods arrivals; the release orders this batch's sweep output too
+    __threadfence();
+    if (lane == 0) atomicAdd(ready, 1u);
 }
 
 // ----------------------------------------------------------------------------
@@ -997,7 +1002,8 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                                                      uint32_t seed32, const u64 *__restrict__ tile_keys,
                                                      const uint32_t *__restrict__ tile_flags, u64 *__restrict__ spec,
                                                      uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
-                                                     uint32_t n_tiles, const uint32_t *__restrict__ prev_in,
+                                                     uint32_t n_tiles, uint32_t *__restrict__ ready,
+                                                     const uint32_t *__restrict__ prev_in,
                                                      uint32_t *__restrict__ prev_out, ms_result *__restrict__ results,
                                                      uint32_t *__restrict__ stats) {
     // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
@@ -1009,6 +1015,18 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
         if (lane == 0) atomicOr(&stats[0], 1u);
         return;
+    }
+    {  // this batch's speculation: k_topk_merge publishes n_pods arrivals
+        uint32_t it = 0;
+        while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n_pods) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++it == (1u << 24)) {  // ~seconds: never expected; report instead of hanging
+                if (lane == 0) atomicOr(&stats[0], 2u);
+                return;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (lane == 0) *ready = 0;  // the next merge into this buffer follows this batch's end
     }
     MS_VST_DECL
     // prologue: touched map, pods, speculative winners and their batch-start records (slot p)
@@ -1521,13 +1539,13 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
                                unsigned long long *spec, uint32_t *spec_flags, const unsigned long long *top4,
-                               uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out, ms_result *results,
-                               uint32_t *stats, hipStream_t s) {
+                               uint32_t n_tiles, uint32_t *ready, const uint32_t *prev_in, uint32_t *prev_out,
+                               ms_result *results, uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
 #define MS_VAL(J)                                                                                          \
     hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys, \
-                       tile_flags, spec, spec_flags, top4, n_tiles, prev_in, prev_out, results, stats)
+                       tile_flags, spec, spec_flags, top4, n_tiles, ready, prev_in, prev_out, results, stats)
     if (n_tiles <= 64) MS_VAL(1);
     else if (n_tiles <= 128) MS_VAL(2);
     else if (n_tiles <= 256) MS_VAL(4);
@@ -1538,10 +1556,11 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
 }
 
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, uint32_t n_pods, uint32_t n_tiles,
-                             unsigned long long *top, hipStream_t s) {
+                             unsigned long long *top, uint32_t *ready, hipStream_t s) {
     if (n_pods == 0 || n_tiles == 0) return hipSuccess;
     if (n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
-#define MS_MERGE(J) hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, n_pods, n_tiles, top)
+#define MS_MERGE(J) \
+    hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, n_pods, n_tiles, top, ready)
     if (n_tiles <= 64) MS_MERGE(1);
     else if (n_tiles <= 128) MS_MERGE(2);
     else if (n_tiles <= 256) MS_MERGE(4);

@@ -203,6 +203,7 @@ def test_resource_exact_sequential(oracle, n_nodes, n_pods):
         res = e.schedule(pr, MODE_SEQUENTIAL)
         assert_same(res, o)
         assert_table_equal(e, o["cols"], n_nodes)
+        assert e.info()._pad == 0  # validator capacity / hand-off flags
 
 
 def test_config_e_prefix(oracle):
@@ -213,6 +214,7 @@ def test_config_e_prefix(oracle):
     with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=1) as e:
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
         assert_table_equal(e, o["cols"], 50_000)
+        assert e.info()._pad == 0
 
 
 def test_commit_uncommit(oracle):
@@ -238,11 +240,14 @@ def test_chunked_batches(oracle):
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
 
 
+@pytest.mark.parametrize("pipe", ["1", "0"])
 @pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
-def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch):
+def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch, pipe):
     # speculative batch boundaries must not change placements: 50 nodes (one
-    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted)
+    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted); with and
+    # without the next batch's speculation overlapping validation
     monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
+    monkeypatch.setenv("MINISCHED_SEQ_PIPE", pipe)
     for n_nodes, n_pods in ((50, 600), (2500, 3000)):
         seed = 11 * n_nodes + int(batch)
         nr = synth.nodes(n_nodes, seed=seed, resources=True)
@@ -251,6 +256,7 @@ def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch):
         with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed) as e:
             assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
             assert_table_equal(e, o["cols"], n_nodes)
+            assert e.info()._pad == 0
 
 
 @pytest.mark.parametrize("n_nodes", [20_000, 100_000, 140_000])
