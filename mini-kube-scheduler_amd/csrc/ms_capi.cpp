@@ -56,12 +56,11 @@ struct ms_ctx {
     uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
     unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
-    uint32_t *d_ready = nullptr;           // merge -> validator hand-off counters (x2)
     // pipelined sequential engine: batch k+1's speculation (seq_stream) runs
     // while batch k validates (caller stream); every buffer above is double-
     // buffered by batch parity
     hipStream_t seq_stream = nullptr;
-    hipEvent_t ev_valid[2] = {nullptr, nullptr}, ev_seq = nullptr;
+    hipEvent_t ev_valid[2] = {nullptr, nullptr}, ev_swept[2] = {nullptr, nullptr}, ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
 
@@ -105,7 +104,7 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_ready, c->d_overflow, c->d_pstream};
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -114,6 +113,7 @@ void free_all(ms_ctx *c) {
     if (c->pstream_ev) (void)hipEventDestroy(c->pstream_ev);
     for (int i = 0; i < 2; ++i) {
         if (c->ev_valid[i]) (void)hipEventDestroy(c->ev_valid[i]);
+        if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
     }
     if (c->ev_seq) (void)hipEventDestroy(c->ev_seq);
     if (c->seq_stream) {
@@ -186,12 +186,13 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
         MS_HIP(c, hipStreamCreateWithFlags(&c->seq_stream, hipStreamNonBlocking));
         for (int i = 0; i < 2; ++i) {
             MS_HIP(c, hipEventCreateWithFlags(&c->ev_valid[i], hipEventDisableTiming));
+            MS_HIP(c, hipEventCreateWithFlags(&c->ev_swept[i], hipEventDisableTiming));
         }
         MS_HIP(c, hipEventCreateWithFlags(&c->ev_seq, hipEventDisableTiming));
     }
     if (n_tiles <= c->tile_cap) return MS_OK;
     MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
-    void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_ready};
+    void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev};
     for (void *q : old)
         if (q) (void)hipFree(q);
     c->d_tile_keys = nullptr;
@@ -200,7 +201,6 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     c->d_spec_flags = nullptr;
     c->d_top4 = nullptr;
     c->d_prev = nullptr;
-    c->d_ready = nullptr;
     c->tile_cap = 0;
     const size_t B = seq_batch_limit(), n = 2 * B * n_tiles;
     if (hipMalloc((void **)&c->d_tile_keys, n * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
@@ -208,12 +208,10 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
         hipMalloc((void **)&c->d_spec, 2 * B * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&c->d_spec_flags, 2 * B * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&c->d_top4, 2 * B * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void **)&c->d_prev, 2 * (B + 1) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&c->d_ready, 2 * sizeof(uint32_t)) != hipSuccess)
+        hipMalloc((void **)&c->d_prev, 2 * (B + 1) * sizeof(uint32_t)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential-engine scratch");
     MS_HIP(c, hipMemsetAsync(c->d_spec, 0, 2 * B * sizeof(unsigned long long), c->stream));
     MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, 2 * B * sizeof(uint32_t), c->stream));
-    MS_HIP(c, hipMemsetAsync(c->d_ready, 0, 2 * sizeof(uint32_t), c->stream));
     MS_HIP(c, hipStreamSynchronize(c->stream));
     c->tile_cap = n_tiles;
     return MS_OK;
@@ -249,10 +247,10 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     if (rc) return rc;
     // Batch k: speculative sweep + top-4 merge on seq_stream into buffer k&1, after
     // validation k-2 (which last read that buffer, and whose binds the sweep must
-    // see); validation k on s. It is launched right behind validation k-1 and waits
-    // on the device for merge k's arrivals (d_ready): one spinning wave, and merge k
-    // depends only on validations that precede it on s, so no cycle; a stream event
-    // there cost ~12 us per batch. Validation k marks the nodes batch k-1 bound as
+    // see); validation k on s after merge k (stream events only: a device-side
+    // wait would stall wherever dispatches are serialised, e.g. under counter
+    // profiling; an event costs ~6 us when already signalled, ~11 us otherwise,
+    // tools/ubench/xstream). Validation k marks the nodes batch k-1 bound as
     // touched (prev rows): sweep k may have run concurrently with it.
     MS_HIP(c, hipEventRecord(c->ev_seq, s));
     MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_seq, 0));
@@ -270,9 +268,12 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         if (k >= (pipe ? 2u : 1u)) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[pipe ? par : par ^ 1u], 0));
         MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, n_tiles,
                                           c->seq_stream));
-        MS_HIP(c, launch_topk_merge(tk, nb, n_tiles, top, c->d_ready + par, c->seq_stream));
+        MS_HIP(c, launch_topk_merge(tk, nb, n_tiles, top, c->seq_stream));
+        MS_HIP(c, hipEventRecord(c->ev_swept[par], c->seq_stream));
+        MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[par], 0));
         const uint32_t *prev_in = (pipe && k) ? c->d_prev + (SB + 1) * (par ^ 1u) : nullptr;
-        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, n_tiles, c->d_ready + par, prev_in,
+        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, n_tiles,
+                                      prev_in,
                                       c->d_prev + (SB + 1) * par, d_res + s0, c->d_overflow, s));
         MS_HIP(c, hipEventRecord(c->ev_valid[par], s));
     }

@@ -111,14 +111,13 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 // binds to the table. Single workgroup.
 // Global speculative top-4 keys per pod (top[p*4 + r]) from the per-tile lists.
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, uint32_t n_pods, uint32_t n_tiles,
-                             unsigned long long *top, uint32_t *ready, hipStream_t s);
+                             unsigned long long *top, hipStream_t s);
 // stats: u32[6] = overflow flags, re-swept tiles, recomputed entries, pods,
 // speculation misses, pods whose speculative winner was touched.
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys,
                                const uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
-                               const unsigned long long *top4, uint32_t n_tiles, uint32_t *ready,
-                               const uint32_t *prev_in, uint32_t *prev_out, ms_result *results, uint32_t *stats, hipStream_t s);
+                               const unsigned long long *top4, uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out, ms_result *results, uint32_t *stats, hipStream_t s);
 // Rows the sequential engine's validator supports (tile lists held in registers).
 uint32_t seq_max_rows();
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,

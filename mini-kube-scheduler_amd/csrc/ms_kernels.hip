@@ -417,63 +417,76 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
 // K3: NodeUnschedulable + NodeResourcesFit filters, NodeNumber + LeastAllocated
 // scores (upstream v1.22 semantics restated in oracle/ms_oracle.c).
 // ----------------------------------------------------------------------------
+// LeastAllocated (k8s@v1.22.0 least_allocated.go leastRequestedScore) per
+// resource: capacity 0 or requested > capacity -> 0, else
+// floor((capacity - requested) * 100 / capacity), requested = NonZeroRequested
+// + the pod's non-zero request n. With av = capacity - NonZeroRequested and
+// d = av - n, the f32 estimate x = (f32(av) - f32(n)) * f32(100/capacity) is
+// within 4e-5 of q = 100 d / capacity whenever 0 <= d (then n <= av <= capacity:
+// every operand's rounding is relative to at most capacity). So with
+// m = round(x), floor(q) is m or m - 1, and ONE exact int64 comparison
+// 100 d >= m * capacity decides it. 100 d = a100 - n100 with a100 = 100 av per
+// node and n100 = 100 min(n, 2^55) per pod; valid (d >= 0) <=> 100 d >= 0.
+// Rows with capacity >= 2^53 (beyond any real allocatable) hold av in the a100
+// field and take plain int64 arithmetic (kHuge, chosen per wave).
+constexpr int64_t kHugeCap = 1ll << 53;
+
 struct FullRow {
-    int64_t free_cpu, free_mem;    // Allocatable - Requested
-    int64_t nz_cpu, nz_mem;        // NonZeroRequested
-    int64_t alloc_cpu, alloc_mem;  // Allocatable
-    double inv_cpu, inv_mem;       // 1/Allocatable (f64), for the LeastAllocated quotient
-    int32_t room;                  // AllowedPodNumber - len(Pods)
-    uint32_t fd;                   // flags | digit << 8
+    int64_t fr_cpu, fr_mem;      // Allocatable - Requested          (NodeResourcesFit)
+    int64_t a100_cpu, a100_mem;  // 100 (Allocatable - NonZeroRequested); av itself when huge
+    int64_t cap_cpu, cap_mem;    // Allocatable
+    float avf_cpu, avf_mem;      // f32(Allocatable - NonZeroRequested)
+    float r_cpu, r_mem;          // f32(100 / Allocatable), 0 when Allocatable == 0
+    int32_t room;                // AllowedPodNumber - len(Pods)
+    uint32_t fd;                 // flags | digit << 8
 };
 
-__device__ __forceinline__ double recip(int64_t c) { return c > 0 ? 1.0 / (double)c : 0.0; }
+__device__ __forceinline__ float r100(int64_t cap) { return cap > 0 ? 100.0f / (float)cap : 0.0f; }
 
-__device__ __forceinline__ FullRow load_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
+__device__ __forceinline__ FullRow make_row(int64_t alloc_cpu, int64_t alloc_mem, int64_t req_cpu, int64_t req_mem,
+                                            int64_t nz_cpu, int64_t nz_mem, int32_t room, uint32_t fd) {
     FullRow x;
-    if (r >= n_rows) {
-        x.free_cpu = x.free_mem = x.nz_cpu = x.nz_mem = x.alloc_cpu = x.alloc_mem = 0;
-        x.inv_cpu = x.inv_mem = 0.0;
-        x.room = 0;
-        x.fd = kNodeAbsent | (0xFFu << 8);
-        return x;
-    }
-    x.alloc_cpu = t.alloc_cpu[r];
-    x.alloc_mem = t.alloc_mem[r];
-    x.inv_cpu = recip(x.alloc_cpu);
-    x.inv_mem = recip(x.alloc_mem);
-    x.free_cpu = x.alloc_cpu - t.req_cpu[r];
-    x.free_mem = x.alloc_mem - t.req_mem[r];
-    x.nz_cpu = t.nz_cpu[r];
-    x.nz_mem = t.nz_mem[r];
-    x.room = t.allowed_pods[r] - t.pod_count[r];
-    x.fd = (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8);
+    x.cap_cpu = alloc_cpu;
+    x.cap_mem = alloc_mem;
+    x.fr_cpu = alloc_cpu - req_cpu;
+    x.fr_mem = alloc_mem - req_mem;
+    const int64_t av_cpu = alloc_cpu - nz_cpu, av_mem = alloc_mem - nz_mem;
+    x.a100_cpu = alloc_cpu >= kHugeCap ? av_cpu : av_cpu * 100;
+    x.a100_mem = alloc_mem >= kHugeCap ? av_mem : av_mem * 100;
+    x.avf_cpu = (float)av_cpu;
+    x.avf_mem = (float)av_mem;
+    x.r_cpu = r100(alloc_cpu);
+    x.r_mem = r100(alloc_mem);
+    x.room = room;
+    x.fd = fd;
     return x;
 }
 
-// floor(num/den) for 0 <= num <= 100*den, den > 0, given inv = RN(1/den): the
-// f64 product is within a few ulps of the quotient (<= 100), so it is off by at
-// most one and one integer fix-up makes it exact. num >= 2^53 (beyond any cpu
-// millicores or memory bytes x 100 below 90 PB) takes the integer division.
-__device__ __forceinline__ int64_t div_floor_recip(int64_t num, int64_t den, double inv) {
-    if (num < (1ll << 53)) {
-        int64_t q = (int64_t)((double)num * inv);
-        const int64_t r = num - q * den;
-        if (r < 0) q -= 1;
-        else if (r >= den) q += 1;
-        return q;
-    }
-    return num / den;
+__device__ __forceinline__ FullRow load_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
+    if (r >= n_rows) return make_row(0, 0, 0, 0, 0, 0, 0, kNodeAbsent | (0xFFu << 8));
+    return make_row(t.alloc_cpu[r], t.alloc_mem[r], t.req_cpu[r], t.req_mem[r], t.nz_cpu[r], t.nz_mem[r],
+                    t.allowed_pods[r] - t.pod_count[r], (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8));
 }
 
-// leastRequestedScore (k8s@v1.22.0 least_allocated.go)
-__device__ __forceinline__ int64_t least_requested(int64_t requested, int64_t capacity, double inv) {
-    if (capacity == 0) return 0;
-    if (requested > capacity) return 0;
-    return div_floor_recip((capacity - requested) * 100, capacity, inv);
+template <bool kHuge = true>
+__device__ __forceinline__ int64_t least_requested(int64_t a100, float avf, int64_t cap, float r, int64_t n,
+                                                   int64_t n100, float nf) {
+    if (kHuge && cap >= kHugeCap) {  // a100 holds av
+        const int64_t d = a100 - n;
+        return (a100 < n) ? 0 : (int64_t)((uint64_t)d * 100u) / cap;
+    }
+    const uint32_t m = (uint32_t)__builtin_fmaf(avf - nf, r, 0.5f);  // round(x); x < 0 -> 0
+    const int64_t d100 = a100 - n100;
+    const uint32_t lo = (uint32_t)cap, hi = (uint32_t)((uint64_t)cap >> 32);
+    const uint64_t mc = (uint64_t)m * lo + ((uint64_t)(m * hi) << 32);  // m * capacity (< 2^60)
+    const uint32_t q = m - (d100 < (int64_t)mc ? 1u : 0u);
+    return d100 >= 0 ? (int64_t)q : 0;
 }
 
 struct PodFull {
-    int64_t rc, rm, nc, nm;
+    int64_t rc, rm, nc, nm;   // requests (Fit) and non-zero requests (LeastAllocated)
+    int64_t n100c, n100m;     // 100 min(nonzero, 2^55)
+    float nfc, nfm;           // f32(nonzero)
     int dig;
     bool tol;
     bool zero_req;
@@ -486,6 +499,10 @@ __device__ __forceinline__ PodFull load_pod(const ms_pod_rec &pr, uint32_t seed3
     q.rm = pr.req_memory;
     q.nc = pr.nonzero_milli_cpu;
     q.nm = pr.nonzero_memory;
+    q.n100c = min(q.nc, 1ll << 55) * 100;
+    q.n100m = min(q.nm, 1ll << 55) * 100;
+    q.nfc = (float)q.nc;
+    q.nfm = (float)q.nm;
     q.dig = pr.name_digit;
     q.tol = pr.tolerates_unschedulable != 0;
     q.zero_req = (q.rc == 0 && q.rm == 0);
@@ -493,25 +510,73 @@ __device__ __forceinline__ PodFull load_pod(const ms_pod_rec &pr, uint32_t seed3
     return q;
 }
 
+__device__ __forceinline__ int64_t readlane_i64(int64_t v, uint32_t l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), (int)l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Sweeps hold up to 64 pods lane-resident (one parallel load, no per-pod
+// memory round trip) and broadcast pod i with readlanes.
+struct PodLanes {
+    PodFull q;
+};
+
+__device__ __forceinline__ PodLanes stage_pods(const ms_pod_rec *__restrict__ pods, uint32_t g, uint32_t cnt,
+                                               uint32_t lane, uint32_t seed32) {
+    PodLanes m;
+    ms_pod_rec z = {};
+    m.q = load_pod(lane < cnt ? pods[g + lane] : z, seed32);
+    return m;
+}
+
+__device__ __forceinline__ PodFull pod_of_lane(const PodLanes &m, uint32_t i) {
+    PodFull q;
+    q.rc = readlane_i64(m.q.rc, i);
+    q.rm = readlane_i64(m.q.rm, i);
+    q.nc = readlane_i64(m.q.nc, i);
+    q.nm = readlane_i64(m.q.nm, i);
+    q.n100c = readlane_i64(m.q.n100c, i);
+    q.n100m = readlane_i64(m.q.n100m, i);
+    q.nfc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.q.nfc), (int)i));
+    q.nfm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.q.nfm), (int)i));
+    q.A = (uint32_t)__builtin_amdgcn_readlane((int)m.q.A, (int)i);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(
+        (int)(((uint32_t)m.q.dig & 0xFFu) | (m.q.tol ? 0x100u : 0u) | (m.q.zero_req ? 0x200u : 0u)), (int)i);
+    q.dig = (int)(int8_t)(b & 0xFFu);
+    q.tol = (b & 0x100u) != 0;
+    q.zero_req = (b & 0x200u) != 0;
+    return q;
+}
+
 // Evaluates one (pod,node) pair: returns the packed key (0 when filtered out)
 // and sets the first-failing filter plugin (minisched.go:130-137 breaks on
 // the first failure, so a node rejected by NU is never charged to NRF).
+template <bool kHuge = true>
 __device__ __forceinline__ u64 eval_full(const FullRow &x, uint32_t ord, const PodFull &q,
                                          uint32_t &nu, uint32_t &nrf) {
-    nu = 0;
-    nrf = 0;
     const uint32_t fl = x.fd & 0xFFu;
-    if (fl & kNodeAbsent) return 0;
-    if ((fl & kNodeUnschedulable) && !q.tol) { nu = 1; return 0; }
+    const bool absent = (fl & kNodeAbsent) != 0;
+    const bool f_nu = !absent && (fl & kNodeUnschedulable) != 0 && !q.tol;
     bool bad = x.room < 1;  // len(Pods)+1 > AllowedPodNumber
-    if (!q.zero_req) bad = bad || (q.rc > x.free_cpu) || (q.rm > x.free_mem);
-    if (bad) { nrf = 1; return 0; }
-    const int nd = (int)(x.fd >> 8);
-    const uint32_t nn = (nd == q.dig) ? 10u : 0u;
-    const int64_t s_cpu = least_requested(x.nz_cpu + q.nc, x.alloc_cpu, x.inv_cpu);
-    const int64_t s_mem = least_requested(x.nz_mem + q.nm, x.alloc_mem, x.inv_mem);
+    if (!q.zero_req) bad = bad || (q.rc > x.fr_cpu) || (q.rm > x.fr_mem);
+    const bool f_nrf = !absent && !f_nu && bad;
+    nu = f_nu ? 1u : 0u;
+    nrf = f_nrf ? 1u : 0u;
+    const int64_t s_cpu = least_requested<kHuge>(x.a100_cpu, x.avf_cpu, x.cap_cpu, x.r_cpu, q.nc, q.n100c, q.nfc);
+    const int64_t s_mem = least_requested<kHuge>(x.a100_mem, x.avf_mem, x.cap_mem, x.r_mem, q.nm, q.n100m, q.nfm);
+    const uint32_t nn = ((int)(x.fd >> 8) == q.dig) ? 10u : 0u;
     const uint32_t la = (uint32_t)((s_cpu + s_mem) / 2);
-    return make_key(nn + la, tb_hash(q.A, ord), ord);
+    const u64 key = make_key(nn + la, tb_hash(q.A, ord), ord);
+    return (absent || f_nu || bad) ? 0ull : key;
+}
+
+// Whether any of the wave's rows needs the int64 LeastAllocated path.
+__device__ __forceinline__ bool rows_huge(const FullRow *x) {
+    bool h = false;
+#pragma unroll
+    for (int s = 0; s < kFullSlots; ++s) h = h || x[s].cap_cpu >= kHugeCap || x[s].cap_mem >= kHugeCap;
+    return __ballot(h) != 0;
 }
 
 // Batched resource-aware sweep: atomicMax into keys[P] / atomicOr into flags[P].
@@ -525,35 +590,36 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full(NodeTable t, uint32
 #pragma unroll
     for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
     const uint32_t ord0 = t.base + row0;
-
+    const bool huge = rows_huge(x);
     const uint32_t pbeg = blockIdx.y * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
-    u64 mine = 0;
-    uint32_t myflag = 0;
-    for (uint32_t p = pbeg; p < pend; ++p) {
-        const PodFull q = load_pod(pods[p], seed32);
-        u64 best = 0;
-        uint32_t nu_any = 0, nrf_any = 0;
+    for (uint32_t g = pbeg; g < pend; g += 64) {
+        const uint32_t cnt = min(64u, pend - g);
+        const PodLanes m = stage_pods(pods, g, cnt, lane, seed32);
+        u64 mine = 0;
+        uint32_t myflag = 0;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const PodFull q = pod_of_lane(m, i);
+            u64 best = 0;
+            uint32_t nu_any = 0, nrf_any = 0;
 #pragma unroll
-        for (int s = 0; s < kFullSlots; ++s) {
-            uint32_t nu, nrf;
-            const u64 k = eval_full(x[s], ord0 + s, q, nu, nrf);
-            best = umax64(best, k);
-            nu_any |= nu;
-            nrf_any |= nrf;
-        }
-        best = wave_max_u64(best);
-        const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
-        const uint32_t slot = (p - pbeg) & 63u;
-        if (lane == slot) { mine = best; myflag = f; }
-        if (slot == 63u || p + 1 == pend) {
-            const uint32_t pp = p - slot + lane;
-            if (lane <= slot) {
-                if (mine) atomicMax(&keys[pp], mine);
-                if (myflag) atomicOr(&pflags[pp], myflag);
+            for (int s = 0; s < kFullSlots; ++s) {
+                uint32_t nu, nrf;
+                best = umax64(best, huge ? eval_full<true>(x[s], ord0 + s, q, nu, nrf)
+                                         : eval_full<false>(x[s], ord0 + s, q, nu, nrf));
+                nu_any |= nu;
+                nrf_any |= nrf;
             }
-            mine = 0;
-            myflag = 0;
+            best = wave_max_u64(best);
+            const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
+            if (lane == i) {
+                mine = best;
+                myflag = f;
+            }
+        }
+        if (lane < cnt) {
+            if (mine) atomicMax(&keys[g + lane], mine);
+            if (myflag) atomicOr(&pflags[g + lane], myflag);
         }
     }
 }
@@ -581,31 +647,20 @@ __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
 constexpr int kTopK = 4;
 static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
 
-__global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, uint32_t n_rows,
-                                                                  const ms_pod_rec *__restrict__ pods,
-                                                                  uint32_t n_pods, uint32_t chunk, uint32_t seed32,
-                                                                  u64 *__restrict__ tile_keys,
-                                                                  uint32_t *__restrict__ tile_flags,
-                                                                  u64 *__restrict__ spec,
-                                                                  uint32_t *__restrict__ spec_flags, uint32_t n_tiles) {
-    const uint32_t lane = lane_id();
-    const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
-    if (tile >= n_tiles) return;  // wave-uniform; no block barriers in this kernel
-    const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
-    FullRow x[kFullSlots];
-#pragma unroll
-    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
-    const uint32_t ord0 = t.base + row0;
-    const uint32_t pbeg = blockIdx.y * chunk;
-    const uint32_t pend = min(n_pods, pbeg + chunk);
-    for (uint32_t p = pbeg; p < pend; ++p) {
-        const PodFull q = load_pod(pods[p], seed32);
+template <bool kHuge>
+__device__ __forceinline__ void sweep_topk_pods(const FullRow *x, uint32_t ord0, const PodLanes &m, uint32_t pbeg,
+                                                uint32_t cnt, uint32_t lane, uint32_t tile, uint32_t n_tiles,
+                                                u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags,
+                                                u64 *__restrict__ spec, uint32_t *__restrict__ spec_flags) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t p = pbeg + i;
+        const PodFull q = pod_of_lane(m, i);
         u64 k[kFullSlots];
         uint32_t nu_any = 0, nrf_any = 0;
 #pragma unroll
         for (int s = 0; s < kFullSlots; ++s) {
             uint32_t nu, nrf;
-            k[s] = eval_full(x[s], ord0 + s, q, nu, nrf);
+            k[s] = eval_full<kHuge>(x[s], ord0 + s, q, nu, nrf);
             nu_any |= nu;
             nrf_any |= nrf;
         }
@@ -618,9 +673,9 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
         u64 out = 0;
 #pragma unroll
         for (int j = 0; j < kTopK; ++j) {
-            const u64 m = wave_max_u64_dpp(k[0]);
-            if (lane == (uint32_t)j) out = m;
-            if (m != 0 && k[0] == m) {  // the owning lane pops its head
+            const u64 mx = wave_max_u64_dpp(k[0]);
+            if (lane == (uint32_t)j) out = mx;
+            if (mx != 0 && k[0] == mx) {  // the owning lane pops its head
                 k[0] = k[1];
                 k[1] = k[2];
                 k[2] = k[3];
@@ -638,6 +693,28 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
     }
 }
 
+__global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, uint32_t n_rows,
+                                                                  const ms_pod_rec *__restrict__ pods,
+                                                                  uint32_t n_pods, uint32_t chunk, uint32_t seed32,
+                                                                  u64 *__restrict__ tile_keys,
+                                                                  uint32_t *__restrict__ tile_flags,
+                                                                  u64 *__restrict__ spec,
+                                                                  uint32_t *__restrict__ spec_flags, uint32_t n_tiles) {
+    const uint32_t lane = lane_id();
+    const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
+    if (tile >= n_tiles) return;  // wave-uniform; no block barriers in this kernel
+    const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
+    FullRow x[kFullSlots];
+#pragma unroll
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
+    const uint32_t ord0 = t.base + row0;
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t cnt = min(min(chunk, 64u), n_pods - pbeg);  // host: chunk <= 64
+    const PodLanes m = stage_pods(pods, pbeg, cnt, lane, seed32);
+    if (rows_huge(x)) sweep_topk_pods<true>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags, spec, spec_flags);
+    else sweep_topk_pods<false>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags, spec, spec_flags);
+}
+
 // ----------------------------------------------------------------------------
 // Global speculative top-4 per pod, merged from the per-tile top-4 lists (one
 // wave per pod). Exact: the global rank-r entry (r < 4) is within its tile's
@@ -645,8 +722,7 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
 // ----------------------------------------------------------------------------
 template <int J>
 __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys, uint32_t n_pods,
-                                                   uint32_t n_tiles, u64 *__restrict__ top,
-                                                   uint32_t *__restrict__ ready) {
+                                                   uint32_t n_tiles, u64 *__restrict__ top) {
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_pods) return;
     u64 e[J][kTopK];
@@ -683,10 +759,6 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
-    // publish: the validator of this batch (already running on another stream)
-    // waits for n_pods arrivals; the release orders this batch's sweep output too
-    __threadfence();
-    if (lane == 0) atomicAdd(ready, 1u);
 }
 
 // ----------------------------------------------------------------------------
@@ -721,7 +793,7 @@ constexpr int kClaimBits = 12;          // claim table: 64 lanes in 4096 buckets
 constexpr int kClaimCap = 1 << kClaimBits;
 constexpr uint32_t kForceSlow = 0xFFFFu;  // spec_slot: speculation could not be re-resolved
 
-// LDS record of a touched node, one i64 (or f64 bit pattern) per field
+// LDS record of a touched node, one i64 per field (F_INV_*: f32 bits of 100 / Allocatable)
 enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALLOC_MEM, F_CNT, F_ALLOWED, F_FD,
                 F_ROW, F_INV_CPU, F_INV_MEM };
 
@@ -768,17 +840,10 @@ __device__ __forceinline__ int map_find(const SeqShared &S, uint32_t row) {
 
 __device__ __forceinline__ FullRow slot_row(const SeqShared &S, int sl) {
     const int64_t *r = S.rec[sl];
-    FullRow x;
-    x.alloc_cpu = r[F_ALLOC_CPU];
-    x.alloc_mem = r[F_ALLOC_MEM];
-    x.free_cpu = x.alloc_cpu - r[F_REQ_CPU];
-    x.free_mem = x.alloc_mem - r[F_REQ_MEM];
-    x.nz_cpu = r[F_NZ_CPU];
-    x.nz_mem = r[F_NZ_MEM];
-    x.inv_cpu = __longlong_as_double(r[F_INV_CPU]);
-    x.inv_mem = __longlong_as_double(r[F_INV_MEM]);
-    x.room = (int32_t)(r[F_ALLOWED] - r[F_CNT]);
-    x.fd = (uint32_t)r[F_FD];
+    FullRow x = make_row(r[F_ALLOC_CPU], r[F_ALLOC_MEM], r[F_REQ_CPU], r[F_REQ_MEM], r[F_NZ_CPU], r[F_NZ_MEM],
+                         (int32_t)(r[F_ALLOWED] - r[F_CNT]), (uint32_t)r[F_FD]);
+    x.r_cpu = __uint_as_float((uint32_t)r[F_INV_CPU]);  // (the division above is dead)
+    x.r_mem = __uint_as_float((uint32_t)r[F_INV_MEM]);
     return x;
 }
 
@@ -803,8 +868,8 @@ __device__ __forceinline__ void load_rec(SeqShared &S, const NodeTable &t, uint3
 #pragma unroll
     for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
     rec[F_ROW] = r;
-    rec[F_INV_CPU] = __double_as_longlong(recip(rec[F_ALLOC_CPU]));
-    rec[F_INV_MEM] = __double_as_longlong(recip(rec[F_ALLOC_MEM]));
+    rec[F_INV_CPU] = __float_as_uint(r100(rec[F_ALLOC_CPU]));
+    rec[F_INV_MEM] = __float_as_uint(r100(rec[F_ALLOC_MEM]));
 }
 
 __device__ __forceinline__ uint32_t row_of_key(u64 k, uint32_t base) {
@@ -1002,7 +1067,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                                                      uint32_t seed32, const u64 *__restrict__ tile_keys,
                                                      const uint32_t *__restrict__ tile_flags, u64 *__restrict__ spec,
                                                      uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
-                                                     uint32_t n_tiles, uint32_t *__restrict__ ready,
+                                                     uint32_t n_tiles,
                                                      const uint32_t *__restrict__ prev_in,
                                                      uint32_t *__restrict__ prev_out, ms_result *__restrict__ results,
                                                      uint32_t *__restrict__ stats) {
@@ -1015,18 +1080,6 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
         if (lane == 0) atomicOr(&stats[0], 1u);
         return;
-    }
-    {  // this batch's speculation: k_topk_merge publishes n_pods arrivals
-        uint32_t it = 0;
-        while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n_pods) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++it == (1u << 24)) {  // ~seconds: never expected; report instead of hanging
-                if (lane == 0) atomicOr(&stats[0], 2u);
-                return;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (lane == 0) *ready = 0;  // the next merge into this buffer follows this batch's end
     }
     MS_VST_DECL
     // prologue: touched map, pods, speculative winners and their batch-start records (slot p)
@@ -1250,8 +1303,8 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                     int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
                     const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
                     if (lane == (uint32_t)F_ROW) v = row;
-                    if (lane == (uint32_t)F_INV_CPU) v = __double_as_longlong(recip(capc));
-                    if (lane == (uint32_t)F_INV_MEM) v = __double_as_longlong(recip(capm));
+                    if (lane == (uint32_t)F_INV_CPU) v = __float_as_uint(r100(capc));
+                    if (lane == (uint32_t)F_INV_MEM) v = __float_as_uint(r100(capm));
                     if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
                     }
                     if (lane == s) {
@@ -1529,7 +1582,7 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
     uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
-    if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::max(1, atoi(e));
+    if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::min(64, std::max(1, atoi(e)));
     const dim3 grid(gx, cdiv(n_pods, chunk));
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
                        tile_keys, tile_flags, spec, spec_flags, n_tiles);
@@ -1539,13 +1592,13 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
                                unsigned long long *spec, uint32_t *spec_flags, const unsigned long long *top4,
-                               uint32_t n_tiles, uint32_t *ready, const uint32_t *prev_in, uint32_t *prev_out,
+                               uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out,
                                ms_result *results, uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
 #define MS_VAL(J)                                                                                          \
     hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys, \
-                       tile_flags, spec, spec_flags, top4, n_tiles, ready, prev_in, prev_out, results, stats)
+                       tile_flags, spec, spec_flags, top4, n_tiles, prev_in, prev_out, results, stats)
     if (n_tiles <= 64) MS_VAL(1);
     else if (n_tiles <= 128) MS_VAL(2);
     else if (n_tiles <= 256) MS_VAL(4);
@@ -1556,11 +1609,10 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
 }
 
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, uint32_t n_pods, uint32_t n_tiles,
-                             unsigned long long *top, uint32_t *ready, hipStream_t s) {
+                             unsigned long long *top, hipStream_t s) {
     if (n_pods == 0 || n_tiles == 0) return hipSuccess;
     if (n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
-#define MS_MERGE(J) \
-    hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, n_pods, n_tiles, top, ready)
+#define MS_MERGE(J) hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, n_pods, n_tiles, top)
     if (n_tiles <= 64) MS_MERGE(1);
     else if (n_tiles <= 128) MS_MERGE(2);
     else if (n_tiles <= 256) MS_MERGE(4);
