@@ -266,9 +266,8 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         unsigned long long *sp = c->d_spec + SB * par, *top = c->d_top4 + (size_t)SB * seq_topk() * par;
         uint32_t *sf = c->d_spec_flags + SB * par;
         if (k >= (pipe ? 2u : 1u)) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[pipe ? par : par ^ 1u], 0));
-        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, n_tiles,
-                                          c->seq_stream));
-        MS_HIP(c, launch_topk_merge(tk, nb, n_tiles, top, c->seq_stream));
+        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, tk, tf, n_tiles, c->seq_stream));
+        MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->seq_stream));
         MS_HIP(c, hipEventRecord(c->ev_swept[par], c->seq_stream));
         MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[par], 0));
         const uint32_t *prev_in = (pipe && k) ? c->d_prev + (SB + 1) * (par ^ 1u) : nullptr;

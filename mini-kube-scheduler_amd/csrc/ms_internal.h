@@ -105,18 +105,20 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 // zero on entry (k_validate_seq zeroes the entries it consumed).
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
-                                   uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
-                                   uint32_t n_tiles, hipStream_t s);
+                                   uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s);
 // In-order validation of a speculative batch; writes results and commits
 // binds to the table. Single workgroup.
 // Global speculative top-4 keys per pod (top[p*4 + r]) from the per-tile lists.
-hipError_t launch_topk_merge(const unsigned long long *tile_keys, uint32_t n_pods, uint32_t n_tiles,
-                             unsigned long long *top, hipStream_t s);
+// Per pod: global speculative top-4 from the tile lists, the speculative
+// winner (rank 0) and the filters of tiles with no feasible row.
+hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
+                             uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
+                             hipStream_t s);
 // stats: u32[6] = overflow flags, re-swept tiles, recomputed entries, pods,
 // speculation misses, pods whose speculative winner was touched.
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys,
-                               const uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
+                               const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
                                const unsigned long long *top4, uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out, ms_result *results, uint32_t *stats, hipStream_t s);
 // Rows the sequential engine's validator supports (tile lists held in registers).
 uint32_t seq_max_rows();

@@ -650,8 +650,7 @@ static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort
 template <bool kHuge>
 __device__ __forceinline__ void sweep_topk_pods(const FullRow *x, uint32_t ord0, const PodLanes &m, uint32_t pbeg,
                                                 uint32_t cnt, uint32_t lane, uint32_t tile, uint32_t n_tiles,
-                                                u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags,
-                                                u64 *__restrict__ spec, uint32_t *__restrict__ spec_flags) {
+                                                u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
     for (uint32_t i = 0; i < cnt; ++i) {
         const uint32_t p = pbeg + i;
         const PodFull q = pod_of_lane(m, i);
@@ -685,11 +684,7 @@ __device__ __forceinline__ void sweep_topk_pods(const FullRow *x, uint32_t ord0,
         const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
         const size_t cell = (size_t)p * n_tiles + tile;
         if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out;
-        if (lane == 0) {
-            tile_flags[cell] = f;
-            if (out) atomicMax(&spec[p], out);  // speculative global winner (zeroed by the validator)
-            else if (f) atomicOr(&spec_flags[p], f);  // filters of tiles with no feasible row
-        }
+        if (lane == 0) tile_flags[cell] = f;
     }
 }
 
@@ -697,9 +692,7 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
                                                                   const ms_pod_rec *__restrict__ pods,
                                                                   uint32_t n_pods, uint32_t chunk, uint32_t seed32,
                                                                   u64 *__restrict__ tile_keys,
-                                                                  uint32_t *__restrict__ tile_flags,
-                                                                  u64 *__restrict__ spec,
-                                                                  uint32_t *__restrict__ spec_flags, uint32_t n_tiles) {
+                                                                  uint32_t *__restrict__ tile_flags, uint32_t n_tiles) {
     const uint32_t lane = lane_id();
     const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
     if (tile >= n_tiles) return;  // wave-uniform; no block barriers in this kernel
@@ -711,8 +704,8 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
     const uint32_t pbeg = blockIdx.y * chunk;
     const uint32_t cnt = min(min(chunk, 64u), n_pods - pbeg);  // host: chunk <= 64
     const PodLanes m = stage_pods(pods, pbeg, cnt, lane, seed32);
-    if (rows_huge(x)) sweep_topk_pods<true>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags, spec, spec_flags);
-    else sweep_topk_pods<false>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags, spec, spec_flags);
+    if (rows_huge(x)) sweep_topk_pods<true>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags);
+    else sweep_topk_pods<false>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags);
 }
 
 // ----------------------------------------------------------------------------
@@ -721,23 +714,28 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
 // top r+1, so it is in its tile's list.
 // ----------------------------------------------------------------------------
 template <int J>
-__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys, uint32_t n_pods,
-                                                   uint32_t n_tiles, u64 *__restrict__ top) {
+__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
+                                                   const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
+                                                   uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
+                                                   uint32_t *__restrict__ spec_flags) {
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_pods) return;
     u64 e[J][kTopK];
     uint32_t pos[J];
+    uint32_t fl = 0;  // filters of this lane's tiles that have no feasible row
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const uint32_t tt = lane + 64u * j;
         pos[j] = tt < n_tiles ? 0u : (uint32_t)kTopK;
         const uint32_t tc = min(tt, n_tiles - 1);
+        const uint32_t tf = tile_flags[(size_t)p * n_tiles + tc];
         const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + ((size_t)p * n_tiles + tc) * kTopK);
         const uint4 a = q[0], b = q[1];
         e[j][0] = ((u64)a.y << 32) | a.x;
         e[j][1] = ((u64)a.w << 32) | a.z;
         e[j][2] = ((u64)b.y << 32) | b.x;
         e[j][3] = ((u64)b.w << 32) | b.z;
+        if (tt < n_tiles && e[j][0] == 0) fl |= tf;
     }
     u64 out = 0;
 #pragma unroll
@@ -759,6 +757,12 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
+    // the speculative winner (rank 0) and, when no row is feasible, the filters
+    const uint32_t f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+    if (lane == 0) {
+        spec[p] = out;
+        spec_flags[p] = f;
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1065,8 +1069,8 @@ template <int J>  // tile lists per lane: n_tiles <= 64 * J
 __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_rows,
                                                      const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
                                                      uint32_t seed32, const u64 *__restrict__ tile_keys,
-                                                     const uint32_t *__restrict__ tile_flags, u64 *__restrict__ spec,
-                                                     uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
+                                                     const uint32_t *__restrict__ tile_flags, const u64 *__restrict__ spec,
+                                                     const uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
                                                      uint32_t n_tiles,
                                                      const uint32_t *__restrict__ prev_in,
                                                      uint32_t *__restrict__ prev_out, ms_result *__restrict__ results,
@@ -1105,8 +1109,6 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         S.spec_flags[i] = spec_flags[i];
 #pragma unroll
         for (int k = 0; k < kTopK; ++k) S.top4[i][k] = top4[(size_t)i * kTopK + k];
-        spec[i] = 0;  // the next batch's sweep accumulates here again
-        spec_flags[i] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1576,8 +1578,7 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
-                                   uint32_t *tile_flags, unsigned long long *spec, uint32_t *spec_flags,
-                                   uint32_t n_tiles, hipStream_t s) {
+                                   uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s) {
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
     if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
@@ -1585,13 +1586,13 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::min(64, std::max(1, atoi(e)));
     const dim3 grid(gx, cdiv(n_pods, chunk));
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
-                       tile_keys, tile_flags, spec, spec_flags, n_tiles);
+                       tile_keys, tile_flags, n_tiles);
     return hipGetLastError();
 }
 
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
-                               unsigned long long *spec, uint32_t *spec_flags, const unsigned long long *top4,
+                               const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
                                uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out,
                                ms_result *results, uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
@@ -1608,11 +1609,14 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
     return hipGetLastError();
 }
 
-hipError_t launch_topk_merge(const unsigned long long *tile_keys, uint32_t n_pods, uint32_t n_tiles,
-                             unsigned long long *top, hipStream_t s) {
+hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
+                             uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
+                             hipStream_t s) {
     if (n_pods == 0 || n_tiles == 0) return hipSuccess;
     if (n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
-#define MS_MERGE(J) hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, n_pods, n_tiles, top)
+#define MS_MERGE(J)                                                                                           \
+    hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, tile_flags, n_pods, n_tiles, top, \
+                       spec, spec_flags)
     if (n_tiles <= 64) MS_MERGE(1);
     else if (n_tiles <= 128) MS_MERGE(2);
     else if (n_tiles <= 256) MS_MERGE(4);
