@@ -10,6 +10,8 @@ One step = the whole batch through the hot path with inputs resident in HBM:
   ms_sweep_device (fused filter->score->argmax over this rank's node shard)
   -> all_reduce(keys, MAX) over RCCL (N > 1)
   -> ms_decode_device (packed key -> node / code / score / FitError mask).
+For N > 1 step k's all-reduce overlaps step k+1's sweep and step k's decode
+follows it (two key buffers); the last step is drained before the clock stops.
 value = P * N_total / step time (max over ranks), i.e. whole-job evals/s.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver
@@ -121,9 +123,14 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
-    # N > 1: pod chunks so each chunk's RCCL all-reduce overlaps the next sweep
+    # N > 1: each step's RCCL all-reduce overlaps the next step's sweep (two key
+    # buffers, sharded.CrossStepPipeline); the last step's combine + decode are
+    # drained inside the timed region. MINISCHED_BENCH_PIPE=0 falls back to
+    # in-step pod chunks (MINISCHED_BENCH_CHUNKS) whose reductions overlap the
+    # following chunk's sweep.
+    pipe = world > 1 and os.environ.get("MINISCHED_BENCH_PIPE", "1") != "0"
     chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
-    cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks)
+    cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe)
     results = cyc.results
 
     sweep_events = []
@@ -140,6 +147,7 @@ def main():
 
     for _ in range(args.warmup):
         step(False)
+    cyc.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -147,6 +155,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
+    cyc.finish()  # pipelined: the last step's combine + decode
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -211,6 +220,7 @@ def main():
             "pods_per_s": P * args.steps / elapsed,
             "device_ms_per_step": step_dev_ms,
             "pod_chunks": len(cyc.chunks),
+            "cross_step_pipeline": pipe,
             "pods_scheduled": ok,
             "roofline": {
                 "bound": "hbm",

@@ -216,9 +216,11 @@ __device__ __forceinline__ uint32_t gather4(uint32_t x, int bit) {
 // complements; 0xFF ("no digit") is 15 in the low nibble and matches nothing.
 __device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ nflags,
                                                    const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-                                                   uint32_t row0, Bits32Cols &c) {
+                                                   uint32_t row0, uint32_t rpl, Bits32Cols &c) {
+    // rows row0 .. row0+rpl-1 (rpl <= 32 rows per lane, wave-uniform); slots >= rpl are absent
     uint32_t dv[8], fv[8];
-    if (row0 + 32 <= n_rows) {
+    const bool full = row0 + rpl <= n_rows;  // lane-varying only in a shard's last wave
+    if (rpl == 32u && full) {
         const uint4 *dp = reinterpret_cast<const uint4 *>(ndigit + row0);
         const uint4 *fp = reinterpret_cast<const uint4 *>(nflags + row0);
         const uint4 d0 = dp[0], d1 = dp[1], f0 = fp[0], f1 = fp[1];
@@ -226,6 +228,15 @@ __device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ n
         dv[4] = d1.x; dv[5] = d1.y; dv[6] = d1.z; dv[7] = d1.w;
         fv[0] = f0.x; fv[1] = f0.y; fv[2] = f0.z; fv[3] = f0.w;
         fv[4] = f1.x; fv[5] = f1.y; fv[6] = f1.z; fv[7] = f1.w;
+    } else if ((rpl & 3u) == 0u && full) {  // row0 % 4 == 0: dword loads
+        const uint32_t *dp = reinterpret_cast<const uint32_t *>(ndigit + row0);
+        const uint32_t *fp = reinterpret_cast<const uint32_t *>(nflags + row0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool in = 4u * k < rpl;
+            dv[k] = in ? dp[k] : 0xFFFFFFFFu;
+            fv[k] = in ? fp[k] : kNodeAbsent * 0x01010101u;
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -234,8 +245,9 @@ __device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ n
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t r = row0 + 4 * k + j;
-                dv[k] |= (r < n_rows ? (uint32_t)ndigit[r] : 0xFFu) << (8 * j);
-                fv[k] |= (r < n_rows ? (uint32_t)nflags[r] : (uint32_t)kNodeAbsent) << (8 * j);
+                const bool in = (uint32_t)(4 * k + j) < rpl && r < n_rows;
+                dv[k] |= (in ? (uint32_t)ndigit[r] : 0xFFu) << (8 * j);
+                fv[k] |= (in ? (uint32_t)nflags[r] : (uint32_t)kNodeAbsent) << (8 * j);
             }
         }
     }
@@ -330,22 +342,22 @@ __device__ __forceinline__ void pair_winners(uint32_t ca, uint32_t cb, u64 va, u
 template <bool WANT_FLAGS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v6(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk, u64 *__restrict__ keys,
-    uint32_t *__restrict__ pflags) {
+    uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
+    u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
     __shared__ uint32_t raw[10][64];  // one-hot masks for tolerating pods
     const uint32_t lane = lane_id();
-    const uint32_t wave_row0 = blockIdx.x * kK1WaveRows;
+    const uint32_t wave_row0 = blockIdx.x * 64u * rpl;
     const uint32_t pbeg = blockIdx.y * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
     if (wave_row0 >= n_rows || pbeg >= pend) return;  // wave-uniform
-    const uint32_t row0 = wave_row0 + lane * 32u;
+    const uint32_t row0 = wave_row0 + lane * rpl;
 
     u32x16 tabN;  // [d] = rows with digit d passing NodeUnschedulable for a non-tolerating pod
     uint32_t feasN, feasT;
     bool wave_unsched;
     {
         Bits32Cols c;
-        load_bits32_planes(nflags, ndigit, n_rows, row0, c);
+        load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
         feasN = ~(c.absent | c.unsched);
         feasT = ~c.absent;
         tabN = (u32x16)(0u);
@@ -406,7 +418,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
         // flush: lane j holds pod g+j's wave winner -> packed key (minisched_gpu.h)
         const uint32_t L = m_info & 127u;
         if (lane < gn && L < 64u) {
-            const uint32_t ord = node_base + wave_row0 + L * 32u + (31u - (m_key & 31u));
+            const uint32_t ord = node_base + wave_row0 + L * rpl + (31u - (m_key & 31u));
             atomicMax(&keys[g + lane], make_key((m_info & 128u) ? 10u : 0u, m_key & ~31u, ord));
         }
         if (WANT_FLAGS && lane < gn && myflag) atomicOr(&pflags[g + lane], myflag);
@@ -1509,11 +1521,24 @@ static int k1_variant() {
     return K1_V6;
 }
 
-// One-round grid: as many pod chunks as resident waves allow, so every
-// wave sweeps the same pod count in a single round. MINISCHED_K1_ROUNDS
-// (default 1) multiplies the pod chunks for experiments.
-typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, const uint2 *, uint32_t, uint32_t,
-                         unsigned long long *, uint32_t *);
+// Geometry. Rows: the shard's rows are spread evenly over ceil(n_rows/2048)
+// waves at rpl <= 32 rows per lane (a multiple of 4 when that keeps the wave
+// count, so the tile loads stay dword-aligned); a small shard (12.5k rows at
+// 8 GPUs) then has no near-empty last wave, whose pods would cost as much as a
+// full wave's. Pods: a one-round grid, as many pod chunks as resident waves
+// allow, so every wave sweeps the same pod count in a single round; chunks are
+// even (pods are read in pairs). MINISCHED_K1_ROUNDS (default 1) multiplies
+// the pod chunks and MINISCHED_K1_RPL fixes rpl, for experiments.
+typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, uint32_t, const uint2 *, uint32_t,
+                         uint32_t, unsigned long long *, uint32_t *);
+
+static uint32_t k1_rows_per_lane(uint32_t n_rows) {
+    if (const char *e = getenv("MINISCHED_K1_RPL")) return (uint32_t)std::min(32, std::max(1, atoi(e)));
+    const uint32_t waves = std::max(1u, cdiv(n_rows, kK1WaveRows));
+    const uint32_t r = std::max(1u, cdiv(n_rows, 64u * waves));
+    const uint32_t r4 = (r + 3u) & ~3u;
+    return cdiv(n_rows, 64u * r4) == waves ? r4 : r;
+}
 
 template <bool WANT_FLAGS>
 static hipError_t launch_v6(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
@@ -1528,13 +1553,14 @@ static hipError_t launch_v6(const NodeTable &t, uint32_t n_rows, const uint2 *ps
     }
     uint32_t rounds = 1;
     if (const char *r = getenv("MINISCHED_K1_ROUNDS")) rounds = (uint32_t)std::max(1, atoi(r));
-    const uint32_t gx = cdiv(n_rows, kK1WaveRows);
+    const uint32_t rpl = k1_rows_per_lane(n_rows);
+    const uint32_t gx = cdiv(n_rows, 64u * rpl);
     const uint32_t resident = (uint32_t)blocks_per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
     uint32_t chunks = std::max<uint32_t>(1, resident / gx) * rounds;
-    chunks = std::min<uint32_t>(chunks, cdiv(n_pods, 64));
-    const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 64) * 64;
-    hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags, t.digit, n_rows, t.base, ps,
-                       n_pods, chunk, keys, flags);
+    chunks = std::min<uint32_t>(chunks, cdiv(n_pods, 2));
+    const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 2) * 2;
+    hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags, t.digit, n_rows, t.base, rpl,
+                       ps, n_pods, chunk, keys, flags);
     return hipGetLastError();
 }
 

@@ -60,19 +60,65 @@ def chunk_bounds(n: int, chunks: int):
     return [(a, min(n, a + step)) for a in range(0, n, step)]
 
 
+class CrossStepPipeline:
+    """Overlaps batch k's cross-shard combine with batch k+1's sweep.
+
+    Two key buffers alternate between batches. step(batch) sweeps the batch
+    into its buffer, starts the async combine of that buffer, then waits for
+    the PREVIOUS batch's combine and decodes it; finish() drains the last one.
+    On the device stream this orders  sweep k+1 -> wait(combine k) -> decode k,
+    so the collective of batch k runs while batch k+1 sweeps. Buffer b is
+    swept again only two batches later, after its decode (stream order).
+
+    sweep(buf, batch), decode(buf, batch): enqueue work; combine(buf) -> list
+    of async works (torch.distributed) whose wait() orders the caller's stream.
+    """
+
+    def __init__(self, sweep, combine, decode):
+        self._sweep, self._combine, self._decode = sweep, combine, decode
+        self._n = 0
+        self._pending = None  # (works, buf, batch)
+
+    def step(self, batch=None):
+        buf = self._n & 1
+        self._n += 1
+        self._sweep(buf, batch)
+        works = self._combine(buf)
+        self._drain()
+        self._pending = (works, buf, batch)
+
+    def _drain(self):
+        if self._pending is not None:
+            works, buf, batch = self._pending
+            self._pending = None
+            for w in works:
+                w.wait()
+            self._decode(buf, batch)
+
+    def finish(self):
+        self._drain()
+
+
 class ShardedCycle:
     """One rank's engine + device buffers for a fixed pod batch (bench / service loop).
 
     step() = per pod chunk: sweep this rank's node shard, then an async RCCL
     MAX all-reduce of the chunk's keys that overlaps the next chunk's sweep;
     finally decode every chunk once its reduction has landed.
+
+    With pipeline=True (N > 1) a step is instead one whole-batch sweep whose
+    all-reduce overlaps the NEXT step's sweep (CrossStepPipeline, two key
+    buffers); the step's decode lands one step later and finish() drains the
+    last one. Pod chunks within a step cost more sweep time than the overlap
+    saves at small shards (tools/shard_probe.py), so the pipelined form uses
+    one chunk.
     """
 
     POD_BYTES = 40
     RESULT_BYTES = 24
 
     def __init__(self, engine, n_nodes_global: int, n_pods: int, pods_dev, stream, want_flags: bool = False,
-                 group=None, chunks: int = 1):
+                 group=None, chunks: int = 1, pipeline: bool = False):
         import torch
 
         self.eng = engine
@@ -82,27 +128,39 @@ class ShardedCycle:
         self.stream = stream
         self.group = group
         dev = pods_dev.device
-        self.keys = torch.empty(n_pods, dtype=torch.int64, device=dev)
-        self.flags = torch.empty(n_pods, dtype=torch.int32, device=dev) if want_flags else None
+        nbuf = 2 if pipeline else 1
+        self._keys = [torch.empty(n_pods, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+        self._flags = ([torch.empty(n_pods, dtype=torch.int32, device=dev) for _ in range(nbuf)]
+                       if want_flags else [None] * nbuf)
+        self.keys, self.flags = self._keys[0], self._flags[0]
         self.results = torch.empty(n_pods * self.RESULT_BYTES, dtype=torch.uint8, device=dev)
-        self.chunks = chunk_bounds(n_pods, chunks)
+        self.chunks = chunk_bounds(n_pods, 1 if pipeline else chunks)
+        self._pipe = None
+        if pipeline:
+            self._pipe = CrossStepPipeline(
+                lambda buf, _b: self.sweep(0, self.P, buf),
+                lambda buf: combine_(self._keys[buf], self._flags[buf], self.group, async_op=True),
+                lambda buf, _b: self.decode(0, self.P, buf))
 
-    def _ptrs(self, a):
+    def _ptrs(self, a, buf=0):
         pods = self.pods.data_ptr() + a * self.POD_BYTES
-        keys = self.keys.data_ptr() + a * 8
-        flags = self.flags.data_ptr() + a * 4 if self.flags is not None else 0
+        keys = self._keys[buf].data_ptr() + a * 8
+        flags = self._flags[buf].data_ptr() + a * 4 if self._flags[buf] is not None else 0
         return pods, keys, flags
 
-    def sweep(self, a, b):
-        pods, keys, flags = self._ptrs(a)
+    def sweep(self, a, b, buf=0):
+        pods, keys, flags = self._ptrs(a, buf)
         self.eng.sweep_device(b - a, pods, keys, flags, self.stream.cuda_stream)
 
-    def decode(self, a, b):
-        pods, keys, flags = self._ptrs(a)
+    def decode(self, a, b, buf=0):
+        pods, keys, flags = self._ptrs(a, buf)
         res = self.results.data_ptr() + a * self.RESULT_BYTES
         self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self.stream.cuda_stream)
 
     def step(self, world: int, on_sweep=None):
+        if self._pipe is not None and world > 1:
+            self._pipe.step()
+            return
         pending = []
         for a, b in self.chunks:
             self.sweep(a, b)
@@ -116,3 +174,8 @@ class ShardedCycle:
                 for w in pending[i]:
                     w.wait()
             self.decode(a, b)
+
+    def finish(self):
+        """Drains a pipelined step's pending combine + decode (no-op otherwise)."""
+        if self._pipe is not None:
+            self._pipe.finish()

@@ -89,6 +89,23 @@ def test_nunn_random_sizes(oracle, k1_variant, n_nodes, n_pods):
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 
+@pytest.mark.parametrize("rpl", [None, "1", "7", "28", "29", "31", "32"])
+@pytest.mark.parametrize("n_nodes,node_base", [(12_500, 37_500), (25_000, 0), (3001, 99_000)])
+def test_nunn_rows_per_lane(oracle, monkeypatch, rpl, n_nodes, node_base):
+    # K1's row geometry (rows per lane, balanced waves over a shard, byte/dword/vector
+    # tile loads) and the global-ordinal arithmetic of a shard that starts at node_base
+    if rpl is not None:
+        monkeypatch.setenv("MINISCHED_K1_RPL", rpl)
+    seed = 77 + n_nodes
+    nr = synth.nodes(n_nodes, seed=seed, start=node_base)
+    pr = synth.pods(1000, seed=seed)
+    pr["tolerates_unschedulable"][::9] = 1
+    nr["name_digit"][::13] = 0xFF
+    o = oracle.schedule(nr, pr, seed=seed, node_base=node_base)
+    with engine_with(nr, seed=seed, node_base=node_base) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+
+
 def test_nunn_edge_cases(oracle, k1_variant):
     pr = synth.pods(130, seed=4)
     # empty table: FitError with an empty mask

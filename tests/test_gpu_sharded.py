@@ -1,0 +1,78 @@
+"""N > 1 bench path on one GPU: two ranks (gloo, both on cuda:0) run
+sharded.ShardedCycle exactly as bench.py does — the HIP sweep of each node
+shard, the cross-shard MAX combine, the decode — in both the pipelined
+(cross-step) and the in-step chunked forms, and every rank's decoded results
+must equal the oracle's over the whole cluster.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from minisched_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+N_NODES, N_PODS, SEED = 30_000, 5_000, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, pipeline, chunks, q):
+    import torch
+    import torch.distributed as dist
+
+    from minisched_amd import _lib, sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = sharded.shard_bounds(N_NODES, rank, world)
+        eng = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NN, node_base=lo, seed=SEED)
+        eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=SEED, start=lo))
+        eng.flush()
+        pods = torch.from_numpy(synth.pods(N_PODS, seed=SEED).view(np.uint8).copy()).to(dev)
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
+        cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, chunks=chunks, pipeline=pipeline)
+        for _ in range(3):
+            cyc.step(world)
+        cyc.finish()
+        torch.cuda.synchronize()
+        res = cyc.results.cpu().numpy().view(_lib.RESULT).copy()
+        eng.close()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception as e:  # reported to the parent, which fails the test
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.parametrize("pipeline,chunks", [(True, 1), (False, 3)])
+def test_two_rank_sharded_cycle_on_gpu(oracle, pipeline, chunks):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pipeline, chunks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=110) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [e for _, _, e in got if e]
+    assert not errs, errs
+    o = oracle.schedule(synth.nodes(N_NODES, seed=SEED), synth.pods(N_PODS, seed=SEED), seed=SEED)
+    for rank, res, _ in got:
+        for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
+            assert np.array_equal(res[k_res], o[k_or]), f"rank {rank} {k_res}"

@@ -117,3 +117,60 @@ def test_chunk_bounds():
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert all(a % 64 == 0 for a, _ in spans)
             assert len(spans) <= c
+
+
+def _pipe_worker(rank, world, port, n_nodes, batches, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "mini-kube-scheduler_amd"))
+    import _oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nr = synth.nodes(n_nodes, seed=21)
+    lo, hi = sharded.shard_bounds(n_nodes, rank, world)
+    keys = [torch.zeros(batches[0], dtype=torch.int64) for _ in range(2)]
+    out = {}
+
+    def sweep(buf, k):  # this rank's shard of batch k (the oracle stands in for the HIP sweep)
+        pr = synth.pods(batches[k], seed=100 + k)
+        o = _oracle.schedule(nr[lo:hi], pr, seed=21, node_base=lo)
+        keys[buf][: batches[k]] = torch.from_numpy(o["key"].view(np.int64).copy())
+
+    def combine(buf):
+        return sharded.combine_(keys[buf], None, async_op=True)
+
+    def decode(buf, k):
+        out[k] = keys[buf][: batches[k]].numpy().view(np.uint64).copy()
+
+    pipe = sharded.CrossStepPipeline(sweep, combine, decode)
+    for k in range(len(batches)):
+        pipe.step(k)
+        assert len(out) == k  # batch k decodes one step later
+    pipe.finish()
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_cross_step_pipeline_gloo(oracle):
+    # bench.py's N > 1 step: batch k's all-reduce overlaps batch k+1's sweep, two
+    # key buffers alternate; every batch must decode to the single-process result
+    world, n_nodes, batches = 2, 1500, [256, 200, 256, 131, 256]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, n_nodes, batches, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nr = synth.nodes(n_nodes, seed=21)
+    for k, n in enumerate(batches):
+        full = oracle.schedule(nr, synth.pods(n, seed=100 + k), seed=21)
+        for rank, out in got:
+            assert np.array_equal(out[k], full["key"]), f"rank {rank} batch {k}"
