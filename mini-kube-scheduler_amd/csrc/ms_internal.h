@@ -28,7 +28,6 @@ constexpr uint32_t kGolden32 = 0x9E3779B1u;  // LDS map hashing in the validator
 
 // K1 v5 geometry: a wave owns 64 lanes x 32 rows; the pod stream is padded
 // so the sweep's one-step-ahead prefetch of a pod pair stays in bounds.
-constexpr uint32_t kK1WaveRows = 64u * 32u;  // K1 rows per wave at most (32 per lane)
 constexpr uint32_t kPodStreamPad = 4;
 
 // Device-resident node table, structure of arrays, indexed by LOCAL ordinal.

@@ -1521,20 +1521,31 @@ static int k1_variant() {
     return K1_V6;
 }
 
-// Geometry. Rows: the shard's rows are spread evenly over ceil(n_rows/2048)
-// waves at rpl <= 32 rows per lane (a multiple of 4 when that keeps the wave
-// count, so the tile loads stay dword-aligned); a small shard (12.5k rows at
-// 8 GPUs) then has no near-empty last wave, whose pods would cost as much as a
-// full wave's. Pods: a one-round grid, as many pod chunks as resident waves
-// allow, so every wave sweeps the same pod count in a single round; chunks are
-// even (pods are read in pairs). MINISCHED_K1_ROUNDS (default 1) multiplies
-// the pod chunks and MINISCHED_K1_RPL fixes rpl, for experiments.
+// Geometry. Rows: at most kK1MaxRpl = 28 rows per lane. The candidate loop
+// runs to the LANE MAXIMUM of a pod's candidates, which grows with the rows a
+// lane holds; 28 beat 32 at every shard size measured (config C 0.586 vs
+// 0.601 ms, 25k rows 0.162 vs 0.177, 12.5k rows 0.094 vs 0.109;
+// profiles/r01e_rpl_sweep.jsonl) despite 14% more waves. A shard's rows are
+// spread evenly over its waves (no near-empty last wave, whose pods would cost
+// a full wave's), rounded up to a multiple of 4 when that keeps the wave count
+// so the tile loads stay dword-aligned (the byte-load path costs ~8%).
+// Pods: each wave sweeps a chunk of at most kK1WavePods = 96 pods (even: pods
+// are read in pairs), fewer when one round of resident waves already covers
+// the batch. Short waves in several rounds let the dispatcher even out the
+// SIMDs: config C runs 0.589 ms with one round of 685-pod waves and 0.537 ms
+// with ~85-pod waves; small shards are best near one round (12.5k rows: 86
+// pods per wave; profiles/r01e_k1_rounds.jsonl, r01e_k1_chunk.jsonl). MINISCHED_K1_ROUNDS=r
+// instead splits the one-round chunk r ways, MINISCHED_K1_CHUNK fixes the chunk
+// and MINISCHED_K1_RPL the rows per lane (<= 32), for experiments.
 typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, uint32_t, const uint2 *, uint32_t,
                          uint32_t, unsigned long long *, uint32_t *);
 
+constexpr uint32_t kK1MaxRpl = 28;
+constexpr uint32_t kK1WavePods = 96;
+
 static uint32_t k1_rows_per_lane(uint32_t n_rows) {
     if (const char *e = getenv("MINISCHED_K1_RPL")) return (uint32_t)std::min(32, std::max(1, atoi(e)));
-    const uint32_t waves = std::max(1u, cdiv(n_rows, kK1WaveRows));
+    const uint32_t waves = std::max(1u, cdiv(n_rows, 64u * kK1MaxRpl));
     const uint32_t r = std::max(1u, cdiv(n_rows, 64u * waves));
     const uint32_t r4 = (r + 3u) & ~3u;
     return cdiv(n_rows, 64u * r4) == waves ? r4 : r;
@@ -1551,14 +1562,14 @@ static hipError_t launch_v6(const NodeTable &t, uint32_t n_rows, const uint2 *ps
         if (e != hipSuccess) return e;
         blocks_per_cu = nb > 0 ? nb : 1;
     }
-    uint32_t rounds = 1;
-    if (const char *r = getenv("MINISCHED_K1_ROUNDS")) rounds = (uint32_t)std::max(1, atoi(r));
     const uint32_t rpl = k1_rows_per_lane(n_rows);
     const uint32_t gx = cdiv(n_rows, 64u * rpl);
     const uint32_t resident = (uint32_t)blocks_per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
-    uint32_t chunks = std::max<uint32_t>(1, resident / gx) * rounds;
-    chunks = std::min<uint32_t>(chunks, cdiv(n_pods, 2));
-    const uint32_t chunk = cdiv(cdiv(n_pods, chunks), 2) * 2;
+    const uint32_t one_round = cdiv(cdiv(n_pods, std::max<uint32_t>(1, resident / gx)), 2) * 2;
+    uint32_t chunk = std::min(one_round, kK1WavePods);
+    if (const char *r = getenv("MINISCHED_K1_ROUNDS"))
+        chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 2) * 2;
+    if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(2, atoi(c)), 2) * 2;
     hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags, t.digit, n_rows, t.base, rpl,
                        ps, n_pods, chunk, keys, flags);
     return hipGetLastError();
