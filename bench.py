@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
 METRIC = "pod×node filter+score evals/sec and pods scheduled/sec at 100k nodes, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_EVAL = {"NU+NN": 2, "NU+NRF+NN+LA": 58}
-K1_KERNELS = {"v0": "k_sweep_nunn", "v6": "k_sweep_nunn_v6"}
+K1_KERNELS = {"v0": "k_sweep_nunn", "v7": "k_sweep_nunn_v7"}
 
 
 def parse():
@@ -189,7 +189,7 @@ def main():
         if os.path.exists(args.traffic_json) and world == 1:
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("kernel") == K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v6")):
+                if tj.get("kernel") == K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v7")):
                     traffic = tj.get("hbm_bytes_per_launch")
                     # the sweep keeps node columns in registers, so issue, not HBM, binds it
                     limiter = {"kind": "VALU issue", "valu_busy_frac": tj.get("valu_busy_frac"),
@@ -229,7 +229,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v6"), "k_sweep_nunn_v6"),
+                "kernel": K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v7"), "k_sweep_nunn_v7"),
                 "kernel_ms": sweep_ms,
                 "algorithmic_bytes_per_launch": local_evals * BYTES_PER_EVAL[plugins],
                 "limiter": limiter,

@@ -22,11 +22,12 @@
  * split across GPUs. The tie-break that replaces rand.Intn
  * (minisched.go:316-321) is the packed key
  *     key = score<<52 | h32(seed,pod,node)<<20 | (0xFFFFF - node),
- *     h32 = mix32(fmix32(seed32 ^ pod_ordinal) + node * 0x9E3779) & ~31,
+ *     h32 = mix32(fmix32(seed32 ^ pod_ordinal) + node * 0x9E3779),
  *     seed32 = (uint32)(seed ^ seed>>32),
- * (rule "r2"; fmix32 = murmur3 finaliser; mix32(x) = x^=x>>16, x*=0x85ebca6b,
- * x^=x>>16, x*=0xc2b2ae35; all arithmetic mod 2^32). Maximum wins: the highest hash, then
- * the lowest ordinal. It is a pure function of (seed, pod, node) so the
+ * (rule "r3"; fmix32 = murmur3 finaliser; mix32(x) = x^=x>>16, x*=0x85ebca6b,
+ * x^=x>>16, x*=0xc2b2ae35; all arithmetic mod 2^32). Maximum wins: the highest
+ * score, then the highest hash. For one pod h32 is a bijection of the node
+ * ordinal, so hashes never tie. It is a pure function of (seed, pod, node) so the
  * result does not depend on scan order, sharding or reduction tree
  * (DESIGN.md §2).
  */

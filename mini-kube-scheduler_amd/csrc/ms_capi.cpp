@@ -374,7 +374,8 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     NodeTable &t = c->t;
     t.cap = cfg->max_nodes;
     t.base = cfg->node_base;
-    bool ok = hipMalloc((void **)&t.flags, n) == hipSuccess && hipMalloc((void **)&t.digit, n) == hipSuccess &&
+    bool ok = hipMalloc((void **)&t.flags, n + kColumnPad) == hipSuccess &&
+              hipMalloc((void **)&t.digit, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.alloc_cpu, n * 8) == hipSuccess &&

@@ -26,9 +26,12 @@ constexpr int kFullTile = kFullThreads * kFullSlots;      // nodes per block
 
 constexpr uint32_t kGolden32 = 0x9E3779B1u;  // LDS map hashing in the validator
 
-// K1 v5 geometry: a wave owns 64 lanes x 32 rows; the pod stream is padded
-// so the sweep's one-step-ahead prefetch of a pod pair stays in bounds.
-constexpr uint32_t kPodStreamPad = 4;
+// K1 v7 reads the pod stream in 8-pod groups, one group ahead; the stream is
+// padded so those reads stay in bounds.
+constexpr uint32_t kPodStreamPad = 16;
+// Bytes of padding after the flags/digit columns: K1 v7 reads a lane's rows
+// as an aligned dword window that may run up to 7 bytes past the last row.
+constexpr uint32_t kColumnPad = 64;
 
 // Device-resident node table, structure of arrays, indexed by LOCAL ordinal.
 struct NodeTable {
@@ -63,13 +66,16 @@ __host__ __device__ inline uint32_t fmix32(uint32_t h) {
 }
 __host__ __device__ inline uint32_t seed32_of(uint64_t seed) { return (uint32_t)(seed ^ (seed >> 32)); }
 
-// Tie-break hash (minisched_gpu.h, rule "r2"; oracle/ms_oracle.c msor_tb_hash):
-//   A = fmix32(seed32 ^ pod_ordinal); h = mix32(A + node_ordinal * kG24) & ~31
+// Tie-break hash (minisched_gpu.h, rule "r3"; oracle/ms_oracle.c msor_tb_hash):
+//   A = fmix32(seed32 ^ pod_ordinal); h = mix32(A + node_ordinal * kG24)
 // mix32(x): x ^= x>>16; x *= 0x85ebca6b; x ^= x>>16; x *= 0xc2b2ae35 (both
 // xor-shifts by 16, one SDWA v_xor each). node_ordinal < 2^20, so the
-// product is one v_mad_u32_u24, and the dropped low 5 bits leave room for a
-// lane's row slot in the sweep's 32-bit lane keys.
+// product is one v_mad_u32_u24. For a fixed pod h is a bijection of the
+// ordinal (odd multipliers, xor-shifts by 16 are involutions), so no two nodes
+// of one pod share a hash and tb_unhash recovers the ordinal from h alone: the
+// sweep reduces bare 32-bit hashes and never carries the row along.
 constexpr uint32_t kG24 = 0x9E3779u;  // odd, 24-bit
+constexpr uint32_t kG24Inv = 0xF2B382C9u;  // kG24^-1 mod 2^32
 __host__ __device__ inline uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x85ebca6bu;
@@ -77,12 +83,21 @@ __host__ __device__ inline uint32_t mix32(uint32_t x) {
     x *= 0xc2b2ae35u;
     return x;
 }
+__host__ __device__ inline uint32_t unmix32(uint32_t h) {
+    h *= 0x7ED1B41Du;  // 0xc2b2ae35^-1
+    h ^= h >> 16;
+    h *= 0xA5CB9243u;  // 0x85ebca6b^-1
+    h ^= h >> 16;
+    return h;
+}
 __host__ __device__ inline uint32_t tb_pod(uint32_t seed32, uint32_t pod_ordinal) {
     return fmix32(seed32 ^ pod_ordinal);
 }
 __host__ __device__ inline uint32_t tb_hash(uint32_t A, uint32_t node_ordinal) {
-    return mix32(A + node_ordinal * kG24) & ~31u;
+    return mix32(A + node_ordinal * kG24);
 }
+// The node ordinal whose tb_hash under pod half A is h.
+__host__ __device__ inline uint32_t tb_unhash(uint32_t A, uint32_t h) { return (unmix32(h) - A) * kG24Inv; }
 
 // ---- launchers (ms_kernels.hip) -------------------------------------------
 // All return hipError_t of the launch; none synchronises.

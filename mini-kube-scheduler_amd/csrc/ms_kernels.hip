@@ -139,8 +139,8 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
 //   .x = A = tb_pod(seed32, ordinal)   (the pod half of the tie-break hash)
 //   .y = class = digit (0..9, 10 = name does not end in a digit) | tolerates << 4
 // Every node wave reads it through the scalar cache, two pods per 16-byte load.
-// The buffer carries kPodStreamPad padding entries so the one-step-ahead
-// prefetch never needs a bounds check.
+// The buffer carries kPodStreamPad padding entries so the sweep's reads of
+// whole 8-pod groups, one group ahead, never need a bounds check.
 // ----------------------------------------------------------------------------
 __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t seed32,
                            uint2 *__restrict__ ps, u64 *__restrict__ keys, uint32_t *__restrict__ flags) {
@@ -157,50 +157,37 @@ __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint
 }
 
 // ----------------------------------------------------------------------------
-// K1 v6, the production NU+NN sweep: bit-sliced node columns, pod classes.
+// K1 v7, the production NU+NN sweep: per-wave candidate lists by pod class.
 //
-// Layout: a wave owns 2048 consecutive rows, 32 per lane, for its whole
-// lifetime, and streams a chunk of pods through them. At load each lane turns
-// its 32 digit bytes into four bit planes and then ten one-hot masks (bit s
+// Layout: a wave owns 64 lanes x rpl (<= 32) consecutive rows for its whole
+// lifetime and streams a chunk of pods through them. At load each lane turns
+// its digit bytes into four bit planes and then ten one-hot row masks (bit s
 // <=> row row0+s has name digit d), and its flag bytes into unschedulable /
-// absent masks. tabN[d] = onehot[d] & (rows passing NodeUnschedulable for a
-// non-tolerating pod) lives in registers; a pod's filter+score over its 32
-// rows is one register read at a wave-uniform index (v_movrels). Tolerating
-// pods (rare) read the raw one-hot masks from LDS behind a wave-uniform
-// branch. Every pair is still evaluated from that node's own columns, 32
-// pairs per register; nothing is shared between pods but the node columns.
+// absent masks. For a non-tolerating pod of digit d the lane's candidates
+// (rows passing NodeUnschedulable that score NodeNumber's 10) are the set bits
+// of onehot[d] & feasible; there are at most K of them per lane when rpl <=
+// 10K (digits of consecutive names cycle). Each lane keeps, per class d, the
+// hash inputs (node_ordinal * kG24) of those rows in K registers, padded with
+// a duplicate of one of the wave's own class-d candidates, so a pod costs K
+// hashes per lane with no bit scanning and no lane-divergent loop: the
+// filter+score of all the lane's rows is the class-list lookup, and the
+// tie-break hash (rule r3) of each candidate is v_add + mix32. A class with
+// more than K candidates in some lane of the wave, a tolerating pod, and a
+// pod whose digit has no feasible row in the wave (every feasible row scores
+// 0) take the general path: the lane's mask from LDS / registers and a
+// branch-free v_ffbl loop over it.
 //
-// Argmax: NodeNumber's only non-zero score is 10, so a wave's best score is
-// 10 as soon as any lane has a candidate (ballot). Each lane then scores its
-// own candidates by the tie-break hash, one v_mad_u32_u24 + mix32 each, into
-// the u32 lane key h27<<5 | (31-slot) (max = highest hash, then lowest row);
-// a DPP max + ballot finds the wave's winner (lowest lane = lowest ordinal on
-// equal hashes). Pods go in pairs: their candidate loops share one
-// lane-divergent, branch-free loop (the carry of cand-1 is the "live"
-// predicate of a v_cndmask, no exec-mask SALU per candidate) and their DPP
-// reductions interleave. A pod's wave result (lane key, winner lane | score
-// flag) lands in one lane of two registers (v_writelane); every 64 pods the
-// lanes assemble the 64-bit packed keys and leave as one coalesced atomicMax
-// wave-instruction.
+// Argmax: rule r3 makes the hash a bijection of the node ordinal for a pod,
+// so the wave only needs the maximum hash; tb_unhash returns its row. Lane
+// maxima of 8 pods are reduced together by a transposed butterfly
+// (v_permlane32_swap, v_permlane16_swap, one DPP row_ror:8 exchange, then
+// three DPP steps): 2.25 VALU per pod instead of a 6-step DPP chain per pod.
+// The 8 results go to LDS and every 64 pods the lanes unhash and leave as one
+// coalesced atomicMax wave-instruction.
 //
-// Grid: one block = one wave; grid.x = node waves, grid.y = pod chunks sized
-// so that all waves are resident at once (launch_v6).
+// Grid: one block = one wave; grid.x = node waves, grid.y = pod chunks
+// (launch_v7).
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ void wave_max_u32_dpp2(uint32_t &a, uint32_t &b) {
-#define MS_DPP2(CTRL, RM)                                                                       \
-    a = max(a, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, CTRL, RM, 0xF, false));        \
-    b = max(b, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, CTRL, RM, 0xF, false));
-    MS_DPP2(0x111, 0xF)  // row_shr:1
-    MS_DPP2(0x112, 0xF)  // row_shr:2
-    MS_DPP2(0x114, 0xF)  // row_shr:4
-    MS_DPP2(0x118, 0xF)  // row_shr:8
-    MS_DPP2(0x142, 0xA)  // row_bcast:15
-    MS_DPP2(0x143, 0xC)  // row_bcast:31
-#undef MS_DPP2
-    a = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
-    b = (uint32_t)__builtin_amdgcn_readlane((int)b, 63);
-}
-
 struct Bits32Cols {
     uint32_t onehot[10];
     uint32_t unsched, absent;
@@ -211,31 +198,34 @@ __device__ __forceinline__ uint32_t gather4(uint32_t x, int bit) {
     return ((((x >> bit) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
 }
 
-// Bit planes of the 32 digit bytes (bit i of every byte in one register, four
-// rows per multiply), then onehot[v] = AND of the four planes or their
+// Bit planes of the lane's digit bytes (bit i of every byte in one register,
+// four rows per multiply), then onehot[v] = AND of the four planes or their
 // complements; 0xFF ("no digit") is 15 in the low nibble and matches nothing.
+// Rows row0 .. row0+rpl-1 (rpl <= 32, wave-uniform); slots >= rpl are absent.
+// The columns carry 64 bytes of padding, so the aligned dword window of a
+// full lane may read up to 7 bytes past row0 + rpl.
 __device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ nflags,
                                                    const uint8_t *__restrict__ ndigit, uint32_t n_rows,
                                                    uint32_t row0, uint32_t rpl, Bits32Cols &c) {
-    // rows row0 .. row0+rpl-1 (rpl <= 32 rows per lane, wave-uniform); slots >= rpl are absent
     uint32_t dv[8], fv[8];
-    const bool full = row0 + rpl <= n_rows;  // lane-varying only in a shard's last wave
-    if (rpl == 32u && full) {
-        const uint4 *dp = reinterpret_cast<const uint4 *>(ndigit + row0);
-        const uint4 *fp = reinterpret_cast<const uint4 *>(nflags + row0);
-        const uint4 d0 = dp[0], d1 = dp[1], f0 = fp[0], f1 = fp[1];
-        dv[0] = d0.x; dv[1] = d0.y; dv[2] = d0.z; dv[3] = d0.w;
-        dv[4] = d1.x; dv[5] = d1.y; dv[6] = d1.z; dv[7] = d1.w;
-        fv[0] = f0.x; fv[1] = f0.y; fv[2] = f0.z; fv[3] = f0.w;
-        fv[4] = f1.x; fv[5] = f1.y; fv[6] = f1.z; fv[7] = f1.w;
-    } else if ((rpl & 3u) == 0u && full) {  // row0 % 4 == 0: dword loads
-        const uint32_t *dp = reinterpret_cast<const uint32_t *>(ndigit + row0);
-        const uint32_t *fp = reinterpret_cast<const uint32_t *>(nflags + row0);
+    if (row0 + rpl <= n_rows) {  // lane-varying only in a shard's last wave
+        const uint32_t *dp = reinterpret_cast<const uint32_t *>(ndigit + (row0 & ~3u));
+        const uint32_t *fp = reinterpret_cast<const uint32_t *>(nflags + (row0 & ~3u));
+        const uint32_t sh = (row0 & 3u) * 8u;
+        uint32_t dw[9], fw[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const bool in = 4u * k < rpl + 3u;  // wave-uniform: skip dwords past the lane's rows
+            dw[k] = in ? dp[k] : 0xFFFFFFFFu;
+            fw[k] = in ? fp[k] : 0u;
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const bool in = 4u * k < rpl;
-            dv[k] = in ? dp[k] : 0xFFFFFFFFu;
-            fv[k] = in ? fp[k] : kNodeAbsent * 0x01010101u;
+            // bytes 4k .. 4k+3 of the lane's window; slots >= rpl become absent
+            const uint32_t nv = rpl > 4u * k ? min(4u, rpl - 4u * k) : 0u;
+            const uint32_t keep = nv >= 4u ? 0xFFFFFFFFu : (1u << (8u * nv)) - 1u;
+            dv[k] = (__builtin_amdgcn_alignbit(dw[k + 1], dw[k], sh) & keep) | ~keep;
+            fv[k] = (__builtin_amdgcn_alignbit(fw[k + 1], fw[k], sh) & keep) | (kNodeAbsent * 0x01010101u & ~keep);
         }
     } else {
 #pragma unroll
@@ -266,23 +256,6 @@ __device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ n
                       ((v & 8) ? pl[3] : ~pl[3]);
 }
 
-// v_writelane_b32: lane `lane` of v takes the wave-uniform value x. gfx950
-// VOP3 reads one SGPR per instruction, so a dynamic lane index goes through
-// m0; the asm sets m0 itself right before the write, and the kernels using it
-// keep nothing of their own in m0 (checked in `make asm`), hence the pragma.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t lane) {
-    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(v)
-                 : "s"(__builtin_amdgcn_readfirstlane(x)), "s"(__builtin_amdgcn_readfirstlane(lane))
-                 : "m0");
-    return v;
-}
-#pragma clang diagnostic pop
-
-typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
-
 // Row slot of the lowest candidate (v_ffbl; 0xFFFFFFFF for an empty mask).
 __device__ __forceinline__ uint32_t first_slot(uint32_t m) {
     uint32_t s;
@@ -290,61 +263,88 @@ __device__ __forceinline__ uint32_t first_slot(uint32_t m) {
     return s;
 }
 
-// Lane key of slot s: (tb_hash & ~31) | (31 - s). AH = A + (ordinal of row0) * kG24.
-__device__ __forceinline__ uint32_t lane_key(uint32_t AH, uint32_t s) {
-    const uint32_t h = mix32(AH + __umul24(s, kG24));  // s < 32: v_mad_u32_u24
-    uint32_t k;  // bit i = ((31 >> i) & 1) ? ~s : h
-    asm("v_bitop3_b32 %0, %1, 31, %2 bitop3:0x74" : "=v"(k) : "v"(h), "v"(s));
-    return k;
-}
+typedef uint32_t u32x10 __attribute__((ext_vector_type(10)));
 
-struct PodLane6 {
-    uint32_t AH;    // A + hterm0
-    uint32_t cand;  // candidates not yet hashed
-    uint32_t kb;    // lane best key
+template <int K>
+struct ClassLists {
+    u32x10 h[K];  // h[i][d]: node_ordinal * kG24 of the lane's i-th class-d candidate (padded)
 };
 
-// one candidate step without exec masking: dead lanes (cand == 0) keep kb
-__device__ __forceinline__ void pod_step6(PodLane6 &q) {
-    const uint32_t s = first_slot(q.cand);
-    const bool live = q.cand != 0;  // = carry of cand + 0xFFFFFFFF
-    q.cand &= q.cand - 1;
-    const uint32_t k = lane_key(q.AH, s);
-    q.kb = live ? max(q.kb, k) : q.kb;
-}
-
-// Wave winners of two pods: candidate rows ca/cb (lanes with any: va/vb),
-// AH = A + hterm0. L = winner lane (64: no feasible row), kL = its lane key.
-__device__ __forceinline__ void pair_winners(uint32_t ca, uint32_t cb, u64 va, u64 vb, uint32_t AHa, uint32_t AHb,
-                                             uint32_t &La, uint32_t &kLa, uint32_t &Lb, uint32_t &kLb) {
-    PodLane6 a, b;
-    a.AH = AHa;
-    b.AH = AHb;
-    a.kb = lane_key(a.AH, first_slot(ca));  // lowest candidate; garbage on empty lanes, masked below
-    b.kb = lane_key(b.AH, first_slot(cb));
-    a.cand = ca & (ca - 1);
-    b.cand = cb & (cb - 1);
-    while (a.cand | b.cand) {  // lane-divergent trip count, branch-free body
-        pod_step6(a);
-        pod_step6(b);
+// Per-lane maximum of 8 registers, reduced over the wave; pod j's maximum
+// lands in lanes 8k with j = rev3(k) (lanes 0, 8, .., 56 hold pods 0, 4, 2, 6,
+// 1, 5, 3, 7). Other lanes hold partial maxima.
+__device__ __forceinline__ uint32_t reduce8(const uint32_t (&r)[8], uint32_t lane) {
+    uint32_t s[4], t[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // lanes < 32: pod 2i, lanes >= 32: pod 2i+1
+        const auto p = __builtin_amdgcn_permlane32_swap(r[2 * i], r[2 * i + 1], false, false);
+        s[i] = max((uint32_t)p[0], (uint32_t)p[1]);
     }
-    uint32_t ka = ca != 0 ? a.kb : 0u, kbm = cb != 0 ? b.kb : 0u;
-    wave_max_u32_dpp2(ka, kbm);
-    // same 27-bit hash as the max (lane keys never exceed it): lowest lane wins
-    const u64 wa = __ballot(a.kb >= (ka & ~31u)) & va;
-    const u64 wb = __ballot(b.kb >= (kbm & ~31u)) & vb;
-    La = wa ? (uint32_t)__builtin_ctzll(wa) : 64u;
-    Lb = wb ? (uint32_t)__builtin_ctzll(wb) : 64u;
-    kLa = (uint32_t)__builtin_amdgcn_readlane((int)a.kb, (int)(La & 63u));
-    kLb = (uint32_t)__builtin_amdgcn_readlane((int)b.kb, (int)(Lb & 63u));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // rows 0..3: pods 4i+0, 4i+2, 4i+1, 4i+3
+        const auto p = __builtin_amdgcn_permlane16_swap(s[2 * i], s[2 * i + 1], false, false);
+        t[i] = max((uint32_t)p[0], (uint32_t)p[1]);
+    }
+    // within each row: lanes 0-7 keep t[0]'s pod, lanes 8-15 t[1]'s (row_ror:8 = lane ^ 8)
+    const bool hi8 = (lane & 8u) != 0;
+    const uint32_t keep = hi8 ? t[1] : t[0], send = hi8 ? t[0] : t[1];
+    uint32_t u = max(keep, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x128, 0xF, 0xF, false));
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x104, 0xF, 0xF, false)); // row_shl:4
+    return u;
 }
 
-template <bool WANT_FLAGS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v6(
+__device__ __forceinline__ uint32_t rev3(uint32_t k) { return ((k & 1u) << 2) | (k & 2u) | ((k >> 2) & 1u); }
+
+// Wave state a pod is evaluated against.
+template <int K>
+struct WaveRows {
+    ClassLists<K> L;
+    uint32_t feasN, feasT;  // rows passing NodeUnschedulable for a non-tolerating / tolerating pod
+    uint32_t hterm0;        // (ordinal of the lane's first row) * kG24
+    uint32_t fast;          // wave-uniform: bit d = class d takes the list path
+};
+
+// One pod (pod stream entry: A, cls). Returns the lane's maximum candidate
+// hash (only meaningful when the wave has a candidate: *found).
+template <int K>
+__device__ __forceinline__ uint32_t eval_pod(const WaveRows<K> &w, const uint32_t (*raw)[64], uint32_t lane,
+                                             uint32_t A, uint32_t cls, bool &found, bool &s10) {
+    if ((w.fast >> cls) & 1u) {  // cls < 10: not tolerating, class lists fit
+        uint32_t h[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) h[i] = mix32(A + w.L.h[i][cls]);
+        uint32_t kb = h[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i) kb = max(kb, h[i]);
+        found = s10 = true;
+        return kb;
+    }
+    const uint32_t d = cls & 15u;
+    const bool tol = cls >= 16u;
+    uint32_t m = d < 10u ? (raw[d][lane] & (tol ? w.feasT : w.feasN)) : 0u;
+    s10 = __ballot(m != 0) != 0;
+    if (!s10) m = tol ? w.feasT : w.feasN;  // no digit match in this wave: every feasible row scores 0
+    found = s10 || __ballot(m != 0) != 0;
+    const uint32_t AH = A + w.hterm0;
+    uint32_t kb = 0;
+    while (__ballot(m != 0)) {  // lane-divergent trip count, branch-free body
+        const uint32_t s = first_slot(m);
+        const bool live = m != 0;
+        m &= m - 1u;
+        kb = max(kb, mix32(live ? AH + __umul24(s, kG24) : 0u));  // mix32(0) = 0
+    }
+    return kb;
+}
+
+template <int K, bool WANT_FLAGS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_sweep_nunn_v7(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
     u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
-    __shared__ uint32_t raw[10][64];  // one-hot masks for tolerating pods
+    __shared__ uint32_t raw[10][64];  // one-hot masks for the general path
+    __shared__ uint32_t slot[64];     // wave maxima of the current 64 pods
     const uint32_t lane = lane_id();
     const uint32_t wave_row0 = blockIdx.x * 64u * rpl;
     const uint32_t pbeg = blockIdx.y * chunk;
@@ -352,76 +352,78 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
     if (wave_row0 >= n_rows || pbeg >= pend) return;  // wave-uniform
     const uint32_t row0 = wave_row0 + lane * rpl;
 
-    u32x16 tabN;  // [d] = rows with digit d passing NodeUnschedulable for a non-tolerating pod
-    uint32_t feasN, feasT;
+    WaveRows<K> w;
     bool wave_unsched;
     {
         Bits32Cols c;
         load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
-        feasN = ~(c.absent | c.unsched);
-        feasT = ~c.absent;
-        tabN = (u32x16)(0u);
+        w.feasN = ~(c.absent | c.unsched);
+        w.feasT = ~c.absent;
+        w.hterm0 = (node_base + row0) * kG24;
+        w.fast = 0;
+        wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
 #pragma unroll
         for (int d = 0; d < 10; ++d) {
-            tabN[d] = c.onehot[d] & feasN;
             raw[d][lane] = c.onehot[d];
+            uint32_t m = c.onehot[d] & w.feasN;
+            const uint32_t cnt = __popc(m);
+            const u64 any = __ballot(m != 0);
+            const bool ovf = __ballot(cnt > (uint32_t)K) != 0;
+            const uint32_t first = w.hterm0 + __umul24(first_slot(m), kG24);
+            const uint32_t donor =
+                (uint32_t)__builtin_amdgcn_readlane((int)first, any ? (int)__builtin_ctzll(any) : 0);
+            const uint32_t pad = cnt ? first : donor;  // a class-d candidate of this wave
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint32_t v = w.hterm0 + __umul24(first_slot(m), kG24);
+                m &= m - 1u;
+                w.L.h[i][d] = (uint32_t)i < cnt ? v : pad;
+            }
+            if (any && !ovf) w.fast |= 1u << d;
         }
-        wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
-        // each wave reads only its own lanes' entries: no workgroup barrier needed
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        // each lane reads only its own raw[][] entries: no barrier needed
     }
-    const uint32_t hterm0 = (node_base + row0) * kG24;
 
     const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
-    uint4 nx = q4[0];
-    for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod groups: one flush each
+    uint4 nx0 = q4[0], nx1 = q4[1], nx2 = q4[2], nx3 = q4[3];
+    for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod blocks: one flush each
         const uint32_t gn = min(64u, pend - g);
-        uint32_t m_key = 0, m_info = 0xFFFFFFFFu, myflag = 0;  // info: winner lane (64: none) | score10 << 7
-        for (uint32_t i = 0; i < gn; i += 2) {
-            const uint4 w = nx;
-            ++q4;
-            nx = q4[0];  // prefetch; the stream is padded past n_pods
-            uint32_t ca, cb;
-            {
-                const uint32_t da = w.y & 15u, db = w.w & 15u;
-                ca = (w.y >= 16) ? (da < 10 ? raw[da][lane] & feasT : 0u) : tabN[da];
-                cb = (w.w >= 16) ? (db < 10 ? raw[db][lane] & feasT : 0u) : tabN[db];
-            }
-            u64 va = __ballot(ca != 0), vb = __ballot(cb != 0);  // lanes holding candidates
-            const bool a10 = va != 0, b10 = vb != 0;               // wave-uniform best score 10
-            uint32_t La, kLa, Lb, kLb;
-            if (a10 && b10) {
-                pair_winners(ca, cb, va, vb, w.x + hterm0, w.z + hterm0, La, kLa, Lb, kLb);
-            } else {  // rare: no digit match in this wave, the pod's feasible rows all score 0
-                if (!a10) {
-                    ca = (w.y >= 16) ? feasT : feasN;
-                    va = __ballot(ca != 0);
+        u64 found = 0, s10m = 0, num = 0;
+        for (uint32_t sub = 0; sub < gn; sub += 8) {
+            const uint32_t e[16] = {nx0.x, nx0.y, nx0.z, nx0.w, nx1.x, nx1.y, nx1.z, nx1.w,
+                                    nx2.x, nx2.y, nx2.z, nx2.w, nx3.x, nx3.y, nx3.z, nx3.w};
+            q4 += 4;
+            nx0 = q4[0];  // prefetch the next 8 pods; the stream is padded past n_pods
+            nx1 = q4[1];
+            nx2 = q4[2];
+            nx3 = q4[3];
+            uint32_t r[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                r[j] = 0;
+                if (sub + j < gn) {
+                    bool f, s;
+                    r[j] = eval_pod<K>(w, raw, lane, e[2 * j], e[2 * j + 1], f, s);
+                    // wave-uniform outcome bits, kept in SGPRs
+                    const uint32_t fs = (uint32_t)__builtin_amdgcn_readfirstlane((f ? 1 : 0) | (s ? 2 : 0));
+                    found |= (u64)(fs & 1u) << (sub + j);
+                    s10m |= (u64)(fs >> 1) << (sub + j);
+                    if (WANT_FLAGS) num |= (u64)(e[2 * j + 1] < 16u && wave_unsched) << (sub + j);
                 }
-                if (!b10) {
-                    cb = (w.w >= 16) ? feasT : feasN;
-                    vb = __ballot(cb != 0);
-                }
-                pair_winners(ca, cb, va, vb, w.x + hterm0, w.z + hterm0, La, kLa, Lb, kLb);
             }
-            m_key = writelane(m_key, kLa, i);
-            m_info = writelane(m_info, La | (a10 ? 128u : 0u), i);
-            if (i + 1 < gn) {
-                m_key = writelane(m_key, kLb, i + 1);
-                m_info = writelane(m_info, Lb | (b10 ? 128u : 0u), i + 1);
-            }
-            if (WANT_FLAGS) {  // NodeUnschedulable rejected >= 1 row of this wave for the pod
-                myflag = writelane(myflag, (w.y < 16 && wave_unsched) ? 1u : 0u, i);
-                myflag = writelane(myflag, (w.w < 16 && wave_unsched) ? 1u : 0u, i + 1);
-            }
+            const uint32_t u = reduce8(r, lane);
+            if ((lane & 7u) == 0u) slot[sub + rev3(lane >> 3)] = u;
         }
-        // flush: lane j holds pod g+j's wave winner -> packed key (minisched_gpu.h)
-        const uint32_t L = m_info & 127u;
-        if (lane < gn && L < 64u) {
-            const uint32_t ord = node_base + wave_row0 + L * rpl + (31u - (m_key & 31u));
-            atomicMax(&keys[g + lane], make_key((m_info & 128u) ? 10u : 0u, m_key & ~31u, ord));
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < gn && ((found >> lane) & 1u)) {
+            const uint32_t h = slot[lane];
+            const uint32_t ord = tb_unhash(ps[g + lane].x, h);
+            atomicMax(&keys[g + lane], make_key(((s10m >> lane) & 1u) ? 10u : 0u, h, ord));
         }
-        if (WANT_FLAGS && lane < gn && myflag) atomicOr(&pflags[g + lane], myflag);
+        if (WANT_FLAGS && lane < gn && ((num >> lane) & 1u)) atomicOr(&pflags[g + lane], 1u);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1513,48 +1515,42 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 
 // K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
 // interleave variants inside one process: "v0" (hash every pair, the plain
-// cross-check) or the default v6.
-enum K1Variant { K1_V0 = 0, K1_V6 = 6 };
+// cross-check) or the default v7.
+enum K1Variant { K1_V0 = 0, K1_V7 = 7 };
 static int k1_variant() {
     const char *e = getenv("MINISCHED_K1");
     if (e && e[0] == 'v' && e[1] == '0') return K1_V0;
-    return K1_V6;
+    return K1_V7;
 }
 
-// Geometry. Rows: at most kK1MaxRpl = 28 rows per lane. The candidate loop
-// runs to the LANE MAXIMUM of a pod's candidates, which grows with the rows a
-// lane holds; 28 beat 32 at every shard size measured (config C 0.586 vs
-// 0.601 ms, 25k rows 0.162 vs 0.177, 12.5k rows 0.094 vs 0.109;
-// profiles/r01e_rpl_sweep.jsonl) despite 14% more waves. A shard's rows are
-// spread evenly over its waves (no near-empty last wave, whose pods would cost
-// a full wave's), rounded up to a multiple of 4 when that keeps the wave count
-// so the tile loads stay dword-aligned (the byte-load path costs ~8%).
-// Pods: each wave sweeps a chunk of at most kK1WavePods = 96 pods (even: pods
-// are read in pairs), fewer when one round of resident waves already covers
-// the batch. Short waves in several rounds let the dispatcher even out the
-// SIMDs: config C runs 0.589 ms with one round of 685-pod waves and 0.537 ms
-// with ~85-pod waves; small shards are best near one round (12.5k rows: 86
-// pods per wave; profiles/r01e_k1_rounds.jsonl, r01e_k1_chunk.jsonl). MINISCHED_K1_ROUNDS=r
-// instead splits the one-round chunk r ways, MINISCHED_K1_CHUNK fixes the chunk
-// and MINISCHED_K1_RPL the rows per lane (<= 32), for experiments.
+// Geometry. Rows: at most kK1MaxRpl = 30 rows per lane, spread evenly over
+// the shard's waves (no near-empty last wave, whose pods would cost a full
+// wave's). A lane of rpl consecutive names holds at most ceil(rpl/10) rows of
+// one digit, so K = ceil(rpl/10) list entries per class keep the synthetic
+// clusters on the list path; 30 rows is the most that K = 3 covers.
+// Pods: each wave sweeps a chunk of at most kK1WavePods pods (a multiple of
+// 8: pods are read and reduced in groups of 8), fewer when one round of
+// resident waves already covers the batch: short waves in several rounds let
+// the dispatcher even out the SIMDs (profiles/r01e_k1_rounds.jsonl).
+// MINISCHED_K1_ROUNDS=r instead splits the one-round chunk r ways,
+// MINISCHED_K1_CHUNK fixes the chunk and MINISCHED_K1_RPL the rows per lane
+// (<= 32), for experiments.
 typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, uint32_t, const uint2 *, uint32_t,
                          uint32_t, unsigned long long *, uint32_t *);
 
-constexpr uint32_t kK1MaxRpl = 28;
+constexpr uint32_t kK1MaxRpl = 30;
 constexpr uint32_t kK1WavePods = 96;
 
 static uint32_t k1_rows_per_lane(uint32_t n_rows) {
     if (const char *e = getenv("MINISCHED_K1_RPL")) return (uint32_t)std::min(32, std::max(1, atoi(e)));
     const uint32_t waves = std::max(1u, cdiv(n_rows, 64u * kK1MaxRpl));
-    const uint32_t r = std::max(1u, cdiv(n_rows, 64u * waves));
-    const uint32_t r4 = (r + 3u) & ~3u;
-    return cdiv(n_rows, 64u * r4) == waves ? r4 : r;
+    return std::max(1u, cdiv(n_rows, 64u * waves));
 }
 
-template <bool WANT_FLAGS>
-static hipError_t launch_v6(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
+template <int K, bool WANT_FLAGS>
+static hipError_t launch_v7(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps, uint32_t n_pods,
                             unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
-    const K1Kernel kern = k_sweep_nunn_v6<WANT_FLAGS>;
+    const K1Kernel kern = k_sweep_nunn_v7<K, WANT_FLAGS>;
     static int blocks_per_cu = 0;
     if (!blocks_per_cu) {
         int nb = 0;
@@ -1562,17 +1558,25 @@ static hipError_t launch_v6(const NodeTable &t, uint32_t n_rows, const uint2 *ps
         if (e != hipSuccess) return e;
         blocks_per_cu = nb > 0 ? nb : 1;
     }
-    const uint32_t rpl = k1_rows_per_lane(n_rows);
     const uint32_t gx = cdiv(n_rows, 64u * rpl);
     const uint32_t resident = (uint32_t)blocks_per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
-    const uint32_t one_round = cdiv(cdiv(n_pods, std::max<uint32_t>(1, resident / gx)), 2) * 2;
+    const uint32_t one_round = cdiv(cdiv(n_pods, std::max<uint32_t>(1, resident / gx)), 8) * 8;
     uint32_t chunk = std::min(one_round, kK1WavePods);
     if (const char *r = getenv("MINISCHED_K1_ROUNDS"))
-        chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 2) * 2;
-    if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(2, atoi(c)), 2) * 2;
+        chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 8) * 8;
+    if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags, t.digit, n_rows, t.base, rpl,
                        ps, n_pods, chunk, keys, flags);
     return hipGetLastError();
+}
+
+template <bool WANT_FLAGS>
+static hipError_t launch_v7_rows(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
+                                 unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
+    const uint32_t rpl = k1_rows_per_lane(n_rows);
+    if (rpl <= 20) return launch_v7<2, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    if (rpl <= 30) return launch_v7<3, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    return launch_v7<4, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
 }
 
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
@@ -1597,8 +1601,8 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
                                t.base, pods, n_pods, chunk, seed32, keys, flags);
         return hipGetLastError();
     }
-    return flags ? launch_v6<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
-                 : launch_v6<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
+    return flags ? launch_v7_rows<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
+                 : launch_v7_rows<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
 }
 
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,

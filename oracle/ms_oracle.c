@@ -41,11 +41,12 @@ uint32_t msor_mix32(uint32_t x) {
     return x;
 }
 
-/* Tie-break hash, rule "r2" (include/minisched_gpu.h): the pod half A is
- * msor_pod_hash, the node enters additively as ordinal * 0x9E3779 (a 24-bit
- * odd constant), and the low 5 bits of the result are dropped. */
+/* Tie-break hash, rule "r3" (include/minisched_gpu.h): the pod half A is
+ * msor_pod_hash and the node enters additively as ordinal * 0x9E3779 (a 24-bit
+ * odd constant). For one pod it is a bijection of the node ordinal, so two
+ * nodes never tie on it. */
 uint32_t msor_tb_hash(uint32_t pod_hash, uint32_t node) {
-    return msor_mix32(pod_hash + node * 0x9E3779u) & ~31u;
+    return msor_mix32(pod_hash + node * 0x9E3779u);
 }
 
 uint32_t msor_h32(uint64_t seed, uint32_t pod, uint32_t node) {

@@ -27,7 +27,7 @@ def seed32(seed):
 
 
 def mix32(x):
-    """Mixer of rule r2: xor-shift 16, multiply, xor-shift 16, multiply."""
+    """Mixer of rule r3: xor-shift 16, multiply, xor-shift 16, multiply."""
     x &= 0xFFFFFFFF
     x ^= x >> 16
     x = (x * 0x85EBCA6B) & 0xFFFFFFFF
@@ -37,9 +37,9 @@ def mix32(x):
 
 
 def h32(seed, pod_ord, node_ord):
-    """Tie-break hash, rule r2 (include/minisched_gpu.h)."""
+    """Tie-break hash, rule r3 (include/minisched_gpu.h)."""
     a = fmix32(seed32(seed) ^ pod_ord)
-    return mix32(a + node_ord * 0x9E3779) & 0xFFFFFFE0
+    return mix32(a + node_ord * 0x9E3779)
 
 
 def key(score, h, node_ord):

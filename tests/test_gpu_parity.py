@@ -68,7 +68,7 @@ def test_readme_scenario_gpu(oracle):
         assert e.read(9, 1)["pod_count"][0] == 1  # assume-on-select
 
 
-@pytest.fixture(params=["v6", "v0"])
+@pytest.fixture(params=["v7", "v0"])
 def k1_variant(request, monkeypatch):
     # both NU+NN sweep kernels stay bit-exact (v0, hash every pair, is the plain cross-check)
     monkeypatch.setenv("MINISCHED_K1", request.param)
@@ -89,7 +89,7 @@ def test_nunn_random_sizes(oracle, k1_variant, n_nodes, n_pods):
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 
-@pytest.mark.parametrize("rpl", [None, "1", "7", "28", "29", "31", "32"])
+@pytest.mark.parametrize("rpl", [None, "1", "7", "20", "21", "28", "29", "30", "31", "32"])
 @pytest.mark.parametrize("n_nodes,node_base", [(12_500, 37_500), (25_000, 0), (3001, 99_000)])
 def test_nunn_rows_per_lane(oracle, monkeypatch, rpl, n_nodes, node_base):
     # K1's row geometry (rows per lane, balanced waves over a shard, byte/dword/vector
@@ -103,6 +103,28 @@ def test_nunn_rows_per_lane(oracle, monkeypatch, rpl, n_nodes, node_base):
     nr["name_digit"][::13] = 0xFF
     o = oracle.schedule(nr, pr, seed=seed, node_base=node_base)
     with engine_with(nr, seed=seed, node_base=node_base) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+
+
+@pytest.mark.parametrize("layout", ["runs", "skewed", "single"])
+def test_nunn_uneven_digits(oracle, layout):
+    # K1 v7 keeps at most K rows per (lane, digit) in its class lists; clusters whose
+    # name digits do not cycle overflow them and take the general path for that class
+    # (runs of equal digits, a skewed digit mix, every name ending in the same digit)
+    n_nodes = 9000
+    seed = {"runs": 11, "skewed": 12, "single": 13}[layout]
+    rng = np.random.default_rng(seed)
+    nr = synth.nodes(n_nodes, seed=seed)
+    if layout == "runs":
+        nr["name_digit"] = (np.arange(n_nodes) // 37) % 10
+    elif layout == "skewed":
+        nr["name_digit"] = np.where(rng.random(n_nodes) < 0.6, 3, rng.integers(0, 10, n_nodes))
+    else:
+        nr["name_digit"] = 7
+    pr = synth.pods(777, seed=seed)
+    pr["tolerates_unschedulable"][::6] = 1
+    o = oracle.schedule(nr, pr, seed=seed)
+    with engine_with(nr, seed=seed) as e:
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 

@@ -230,7 +230,7 @@ def test_sequential_equals_batched_for_nunn(oracle):
 
 @pytest.mark.parametrize("T,stride", [(2, 1), (3, 1), (10, 1), (64, 1), (16, 10), (32, 1000)])
 def test_tiebreak_uniform_over_tied_nodes(T, stride):
-    # Rule r2 (minisched_gpu.h) stands in for selectHost's reservoir choice
+    # Rule r3 (minisched_gpu.h) stands in for selectHost's reservoir choice
     # (minisched.go:316-321): over many pods each of T tied nodes must win
     # about 1/T of the time, also for consecutive ordinals (the additive
     # node term's weakest case). Chi-square against uniform, 5-sigma bound.
@@ -245,3 +245,25 @@ def test_tiebreak_uniform_over_tied_nodes(T, stride):
     chi2 = float(((wins - exp) ** 2 / exp).sum())
     dof = T - 1
     assert chi2 < dof + 5 * np.sqrt(2 * dof), (chi2, wins.tolist())
+
+
+def test_tiebreak_hash_is_invertible():
+    # Rule r3: for one pod the hash is a bijection of the node ordinal, so hashes never
+    # tie and K1 recovers the winning row from its hash alone (ms_internal.h tb_unhash,
+    # same constants: the inverses of 0xc2b2ae35, 0x85ebca6b and 0x9E3779 mod 2^32)
+    rng = np.random.default_rng(5)
+    M = 0xFFFFFFFF
+
+    def unhash(a, h):
+        h = (h * 0x7ED1B41D) & M
+        h ^= h >> 16
+        h = (h * 0xA5CB9243) & M
+        h ^= h >> 16
+        return ((h - a) * 0xF2B382C9) & M
+
+    for _ in range(2000):
+        seed, pod, node = int(rng.integers(0, 2**63)), int(rng.integers(0, 2**32)), int(rng.integers(0, 0xFFFFF))
+        a = _pyref.fmix32(_pyref.seed32(seed) ^ pod)
+        assert unhash(a, _pyref.h32(seed, pod, node)) == node
+    hs = {_pyref.h32(9, 4242, n) for n in range(20000)}
+    assert len(hs) == 20000
