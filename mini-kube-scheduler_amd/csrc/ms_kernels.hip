@@ -306,28 +306,52 @@ struct WaveRows {
     uint32_t fast;          // wave-uniform: bit d = class d takes the list path
 };
 
-// One pod (pod stream entry: A, cls). Returns the lane's maximum candidate
-// hash (only meaningful when the wave has a candidate: *found).
+// List path of one pod: the lane's maximum hash over its K class-d entries.
 template <int K>
-__device__ __forceinline__ uint32_t eval_pod(const WaveRows<K> &w, const uint32_t (*raw)[64], uint32_t lane,
-                                             uint32_t A, uint32_t cls, bool &found, bool &s10) {
-    if ((w.fast >> cls) & 1u) {  // cls < 10: not tolerating, class lists fit
-        uint32_t h[K];
+__device__ __forceinline__ uint32_t list_max(const ClassLists<K> &L, uint32_t A, uint32_t d) {
+    uint32_t h[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i) h[i] = mix32(A + w.L.h[i][cls]);
-        uint32_t kb = h[0];
+    for (int i = 0; i < K; ++i) h[i] = mix32(A + L.h[i][d]);
+    uint32_t kb = h[0];
 #pragma unroll
-        for (int i = 1; i < K; ++i) kb = max(kb, h[i]);
-        found = s10 = true;
-        return kb;
-    }
+    for (int i = 1; i < K; ++i) kb = max(kb, h[i]);
+    return kb;
+}
+
+// list_max<3> with the class index applied to the adds themselves: under
+// s_set_gpr_idx_on (SRC0 mode) a VALU's first source register is offset by
+// the class, so v_add reads h[i][d] directly and the K indexed v_mov copies
+// disappear. The lists are pinned to v[40:69] for this (the register
+// allocator keeps them there for the kernel's lifetime: `make asm` shows no
+// copies into that range in the pod loop).
+__device__ __forceinline__ uint32_t list_max3_idx(const ClassLists<3> &L, uint32_t A, uint32_t d) {
+    uint32_t x0, x1, x2;
+    asm volatile(
+        "s_set_gpr_idx_on %[d], gpr_idx(SRC0)\n\t"
+        "v_add_u32_e64 %[x0], v40, %[A]\n\t"
+        "v_add_u32_e64 %[x1], v50, %[A]\n\t"
+        "v_add_u32_e64 %[x2], v60, %[A]\n\t"
+        "s_set_gpr_idx_off"
+        : [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2)
+        : [d] "s"(d), [A] "s"(A), "{v[40:49]}"(L.h[0]), "{v[50:59]}"(L.h[1]), "{v[60:69]}"(L.h[2]));
+    return max(max(mix32(x0), mix32(x1)), mix32(x2));
+}
+
+// General path of one pod (pod stream entry: A, cls): tolerating pods, classes
+// whose lists overflowed, pods with no digit match in the wave. Returns the
+// lane's maximum candidate hash; fs (wave-uniform) bit 0 = the wave has a
+// feasible row for the pod, bit 1 = the best score is NodeNumber's 10.
+__device__ __forceinline__ uint32_t eval_general(uint32_t feasN, uint32_t feasT, uint32_t hterm0,
+                                                 const uint32_t (*raw)[64], uint32_t lane, uint32_t A, uint32_t cls,
+                                                 uint32_t &fs) {
     const uint32_t d = cls & 15u;
     const bool tol = cls >= 16u;
-    uint32_t m = d < 10u ? (raw[d][lane] & (tol ? w.feasT : w.feasN)) : 0u;
-    s10 = __ballot(m != 0) != 0;
-    if (!s10) m = tol ? w.feasT : w.feasN;  // no digit match in this wave: every feasible row scores 0
-    found = s10 || __ballot(m != 0) != 0;
-    const uint32_t AH = A + w.hterm0;
+    uint32_t m = d < 10u ? (raw[d][lane] & (tol ? feasT : feasN)) : 0u;
+    const bool s10 = __ballot(m != 0) != 0;
+    if (!s10) m = tol ? feasT : feasN;  // no digit match in this wave: every feasible row scores 0
+    const bool found = s10 || __ballot(m != 0) != 0;
+    fs = (uint32_t)__builtin_amdgcn_readfirstlane((found ? 1 : 0) | (s10 ? 2 : 0));
+    const uint32_t AH = A + hterm0;
     uint32_t kb = 0;
     while (__ballot(m != 0)) {  // lane-divergent trip count, branch-free body
         const uint32_t s = first_slot(m);
@@ -397,20 +421,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             nx1 = q4[1];
             nx2 = q4[2];
             nx3 = q4[3];
+            // Pods past the chunk's end in its last group are evaluated too (the
+            // stream is padded; a chunk is a multiple of 8 pods, so only the batch's
+            // last group is partial) and masked out of the outcome bits.
             uint32_t r[8];
+            u64 gfound = 0, gs10 = 0, gnum = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                r[j] = 0;
-                if (sub + j < gn) {
-                    bool f, s;
-                    r[j] = eval_pod<K>(w, raw, lane, e[2 * j], e[2 * j + 1], f, s);
-                    // wave-uniform outcome bits, kept in SGPRs
-                    const uint32_t fs = (uint32_t)__builtin_amdgcn_readfirstlane((f ? 1 : 0) | (s ? 2 : 0));
-                    found |= (u64)(fs & 1u) << (sub + j);
-                    s10m |= (u64)(fs >> 1) << (sub + j);
-                    if (WANT_FLAGS) num |= (u64)(e[2 * j + 1] < 16u && wave_unsched) << (sub + j);
-                }
+                const uint32_t A = e[2 * j], cls = e[2 * j + 1];
+                uint32_t fs = 3u;          // found, score 10
+                if ((w.fast >> cls) & 1u) {  // cls < 10: not tolerating, class lists fit
+                    if constexpr (K == 3)
+                        r[j] = list_max3_idx(w.L, A, cls);  // the production geometry (30 rows per lane)
+                    else
+                        r[j] = list_max<K>(w.L, A, cls);
+                } else
+                    r[j] = eval_general(w.feasN, w.feasT, w.hterm0, raw, lane, A, cls, fs);
+                gfound |= (u64)(fs & 1u) << j;
+                gs10 |= (u64)(fs >> 1) << j;
+                if (WANT_FLAGS) gnum |= (u64)(cls < 16u && wave_unsched) << j;
             }
+            const u64 gmask = gn - sub >= 8u ? 0xFFull : (1ull << (gn - sub)) - 1ull;
+            found |= (gfound & gmask) << sub;
+            s10m |= (gs10 & gmask) << sub;
+            if (WANT_FLAGS) num |= (gnum & gmask) << sub;
             const uint32_t u = reduce8(r, lane);
             if ((lane & 7u) == 0u) slot[sub + rev3(lane >> 3)] = u;
         }
@@ -1528,10 +1562,12 @@ static int k1_variant() {
 // wave's). A lane of rpl consecutive names holds at most ceil(rpl/10) rows of
 // one digit, so K = ceil(rpl/10) list entries per class keep the synthetic
 // clusters on the list path; 30 rows is the most that K = 3 covers.
-// Pods: each wave sweeps a chunk of at most kK1WavePods pods (a multiple of
-// 8: pods are read and reduced in groups of 8), fewer when one round of
-// resident waves already covers the batch: short waves in several rounds let
-// the dispatcher even out the SIMDs (profiles/r01e_k1_rounds.jsonl).
+// Pods: each wave sweeps a chunk of pods (a multiple of 8: pods are read and
+// reduced in groups of 8) sized for about four rounds of resident waves,
+// within [kK1WavePods, 2 kK1WavePods], and never more than one round: short
+// waves in several rounds let the dispatcher even out the SIMDs, long ones
+// amortise the tile build (profiles/r01g_geom.jsonl: 192 pods per wave at
+// 100k rows, 96 at 25k and 12.5k).
 // MINISCHED_K1_ROUNDS=r instead splits the one-round chunk r ways,
 // MINISCHED_K1_CHUNK fixes the chunk and MINISCHED_K1_RPL the rows per lane
 // (<= 32), for experiments.
@@ -1551,17 +1587,18 @@ template <int K, bool WANT_FLAGS>
 static hipError_t launch_v7(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps, uint32_t n_pods,
                             unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
     const K1Kernel kern = k_sweep_nunn_v7<K, WANT_FLAGS>;
-    static int blocks_per_cu = 0;
-    if (!blocks_per_cu) {
+    static int bpc = 0;
+    if (!bpc) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64, 0);
         if (e != hipSuccess) return e;
-        blocks_per_cu = nb > 0 ? nb : 1;
+        bpc = nb > 0 ? nb : 1;
     }
     const uint32_t gx = cdiv(n_rows, 64u * rpl);
-    const uint32_t resident = (uint32_t)blocks_per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256);
+    const uint32_t resident = (uint32_t)bpc * (uint32_t)(num_cus > 0 ? num_cus : 256);
     const uint32_t one_round = cdiv(cdiv(n_pods, std::max<uint32_t>(1, resident / gx)), 8) * 8;
-    uint32_t chunk = std::min(one_round, kK1WavePods);
+    // about four rounds of waves, between kK1WavePods and 2 kK1WavePods pods each
+    uint32_t chunk = std::min(one_round, std::min(2 * kK1WavePods, std::max(kK1WavePods, cdiv(one_round, 32) * 8)));
     if (const char *r = getenv("MINISCHED_K1_ROUNDS"))
         chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 8) * 8;
     if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;

@@ -91,7 +91,7 @@ def test_nunn_random_sizes(oracle, k1_variant, n_nodes, n_pods):
 
 @pytest.mark.parametrize("rpl", [None, "1", "7", "20", "21", "28", "29", "30", "31", "32"])
 @pytest.mark.parametrize("n_nodes,node_base", [(12_500, 37_500), (25_000, 0), (3001, 99_000)])
-def test_nunn_rows_per_lane(oracle, monkeypatch, rpl, n_nodes, node_base):
+def test_nunn_rows_per_lane(oracle, monkeypatch, k1_variant, rpl, n_nodes, node_base):
     # K1's row geometry (rows per lane, balanced waves over a shard, byte/dword/vector
     # tile loads) and the global-ordinal arithmetic of a shard that starts at node_base
     if rpl is not None:

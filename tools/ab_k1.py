@@ -20,7 +20,7 @@ def main():
     N = int(os.environ.get("AB_NODES", 100_000))
     P = int(os.environ.get("AB_PODS", 100_000))
     rounds = int(os.environ.get("AB_ROUNDS", 8))
-    variants = os.environ.get("AB_VARIANTS", "v6,v0").split(",")
+    variants = os.environ.get("AB_VARIANTS", "v7,v0").split(",")
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(s)

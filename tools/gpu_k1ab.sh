@@ -9,6 +9,6 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 1
 rc=$?
 tail -3 gpurun_out/pytest_${TAG}.log
 [ $rc -eq 0 ] || { echo "parity failed rc=$rc"; grep -m5 -B5 "Error\|assert" gpurun_out/pytest_${TAG}.log; exit $rc; }
-AB_VARIANTS=${AB_VARIANTS:-v6,v0} AB_ROUNDS=10 timeout -k 10 180 python tools/ab_k1.py \
+AB_VARIANTS=${AB_VARIANTS:-v7,v0} AB_ROUNDS=10 timeout -k 10 180 python tools/ab_k1.py \
     > gpurun_out/ab_${TAG}.json 2> gpurun_out/ab_${TAG}.err || { echo ab failed; tail gpurun_out/ab_${TAG}.err; exit 1; }
 cat gpurun_out/ab_${TAG}.json

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""K1 geometry sweep in ONE process: rows per lane x pods per wave, per shard size.
+
+Each launch reads MINISCHED_K1_RPL / MINISCHED_K1_CHUNK from the environment
+(ms_kernels.hip launch_v7), so the variants interleave round by round on one
+device. Prints one JSON line per (shard rows, rpl, chunk): median / min kernel
+ms by HIP events on the launch stream. Keys are checked identical per shard.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
+
+
+def main():
+    import torch
+
+    from minisched_amd import _lib, synth
+
+    P = int(os.environ.get("GEOM_PODS", 100_000))
+    rounds = int(os.environ.get("GEOM_ROUNDS", 6))
+    shards = [int(x) for x in os.environ.get("GEOM_SHARDS", "100000,50000,25000,12500").split(",")]
+    rpls = os.environ.get("GEOM_RPL", "20,30,32").split(",")
+    chunks = os.environ.get("GEOM_CHUNK", "0,48,96,192,384").split(",")
+    k1s = os.environ.get("GEOM_K1", "v7").split(",")
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(s)
+    pods = torch.from_numpy(synth.pods(P, seed=1).view(np.uint8).copy()).to(dev)
+    for N in shards:
+        eng = _lib.Engine(max_nodes=N, seed=1)
+        eng.upsert(np.arange(N), synth.nodes(N, seed=1))
+        eng.flush()
+        variants = [(r, c, k) for r in rpls for c in chunks for k in k1s]
+        keys = {v: torch.empty(P, dtype=torch.int64, device=dev) for v in variants}
+        times = {v: [] for v in variants}
+        for rd in range(rounds + 1):
+            for v in variants:
+                os.environ["MINISCHED_K1_RPL"] = v[0]
+                os.environ["MINISCHED_K1"] = v[2]
+                if v[1] == "0":
+                    os.environ.pop("MINISCHED_K1_CHUNK", None)
+                else:
+                    os.environ["MINISCHED_K1_CHUNK"] = v[1]
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                eng.sweep_device(P, pods.data_ptr(), keys[v].data_ptr(), 0, s.cuda_stream)
+                b.record(s)
+                b.synchronize()
+                if rd:
+                    times[v].append(a.elapsed_time(b))
+        ref = keys[variants[0]]
+        same = all(torch.equal(ref, keys[v]) for v in variants[1:])
+        for v in variants:
+            t = times[v]
+            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2],
+                              "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                              "keys_identical": bool(same)}), flush=True)
+        eng.close()
+    os.environ.pop("MINISCHED_K1_RPL", None)
+    os.environ.pop("MINISCHED_K1_CHUNK", None)
+
+
+if __name__ == "__main__":
+    main()

@@ -12,7 +12,7 @@ import os
 import shutil
 import sys
 
-src, tag, kernel_key = sys.argv[1], sys.argv[2], (sys.argv[3] if len(sys.argv) > 3 else "k_sweep_nunn_v6")
+src, tag, kernel_key = sys.argv[1], sys.argv[2], (sys.argv[3] if len(sys.argv) > 3 else "k_sweep_nunn_v7")
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 

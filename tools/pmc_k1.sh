@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counter passes for one K1 variant (tools/ab_k1.py), one --pmc run per pass.
 set -o pipefail
-V=${1:-v6}
+V=${1:-v7}
 OUT=gpurun_out/pmc_${V}
 mkdir -p $OUT
 export TMPDIR=/tmp
