@@ -362,23 +362,31 @@ __device__ __forceinline__ uint32_t eval_general(uint32_t feasN, uint32_t feasT,
     return kb;
 }
 
-template <int K, bool WANT_FLAGS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_sweep_nunn_v7(
+// W waves per workgroup share one node tile: wave 0 builds it and hands the
+// class lists and masks to the others through LDS, so the tile build (about
+// 550 VALU per wave) is paid once per W pod chunks.
+template <int K, bool WANT_FLAGS, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(7))) void k_sweep_nunn_v7(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
     u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
     __shared__ uint32_t raw[10][64];  // one-hot masks for the general path
-    __shared__ uint32_t slot[64];     // wave maxima of the current 64 pods
+    __shared__ uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
+    __shared__ uint32_t tile[W > 1 ? 10 * K + 3 : 1][64];  // wave 0's lists, feasN, feasT, hterm0
+    __shared__ uint32_t tile_bits[2];                       // fast classes, wave_unsched
     const uint32_t lane = lane_id();
+    const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+    uint32_t *slot = slots[wv];
     const uint32_t wave_row0 = blockIdx.x * 64u * rpl;
-    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pbeg = (blockIdx.y * W + wv) * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
-    if (wave_row0 >= n_rows || pbeg >= pend) return;  // wave-uniform
+    if (wave_row0 >= n_rows) return;                 // block-uniform
+    if (W == 1 && pbeg >= pend) return;              // wave-uniform (W > 1: after the hand-off)
     const uint32_t row0 = wave_row0 + lane * rpl;
 
     WaveRows<K> w;
     bool wave_unsched;
-    {
+    if (wv == 0) {
         Bits32Cols c;
         load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
         w.feasN = ~(c.absent | c.unsched);
@@ -405,7 +413,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             }
             if (any && !ovf) w.fast |= 1u << d;
         }
-        // each lane reads only its own raw[][] entries: no barrier needed
+        if (W > 1) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int d = 0; d < 10; ++d) tile[i * 10 + d][lane] = w.L.h[i][d];
+            tile[10 * K][lane] = w.feasN;
+            tile[10 * K + 1][lane] = w.feasT;
+            tile[10 * K + 2][lane] = w.hterm0;
+            if (lane == 0) {
+                tile_bits[0] = w.fast;
+                tile_bits[1] = wave_unsched ? 1u : 0u;
+            }
+        }
+        // W == 1: each lane reads only its own raw[][] entries, no barrier needed
+    }
+    if (W > 1) {
+        __syncthreads();
+        if (wv != 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+#pragma unroll
+                for (int d = 0; d < 10; ++d) w.L.h[i][d] = tile[i * 10 + d][lane];
+            w.feasN = tile[10 * K][lane];
+            w.feasT = tile[10 * K + 1][lane];
+            w.hterm0 = tile[10 * K + 2][lane];
+            w.fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)tile_bits[0]);
+            wave_unsched = __builtin_amdgcn_readfirstlane((int)tile_bits[1]) != 0;
+        }
+        if (pbeg >= pend) return;  // wave-uniform
     }
 
     const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
@@ -413,6 +449,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
     for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod blocks: one flush each
         const uint32_t gn = min(64u, pend - g);
         u64 found = 0, s10m = 0, num = 0;
+        // the flush's pod halves A (for tb_unhash), loaded now so the load's latency
+        // hides under the block's sweep instead of stalling the flush
+        const uint32_t a_flush = lane < gn ? ps[g + lane].x : 0u;
         for (uint32_t sub = 0; sub < gn; sub += 8) {
             const uint32_t e[16] = {nx0.x, nx0.y, nx0.z, nx0.w, nx1.x, nx1.y, nx1.z, nx1.w,
                                     nx2.x, nx2.y, nx2.z, nx2.w, nx3.x, nx3.y, nx3.z, nx3.w};
@@ -452,7 +491,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
         __builtin_amdgcn_wave_barrier();
         if (lane < gn && ((found >> lane) & 1u)) {
             const uint32_t h = slot[lane];
-            const uint32_t ord = tb_unhash(ps[g + lane].x, h);
+            const uint32_t ord = tb_unhash(a_flush, h);
             atomicMax(&keys[g + lane], make_key(((s10m >> lane) & 1u) ? 10u : 0u, h, ord));
         }
         if (WANT_FLAGS && lane < gn && ((num >> lane) & 1u)) atomicOr(&pflags[g + lane], 1u);
@@ -1575,6 +1614,7 @@ typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, u
                          uint32_t, unsigned long long *, uint32_t *);
 
 constexpr uint32_t kK1MaxRpl = 30;
+constexpr int kK1Waves = 4;  // waves per workgroup sharing one tile build (MINISCHED_K1_WAVES; profiles/r01i_k1_waves.jsonl)
 constexpr uint32_t kK1WavePods = 96;
 
 static uint32_t k1_rows_per_lane(uint32_t n_rows) {
@@ -1583,37 +1623,49 @@ static uint32_t k1_rows_per_lane(uint32_t n_rows) {
     return std::max(1u, cdiv(n_rows, 64u * waves));
 }
 
-template <int K, bool WANT_FLAGS>
+template <int K, bool WANT_FLAGS, int W>
 static hipError_t launch_v7(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps, uint32_t n_pods,
                             unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
-    const K1Kernel kern = k_sweep_nunn_v7<K, WANT_FLAGS>;
-    static int bpc = 0;
+    const K1Kernel kern = k_sweep_nunn_v7<K, WANT_FLAGS, W>;
+    static int bpc = 0;  // resident blocks per CU (one per template instance)
     if (!bpc) {
         int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64, 0);
+        hipError_t e =
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64 * W, 0);
         if (e != hipSuccess) return e;
         bpc = nb > 0 ? nb : 1;
     }
     const uint32_t gx = cdiv(n_rows, 64u * rpl);
-    const uint32_t resident = (uint32_t)bpc * (uint32_t)(num_cus > 0 ? num_cus : 256);
+    const uint32_t resident = (uint32_t)bpc * W * (uint32_t)(num_cus > 0 ? num_cus : 256);  // waves
     const uint32_t one_round = cdiv(cdiv(n_pods, std::max<uint32_t>(1, resident / gx)), 8) * 8;
     // about four rounds of waves, between kK1WavePods and 2 kK1WavePods pods each
     uint32_t chunk = std::min(one_round, std::min(2 * kK1WavePods, std::max(kK1WavePods, cdiv(one_round, 32) * 8)));
     if (const char *r = getenv("MINISCHED_K1_ROUNDS"))
         chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 8) * 8;
     if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
-    hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk)), dim3(64), 0, s, t.flags, t.digit, n_rows, t.base, rpl,
-                       ps, n_pods, chunk, keys, flags);
+    hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk * W)), dim3(64 * W), 0, s, t.flags, t.digit, n_rows,
+                       t.base, rpl, ps, n_pods, chunk, keys, flags);
     return hipGetLastError();
+}
+
+template <int K, bool WANT_FLAGS>
+static hipError_t launch_v7_waves(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps,
+                                  uint32_t n_pods, unsigned long long *keys, uint32_t *flags, int num_cus,
+                                  hipStream_t s) {
+    int w = kK1Waves;
+    if (const char *e = getenv("MINISCHED_K1_WAVES")) w = atoi(e);
+    if (w >= 4) return launch_v7<K, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    if (w == 2) return launch_v7<K, WANT_FLAGS, 2>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    return launch_v7<K, WANT_FLAGS, 1>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
 }
 
 template <bool WANT_FLAGS>
 static hipError_t launch_v7_rows(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
                                  unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
     const uint32_t rpl = k1_rows_per_lane(n_rows);
-    if (rpl <= 20) return launch_v7<2, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-    if (rpl <= 30) return launch_v7<3, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-    return launch_v7<4, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    if (rpl <= 20) return launch_v7_waves<2, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    if (rpl <= 30) return launch_v7_waves<3, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
+    return launch_v7_waves<4, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
 }
 
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,

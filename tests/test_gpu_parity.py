@@ -68,11 +68,14 @@ def test_readme_scenario_gpu(oracle):
         assert e.read(9, 1)["pod_count"][0] == 1  # assume-on-select
 
 
-@pytest.fixture(params=["v7", "v0"])
+@pytest.fixture(params=["v7", "v7w2", "v7w4", "v0"])
 def k1_variant(request, monkeypatch):
-    # both NU+NN sweep kernels stay bit-exact (v0, hash every pair, is the plain cross-check)
-    monkeypatch.setenv("MINISCHED_K1", request.param)
-    return request.param
+    # every NU+NN sweep form stays bit-exact: v7 with 1, 2 or 4 waves per workgroup sharing
+    # one tile build, and v0 (hash every pair), the plain cross-check
+    v = request.param
+    monkeypatch.setenv("MINISCHED_K1", v[:2])
+    monkeypatch.setenv("MINISCHED_K1_WAVES", v[3:] if "w" in v else "1")
+    return v
 
 
 @pytest.mark.parametrize("n_nodes", [1, 15, 16, 17, 1000, 2047, 2048, 2049, 4096, 8193, 12345])

@@ -27,6 +27,8 @@ def main():
     rpls = os.environ.get("GEOM_RPL", "20,30,32").split(",")
     chunks = os.environ.get("GEOM_CHUNK", "0,48,96,192,384").split(",")
     k1s = os.environ.get("GEOM_K1", "v7").split(",")
+    waves = os.environ.get("GEOM_WAVES", "1").split(",")
+    reps = int(os.environ.get("GEOM_REPS", 1))  # back-to-back launches per timing (hides launch gaps)
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(s)
@@ -35,34 +37,37 @@ def main():
         eng = _lib.Engine(max_nodes=N, seed=1)
         eng.upsert(np.arange(N), synth.nodes(N, seed=1))
         eng.flush()
-        variants = [(r, c, k) for r in rpls for c in chunks for k in k1s]
+        variants = [(r, c, k, wv) for r in rpls for c in chunks for k in k1s for wv in waves]
         keys = {v: torch.empty(P, dtype=torch.int64, device=dev) for v in variants}
         times = {v: [] for v in variants}
         for rd in range(rounds + 1):
             for v in variants:
                 os.environ["MINISCHED_K1_RPL"] = v[0]
                 os.environ["MINISCHED_K1"] = v[2]
+                os.environ["MINISCHED_K1_WAVES"] = v[3]
                 if v[1] == "0":
                     os.environ.pop("MINISCHED_K1_CHUNK", None)
                 else:
                     os.environ["MINISCHED_K1_CHUNK"] = v[1]
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(s)
-                eng.sweep_device(P, pods.data_ptr(), keys[v].data_ptr(), 0, s.cuda_stream)
+                for _ in range(reps):
+                    eng.sweep_device(P, pods.data_ptr(), keys[v].data_ptr(), 0, s.cuda_stream)
                 b.record(s)
                 b.synchronize()
                 if rd:
-                    times[v].append(a.elapsed_time(b))
+                    times[v].append(a.elapsed_time(b) / reps)
         ref = keys[variants[0]]
         same = all(torch.equal(ref, keys[v]) for v in variants[1:])
         for v in variants:
             t = times[v]
-            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2],
-                              "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2], "waves": int(v[3]),
+                              "reps": reps, "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                               "keys_identical": bool(same)}), flush=True)
         eng.close()
     os.environ.pop("MINISCHED_K1_RPL", None)
     os.environ.pop("MINISCHED_K1_CHUNK", None)
+    os.environ.pop("MINISCHED_K1_WAVES", None)
 
 
 if __name__ == "__main__":
