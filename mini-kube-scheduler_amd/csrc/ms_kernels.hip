@@ -321,19 +321,19 @@ __device__ __forceinline__ uint32_t list_max(const ClassLists<K> &L, uint32_t A,
 // list_max<3> with the class index applied to the adds themselves: under
 // s_set_gpr_idx_on (SRC0 mode) a VALU's first source register is offset by
 // the class, so v_add reads h[i][d] directly and the K indexed v_mov copies
-// disappear. The lists are pinned to v[40:69] for this (the register
+// disappear. The lists are pinned to v[34:63] for this (the register
 // allocator keeps them there for the kernel's lifetime: `make asm` shows no
 // copies into that range in the pod loop).
 __device__ __forceinline__ uint32_t list_max3_idx(const ClassLists<3> &L, uint32_t A, uint32_t d) {
     uint32_t x0, x1, x2;
     asm volatile(
         "s_set_gpr_idx_on %[d], gpr_idx(SRC0)\n\t"
-        "v_add_u32_e64 %[x0], v40, %[A]\n\t"
-        "v_add_u32_e64 %[x1], v50, %[A]\n\t"
-        "v_add_u32_e64 %[x2], v60, %[A]\n\t"
+        "v_add_u32_e64 %[x0], v34, %[A]\n\t"
+        "v_add_u32_e64 %[x1], v44, %[A]\n\t"
+        "v_add_u32_e64 %[x2], v54, %[A]\n\t"
         "s_set_gpr_idx_off"
         : [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2)
-        : [d] "s"(d), [A] "s"(A), "{v[40:49]}"(L.h[0]), "{v[50:59]}"(L.h[1]), "{v[60:69]}"(L.h[2]));
+        : [d] "s"(d), [A] "s"(A), "{v[34:43]}"(L.h[0]), "{v[44:53]}"(L.h[1]), "{v[54:63]}"(L.h[2]));
     return max(max(mix32(x0), mix32(x1)), mix32(x2));
 }
 
@@ -366,13 +366,16 @@ __device__ __forceinline__ uint32_t eval_general(uint32_t feasN, uint32_t feasT,
 // class lists and masks to the others through LDS, so the tile build (about
 // 550 VALU per wave) is paid once per W pod chunks.
 template <int K, bool WANT_FLAGS, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(7))) void k_sweep_nunn_v7(
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v7(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
     u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
     __shared__ uint32_t raw[10][64];  // one-hot masks for the general path
     __shared__ uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
-    __shared__ uint32_t tile[W > 1 ? 10 * K + 3 : 1][64];  // wave 0's lists, feasN, feasT, hterm0
+    // wave 0's class lists (W > 1), then feasN, feasT, hterm0: the general path reads
+    // those three from here, so they hold no VGPRs through the pod loop
+    constexpr int kMisc = W > 1 ? 10 * K : 0;
+    __shared__ uint32_t tile[kMisc + 3][64];
     __shared__ uint32_t tile_bits[2];                       // fast classes, wave_unsched
     const uint32_t lane = lane_id();
     const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
@@ -413,14 +416,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(7))) voi
             }
             if (any && !ovf) w.fast |= 1u << d;
         }
+        tile[kMisc][lane] = w.feasN;
+        tile[kMisc + 1][lane] = w.feasT;
+        tile[kMisc + 2][lane] = w.hterm0;
         if (W > 1) {
 #pragma unroll
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int d = 0; d < 10; ++d) tile[i * 10 + d][lane] = w.L.h[i][d];
-            tile[10 * K][lane] = w.feasN;
-            tile[10 * K + 1][lane] = w.feasT;
-            tile[10 * K + 2][lane] = w.hterm0;
             if (lane == 0) {
                 tile_bits[0] = w.fast;
                 tile_bits[1] = wave_unsched ? 1u : 0u;
@@ -435,9 +438,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(7))) voi
             for (int i = 0; i < K; ++i)
 #pragma unroll
                 for (int d = 0; d < 10; ++d) w.L.h[i][d] = tile[i * 10 + d][lane];
-            w.feasN = tile[10 * K][lane];
-            w.feasT = tile[10 * K + 1][lane];
-            w.hterm0 = tile[10 * K + 2][lane];
             w.fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)tile_bits[0]);
             wave_unsched = __builtin_amdgcn_readfirstlane((int)tile_bits[1]) != 0;
         }
@@ -475,7 +475,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(7))) voi
                     else
                         r[j] = list_max<K>(w.L, A, cls);
                 } else
-                    r[j] = eval_general(w.feasN, w.feasT, w.hterm0, raw, lane, A, cls, fs);
+                    r[j] = eval_general(tile[kMisc][lane], tile[kMisc + 1][lane], tile[kMisc + 2][lane], raw, lane,
+                                        A, cls, fs);
                 gfound |= (u64)(fs & 1u) << j;
                 gs10 |= (u64)(fs >> 1) << j;
                 if (WANT_FLAGS) gnum |= (u64)(cls < 16u && wave_unsched) << j;

@@ -61,7 +61,7 @@ def main():
         same = all(torch.equal(ref, keys[v]) for v in variants[1:])
         for v in variants:
             t = times[v]
-            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2], "waves": int(v[3]),
+            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2], "waves": v[3],
                               "reps": reps, "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                               "keys_identical": bool(same)}), flush=True)
         eng.close()
