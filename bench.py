@@ -33,7 +33,9 @@ sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
 METRIC = "pod×node filter+score evals/sec and pods scheduled/sec at 100k nodes, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_EVAL = {"NU+NN": 2, "NU+NRF+NN+LA": 58}
-K1_KERNELS = {"v0": "k_sweep_nunn", "v7": "k_sweep_nunn_v7"}
+# rocprof kernel-name keys; the default (no MINISCHED_K1) is the production choice,
+# k_sweep_nunn_v8 at 100k rows per GPU and k_sweep_nunn_v7 on small shards
+K1_KERNELS = {"v0": "k_sweep_nunn<", "v7": "k_sweep_nunn_v7", "v8": "k_sweep_nunn_v8", None: "k_sweep_nunn_v"}
 
 
 def parse():
@@ -185,12 +187,13 @@ def main():
         value = evals * args.steps / elapsed
         local_evals = float(P) * float(hi - lo)
         achieved = local_evals * BYTES_PER_EVAL[plugins] / (sweep_ms * 1e-3) / 1e9
-        traffic, limiter = None, None
+        traffic, limiter, tj_kernel = None, None, None
         if os.path.exists(args.traffic_json) and world == 1:
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("kernel") == K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v7")):
+                if tj.get("kernel") == K1_KERNELS.get(os.environ.get("MINISCHED_K1")):
                     traffic = tj.get("hbm_bytes_per_launch")
+                    tj_kernel = tj.get("kernel_name")  # the instance rocprof saw
                     # the sweep keeps node columns in registers, so issue, not HBM, binds it
                     limiter = {"kind": "VALU issue", "valu_busy_frac": tj.get("valu_busy_frac"),
                                "valu_insts_per_launch": tj.get("valu_insts_per_launch"),
@@ -229,7 +232,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": K1_KERNELS.get(os.environ.get("MINISCHED_K1", "v7"), "k_sweep_nunn_v7"),
+                "kernel": tj_kernel or K1_KERNELS.get(os.environ.get("MINISCHED_K1"), "k_sweep_nunn_v"),
                 "kernel_ms": sweep_ms,
                 "algorithmic_bytes_per_launch": local_evals * BYTES_PER_EVAL[plugins],
                 "limiter": limiter,

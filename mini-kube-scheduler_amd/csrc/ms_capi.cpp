@@ -68,8 +68,18 @@ struct ms_ctx {
     // another stream first waits for the previous user (pstream_ev)
     uint2 *d_pstream = nullptr;
     uint32_t pstream_cap = 0;
+    uint32_t *d_work = nullptr;  // K1 work-queue counters (kK1MaxColumns), same ordering as d_pstream
     hipStream_t pstream_last = nullptr;
     hipEvent_t pstream_ev = nullptr;
+
+    // Ordering of caller streams after the context stream (node deltas, binds):
+    // ctx_seq counts enqueues on the context stream; a caller stream that was
+    // ordered after it at ctx_seq needs no new cross-stream wait (each costs
+    // ~6 us of device time even when already signalled, tools/ubench/xstream)
+    uint64_t ctx_seq = 0;
+    hipStream_t ordered_stream = nullptr;
+    uint64_t ordered_seq = 0;
+    hipEvent_t ev_order = nullptr;
 
     std::string err;
 };
@@ -104,13 +114,15 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream};
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream,
+                   c->d_work};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
     if (c->pstream_ev) (void)hipEventDestroy(c->pstream_ev);
+    if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     for (int i = 0; i < 2; ++i) {
         if (c->ev_valid[i]) (void)hipEventDestroy(c->ev_valid[i]);
         if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
@@ -163,6 +175,7 @@ int flush_locked(ms_ctx *c) {
     MS_HIP(c, hipMemcpyAsync(c->d_deltas, c->h_deltas, sizeof(NodeDelta) * uniq.size(),
                              hipMemcpyHostToDevice, c->stream));
     MS_HIP(c, launch_apply_deltas(c->t, c->d_deltas, (uint32_t)uniq.size(), c->stream));
+    ++c->ctx_seq;
     return MS_OK;
 }
 
@@ -171,12 +184,13 @@ hipStream_t pick_stream(ms_ctx *c, void *s) { return s ? (hipStream_t)s : c->str
 // Makes work later enqueued on s wait for everything already on the context stream.
 int order_after_ctx_stream(ms_ctx *c, hipStream_t s) {
     if (s == c->stream) return MS_OK;
-    hipEvent_t ev;
-    MS_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    hipError_t e = hipEventRecord(ev, c->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
-    (void)hipEventDestroy(ev);
+    if (s == c->ordered_stream && c->ordered_seq == c->ctx_seq) return MS_OK;  // nothing new on the ctx stream
+    if (!c->ev_order) MS_HIP(c, hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(c->ev_order, c->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, c->ev_order, 0);
     if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("stream ordering: ") + hipGetErrorString(e));
+    c->ordered_stream = s;
+    c->ordered_seq = c->ctx_seq;
     return MS_OK;
 }
 
@@ -281,6 +295,7 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     if (s != c->stream) {
         MS_HIP(c, hipEventRecord(c->ev_seq, s));
         MS_HIP(c, hipStreamWaitEvent(c->stream, c->ev_seq, 0));
+        ++c->ctx_seq;
     }
     return MS_OK;
 }
@@ -294,6 +309,8 @@ int ensure_pstream(ms_ctx *c, uint32_t n_pods) {
     if (c->d_pstream) (void)hipFree(c->d_pstream);
     c->d_pstream = nullptr;
     c->pstream_cap = 0;
+    if (!c->d_work && hipMalloc((void **)&c->d_work, sizeof(uint32_t) * kK1MaxColumns) != hipSuccess)
+        return fail(c, MS_E_OOM, "K1 work counters");
     if (hipMalloc((void **)&c->d_pstream, sizeof(uint2) * cap) != hipSuccess)
         return fail(c, MS_E_OOM, "pod stream");
     c->pstream_cap = cap;
@@ -309,7 +326,7 @@ int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned 
         if (!c->pstream_ev) MS_HIP(c, hipEventCreateWithFlags(&c->pstream_ev, hipEventDisableTiming));
         if (c->pstream_last && c->pstream_last != s) MS_HIP(c, hipStreamWaitEvent(s, c->pstream_ev, 0));
         MS_HIP(c, launch_sweep_nunn(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->d_pstream,
-                                    c->num_cus, s));
+                                    c->d_work, c->num_cus, s));
         MS_HIP(c, hipEventRecord(c->pstream_ev, s));
         c->pstream_last = s;
     } else {
@@ -528,6 +545,7 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     int rc = flush_locked(c);
     if (rc) return rc;
     const hipStream_t s = c->stream;
+    ++c->ctx_seq;
     const uint32_t B = c->batch_cap;
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
@@ -565,6 +583,7 @@ static int bind_common(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod, int s
     if (rc) return rc;
     MS_HIP(c, hipMemcpyAsync(c->d_one, pod, sizeof(ms_pod_rec), hipMemcpyHostToDevice, c->stream));
     MS_HIP(c, launch_bind_one(c->t, ordinal - c->cfg.node_base, c->d_one, sign, c->stream));
+    ++c->ctx_seq;
     MS_HIP(c, hipStreamSynchronize(c->stream));
     return MS_OK;
 }
@@ -601,7 +620,9 @@ int ms_apply_binds_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev
                           void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;
     MS_HIP(c, hipSetDevice(c->cfg.device));
-    MS_HIP(c, launch_apply_binds(c->t, pods_dev, n_pods, results_dev, pick_stream(c, stream)));
+    const hipStream_t s = pick_stream(c, stream);
+    MS_HIP(c, launch_apply_binds(c->t, pods_dev, n_pods, results_dev, s));
+    if (s == c->stream) ++c->ctx_seq;  // table writes on the context stream
     return MS_OK;
 }
 
@@ -616,6 +637,7 @@ int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
     if (rc) return rc;
+    if (s == c->stream) ++c->ctx_seq;  // binds below write the table on the context stream
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA) return run_sequential(c, n_pods, pods_dev, results_dev, s);
     // NU+NN: keys are independent of mutable state -> batched sweep + commit
     const uint32_t B = c->batch_cap;

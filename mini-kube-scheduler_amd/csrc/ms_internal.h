@@ -105,9 +105,11 @@ hipError_t launch_apply_deltas(const NodeTable &t, const NodeDelta *d_deltas, ui
 hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
 // NU+NN sweep: k_pod_prep (pod stream, zeroes keys/flags) then the K1 sweep.
 // pstream holds >= n_pods + kPodStreamPad entries.
+// work: K1 work counters, >= kK1MaxColumns u32 (zeroed by the pod prep as needed).
+constexpr uint32_t kK1MaxColumns = (MS_MAX_ORDINAL + 1) / 64 + 1;
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
-                             int num_cus, hipStream_t s);
+                             uint32_t *work, int num_cus, hipStream_t s);
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s);

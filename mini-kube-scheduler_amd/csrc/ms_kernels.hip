@@ -11,6 +11,7 @@
 // lane-slot, pods wave-uniform (scalar loads), a 64-bit wave max per pod and
 // one coalesced atomicMax wave-instruction per 64 pods.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "ms_internal.h"
@@ -143,8 +144,10 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
 // whole 8-pod groups, one group ahead, never need a bounds check.
 // ----------------------------------------------------------------------------
 __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t seed32,
-                           uint2 *__restrict__ ps, u64 *__restrict__ keys, uint32_t *__restrict__ flags) {
+                           uint2 *__restrict__ ps, u64 *__restrict__ keys, uint32_t *__restrict__ flags,
+                           uint32_t *__restrict__ work, uint32_t n_work) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_work) work[i] = 0;  // K1 v8's per-column work counters
     if (i < n) {
         const ms_pod_rec pr = pods[i];
         const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
@@ -362,88 +365,84 @@ __device__ __forceinline__ uint32_t eval_general(uint32_t feasN, uint32_t feasT,
     return kb;
 }
 
-// W waves per workgroup share one node tile: wave 0 builds it and hands the
-// class lists and masks to the others through LDS, so the tile build (about
-// 550 VALU per wave) is paid once per W pod chunks.
-template <int K, bool WANT_FLAGS, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v7(
-    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
-    u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
-    __shared__ uint32_t raw[10][64];  // one-hot masks for the general path
-    __shared__ uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
-    // wave 0's class lists (W > 1), then feasN, feasT, hterm0: the general path reads
-    // those three from here, so they hold no VGPRs through the pod loop
-    constexpr int kMisc = W > 1 ? 10 * K : 0;
-    __shared__ uint32_t tile[kMisc + 3][64];
-    __shared__ uint32_t tile_bits[2];                       // fast classes, wave_unsched
-    const uint32_t lane = lane_id();
-    const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
-    uint32_t *slot = slots[wv];
-    const uint32_t wave_row0 = blockIdx.x * 64u * rpl;
-    const uint32_t pbeg = (blockIdx.y * W + wv) * chunk;
-    const uint32_t pend = min(n_pods, pbeg + chunk);
-    if (wave_row0 >= n_rows) return;                 // block-uniform
-    if (W == 1 && pbeg >= pend) return;              // wave-uniform (W > 1: after the hand-off)
-    const uint32_t row0 = wave_row0 + lane * rpl;
+// LDS state of a workgroup's node tile: the one-hot masks (general path), wave
+// 0's class lists (W > 1), then feasN, feasT, hterm0 (the general path reads
+// those three from here, so they hold no VGPRs through the pod loop), and the
+// wave-uniform fast-class mask and "some row is unschedulable" bit.
+template <int K, int W>
+struct TileLds {
+    static constexpr int kMisc = W > 1 ? 10 * K : 0;
+    uint32_t raw[10][64];
+    uint32_t tile[kMisc + 3][64];
+    uint32_t bits[2];
+    uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
+};
 
-    WaveRows<K> w;
-    bool wave_unsched;
-    if (wv == 0) {
-        Bits32Cols c;
-        load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
-        w.feasN = ~(c.absent | c.unsched);
-        w.feasT = ~c.absent;
-        w.hterm0 = (node_base + row0) * kG24;
-        w.fast = 0;
-        wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
+// Wave 0: builds the tile of rows wave_row0 + lane*rpl .. (+rpl) into w and LDS.
+template <int K, int W>
+__device__ __forceinline__ void tile_build(TileLds<K, W> &S, const uint8_t *__restrict__ nflags,
+                                           const uint8_t *__restrict__ ndigit, uint32_t n_rows, uint32_t node_base,
+                                           uint32_t row0, uint32_t rpl, uint32_t lane, WaveRows<K> &w,
+                                           bool &wave_unsched) {
+    constexpr int kMisc = TileLds<K, W>::kMisc;
+    Bits32Cols c;
+    load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
+    w.feasN = ~(c.absent | c.unsched);
+    w.feasT = ~c.absent;
+    w.hterm0 = (node_base + row0) * kG24;
+    w.fast = 0;
+    wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
 #pragma unroll
-        for (int d = 0; d < 10; ++d) {
-            raw[d][lane] = c.onehot[d];
-            uint32_t m = c.onehot[d] & w.feasN;
-            const uint32_t cnt = __popc(m);
-            const u64 any = __ballot(m != 0);
-            const bool ovf = __ballot(cnt > (uint32_t)K) != 0;
-            const uint32_t first = w.hterm0 + __umul24(first_slot(m), kG24);
-            const uint32_t donor =
-                (uint32_t)__builtin_amdgcn_readlane((int)first, any ? (int)__builtin_ctzll(any) : 0);
-            const uint32_t pad = cnt ? first : donor;  // a class-d candidate of this wave
+    for (int d = 0; d < 10; ++d) {
+        S.raw[d][lane] = c.onehot[d];
+        uint32_t m = c.onehot[d] & w.feasN;
+        const uint32_t cnt = __popc(m);
+        const u64 any = __ballot(m != 0);
+        const bool ovf = __ballot(cnt > (uint32_t)K) != 0;
+        const uint32_t first = w.hterm0 + __umul24(first_slot(m), kG24);
+        const uint32_t donor = (uint32_t)__builtin_amdgcn_readlane((int)first, any ? (int)__builtin_ctzll(any) : 0);
+        const uint32_t pad = cnt ? first : donor;  // a class-d candidate of this wave
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const uint32_t v = w.hterm0 + __umul24(first_slot(m), kG24);
-                m &= m - 1u;
-                w.L.h[i][d] = (uint32_t)i < cnt ? v : pad;
-            }
-            if (any && !ovf) w.fast |= 1u << d;
+        for (int i = 0; i < K; ++i) {
+            const uint32_t v = w.hterm0 + __umul24(first_slot(m), kG24);
+            m &= m - 1u;
+            w.L.h[i][d] = (uint32_t)i < cnt ? v : pad;
         }
-        tile[kMisc][lane] = w.feasN;
-        tile[kMisc + 1][lane] = w.feasT;
-        tile[kMisc + 2][lane] = w.hterm0;
-        if (W > 1) {
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-#pragma unroll
-                for (int d = 0; d < 10; ++d) tile[i * 10 + d][lane] = w.L.h[i][d];
-            if (lane == 0) {
-                tile_bits[0] = w.fast;
-                tile_bits[1] = wave_unsched ? 1u : 0u;
-            }
-        }
-        // W == 1: each lane reads only its own raw[][] entries, no barrier needed
+        if (any && !ovf) w.fast |= 1u << d;
     }
+    S.tile[kMisc][lane] = w.feasN;
+    S.tile[kMisc + 1][lane] = w.feasT;
+    S.tile[kMisc + 2][lane] = w.hterm0;
     if (W > 1) {
-        __syncthreads();
-        if (wv != 0) {
 #pragma unroll
-            for (int i = 0; i < K; ++i)
+        for (int i = 0; i < K; ++i)
 #pragma unroll
-                for (int d = 0; d < 10; ++d) w.L.h[i][d] = tile[i * 10 + d][lane];
-            w.fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)tile_bits[0]);
-            wave_unsched = __builtin_amdgcn_readfirstlane((int)tile_bits[1]) != 0;
+            for (int d = 0; d < 10; ++d) S.tile[i * 10 + d][lane] = w.L.h[i][d];
+        if (lane == 0) {
+            S.bits[0] = w.fast;
+            S.bits[1] = wave_unsched ? 1u : 0u;
         }
-        if (pbeg >= pend) return;  // wave-uniform
     }
+}
 
+// Waves 1..W-1: the tile wave 0 built (after a workgroup barrier).
+template <int K, int W>
+__device__ __forceinline__ void tile_load(const TileLds<K, W> &S, uint32_t lane, WaveRows<K> &w, bool &wave_unsched) {
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+        for (int d = 0; d < 10; ++d) w.L.h[i][d] = S.tile[i * 10 + d][lane];
+    w.fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.bits[0]);
+    wave_unsched = __builtin_amdgcn_readfirstlane((int)S.bits[1]) != 0;
+}
+
+// One wave sweeps pods [pbeg, pend) of the pod stream against its tile.
+template <int K, bool WANT_FLAGS, int W>
+__device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slot, const WaveRows<K> &w,
+                                           bool wave_unsched, uint32_t lane, const uint2 *__restrict__ ps,
+                                           uint32_t pbeg, uint32_t pend, u64 *__restrict__ keys,
+                                           uint32_t *__restrict__ pflags) {
+    constexpr int kMisc = TileLds<K, W>::kMisc;
     const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
     uint4 nx0 = q4[0], nx1 = q4[1], nx2 = q4[2], nx3 = q4[3];
     for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod blocks: one flush each
@@ -460,23 +459,23 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
             nx1 = q4[1];
             nx2 = q4[2];
             nx3 = q4[3];
-            // Pods past the chunk's end in its last group are evaluated too (the
-            // stream is padded; a chunk is a multiple of 8 pods, so only the batch's
-            // last group is partial) and masked out of the outcome bits.
+            // Pods past the range's end in its last group are evaluated too (the
+            // stream is padded; a range is a multiple of 8 pods except at the
+            // batch's end) and masked out of the outcome bits.
             uint32_t r[8];
             u64 gfound = 0, gs10 = 0, gnum = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t A = e[2 * j], cls = e[2 * j + 1];
-                uint32_t fs = 3u;          // found, score 10
+                uint32_t fs = 3u;            // found, score 10
                 if ((w.fast >> cls) & 1u) {  // cls < 10: not tolerating, class lists fit
                     if constexpr (K == 3)
                         r[j] = list_max3_idx(w.L, A, cls);  // the production geometry (30 rows per lane)
                     else
                         r[j] = list_max<K>(w.L, A, cls);
                 } else
-                    r[j] = eval_general(tile[kMisc][lane], tile[kMisc + 1][lane], tile[kMisc + 2][lane], raw, lane,
-                                        A, cls, fs);
+                    r[j] = eval_general(S.tile[kMisc][lane], S.tile[kMisc + 1][lane], S.tile[kMisc + 2][lane],
+                                        S.raw, lane, A, cls, fs);
                 gfound |= (u64)(fs & 1u) << j;
                 gs10 |= (u64)(fs >> 1) << j;
                 if (WANT_FLAGS) gnum |= (u64)(cls < 16u && wave_unsched) << j;
@@ -498,6 +497,78 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (WANT_FLAGS && lane < gn && ((num >> lane) & 1u)) atomicOr(&pflags[g + lane], 1u);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// K1 v7 grid: grid.x = node waves, grid.y = pod chunk groups. W waves per
+// workgroup share one node tile: wave 0 builds it and hands the class lists and
+// masks to the others through LDS, so the tile build (about 550 VALU per wave)
+// is paid once per W pod chunks.
+template <int K, bool WANT_FLAGS, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v7(
+    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
+    uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
+    u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
+    __shared__ TileLds<K, W> S;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+    const uint32_t wave_row0 = blockIdx.x * 64u * rpl;
+    const uint32_t pbeg = (blockIdx.y * W + wv) * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    if (wave_row0 >= n_rows) return;     // block-uniform
+    if (W == 1 && pbeg >= pend) return;  // wave-uniform (W > 1: after the hand-off)
+    WaveRows<K> w;
+    bool wave_unsched;
+    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane, w,
+                                  wave_unsched);
+    if (W > 1) {
+        __syncthreads();
+        if (wv != 0) tile_load<K, W>(S, lane, w, wave_unsched);
+        if (pbeg >= pend) return;  // wave-uniform
+    }
+    // W == 1: each lane reads only its own LDS entries, no barrier needed
+    sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags);
+}
+
+// K1 v8: the same sweep as a persistent grid with a work queue. One workgroup
+// per resident slot; workgroup b serves node column b % n_cols and takes the
+// column's items (W consecutive pod chunks, one per wave) from the column's
+// counter until it is spent. The tile is built once per workgroup, the next
+// item is claimed while the current one is swept, and the queue evens out the
+// workgroups of a column without rounds of fresh waves. (Moving to another
+// column when the own one is spent needs a tile rebuild inside the loop, and
+// the register pressure of that spills.) col_next[n_cols] must be zero on
+// entry (k_pod_prep zeroes it).
+template <int K, bool WANT_FLAGS, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v8(
+    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
+    uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
+    u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t *__restrict__ col_next, uint32_t n_cols) {
+    __shared__ TileLds<K, W> S;
+    __shared__ uint32_t s_item;
+    const uint32_t lane = lane_id();
+    const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+    const uint32_t per_col = (n_pods + chunk * W - 1) / (chunk * W);  // items per column
+    const uint32_t col = blockIdx.x % n_cols;
+    if (threadIdx.x == 0) s_item = atomicAdd(&col_next[col], 1u);
+    WaveRows<K> w;
+    bool wave_unsched;
+    const uint32_t wave_row0 = col * 64u * rpl;
+    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane, w,
+                                  wave_unsched);
+    __syncthreads();
+    if (W > 1 && wv != 0) tile_load<K, W>(S, lane, w, wave_unsched);
+    uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
+    while (it < per_col) {  // workgroup-uniform
+        uint32_t nxt = 0;
+        if (threadIdx.x == 0) nxt = atomicAdd(&col_next[col], 1u);  // claimed now, read after the sweep
+        const uint32_t pbeg = (it * W + wv) * chunk;
+        const uint32_t pend = min(n_pods, pbeg + chunk);
+        if (pbeg < pend) sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags);
+        __syncthreads();  // every wave has read s_item
+        if (threadIdx.x == 0) s_item = nxt;
+        __syncthreads();
+        it = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
     }
 }
 
@@ -1590,11 +1661,17 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 // K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
 // interleave variants inside one process: "v0" (hash every pair, the plain
 // cross-check) or the default v7.
-enum K1Variant { K1_V0 = 0, K1_V7 = 7 };
+// Default: the persistent v8 for shards of >= kK1V8MinColumns node columns (its
+// per-column counters are contended by too many workgroups on small shards),
+// v7 below (profiles/r01j_k1_v8_ab.jsonl: 100k rows 0.232 vs 0.241 ms, 12.5k
+// rows 0.088 vs 0.049 ms).
+enum K1Variant { K1_V0 = 0, K1_V7 = 7, K1_V8 = 8, K1_AUTO = -1 };
 static int k1_variant() {
     const char *e = getenv("MINISCHED_K1");
     if (e && e[0] == 'v' && e[1] == '0') return K1_V0;
-    return K1_V7;
+    if (e && e[0] == 'v' && e[1] == '8') return K1_V8;
+    if (e && e[0] == 'v' && e[1] == '7') return K1_V7;
+    return K1_AUTO;
 }
 
 // Geometry. Rows: at most kK1MaxRpl = 30 rows per lane, spread evenly over
@@ -1669,14 +1746,62 @@ static hipError_t launch_v7_rows(const NodeTable &t, uint32_t n_rows, const uint
     return launch_v7_waves<4, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
 }
 
+// K1 v8 geometry: the v7 rows per lane; items of W chunks of kK1V8Pods pods
+// (MINISCHED_K1_CHUNK), one persistent workgroup per resident slot.
+constexpr uint32_t kK1V8Pods = 64;
+constexpr uint32_t kK1V8MinColumns = 40;
+
+static uint32_t k1_columns(uint32_t n_rows) { return cdiv(n_rows, 64u * k1_rows_per_lane(n_rows)); }
+
+template <int K, bool WANT_FLAGS, int W>
+static hipError_t launch_v8(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps, uint32_t n_pods,
+                            unsigned long long *keys, uint32_t *flags, uint32_t *work, int num_cus, hipStream_t s) {
+    const auto kern = k_sweep_nunn_v8<K, WANT_FLAGS, W>;
+    static int bpc = 0;  // resident blocks per CU (one per template instance)
+    if (!bpc) {
+        int nb = 0;
+        hipError_t e =
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64 * W, 0);
+        if (e != hipSuccess) return e;
+        bpc = nb > 0 ? nb : 1;
+    }
+    uint32_t chunk = kK1V8Pods;
+    if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
+    const uint32_t n_cols = cdiv(n_rows, 64u * rpl);
+    const uint32_t items = n_cols * cdiv(n_pods, chunk * W);
+    // resident workgroups: 8 waves per SIMD, 4 SIMDs per CU (the occupancy API
+    // under-reports kernels with scratch; MINISCHED_K1_DEBUG prints both)
+    const uint32_t per_cu = std::max<uint32_t>((uint32_t)bpc, 32u / W);
+    const uint32_t blocks = std::min(items, per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256));
+    if (getenv("MINISCHED_K1_DEBUG"))
+        fprintf(stderr, "k1 v8: api blocks/CU %d, used %u, cols %u, items %u, blocks %u, chunk %u\n", bpc, per_cu,
+                n_cols, items, blocks, chunk);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * W), 0, s, t.flags, t.digit, n_rows, t.base, rpl, ps, n_pods,
+                       chunk, keys, flags, work, n_cols);
+    return hipGetLastError();
+}
+
+template <bool WANT_FLAGS>
+static hipError_t launch_v8_rows(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
+                                 unsigned long long *keys, uint32_t *flags, uint32_t *work, int num_cus,
+                                 hipStream_t s) {
+    const uint32_t rpl = k1_rows_per_lane(n_rows);
+    if (rpl <= 20) return launch_v8<2, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, work, num_cus, s);
+    if (rpl <= 30) return launch_v8<3, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, work, num_cus, s);
+    return launch_v8<4, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, work, num_cus, s);
+}
+
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
-                             int num_cus, hipStream_t s) {
+                             uint32_t *work, int num_cus, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     // pod stream + zeroed keys/flags (the sweep's atomicMax/atomicOr targets)
     const uint32_t n_prep = n_pods + kPodStreamPad;
-    hipLaunchKernelGGL(k_pod_prep, dim3(cdiv(n_prep, 256)), dim3(256), 0, s, pods, n_pods, seed32, pstream, keys,
-                       flags);
+    const int var = k1_variant();
+    const bool v8 = var == K1_V8 || (var == K1_AUTO && k1_columns(n_rows) >= kK1V8MinColumns);
+    const uint32_t n_work = v8 ? k1_columns(n_rows) : 0u;
+    hipLaunchKernelGGL(k_pod_prep, dim3(cdiv(std::max(n_prep, n_work), 256)), dim3(256), 0, s, pods, n_pods, seed32,
+                       pstream, keys, flags, work, n_work);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || n_rows == 0) return e;
     if (k1_variant() == K1_V0) {
@@ -1691,6 +1816,9 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
                                t.base, pods, n_pods, chunk, seed32, keys, flags);
         return hipGetLastError();
     }
+    if (v8)
+        return flags ? launch_v8_rows<true>(t, n_rows, pstream, n_pods, keys, flags, work, num_cus, s)
+                     : launch_v8_rows<false>(t, n_rows, pstream, n_pods, keys, flags, work, num_cus, s);
     return flags ? launch_v7_rows<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
                  : launch_v7_rows<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
 }

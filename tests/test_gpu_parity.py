@@ -68,7 +68,7 @@ def test_readme_scenario_gpu(oracle):
         assert e.read(9, 1)["pod_count"][0] == 1  # assume-on-select
 
 
-@pytest.fixture(params=["v7", "v7w2", "v7w4", "v0"])
+@pytest.fixture(params=["v7", "v7w2", "v7w4", "v8", "v0"])
 def k1_variant(request, monkeypatch):
     # every NU+NN sweep form stays bit-exact: v7 with 1, 2 or 4 waves per workgroup sharing
     # one tile build, and v0 (hash every pair), the plain cross-check
@@ -104,6 +104,21 @@ def test_nunn_rows_per_lane(oracle, monkeypatch, k1_variant, rpl, n_nodes, node_
     pr = synth.pods(1000, seed=seed)
     pr["tolerates_unschedulable"][::9] = 1
     nr["name_digit"][::13] = 0xFF
+    o = oracle.schedule(nr, pr, seed=seed, node_base=node_base)
+    with engine_with(nr, seed=seed, node_base=node_base) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+
+
+@pytest.mark.parametrize("n_nodes,node_base", [(100_000, 0), (76_800, 12_345), (50_000, 50_000)])
+def test_nunn_default_kernel_large_shards(oracle, monkeypatch, n_nodes, node_base):
+    # the default K1 choice (persistent v8 from 40 node columns up, v7 below) at shard sizes
+    # on both sides of the switch
+    monkeypatch.delenv("MINISCHED_K1", raising=False)
+    seed = 5 + n_nodes
+    nr = synth.nodes(n_nodes, seed=seed, start=node_base)
+    pr = synth.pods(2000, seed=seed)
+    pr["tolerates_unschedulable"][::7] = 1
+    pr["name_digit"][::97] = -1
     o = oracle.schedule(nr, pr, seed=seed, node_base=node_base)
     with engine_with(nr, seed=seed, node_base=node_base) as e:
         assert_same(e.schedule(pr, MODE_BATCHED), o)

@@ -21,7 +21,7 @@ def main():
 
     from minisched_amd import _lib, synth
 
-    P = int(os.environ.get("GEOM_PODS", 100_000))
+    pod_counts = [int(x) for x in os.environ.get("GEOM_PODS", "100000").split(",")]
     rounds = int(os.environ.get("GEOM_ROUNDS", 6))
     shards = [int(x) for x in os.environ.get("GEOM_SHARDS", "100000,50000,25000,12500").split(",")]
     rpls = os.environ.get("GEOM_RPL", "20,30,32").split(",")
@@ -32,8 +32,9 @@ def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(s)
-    pods = torch.from_numpy(synth.pods(P, seed=1).view(np.uint8).copy()).to(dev)
-    for N in shards:
+    pods_all = torch.from_numpy(synth.pods(max(pod_counts), seed=1).view(np.uint8).copy()).to(dev)
+    for N, P in [(n, p) for n in shards for p in pod_counts]:
+        pods = pods_all[: P * 40]
         eng = _lib.Engine(max_nodes=N, seed=1)
         eng.upsert(np.arange(N), synth.nodes(N, seed=1))
         eng.flush()

@@ -12,7 +12,7 @@ import os
 import shutil
 import sys
 
-src, tag, kernel_key = sys.argv[1], sys.argv[2], (sys.argv[3] if len(sys.argv) > 3 else "k_sweep_nunn_v7")
+src, tag, kernel_key = sys.argv[1], sys.argv[2], (sys.argv[3] if len(sys.argv) > 3 else "k_sweep_nunn_v")
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 
@@ -28,10 +28,11 @@ def per_kernel(path):
 
 stats = os.path.join(src, "stats", "run_kernel_stats.csv")
 shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
-avg_ns = None
+avg_ns, kernel_name = None, None
 for r in csv.DictReader(open(stats)):
     if kernel_key in r["Name"]:
         avg_ns = float(r["AverageNs"])
+        kernel_name = r["Name"].replace("void msgpu::(anonymous namespace)::", "").split("(")[0]
 fetch = per_kernel(os.path.join(src, "fetch", "run_counter_collection.csv")).get("FETCH_SIZE")
 write = per_kernel(os.path.join(src, "write", "run_counter_collection.csv")).get("WRITE_SIZE")
 sq = {}
@@ -40,6 +41,7 @@ if os.path.exists(p):
     sq = per_kernel(p)
 out = {
     "kernel": kernel_key,
+    "kernel_name": kernel_name,
     "kernel_avg_ns_rocprof": avg_ns,
     "FETCH_SIZE_KB_per_launch": fetch,
     "WRITE_SIZE_KB_per_launch": write,
