@@ -374,16 +374,51 @@ struct TileLds {
     static constexpr int kMisc = W > 1 ? 10 * K : 0;
     uint32_t raw[10][64];
     uint32_t tile[kMisc + 3][64];
+    uint32_t tol[K][10][64];  // class lists of tolerating pods (every present row of the digit)
     uint32_t bits[2];
     uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
 };
+
+// Class lists of the wave's rows in m_all (per class d: m_all[d]), padded as in
+// tile_build; returns the wave-uniform mask of classes whose lists fit.
+template <int K, typename Store>
+__device__ __forceinline__ uint32_t build_lists(const uint32_t (&m_all)[10], uint32_t hterm0, Store store) {
+    uint32_t fit = 0;
+#pragma unroll
+    for (int d = 0; d < 10; ++d) {
+        uint32_t m = m_all[d];
+        const uint32_t cnt = __popc(m);
+        const u64 any = __ballot(m != 0);
+        const bool ovf = __ballot(cnt > (uint32_t)K) != 0;
+        const uint32_t first = hterm0 + __umul24(first_slot(m), kG24);
+        const uint32_t donor = (uint32_t)__builtin_amdgcn_readlane((int)first, any ? (int)__builtin_ctzll(any) : 0);
+        const uint32_t pad = cnt ? first : donor;  // a class-d candidate of this wave
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const uint32_t v = hterm0 + __umul24(first_slot(m), kG24);
+            m &= m - 1u;
+            store(i, d, (uint32_t)i < cnt ? v : pad);
+        }
+        if (any && !ovf) fit |= 1u << d;
+    }
+    return fit;
+}
+
+// Tolerating pod of digit d on the list path: the lists live in LDS.
+template <int K, int W>
+__device__ __forceinline__ uint32_t list_max_tol(const TileLds<K, W> &S, uint32_t lane, uint32_t A, uint32_t d) {
+    uint32_t kb = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) kb = max(kb, mix32(A + S.tol[i][d][lane]));
+    return kb;
+}
 
 // Wave 0: builds the tile of rows wave_row0 + lane*rpl .. (+rpl) into w and LDS.
 template <int K, int W>
 __device__ __forceinline__ void tile_build(TileLds<K, W> &S, const uint8_t *__restrict__ nflags,
                                            const uint8_t *__restrict__ ndigit, uint32_t n_rows, uint32_t node_base,
-                                           uint32_t row0, uint32_t rpl, uint32_t lane, WaveRows<K> &w,
-                                           bool &wave_unsched) {
+                                           uint32_t row0, uint32_t rpl, uint32_t lane, uint32_t fast_mask,
+                                           WaveRows<K> &w, bool &wave_unsched) {
     constexpr int kMisc = TileLds<K, W>::kMisc;
     Bits32Cols c;
     load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
@@ -392,24 +427,18 @@ __device__ __forceinline__ void tile_build(TileLds<K, W> &S, const uint8_t *__re
     w.hterm0 = (node_base + row0) * kG24;
     w.fast = 0;
     wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
+    uint32_t mN[10], mT[10];
 #pragma unroll
     for (int d = 0; d < 10; ++d) {
         S.raw[d][lane] = c.onehot[d];
-        uint32_t m = c.onehot[d] & w.feasN;
-        const uint32_t cnt = __popc(m);
-        const u64 any = __ballot(m != 0);
-        const bool ovf = __ballot(cnt > (uint32_t)K) != 0;
-        const uint32_t first = w.hterm0 + __umul24(first_slot(m), kG24);
-        const uint32_t donor = (uint32_t)__builtin_amdgcn_readlane((int)first, any ? (int)__builtin_ctzll(any) : 0);
-        const uint32_t pad = cnt ? first : donor;  // a class-d candidate of this wave
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const uint32_t v = w.hterm0 + __umul24(first_slot(m), kG24);
-            m &= m - 1u;
-            w.L.h[i][d] = (uint32_t)i < cnt ? v : pad;
-        }
-        if (any && !ovf) w.fast |= 1u << d;
+        mN[d] = c.onehot[d] & w.feasN;
+        mT[d] = c.onehot[d] & w.feasT;
     }
+    // non-tolerating classes (fast bits 0..9, lists in registers); tolerating
+    // classes (cls = d | 16: fast bits 16..25, lists in LDS)
+    w.fast = build_lists<K>(mN, w.hterm0, [&](int i, int d, uint32_t v) { w.L.h[i][d] = v; });
+    w.fast |= build_lists<K>(mT, w.hterm0, [&](int i, int d, uint32_t v) { S.tol[i][d][lane] = v; }) << 16;
+    w.fast &= fast_mask;  // (tests and A/B: 0x3FF sends tolerating pods down the general path)
     S.tile[kMisc][lane] = w.feasN;
     S.tile[kMisc + 1][lane] = w.feasT;
     S.tile[kMisc + 2][lane] = w.hterm0;
@@ -468,8 +497,10 @@ __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slo
             for (int j = 0; j < 8; ++j) {
                 const uint32_t A = e[2 * j], cls = e[2 * j + 1];
                 uint32_t fs = 3u;            // found, score 10
-                if ((w.fast >> cls) & 1u) {  // cls < 10: not tolerating, class lists fit
-                    if constexpr (K == 3)
+                if ((w.fast >> cls) & 1u) {  // class lists fit (cls < 10 or 16 <= cls < 26)
+                    if (cls >= 16u)
+                        r[j] = list_max_tol<K, W>(S, lane, A, cls - 16u);  // tolerating pod
+                    else if constexpr (K == 3)
                         r[j] = list_max3_idx(w.L, A, cls);  // the production geometry (30 rows per lane)
                     else
                         r[j] = list_max<K>(w.L, A, cls);
@@ -508,7 +539,7 @@ template <int K, bool WANT_FLAGS, int W>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v7(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
-    u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
+    u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t fast_mask) {
     __shared__ TileLds<K, W> S;
     const uint32_t lane = lane_id();
     const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
@@ -519,8 +550,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
     if (W == 1 && pbeg >= pend) return;  // wave-uniform (W > 1: after the hand-off)
     WaveRows<K> w;
     bool wave_unsched;
-    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane, w,
-                                  wave_unsched);
+    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane,
+                                  fast_mask, w, wave_unsched);
     if (W > 1) {
         __syncthreads();
         if (wv != 0) tile_load<K, W>(S, lane, w, wave_unsched);
@@ -543,7 +574,8 @@ template <int K, bool WANT_FLAGS, int W>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v8(
     const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
     uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
-    u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t *__restrict__ col_next, uint32_t n_cols) {
+    u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t *__restrict__ col_next, uint32_t n_cols,
+    uint32_t fast_mask) {
     __shared__ TileLds<K, W> S;
     __shared__ uint32_t s_item;
     const uint32_t lane = lane_id();
@@ -554,8 +586,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
     WaveRows<K> w;
     bool wave_unsched;
     const uint32_t wave_row0 = col * 64u * rpl;
-    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane, w,
-                                  wave_unsched);
+    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane,
+                                  fast_mask, w, wave_unsched);
     __syncthreads();
     if (W > 1 && wv != 0) tile_load<K, W>(S, lane, w, wave_unsched);
     uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
@@ -1689,7 +1721,14 @@ static int k1_variant() {
 // MINISCHED_K1_CHUNK fixes the chunk and MINISCHED_K1_RPL the rows per lane
 // (<= 32), for experiments.
 typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, uint32_t, const uint2 *, uint32_t,
-                         uint32_t, unsigned long long *, uint32_t *);
+                         uint32_t, unsigned long long *, uint32_t *, uint32_t);
+
+// Classes on K1's list path: bits 0..9 non-tolerating, 16..25 tolerating pods.
+// MINISCHED_K1_TOL=0 sends tolerating pods down the general path (tests, A/B).
+static uint32_t k1_fast_mask() {
+    const char *e = getenv("MINISCHED_K1_TOL");
+    return (e && atoi(e) == 0) ? 0x3FFu : 0x3FF03FFu;
+}
 
 constexpr uint32_t kK1MaxRpl = 30;
 constexpr int kK1Waves = 4;  // waves per workgroup sharing one tile build (MINISCHED_K1_WAVES; profiles/r01i_k1_waves.jsonl)
@@ -1722,7 +1761,7 @@ static hipError_t launch_v7(const NodeTable &t, uint32_t n_rows, uint32_t rpl, c
         chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 8) * 8;
     if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk * W)), dim3(64 * W), 0, s, t.flags, t.digit, n_rows,
-                       t.base, rpl, ps, n_pods, chunk, keys, flags);
+                       t.base, rpl, ps, n_pods, chunk, keys, flags, k1_fast_mask());
     return hipGetLastError();
 }
 
@@ -1777,7 +1816,7 @@ static hipError_t launch_v8(const NodeTable &t, uint32_t n_rows, uint32_t rpl, c
         fprintf(stderr, "k1 v8: api blocks/CU %d, used %u, cols %u, items %u, blocks %u, chunk %u\n", bpc, per_cu,
                 n_cols, items, blocks, chunk);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * W), 0, s, t.flags, t.digit, n_rows, t.base, rpl, ps, n_pods,
-                       chunk, keys, flags, work, n_cols);
+                       chunk, keys, flags, work, n_cols, k1_fast_mask());
     return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ def main():
     chunks = os.environ.get("GEOM_CHUNK", "0,48,96,192,384").split(",")
     k1s = os.environ.get("GEOM_K1", "v7").split(",")
     waves = os.environ.get("GEOM_WAVES", "1").split(",")
+    tols = os.environ.get("GEOM_TOL", "1").split(",")  # MINISCHED_K1_TOL
     reps = int(os.environ.get("GEOM_REPS", 1))  # back-to-back launches per timing (hides launch gaps)
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
@@ -38,7 +39,7 @@ def main():
         eng = _lib.Engine(max_nodes=N, seed=1)
         eng.upsert(np.arange(N), synth.nodes(N, seed=1))
         eng.flush()
-        variants = [(r, c, k, wv) for r in rpls for c in chunks for k in k1s for wv in waves]
+        variants = [(r, c, k, wv, tl) for r in rpls for c in chunks for k in k1s for wv in waves for tl in tols]
         keys = {v: torch.empty(P, dtype=torch.int64, device=dev) for v in variants}
         times = {v: [] for v in variants}
         for rd in range(rounds + 1):
@@ -46,6 +47,7 @@ def main():
                 os.environ["MINISCHED_K1_RPL"] = v[0]
                 os.environ["MINISCHED_K1"] = v[2]
                 os.environ["MINISCHED_K1_WAVES"] = v[3]
+                os.environ["MINISCHED_K1_TOL"] = v[4]
                 if v[1] == "0":
                     os.environ.pop("MINISCHED_K1_CHUNK", None)
                 else:
@@ -62,7 +64,7 @@ def main():
         same = all(torch.equal(ref, keys[v]) for v in variants[1:])
         for v in variants:
             t = times[v]
-            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2], "waves": v[3],
+            print(json.dumps({"shard_rows": N, "pods": P, "rpl": int(v[0]), "chunk": int(v[1]) or "auto", "k1": v[2], "waves": v[3], "tol_lists": v[4],
                               "reps": reps, "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                               "keys_identical": bool(same)}), flush=True)
         eng.close()
