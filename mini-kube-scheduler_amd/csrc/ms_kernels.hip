@@ -307,6 +307,7 @@ struct WaveRows {
     uint32_t feasN, feasT;  // rows passing NodeUnschedulable for a non-tolerating / tolerating pod
     uint32_t hterm0;        // (ordinal of the lane's first row) * kG24
     uint32_t fast;          // wave-uniform: bit d = class d takes the list path
+    uint32_t fast_tol;      // wave-uniform: bit 16+d = tolerating class d takes the list path (LDS)
 };
 
 // List path of one pod: the lane's maximum hash over its K class-d entries.
@@ -375,7 +376,7 @@ struct TileLds {
     uint32_t raw[10][64];
     uint32_t tile[kMisc + 3][64];
     uint32_t tol[K][10][64];  // class lists of tolerating pods (every present row of the digit)
-    uint32_t bits[2];
+    uint32_t bits[3];       // wave 0's fast, wave_unsched, fast_tol
     uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
 };
 
@@ -436,9 +437,9 @@ __device__ __forceinline__ void tile_build(TileLds<K, W> &S, const uint8_t *__re
     }
     // non-tolerating classes (fast bits 0..9, lists in registers); tolerating
     // classes (cls = d | 16: fast bits 16..25, lists in LDS)
-    w.fast = build_lists<K>(mN, w.hterm0, [&](int i, int d, uint32_t v) { w.L.h[i][d] = v; });
-    w.fast |= build_lists<K>(mT, w.hterm0, [&](int i, int d, uint32_t v) { S.tol[i][d][lane] = v; }) << 16;
-    w.fast &= fast_mask;  // (tests and A/B: 0x3FF sends tolerating pods down the general path)
+    w.fast = build_lists<K>(mN, w.hterm0, [&](int i, int d, uint32_t v) { w.L.h[i][d] = v; }) & fast_mask;
+    w.fast_tol = (build_lists<K>(mT, w.hterm0, [&](int i, int d, uint32_t v) { S.tol[i][d][lane] = v; }) << 16) &
+                 fast_mask;  // (tests and A/B: fast_mask 0x3FF sends tolerating pods down the general path)
     S.tile[kMisc][lane] = w.feasN;
     S.tile[kMisc + 1][lane] = w.feasT;
     S.tile[kMisc + 2][lane] = w.hterm0;
@@ -450,6 +451,7 @@ __device__ __forceinline__ void tile_build(TileLds<K, W> &S, const uint8_t *__re
         if (lane == 0) {
             S.bits[0] = w.fast;
             S.bits[1] = wave_unsched ? 1u : 0u;
+            S.bits[2] = w.fast_tol;
         }
     }
 }
@@ -463,6 +465,7 @@ __device__ __forceinline__ void tile_load(const TileLds<K, W> &S, uint32_t lane,
         for (int d = 0; d < 10; ++d) w.L.h[i][d] = S.tile[i * 10 + d][lane];
     w.fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.bits[0]);
     wave_unsched = __builtin_amdgcn_readfirstlane((int)S.bits[1]) != 0;
+    w.fast_tol = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.bits[2]);
 }
 
 // One wave sweeps pods [pbeg, pend) of the pod stream against its tile.
@@ -497,14 +500,16 @@ __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slo
             for (int j = 0; j < 8; ++j) {
                 const uint32_t A = e[2 * j], cls = e[2 * j + 1];
                 uint32_t fs = 3u;            // found, score 10
-                if ((w.fast >> cls) & 1u) {  // class lists fit (cls < 10 or 16 <= cls < 26)
-                    if (cls >= 16u)
-                        r[j] = list_max_tol<K, W>(S, lane, A, cls - 16u);  // tolerating pod
-                    else if constexpr (K == 3)
+                // one SALU bit test on the common path: w.fast holds the non-tolerating
+                // classes only (cls >= 16 shifts them out); w.fast_tol the tolerating ones
+                if ((w.fast >> cls) & 1u) {  // non-tolerating, class lists fit
+                    if constexpr (K == 3)
                         r[j] = list_max3_idx(w.L, A, cls);  // the production geometry (30 rows per lane)
                     else
                         r[j] = list_max<K>(w.L, A, cls);
-                } else
+                } else if ((w.fast_tol >> cls) & 1u)  // tolerating pod, class lists fit (LDS)
+                    r[j] = list_max_tol<K, W>(S, lane, A, cls - 16u);
+                else
                     r[j] = eval_general(S.tile[kMisc][lane], S.tile[kMisc + 1][lane], S.tile[kMisc + 2][lane],
                                         S.raw, lane, A, cls, fs);
                 gfound |= (u64)(fs & 1u) << j;
