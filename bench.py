@@ -132,7 +132,8 @@ def main():
     # following chunk's sweep.
     pipe = world > 1 and os.environ.get("MINISCHED_BENCH_PIPE", "1") != "0"
     chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
-    cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe)
+    cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe,
+                               decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1")
     results = cyc.results
 
     sweep_events = []

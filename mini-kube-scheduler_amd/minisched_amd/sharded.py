@@ -79,12 +79,20 @@ class CrossStepPipeline:
         self._n = 0
         self._pending = None  # (works, buf, batch)
 
-    def step(self, batch=None):
+    def step(self, batch=None, drain_stream=None):
+        """drain_stream (optional torch stream): the previous batch's wait() and
+        decode are issued with it current, off the sweep stream."""
         buf = self._n & 1
         self._n += 1
         self._sweep(buf, batch)
         works = self._combine(buf)
-        self._drain()
+        if drain_stream is None:
+            self._drain()
+        else:
+            import torch
+
+            with torch.cuda.stream(drain_stream):
+                self._drain()
         self._pending = (works, buf, batch)
 
     def _drain(self):
@@ -118,7 +126,7 @@ class ShardedCycle:
     RESULT_BYTES = 24
 
     def __init__(self, engine, n_nodes_global: int, n_pods: int, pods_dev, stream, want_flags: bool = False,
-                 group=None, chunks: int = 1, pipeline: bool = False):
+                 group=None, chunks: int = 1, pipeline: bool = False, decode_stream: bool = False):
         import torch
 
         self.eng = engine
@@ -136,11 +144,22 @@ class ShardedCycle:
         self.results = torch.empty(n_pods * self.RESULT_BYTES, dtype=torch.uint8, device=dev)
         self.chunks = chunk_bounds(n_pods, 1 if pipeline else chunks)
         self._pipe = None
+        # decode_stream=True (opt-in, MINISCHED_DECODE_STREAM=1 in bench.py): the
+        # decode of step k waits for step k's combine on a stream of its own, so
+        # the sweep stream never waits on the collective's stream; the sweep
+        # stream waits only for the decode that last read a key buffer before it
+        # zeroes that buffer again, two steps later. Measured on one GPU it loses:
+        # the extra event/stream calls make the 12.5k-row step host-bound (0.096
+        # vs 0.070 ms; profiles/r01n_decode_stream_ab.jsonl), so it is off.
+        self._dstream = None
+        self._dec_done = [None] * nbuf
+        if pipeline and decode_stream and dev.type == "cuda":
+            self._dstream = torch.cuda.Stream(device=dev)
         if pipeline:
-            self._pipe = CrossStepPipeline(
-                lambda buf, _b: self.sweep(0, self.P, buf),
-                lambda buf: combine_(self._keys[buf], self._flags[buf], self.group, async_op=True),
-                lambda buf, _b: self.decode(0, self.P, buf))
+            self._pipe = CrossStepPipeline(self._pipe_sweep,
+                                           lambda buf: combine_(self._keys[buf], self._flags[buf], self.group,
+                                                                async_op=True),
+                                           lambda buf, _b: self.decode(0, self.P, buf))
 
     def _ptrs(self, a, buf=0):
         pods = self.pods.data_ptr() + a * self.POD_BYTES
@@ -152,14 +171,29 @@ class ShardedCycle:
         pods, keys, flags = self._ptrs(a, buf)
         self.eng.sweep_device(b - a, pods, keys, flags, self.stream.cuda_stream)
 
+    def _pipe_sweep(self, buf, _batch):
+        if self._dec_done[buf] is not None:  # the decode that last read keys[buf]
+            self.stream.wait_event(self._dec_done[buf])
+        self.sweep(0, self.P, buf)
+
     def decode(self, a, b, buf=0):
         pods, keys, flags = self._ptrs(a, buf)
         res = self.results.data_ptr() + a * self.RESULT_BYTES
-        self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self.stream.cuda_stream)
+        if self._dstream is None:
+            self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self.stream.cuda_stream)
+            return
+        import torch
+
+        # called inside CrossStepPipeline's drain with the decode stream current:
+        # the combine's wait() has already ordered this stream after the collective
+        self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self._dstream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(self._dstream)
+        self._dec_done[buf] = ev
 
     def step(self, world: int, on_sweep=None):
         if self._pipe is not None and world > 1:
-            self._pipe.step()
+            self._pipe.step(drain_stream=self._dstream)
             return
         pending = []
         for a, b in self.chunks:
@@ -176,6 +210,17 @@ class ShardedCycle:
             self.decode(a, b)
 
     def finish(self):
-        """Drains a pipelined step's pending combine + decode (no-op otherwise)."""
+        """Drains a pipelined step's pending combine + decode (no-op otherwise).
+
+        With the decode stream, the caller's stream is ordered after the last
+        decode, so a synchronize of it (or of the device) covers the results.
+        """
         if self._pipe is not None:
-            self._pipe.finish()
+            if self._dstream is not None:
+                import torch
+
+                with torch.cuda.stream(self._dstream):
+                    self._pipe.finish()
+                self.stream.wait_stream(self._dstream)
+            else:
+                self._pipe.finish()

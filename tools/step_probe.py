@@ -44,7 +44,8 @@ def main():
         eng = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NN, node_base=lo, seed=1)
         eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=1, start=lo))
         eng.flush()
-        cyc = sharded.ShardedCycle(eng, N, P, pods, stream, pipeline=True)
+        cyc = sharded.ShardedCycle(eng, N, P, pods, stream, pipeline=True,
+                                   decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1")
         for _ in range(5):
             cyc.step(2)
         cyc.finish()
