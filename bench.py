@@ -71,6 +71,7 @@ def cpu_baseline(n_nodes, seed, target_s):
     t0 = time.perf_counter()
     _oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=threads)
     dt = time.perf_counter() - t0
+    faithful = cpu_faithful_1t(nr, n_nodes, seed, target_s / 4)
     return {
         "value": n_pods * n_nodes / dt,
         "unit": "pod×node evals/s",
@@ -79,7 +80,34 @@ def cpu_baseline(n_nodes, seed, target_s):
         "sample": f"oracle/ms_oracle.c msor_schedule_nunn_omp, {n_nodes} nodes x first {n_pods} pods "
         f"({dt:.1f} s, OpenMP {threads} threads); Go reference not buildable offline (GOMAXPROCS n/a)",
         "pods_per_s": n_pods / dt,
+        "faithful_1t": faithful,
     }
+
+
+def cpu_faithful_1t(nr, n_nodes, seed, target_s):
+    """SURVEY §8(d) cpu_faithful: one thread, the reference's per-pair work
+    (last-character name parse per node and pod, per-pod feasible list, score
+    list, then selectHost) — oracle/ms_oracle.c msor_schedule_nunn_names."""
+    import _oracle  # checker only
+
+    from minisched_amd import synth
+
+    node_names = [f"node{i}" for i in range(n_nodes)]
+    flags = np.ascontiguousarray(nr["unschedulable"], dtype=np.uint8)
+
+    def run(n):
+        pr = synth.pods(n, seed=seed)
+        names = [f"pod{j}" for j in range(n)]
+        t0 = time.perf_counter()
+        _oracle.schedule_nunn_names(node_names, flags, names, pr["tolerates_unschedulable"], pr["ordinal"], seed=seed)
+        return time.perf_counter() - t0
+
+    dt = max(run(64), 1e-6)  # (the per-call ctypes name arrays are inside the clock, ~3 %)
+    n = int(min(100_000, max(64, 64 * target_s / dt)))
+    dt = run(n)
+    return {"value": n * n_nodes / dt, "unit": "pod×node evals/s", "cores": 1, "kind": "port",
+            "sample": f"msor_schedule_nunn_names, {n_nodes} node names x first {n} pods ({dt:.1f} s, 1 thread)",
+            "pods_per_s": n / dt}
 
 
 def main():
@@ -127,13 +155,17 @@ def main():
     assert stream.cuda_stream != 0
     # N > 1: each step's RCCL all-reduce overlaps the next step's sweep (two key
     # buffers, sharded.CrossStepPipeline); the last step's combine + decode are
-    # drained inside the timed region. MINISCHED_BENCH_PIPE=0 falls back to
+    # drained inside the timed region. The decode waits for its all-reduce on a
+    # stream of its own and the host, not the sweep stream, waits for a key
+    # buffer's last decode (MINISCHED_DECODE_STREAM=0: the sweep stream waits;
+    # MINISCHED_PIPE_DEPTH: combines in flight). MINISCHED_BENCH_PIPE=0 falls back to
     # in-step pod chunks (MINISCHED_BENCH_CHUNKS) whose reductions overlap the
     # following chunk's sweep.
     pipe = world > 1 and os.environ.get("MINISCHED_BENCH_PIPE", "1") != "0"
     chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
     cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe,
-                               decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1")
+                               decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "1") == "1",
+                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "1")))
     results = cyc.results
 
     sweep_events = []

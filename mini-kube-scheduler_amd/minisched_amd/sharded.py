@@ -61,47 +61,60 @@ def chunk_bounds(n: int, chunks: int):
 
 
 class CrossStepPipeline:
-    """Overlaps batch k's cross-shard combine with batch k+1's sweep.
+    """Overlaps batch k's cross-shard combine with the following batches' sweeps.
 
-    Two key buffers alternate between batches. step(batch) sweeps the batch
-    into its buffer, starts the async combine of that buffer, then waits for
-    the PREVIOUS batch's combine and decodes it; finish() drains the last one.
-    On the device stream this orders  sweep k+1 -> wait(combine k) -> decode k,
-    so the collective of batch k runs while batch k+1 sweeps. Buffer b is
-    swept again only two batches later, after its decode (stream order).
+    depth + 1 key buffers rotate between batches (two by default). step(batch)
+    sweeps the batch into its buffer, starts the async combine of that buffer,
+    then, once `depth` combines are in flight, waits for the OLDEST one and
+    decodes it; finish() drains the rest. With depth 1 the device stream runs
+    sweep k+1 -> wait(combine k) -> decode k, so the collective of batch k runs
+    while batch k+1 sweeps; depth 2 gives each collective two sweeps of slack
+    (a collective slower than one sweep, or a cross-queue wait that lands late,
+    then no longer idles the sweep stream). Buffer b is swept again only
+    depth + 1 batches later, after its decode (stream order).
 
     sweep(buf, batch), decode(buf, batch): enqueue work; combine(buf) -> list
     of async works (torch.distributed) whose wait() orders the caller's stream.
     """
 
-    def __init__(self, sweep, combine, decode):
+    def __init__(self, sweep, combine, decode, depth: int = 1, nbuf: int = 0):
+        if depth < 1 or (nbuf and nbuf < depth + 1):
+            raise ValueError("depth must be >= 1 and nbuf >= depth + 1")
         self._sweep, self._combine, self._decode = sweep, combine, decode
+        self.depth = depth
+        self.nbuf = nbuf or depth + 1
         self._n = 0
-        self._pending = None  # (works, buf, batch)
+        self._pending = []  # [(works, buf, batch)], oldest first
 
     def step(self, batch=None, drain_stream=None):
-        """drain_stream (optional torch stream): the previous batch's wait() and
+        """drain_stream (optional torch stream): the oldest batch's wait() and
         decode are issued with it current, off the sweep stream."""
-        buf = self._n & 1
+        buf = self._n % self.nbuf
         self._n += 1
         self._sweep(buf, batch)
-        works = self._combine(buf)
-        if drain_stream is None:
-            self._drain()
-        else:
-            import torch
+        self._pending.append((self._combine(buf), buf, batch))
+        if len(self._pending) > self.depth:
+            if drain_stream is None:
+                self._drain_one()
+            else:
+                import torch
 
-            with torch.cuda.stream(drain_stream):
-                self._drain()
-        self._pending = (works, buf, batch)
+                prev = torch.cuda.current_stream()
+                torch.cuda.set_stream(drain_stream)
+                try:
+                    self._drain_one()
+                finally:
+                    torch.cuda.set_stream(prev)
+
+    def _drain_one(self):
+        works, buf, batch = self._pending.pop(0)
+        for w in works:
+            w.wait()
+        self._decode(buf, batch)
 
     def _drain(self):
-        if self._pending is not None:
-            works, buf, batch = self._pending
-            self._pending = None
-            for w in works:
-                w.wait()
-            self._decode(buf, batch)
+        while self._pending:
+            self._drain_one()
 
     def finish(self):
         self._drain()
@@ -115,9 +128,9 @@ class ShardedCycle:
     finally decode every chunk once its reduction has landed.
 
     With pipeline=True (N > 1) a step is instead one whole-batch sweep whose
-    all-reduce overlaps the NEXT step's sweep (CrossStepPipeline, two key
-    buffers); the step's decode lands one step later and finish() drains the
-    last one. Pod chunks within a step cost more sweep time than the overlap
+    all-reduce overlaps the next `depth` steps' sweeps (CrossStepPipeline,
+    depth + 1 key buffers); the step's decode lands `depth` steps later and
+    finish() drains the rest. Pod chunks within a step cost more sweep time than the overlap
     saves at small shards (tools/shard_probe.py), so the pipelined form uses
     one chunk.
     """
@@ -126,7 +139,8 @@ class ShardedCycle:
     RESULT_BYTES = 24
 
     def __init__(self, engine, n_nodes_global: int, n_pods: int, pods_dev, stream, want_flags: bool = False,
-                 group=None, chunks: int = 1, pipeline: bool = False, decode_stream: bool = False):
+                 group=None, chunks: int = 1, pipeline: bool = False, decode_stream: bool = False,
+                 depth: int = 1):
         import torch
 
         self.eng = engine
@@ -136,7 +150,9 @@ class ShardedCycle:
         self.stream = stream
         self.group = group
         dev = pods_dev.device
-        nbuf = 2 if pipeline else 1
+        # with the decode stream, two spare key buffers let the host wait for a
+        # buffer's last decode (host-side flow control) long after it finished
+        nbuf = (depth + 3 if decode_stream else depth + 1) if pipeline else 1
         self._keys = [torch.empty(n_pods, dtype=torch.int64, device=dev) for _ in range(nbuf)]
         self._flags = ([torch.empty(n_pods, dtype=torch.int32, device=dev) for _ in range(nbuf)]
                        if want_flags else [None] * nbuf)
@@ -144,22 +160,26 @@ class ShardedCycle:
         self.results = torch.empty(n_pods * self.RESULT_BYTES, dtype=torch.uint8, device=dev)
         self.chunks = chunk_bounds(n_pods, 1 if pipeline else chunks)
         self._pipe = None
-        # decode_stream=True (opt-in, MINISCHED_DECODE_STREAM=1 in bench.py): the
-        # decode of step k waits for step k's combine on a stream of its own, so
-        # the sweep stream never waits on the collective's stream; the sweep
-        # stream waits only for the decode that last read a key buffer before it
-        # zeroes that buffer again, two steps later. Measured on one GPU it loses:
-        # the extra event/stream calls make the 12.5k-row step host-bound (0.096
-        # vs 0.070 ms; profiles/r01n_decode_stream_ab.jsonl), so it is off.
+        # decode_stream=True (bench.py's N > 1 default; MINISCHED_DECODE_STREAM=0 turns
+        # it off; profiles/r01p_pipeline_ab.jsonl: 12.5k-row step 0.061 vs 0.071 ms): the decode of
+        # step k waits for step k's combine on a stream of its own, so the sweep
+        # stream never waits on another queue. A cross-queue wait idles the waiting
+        # stream ~10 us even when its event completed long before
+        # (profiles/r01o_*), and at a 12.5k-row shard that is a sixth of the step.
+        # A key buffer is reused only after its last decode: the HOST waits for
+        # that decode's event (issued two steps earlier, long done unless the host
+        # runs ahead of the device), so the sweep stream carries no waits at all.
         self._dstream = None
-        self._dec_done = [None] * nbuf
+        self._dec_ev = [None] * nbuf
+        self._dec_live = [False] * nbuf
         if pipeline and decode_stream and dev.type == "cuda":
             self._dstream = torch.cuda.Stream(device=dev)
+            self._dec_ev = [torch.cuda.Event() for _ in range(nbuf)]
         if pipeline:
             self._pipe = CrossStepPipeline(self._pipe_sweep,
                                            lambda buf: combine_(self._keys[buf], self._flags[buf], self.group,
                                                                 async_op=True),
-                                           lambda buf, _b: self.decode(0, self.P, buf))
+                                           lambda buf, _b: self.decode(0, self.P, buf), depth=depth, nbuf=nbuf)
 
     def _ptrs(self, a, buf=0):
         pods = self.pods.data_ptr() + a * self.POD_BYTES
@@ -172,8 +192,8 @@ class ShardedCycle:
         self.eng.sweep_device(b - a, pods, keys, flags, self.stream.cuda_stream)
 
     def _pipe_sweep(self, buf, _batch):
-        if self._dec_done[buf] is not None:  # the decode that last read keys[buf]
-            self.stream.wait_event(self._dec_done[buf])
+        if self._dec_live[buf]:  # host waits for the decode that last read keys[buf]
+            self._dec_ev[buf].synchronize()
         self.sweep(0, self.P, buf)
 
     def decode(self, a, b, buf=0):
@@ -182,14 +202,11 @@ class ShardedCycle:
         if self._dstream is None:
             self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self.stream.cuda_stream)
             return
-        import torch
-
         # called inside CrossStepPipeline's drain with the decode stream current:
         # the combine's wait() has already ordered this stream after the collective
         self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self._dstream.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(self._dstream)
-        self._dec_done[buf] = ev
+        self._dec_ev[buf].record(self._dstream)
+        self._dec_live[buf] = True
 
     def step(self, world: int, on_sweep=None):
         if self._pipe is not None and world > 1:
@@ -219,8 +236,12 @@ class ShardedCycle:
             if self._dstream is not None:
                 import torch
 
-                with torch.cuda.stream(self._dstream):
+                prev = torch.cuda.current_stream()
+                torch.cuda.set_stream(self._dstream)
+                try:
                     self._pipe.finish()
+                finally:
+                    torch.cuda.set_stream(prev)
                 self.stream.wait_stream(self._dstream)
             else:
                 self._pipe.finish()

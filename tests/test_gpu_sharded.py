@@ -1,7 +1,7 @@
 """N > 1 bench path on one GPU: two ranks (gloo, both on cuda:0) run
 sharded.ShardedCycle exactly as bench.py does — the HIP sweep of each node
 shard, the cross-shard MAX combine, the decode — in both the pipelined
-(cross-step, with and without its own decode stream) and the in-step chunked
+(cross-step at depth 1 and 2, with and without its own decode stream) and the in-step chunked
 forms, and every rank's decoded results must equal the oracle's over the
 whole cluster.
 """
@@ -27,7 +27,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, pipeline, chunks, dstream, q):
+def _worker(rank, world, port, pipeline, chunks, dstream, depth, q):
     import torch
     import torch.distributed as dist
 
@@ -47,7 +47,7 @@ def _worker(rank, world, port, pipeline, chunks, dstream, q):
         stream = torch.cuda.Stream(device=dev)
         torch.cuda.set_stream(stream)
         cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, chunks=chunks, pipeline=pipeline,
-                                   decode_stream=dstream)
+                                   decode_stream=dstream, depth=depth)
         for _ in range(5):  # both key buffers reused after their decodes
             cyc.step(world)
         cyc.finish()
@@ -60,13 +60,15 @@ def _worker(rank, world, port, pipeline, chunks, dstream, q):
         q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("pipeline,chunks,dstream", [(True, 1, True), (True, 1, False), (False, 3, False)])
-def test_two_rank_sharded_cycle_on_gpu(oracle, pipeline, chunks, dstream):
+@pytest.mark.parametrize("pipeline,chunks,dstream,depth",
+                         [(True, 1, False, 1), (True, 1, False, 2), (True, 1, True, 1), (True, 1, True, 2),
+                          (False, 3, False, 1)])
+def test_two_rank_sharded_cycle_on_gpu(oracle, pipeline, chunks, dstream, depth):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, pipeline, chunks, dstream, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, pipeline, chunks, dstream, depth, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=110) for _ in range(world)]

@@ -119,7 +119,7 @@ def test_chunk_bounds():
             assert len(spans) <= c
 
 
-def _pipe_worker(rank, world, port, n_nodes, batches, q):
+def _pipe_worker(rank, world, port, n_nodes, batches, depth, q):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -132,7 +132,7 @@ def _pipe_worker(rank, world, port, n_nodes, batches, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     nr = synth.nodes(n_nodes, seed=21)
     lo, hi = sharded.shard_bounds(n_nodes, rank, world)
-    keys = [torch.zeros(batches[0], dtype=torch.int64) for _ in range(2)]
+    keys = [torch.zeros(batches[0], dtype=torch.int64) for _ in range(depth + 1)]
     out = {}
 
     def sweep(buf, k):  # this rank's shard of batch k (the oracle stands in for the HIP sweep)
@@ -146,23 +146,24 @@ def _pipe_worker(rank, world, port, n_nodes, batches, q):
     def decode(buf, k):
         out[k] = keys[buf][: batches[k]].numpy().view(np.uint64).copy()
 
-    pipe = sharded.CrossStepPipeline(sweep, combine, decode)
+    pipe = sharded.CrossStepPipeline(sweep, combine, decode, depth=depth)
     for k in range(len(batches)):
         pipe.step(k)
-        assert len(out) == k  # batch k decodes one step later
+        assert len(out) == max(0, k + 1 - depth)  # batch k decodes `depth` steps later
     pipe.finish()
     q.put((rank, out))
     dist.destroy_process_group()
 
 
-def test_cross_step_pipeline_gloo(oracle):
-    # bench.py's N > 1 step: batch k's all-reduce overlaps batch k+1's sweep, two
-    # key buffers alternate; every batch must decode to the single-process result
+@pytest.mark.parametrize("depth", [1, 2])
+def test_cross_step_pipeline_gloo(oracle, depth):
+    # bench.py's N > 1 step: batch k's all-reduce overlaps the next `depth` sweeps,
+    # depth + 1 key buffers rotate; every batch must decode to the single-process result
     world, n_nodes, batches = 2, 1500, [256, 200, 256, 131, 256]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, n_nodes, batches, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, n_nodes, batches, depth, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]
