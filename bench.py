@@ -153,19 +153,21 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
-    # N > 1: each step's RCCL all-reduce overlaps the next step's sweep (two key
-    # buffers, sharded.CrossStepPipeline); the last step's combine + decode are
-    # drained inside the timed region. The decode waits for its all-reduce on a
-    # stream of its own and the host, not the sweep stream, waits for a key
-    # buffer's last decode (MINISCHED_DECODE_STREAM=0: the sweep stream waits;
-    # MINISCHED_PIPE_DEPTH: combines in flight). MINISCHED_BENCH_PIPE=0 falls back to
-    # in-step pod chunks (MINISCHED_BENCH_CHUNKS) whose reductions overlap the
-    # following chunk's sweep.
+    # N > 1: each step's RCCL all-reduce overlaps the following steps' sweeps
+    # (sharded.CrossStepPipeline, depth 3: three all-reduces in flight, four key
+    # buffers); every third step waits for the newest all-reduce once and decodes
+    # three batches (a cross-queue wait idles the sweep stream ~10 us however
+    # early its event completed; profiles/r01t_pipeline_group_ab.jsonl). The last
+    # steps' combines + decodes are drained inside the timed region.
+    # MINISCHED_PIPE_DEPTH / MINISCHED_PIPE_GROUP / MINISCHED_DECODE_STREAM=1 select
+    # the other measured forms; MINISCHED_BENCH_PIPE=0 falls back to in-step pod
+    # chunks (MINISCHED_BENCH_CHUNKS) whose reductions overlap the next chunk's sweep.
     pipe = world > 1 and os.environ.get("MINISCHED_BENCH_PIPE", "1") != "0"
     chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
     cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe,
-                               decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "1") == "1",
-                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "1")))
+                               decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1",
+                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "3")),
+                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "3")))
     results = cyc.results
 
     sweep_events = []

@@ -19,6 +19,7 @@ code runs on CPU tensors with gloo for the tests.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 
@@ -60,6 +61,17 @@ def chunk_bounds(n: int, chunks: int):
     return [(a, min(n, a + step)) for a in range(0, n, step)]
 
 
+def _ordered_backend(group=None) -> bool:
+    """True when the group's collectives complete in issue order on one device
+    stream (torch's "nccl" = RCCL backend); gloo's worker threads give no such order."""
+    import torch.distributed as dist
+
+    try:
+        return dist.is_initialized() and dist.get_backend(group) == "nccl"
+    except Exception:
+        return False
+
+
 class CrossStepPipeline:
     """Overlaps batch k's cross-shard combine with the following batches' sweeps.
 
@@ -77,12 +89,19 @@ class CrossStepPipeline:
     of async works (torch.distributed) whose wait() orders the caller's stream.
     """
 
-    def __init__(self, sweep, combine, decode, depth: int = 1, nbuf: int = 0):
-        if depth < 1 or (nbuf and nbuf < depth + 1):
-            raise ValueError("depth must be >= 1 and nbuf >= depth + 1")
+    def __init__(self, sweep, combine, decode, depth: int = 1, nbuf: int = 0, group: int = 1,
+                 ordered: bool = False):
+        if depth < 1 or (nbuf and nbuf < depth + 1) or not 1 <= group <= depth:
+            raise ValueError("need depth >= 1, nbuf >= depth + 1, 1 <= group <= depth")
         self._sweep, self._combine, self._decode = sweep, combine, decode
         self.depth = depth
         self.nbuf = nbuf or depth + 1
+        # group > 1: drain `group` batches at a time. With ordered=True (RCCL: one
+        # stream per communicator runs the collectives in issue order) only the
+        # newest batch's combine is waited for, so the sweep stream pays one
+        # cross-queue wait per `group` steps instead of one per step.
+        self.group = group
+        self.ordered = ordered
         self._n = 0
         self._pending = []  # [(works, buf, batch)], oldest first
 
@@ -94,27 +113,31 @@ class CrossStepPipeline:
         self._sweep(buf, batch)
         self._pending.append((self._combine(buf), buf, batch))
         if len(self._pending) > self.depth:
+            n = min(self.group, len(self._pending))
             if drain_stream is None:
-                self._drain_one()
+                self._drain_n(n)
             else:
                 import torch
 
                 prev = torch.cuda.current_stream()
                 torch.cuda.set_stream(drain_stream)
                 try:
-                    self._drain_one()
+                    self._drain_n(n)
                 finally:
                     torch.cuda.set_stream(prev)
 
-    def _drain_one(self):
-        works, buf, batch = self._pending.pop(0)
-        for w in works:
-            w.wait()
-        self._decode(buf, batch)
+    def _drain_n(self, n):
+        batch_list, self._pending = self._pending[:n], self._pending[n:]
+        for i, (works, _buf, _batch) in enumerate(batch_list):
+            if not self.ordered or i == n - 1:
+                for w in works:
+                    w.wait()
+        for _works, buf, batch in batch_list:
+            self._decode(buf, batch)
 
     def _drain(self):
-        while self._pending:
-            self._drain_one()
+        if self._pending:
+            self._drain_n(len(self._pending))
 
     def finish(self):
         self._drain()
@@ -140,7 +163,7 @@ class ShardedCycle:
 
     def __init__(self, engine, n_nodes_global: int, n_pods: int, pods_dev, stream, want_flags: bool = False,
                  group=None, chunks: int = 1, pipeline: bool = False, decode_stream: bool = False,
-                 depth: int = 1):
+                 depth: int = 1, drain_group: int = 1):
         import torch
 
         self.eng = engine
@@ -152,7 +175,9 @@ class ShardedCycle:
         dev = pods_dev.device
         # with the decode stream, two spare key buffers let the host wait for a
         # buffer's last decode (host-side flow control) long after it finished
-        nbuf = (depth + 3 if decode_stream else depth + 1) if pipeline else 1
+        # (MINISCHED_PIPE_SPARE overrides the two, for A/B runs)
+        spare = int(os.environ.get("MINISCHED_PIPE_SPARE", "2")) if decode_stream else 0
+        nbuf = depth + 1 + spare if pipeline else 1
         self._keys = [torch.empty(n_pods, dtype=torch.int64, device=dev) for _ in range(nbuf)]
         self._flags = ([torch.empty(n_pods, dtype=torch.int32, device=dev) for _ in range(nbuf)]
                        if want_flags else [None] * nbuf)
@@ -160,15 +185,15 @@ class ShardedCycle:
         self.results = torch.empty(n_pods * self.RESULT_BYTES, dtype=torch.uint8, device=dev)
         self.chunks = chunk_bounds(n_pods, 1 if pipeline else chunks)
         self._pipe = None
-        # decode_stream=True (bench.py's N > 1 default; MINISCHED_DECODE_STREAM=0 turns
-        # it off; profiles/r01p_pipeline_ab.jsonl: 12.5k-row step 0.061 vs 0.071 ms): the decode of
-        # step k waits for step k's combine on a stream of its own, so the sweep
-        # stream never waits on another queue. A cross-queue wait idles the waiting
-        # stream ~10 us even when its event completed long before
-        # (profiles/r01o_*), and at a 12.5k-row shard that is a sixth of the step.
-        # A key buffer is reused only after its last decode: the HOST waits for
-        # that decode's event (issued two steps earlier, long done unless the host
-        # runs ahead of the device), so the sweep stream carries no waits at all.
+        # decode_stream=True (opt-in, MINISCHED_DECODE_STREAM=1 in bench.py): the
+        # decode of step k waits for step k's combine on a stream of its own, so
+        # the sweep stream never waits on another queue (a cross-queue wait idles
+        # the waiting stream ~10 us even when its event completed long before,
+        # profiles/r01o_*). A key buffer is reused only after its last decode: the
+        # HOST waits for that decode's event, so the sweep stream carries no
+        # waits at all. The extra host calls make the small-shard step host-bound,
+        # though, and grouped drains on the sweep stream (depth 3, group 3) measure
+        # better at every shard size (profiles/r01t_pipeline_group_ab.jsonl).
         self._dstream = None
         self._dec_ev = [None] * nbuf
         self._dec_live = [False] * nbuf
@@ -179,7 +204,8 @@ class ShardedCycle:
             self._pipe = CrossStepPipeline(self._pipe_sweep,
                                            lambda buf: combine_(self._keys[buf], self._flags[buf], self.group,
                                                                 async_op=True),
-                                           lambda buf, _b: self.decode(0, self.P, buf), depth=depth, nbuf=nbuf)
+                                           lambda buf, _b: self.decode(0, self.P, buf), depth=depth, nbuf=nbuf,
+                                           group=drain_group, ordered=_ordered_backend(group))
 
     def _ptrs(self, a, buf=0):
         pods = self.pods.data_ptr() + a * self.POD_BYTES

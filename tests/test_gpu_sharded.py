@@ -80,3 +80,54 @@ def test_two_rank_sharded_cycle_on_gpu(oracle, pipeline, chunks, dstream, depth)
     for rank, res, _ in got:
         for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
             assert np.array_equal(res[k_res], o[k_or]), f"rank {rank} {k_res}"
+
+
+def _rccl_worker(port, depth, group, dstream, q):
+    import torch
+    import torch.distributed as dist
+
+    from minisched_amd import _lib, sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        eng = _lib.Engine(max_nodes=N_NODES, plugin_set=_lib.PLUGINS_NU_NN, node_base=0, seed=SEED)
+        eng.upsert(np.arange(N_NODES, dtype=np.uint32), synth.nodes(N_NODES, seed=SEED))
+        eng.flush()
+        pods = torch.from_numpy(synth.pods(N_PODS, seed=SEED).view(np.uint8).copy()).to(dev)
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
+        cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, pipeline=True, decode_stream=dstream,
+                                   depth=depth, drain_group=group)
+        ordered = cyc._pipe.ordered
+        outs = []
+        for k in range(7):  # world > 1 form: RCCL all-reduce per step, grouped drains
+            cyc.step(2)
+        cyc.finish()
+        torch.cuda.synchronize()
+        outs.append(cyc.results.cpu().numpy().view(_lib.RESULT).copy())
+        eng.close()
+        dist.destroy_process_group()
+        q.put((ordered, outs, None))
+    except Exception as e:
+        q.put((None, None, repr(e)))
+
+
+@pytest.mark.parametrize("depth,group,dstream", [(2, 2, False), (3, 3, False), (2, 2, True)])
+def test_rccl_grouped_drain(oracle, depth, group, dstream):
+    # the RCCL backend takes the ordered path (one wait per drained group)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), depth, group, dstream, q))
+    p.start()
+    ordered, outs, err = q.get(timeout=110)
+    p.join(timeout=60)
+    assert err is None, err
+    assert ordered
+    o = oracle.schedule(synth.nodes(N_NODES, seed=SEED), synth.pods(N_PODS, seed=SEED), seed=SEED)
+    for res in outs:
+        for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
+            assert np.array_equal(res[k_res], o[k_or]), k_res

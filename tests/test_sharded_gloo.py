@@ -119,7 +119,7 @@ def test_chunk_bounds():
             assert len(spans) <= c
 
 
-def _pipe_worker(rank, world, port, n_nodes, batches, depth, q):
+def _pipe_worker(rank, world, port, n_nodes, batches, depth, group, q):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -146,24 +146,25 @@ def _pipe_worker(rank, world, port, n_nodes, batches, depth, q):
     def decode(buf, k):
         out[k] = keys[buf][: batches[k]].numpy().view(np.uint64).copy()
 
-    pipe = sharded.CrossStepPipeline(sweep, combine, decode, depth=depth)
+    pipe = sharded.CrossStepPipeline(sweep, combine, decode, depth=depth, group=group)
     for k in range(len(batches)):
         pipe.step(k)
-        assert len(out) == max(0, k + 1 - depth)  # batch k decodes `depth` steps later
+        assert len(out) == k + 1 - len(pipe._pending)  # decoded in order, at most `depth` in flight
+        assert len(pipe._pending) <= depth
     pipe.finish()
     q.put((rank, out))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("depth", [1, 2])
-def test_cross_step_pipeline_gloo(oracle, depth):
+@pytest.mark.parametrize("depth,group", [(1, 1), (2, 1), (2, 2), (3, 3)])
+def test_cross_step_pipeline_gloo(oracle, depth, group):
     # bench.py's N > 1 step: batch k's all-reduce overlaps the next `depth` sweeps,
     # depth + 1 key buffers rotate; every batch must decode to the single-process result
     world, n_nodes, batches = 2, 1500, [256, 200, 256, 131, 256]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, n_nodes, batches, depth, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, n_nodes, batches, depth, group, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=120) for _ in range(world)]

@@ -45,8 +45,9 @@ def main():
         eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=1, start=lo))
         eng.flush()
         cyc = sharded.ShardedCycle(eng, N, P, pods, stream, pipeline=True,
-                                   decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "1") == "1",
-                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "1")))
+                                   decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1",
+                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "3")),
+                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "3")))
         for _ in range(5):
             cyc.step(2)
         cyc.finish()
