@@ -154,11 +154,12 @@ def main():
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
     # N > 1: each step's RCCL all-reduce overlaps the following steps' sweeps
-    # (sharded.CrossStepPipeline, depth 3: three all-reduces in flight, four key
-    # buffers); every third step waits for the newest all-reduce once and decodes
-    # three batches (a cross-queue wait idles the sweep stream ~10 us however
-    # early its event completed; profiles/r01t_pipeline_group_ab.jsonl). The last
-    # steps' combines + decodes are drained inside the timed region.
+    # (sharded.CrossStepPipeline, depth 4: four all-reduces in flight, five key
+    # buffers); every fourth step waits once, for the newest all-reduce, and
+    # decodes four batches in one launch (ms_decode_device_jobs). A cross-queue
+    # wait idles the sweep stream ~10 us however early its event completed
+    # (profiles/r01t_pipeline_group_ab.jsonl, r01v_pipeline_group_decode_jobs_ab.jsonl).
+    # The last steps' combines + decodes are drained inside the timed region.
     # MINISCHED_PIPE_DEPTH / MINISCHED_PIPE_GROUP / MINISCHED_DECODE_STREAM=1 select
     # the other measured forms; MINISCHED_BENCH_PIPE=0 falls back to in-step pod
     # chunks (MINISCHED_BENCH_CHUNKS) whose reductions overlap the next chunk's sweep.
@@ -166,9 +167,8 @@ def main():
     chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
     cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe,
                                decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1",
-                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "3")),
-                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "3")))
-    results = cyc.results
+                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "4")),
+                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "4")))
 
     sweep_events = []
 
@@ -213,7 +213,7 @@ def main():
         kev.append((a, b))
     torch.cuda.synchronize()
     sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
-    res = results.cpu().numpy().view(_lib.RESULT)
+    res = cyc.results.cpu().numpy().view(_lib.RESULT)
     ok = int((res["code"] == _lib.CODE_SUCCESS).sum())
 
     if rank == 0:

@@ -185,6 +185,21 @@ int ms_sweep_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ui
 int ms_decode_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
                      const uint64_t *keys_dev, const uint32_t *flags_dev, uint32_t present_nodes,
                      ms_result *results_dev, void *stream);
+/* ms_decode_device_jobs: ms_decode_device for up to MS_DECODE_MAX_JOBS
+ *   batches in one launch (jobs is a host array; its pointers are device
+ *   pointers). Used by the pipelined multi-GPU step, which drains several
+ *   batches' combined keys at once. Each job needs its own results array. */
+#define MS_DECODE_MAX_JOBS 8
+typedef struct ms_decode_job {
+    const ms_pod_rec *pods;
+    const uint64_t *keys;
+    const uint32_t *flags; /* may be NULL (MS_PLUGINS_NU_NN) */
+    ms_result *results;
+    uint32_t n_pods;
+    uint32_t _pad;
+} ms_decode_job;
+int ms_decode_device_jobs(ms_ctx *ctx, uint32_t n_jobs, const ms_decode_job *jobs, uint32_t present_nodes,
+                          void *stream);
 int ms_apply_binds_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
                           const ms_result *results_dev, void *stream);
 /* Whole exact sequential cycle on device-resident pods (single shard). */

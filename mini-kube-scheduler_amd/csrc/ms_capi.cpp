@@ -616,6 +616,17 @@ int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, con
     return MS_OK;
 }
 
+int ms_decode_device_jobs(ms_ctx *c, uint32_t n_jobs, const ms_decode_job *jobs, uint32_t present_nodes,
+                          void *stream) {
+    if (!valid_ctx(c) || n_jobs > MS_DECODE_MAX_JOBS || (n_jobs && !jobs)) return MS_E_INVAL;
+    for (uint32_t i = 0; i < n_jobs; ++i)
+        if (jobs[i].n_pods && (!jobs[i].pods || !jobs[i].keys || !jobs[i].results)) return MS_E_INVAL;
+    if (n_jobs == 0) return MS_OK;
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    MS_HIP(c, launch_decode_jobs(jobs, n_jobs, present_nodes, pick_stream(c, stream)));
+    return MS_OK;
+}
+
 int ms_apply_binds_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, const ms_result *results_dev,
                           void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;

@@ -140,6 +140,8 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
 uint32_t seq_max_rows();
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
                          const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s);
+// n_jobs in [1, MS_DECODE_MAX_JOBS] (checked by the caller)
+hipError_t launch_decode_jobs(const ms_decode_job *jobs, uint32_t n_jobs, uint32_t present_nodes, hipStream_t s);
 hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32_t n_pods,
                               const ms_result *res, hipStream_t s);
 hipError_t launch_bind_one(const NodeTable &t, uint32_t local, const ms_pod_rec *pod_dev, int sign,

@@ -1565,10 +1565,9 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
 // ----------------------------------------------------------------------------
 // decode / bind commit / deltas
 // ----------------------------------------------------------------------------
-__global__ void k_decode(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const u64 *__restrict__ keys,
-                         const uint32_t *__restrict__ flags, uint32_t present, ms_result *__restrict__ out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_pods) return;
+__device__ __forceinline__ void decode_one(const ms_pod_rec *__restrict__ pods, const u64 *__restrict__ keys,
+                                           const uint32_t *__restrict__ flags, uint32_t present,
+                                           ms_result *__restrict__ out, uint32_t i) {
     const u64 k = keys[i];
     ms_result r;
     r._pad = 0;
@@ -1597,6 +1596,25 @@ __global__ void k_decode(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, c
         r.plugin_mask = 0;
     }
     out[i] = r;
+}
+
+__global__ void k_decode(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const u64 *__restrict__ keys,
+                         const uint32_t *__restrict__ flags, uint32_t present, ms_result *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_pods) decode_one(pods, keys, flags, present, out, i);
+}
+
+// Several batches' decodes in one launch (grid.y = job): the grouped drain of
+// the pipelined multi-GPU step decodes its batches together.
+struct DecodeJobs {
+    ms_decode_job j[MS_DECODE_MAX_JOBS];
+};
+
+__global__ void k_decode_jobs(DecodeJobs jobs, uint32_t present) {
+    const ms_decode_job &jb = jobs.j[blockIdx.y];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < jb.n_pods)
+        decode_one(jb.pods, reinterpret_cast<const u64 *>(jb.keys), jb.flags, present, jb.results, i);
 }
 
 __device__ __forceinline__ void add_pod(const NodeTable &t, uint32_t row, const ms_pod_rec &pr, int sign) {
@@ -1936,6 +1954,18 @@ hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned
     if (n_pods == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, pods, n_pods, keys, flags,
                        present_nodes, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_jobs(const ms_decode_job *jobs, uint32_t n_jobs, uint32_t present_nodes, hipStream_t s) {
+    DecodeJobs dj = {};
+    uint32_t most = 0;
+    for (uint32_t i = 0; i < n_jobs; ++i) {
+        dj.j[i] = jobs[i];
+        most = std::max(most, jobs[i].n_pods);
+    }
+    if (most == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_jobs, dim3(cdiv(most, 256), n_jobs), dim3(256), 0, s, dj, present_nodes);
     return hipGetLastError();
 }
 

@@ -120,9 +120,20 @@ SIGNATURES = {
     "ms_uncommit_bind": (ctypes.c_int, [_vp, _u32, _vp]),
     "ms_sweep_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "ms_decode_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp]),
+    "ms_decode_device_jobs": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp]),
     "ms_apply_binds_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_schedule_sequential_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
 }
+
+DECODE_MAX_JOBS = 8  # MS_DECODE_MAX_JOBS
+
+
+class DecodeJob(ctypes.Structure):  # ms_decode_job
+    _fields_ = [("pods", ctypes.c_void_p), ("keys", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+                ("results", ctypes.c_void_p), ("n_pods", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(DecodeJob) == 40
 
 _LIB: Optional[ctypes.CDLL] = None
 
@@ -265,6 +276,15 @@ class Engine:
                 self.h, n_pods, pods_dev, keys_dev, flags_dev or None, present_nodes, results_dev, stream or None
             ),
         )
+
+    def decode_device_jobs(self, jobs, present_nodes, stream=0):
+        """jobs: [(n_pods, pods_dev, keys_dev, flags_dev or 0, results_dev)], at most
+        DECODE_MAX_JOBS; one launch decodes them all (ms_decode_device_jobs)."""
+        arr = (DecodeJob * max(1, len(jobs)))()
+        for i, (n, pods, keys, flags, res) in enumerate(jobs):
+            arr[i] = DecodeJob(pods, keys, flags or None, res, n, 0)
+        self._check("ms_decode_device_jobs",
+                    self.lib.ms_decode_device_jobs(self.h, len(jobs), arr, present_nodes, stream or None))
 
     def apply_binds_device(self, n_pods, pods_dev, results_dev, stream=0):
         self._check(

@@ -90,7 +90,7 @@ class CrossStepPipeline:
     """
 
     def __init__(self, sweep, combine, decode, depth: int = 1, nbuf: int = 0, group: int = 1,
-                 ordered: bool = False):
+                 ordered: bool = False, decode_many=None):
         if depth < 1 or (nbuf and nbuf < depth + 1) or not 1 <= group <= depth:
             raise ValueError("need depth >= 1, nbuf >= depth + 1, 1 <= group <= depth")
         self._sweep, self._combine, self._decode = sweep, combine, decode
@@ -102,6 +102,8 @@ class CrossStepPipeline:
         # cross-queue wait per `group` steps instead of one per step.
         self.group = group
         self.ordered = ordered
+        # decode_many([(buf, batch), ...]): the drained batches' decodes in one launch
+        self._decode_many = decode_many
         self._n = 0
         self._pending = []  # [(works, buf, batch)], oldest first
 
@@ -132,6 +134,9 @@ class CrossStepPipeline:
             if not self.ordered or i == n - 1:
                 for w in works:
                     w.wait()
+        if self._decode_many is not None and len(batch_list) > 1:
+            self._decode_many([(buf, batch) for _works, buf, batch in batch_list])
+            return
         for _works, buf, batch in batch_list:
             self._decode(buf, batch)
 
@@ -182,7 +187,10 @@ class ShardedCycle:
         self._flags = ([torch.empty(n_pods, dtype=torch.int32, device=dev) for _ in range(nbuf)]
                        if want_flags else [None] * nbuf)
         self.keys, self.flags = self._keys[0], self._flags[0]
-        self.results = torch.empty(n_pods * self.RESULT_BYTES, dtype=torch.uint8, device=dev)
+        # one results array per key buffer: a grouped drain decodes several batches at once
+        self._results = [torch.empty(n_pods * self.RESULT_BYTES, dtype=torch.uint8, device=dev)
+                         for _ in range(nbuf)]
+        self._last = 0  # buffer of the most recently decoded batch
         self.chunks = chunk_bounds(n_pods, 1 if pipeline else chunks)
         self._pipe = None
         # decode_stream=True (opt-in, MINISCHED_DECODE_STREAM=1 in bench.py): the
@@ -205,7 +213,8 @@ class ShardedCycle:
                                            lambda buf: combine_(self._keys[buf], self._flags[buf], self.group,
                                                                 async_op=True),
                                            lambda buf, _b: self.decode(0, self.P, buf), depth=depth, nbuf=nbuf,
-                                           group=drain_group, ordered=_ordered_backend(group))
+                                           group=drain_group, ordered=_ordered_backend(group),
+                                           decode_many=self._decode_many if self._dstream is None else None)
 
     def _ptrs(self, a, buf=0):
         pods = self.pods.data_ptr() + a * self.POD_BYTES
@@ -222,9 +231,26 @@ class ShardedCycle:
             self._dec_ev[buf].synchronize()
         self.sweep(0, self.P, buf)
 
+    @property
+    def results(self):
+        """Decoded ms_result bytes of the most recent batch (valid once its stream work is done)."""
+        return self._results[self._last]
+
+    def _decode_many(self, bufs):
+        from . import _lib
+
+        jobs = []
+        for buf, _batch in bufs:
+            pods, keys, flags = self._ptrs(0, buf)
+            jobs.append((self.P, pods, keys, flags, self._results[buf].data_ptr()))
+        for i in range(0, len(jobs), _lib.DECODE_MAX_JOBS):
+            self.eng.decode_device_jobs(jobs[i:i + _lib.DECODE_MAX_JOBS], self.N, self.stream.cuda_stream)
+        self._last = bufs[-1][0]
+
     def decode(self, a, b, buf=0):
         pods, keys, flags = self._ptrs(a, buf)
-        res = self.results.data_ptr() + a * self.RESULT_BYTES
+        res = self._results[buf].data_ptr() + a * self.RESULT_BYTES
+        self._last = buf
         if self._dstream is None:
             self.eng.decode_device(b - a, pods, keys, flags, self.N, res, self.stream.cuda_stream)
             return

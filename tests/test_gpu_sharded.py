@@ -131,3 +131,41 @@ def test_rccl_grouped_drain(oracle, depth, group, dstream):
     for res in outs:
         for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
             assert np.array_equal(res[k_res], o[k_or]), k_res
+
+
+def test_decode_device_jobs_matches_oracle(oracle):
+    # ms_decode_device_jobs: three batches of different sizes swept into their own
+    # key buffers, decoded in one launch, each equal to the oracle
+    import torch
+
+    from minisched_amd import _lib
+
+    dev = torch.device("cuda:0")
+    n_nodes = 7_000
+    eng = _lib.Engine(max_nodes=n_nodes, plugin_set=_lib.PLUGINS_NU_NN, node_base=0, seed=SEED)
+    try:
+        nr = synth.nodes(n_nodes, seed=SEED)
+        eng.upsert(np.arange(n_nodes, dtype=np.uint32), nr)
+        eng.flush()
+        stream = torch.cuda.Stream(device=dev)
+        sizes = [1000, 333, 2049]
+        batches, jobs = [], []
+        for k, n in enumerate(sizes):
+            pr = synth.pods(n, seed=40 + k)
+            pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+            keys = torch.empty(n, dtype=torch.int64, device=dev)
+            res = torch.full((n * 24,), 0xAB, dtype=torch.uint8, device=dev)
+            eng.sweep_device(n, pods.data_ptr(), keys.data_ptr(), 0, stream.cuda_stream)
+            batches.append((pr, pods, keys, res))
+            jobs.append((n, pods.data_ptr(), keys.data_ptr(), 0, res.data_ptr()))
+        eng.decode_device_jobs(jobs, n_nodes, stream.cuda_stream)
+        torch.cuda.synchronize()
+        for k, (pr, _pods, _keys, res) in enumerate(batches):
+            got = res.cpu().numpy().view(_lib.RESULT)
+            o = oracle.schedule(nr, pr, seed=SEED)
+            for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
+                assert np.array_equal(got[k_res], o[k_or]), f"batch {k} {k_res}"
+        with pytest.raises(RuntimeError):
+            eng.decode_device_jobs(jobs * 3, n_nodes, stream.cuda_stream)  # > MS_DECODE_MAX_JOBS
+    finally:
+        eng.close()

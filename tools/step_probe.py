@@ -46,8 +46,8 @@ def main():
         eng.flush()
         cyc = sharded.ShardedCycle(eng, N, P, pods, stream, pipeline=True,
                                    decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1",
-                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "3")),
-                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "3")))
+                               depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "4")),
+                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "4")))
         for _ in range(5):
             cyc.step(2)
         cyc.finish()
