@@ -473,7 +473,7 @@ template <int K, bool WANT_FLAGS, int W>
 __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slot, const WaveRows<K> &w,
                                            bool wave_unsched, uint32_t lane, const uint2 *__restrict__ ps,
                                            uint32_t pbeg, uint32_t pend, u64 *__restrict__ keys,
-                                           uint32_t *__restrict__ pflags) {
+                                           uint32_t *__restrict__ pflags, uint32_t group_test) {
     constexpr int kMisc = TileLds<K, W>::kMisc;
     const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
     uint4 nx0 = q4[0], nx1 = q4[1], nx2 = q4[2], nx3 = q4[3];
@@ -496,6 +496,23 @@ __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slo
             // batch's end) and masked out of the outcome bits.
             uint32_t r[8];
             u64 gfound = 0, gs10 = 0, gnum = 0;
+            // Group test: when all 8 pods are non-tolerating with fitting class lists
+            // (the common case), one scalar branch per group instead of one per pod,
+            // and the 8 list lookups run straight through (MINISCHED_K1_GROUP=0: off).
+            uint32_t allfast = group_test;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) allfast &= w.fast >> e[2 * j + 1];
+            if (allfast & 1u) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if constexpr (K == 3)
+                        r[j] = list_max3_idx(w.L, e[2 * j], e[2 * j + 1]);
+                    else
+                        r[j] = list_max<K>(w.L, e[2 * j], e[2 * j + 1]);
+                }
+                gfound = gs10 = 0xFFull;
+                if (WANT_FLAGS && wave_unsched) gnum = 0xFFull;  // all 8 are non-tolerating
+            } else
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t A = e[2 * j], cls = e[2 * j + 1];
@@ -563,7 +580,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (pbeg >= pend) return;  // wave-uniform
     }
     // W == 1: each lane reads only its own LDS entries, no barrier needed
-    sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags);
+    sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags,
+                                 fast_mask >> 31);
 }
 
 // K1 v8: the same sweep as a persistent grid with a work queue. One workgroup
@@ -601,7 +619,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
         if (threadIdx.x == 0) nxt = atomicAdd(&col_next[col], 1u);  // claimed now, read after the sweep
         const uint32_t pbeg = (it * W + wv) * chunk;
         const uint32_t pend = min(n_pods, pbeg + chunk);
-        if (pbeg < pend) sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags);
+        if (pbeg < pend) sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags,
+                                 fast_mask >> 31);
         __syncthreads();  // every wave has read s_item
         if (threadIdx.x == 0) s_item = nxt;
         __syncthreads();
@@ -1746,11 +1765,16 @@ static int k1_variant() {
 typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, uint32_t, const uint2 *, uint32_t,
                          uint32_t, unsigned long long *, uint32_t *, uint32_t);
 
-// Classes on K1's list path: bits 0..9 non-tolerating, 16..25 tolerating pods.
+// Classes on K1's list path: bits 0..9 non-tolerating, 16..25 tolerating pods; bit 31
+// enables the per-8-pod group test in sweep_pods.
 // MINISCHED_K1_TOL=0 sends tolerating pods down the general path (tests, A/B).
 static uint32_t k1_fast_mask() {
     const char *e = getenv("MINISCHED_K1_TOL");
-    return (e && atoi(e) == 0) ? 0x3FFu : 0x3FF03FFu;
+    uint32_t m = (e && atoi(e) == 0) ? 0x3FFu : 0x3FF03FFu;
+    // bit 31: K1's per-8-pod group test (MINISCHED_K1_GROUP=0 turns it off for A/B)
+    const char *g = getenv("MINISCHED_K1_GROUP");
+    if (!(g && atoi(g) == 0)) m |= 0x80000000u;
+    return m;
 }
 
 constexpr uint32_t kK1MaxRpl = 30;

@@ -32,7 +32,11 @@ def main():
     times = {v: [] for v in variants}
     for r in range(rounds + 1):
         for v in variants:
-            os.environ["MINISCHED_K1"] = v
+            if "=" in v:  # an env setting read per launch, e.g. MINISCHED_K1_GROUP=0
+                k, val = v.split("=", 1)
+                os.environ[k] = val
+            else:
+                os.environ["MINISCHED_K1"] = v
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
             eng.sweep_device(P, pods.data_ptr(), keys[v].data_ptr(), 0, s.cuda_stream)
