@@ -311,7 +311,9 @@ int ensure_pstream(ms_ctx *c, uint32_t n_pods) {
     c->pstream_cap = 0;
     if (!c->d_work && hipMalloc((void **)&c->d_work, sizeof(uint32_t) * kK1MaxColumns) != hipSuccess)
         return fail(c, MS_E_OOM, "K1 work counters");
-    if (hipMalloc((void **)&c->d_pstream, sizeof(uint2) * cap) != hipSuccess)
+    // cap stream entries, then the per-8-pod class masks (k_pod_prep writes them
+    // right after the call's n_pods + kPodStreamPad entries; launch_sweep_nunn)
+    if (hipMalloc((void **)&c->d_pstream, sizeof(uint2) * cap + sizeof(uint32_t) * (cap / 8 + 4)) != hipSuccess)
         return fail(c, MS_E_OOM, "pod stream");
     c->pstream_cap = cap;
     return MS_OK;

@@ -143,20 +143,30 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
 // The buffer carries kPodStreamPad padding entries so the sweep's reads of
 // whole 8-pod groups, one group ahead, never need a bounds check.
 // ----------------------------------------------------------------------------
+// gmask[q] = OR over pods 8q .. 8q+7 of (1 << class): the sweep's group test is
+// then one scalar AND-NOT against the wave's list-path classes. Groups past the
+// stream read as class 10 (never on the list path).
 __global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t seed32,
                            uint2 *__restrict__ ps, u64 *__restrict__ keys, uint32_t *__restrict__ flags,
-                           uint32_t *__restrict__ work, uint32_t n_work) {
+                           uint32_t *__restrict__ work, uint32_t n_work, uint32_t *__restrict__ gmask) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_work) work[i] = 0;  // K1 v8's per-column work counters
+    uint32_t cls = 10u;
     if (i < n) {
         const ms_pod_rec pr = pods[i];
         const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
-        ps[i] = make_uint2(tb_pod(seed32, pr.ordinal), d | (pr.tolerates_unschedulable ? 16u : 0u));
+        cls = d | (pr.tolerates_unschedulable ? 16u : 0u);
+        ps[i] = make_uint2(tb_pod(seed32, pr.ordinal), cls);
         keys[i] = 0;
         if (flags) flags[i] = 0;
     } else if (i < n + kPodStreamPad) {
         ps[i] = make_uint2(0u, 10u);
     }
+    uint32_t m = 1u << cls;  // blockDim is a multiple of 64: groups of 8 never straddle a wave
+    m |= __shfl_xor(m, 1);
+    m |= __shfl_xor(m, 2);
+    m |= __shfl_xor(m, 4);
+    if ((i & 7u) == 0u && i < n + kPodStreamPad + 16u) gmask[i >> 3] = m;
 }
 
 // ----------------------------------------------------------------------------
@@ -473,10 +483,13 @@ template <int K, bool WANT_FLAGS, int W>
 __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slot, const WaveRows<K> &w,
                                            bool wave_unsched, uint32_t lane, const uint2 *__restrict__ ps,
                                            uint32_t pbeg, uint32_t pend, u64 *__restrict__ keys,
-                                           uint32_t *__restrict__ pflags, uint32_t group_test) {
+                                           uint32_t *__restrict__ pflags, uint32_t group_test,
+                                           const uint32_t *__restrict__ gmask) {
     constexpr int kMisc = TileLds<K, W>::kMisc;
     const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
     uint4 nx0 = q4[0], nx1 = q4[1], nx2 = q4[2], nx3 = q4[3];
+    const uint32_t *__restrict__ gq = gmask + (pbeg >> 3);  // ranges start on 8-pod groups
+    uint32_t gnext = gq[0];
     for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod blocks: one flush each
         const uint32_t gn = min(64u, pend - g);
         u64 found = 0, s10m = 0, num = 0;
@@ -486,6 +499,8 @@ __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slo
         for (uint32_t sub = 0; sub < gn; sub += 8) {
             const uint32_t e[16] = {nx0.x, nx0.y, nx0.z, nx0.w, nx1.x, nx1.y, nx1.z, nx1.w,
                                     nx2.x, nx2.y, nx2.z, nx2.w, nx3.x, nx3.y, nx3.z, nx3.w};
+            const uint32_t gcur = gnext;
+            gnext = *++gq;  // the next group's class mask (written two groups past the stream)
             q4 += 4;
             nx0 = q4[0];  // prefetch the next 8 pods; the stream is padded past n_pods
             nx1 = q4[1];
@@ -497,12 +512,10 @@ __device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slo
             uint32_t r[8];
             u64 gfound = 0, gs10 = 0, gnum = 0;
             // Group test: when all 8 pods are non-tolerating with fitting class lists
-            // (the common case), one scalar branch per group instead of one per pod,
-            // and the 8 list lookups run straight through (MINISCHED_K1_GROUP=0: off).
-            uint32_t allfast = group_test;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) allfast &= w.fast >> e[2 * j + 1];
-            if (allfast & 1u) {
+            // (the common case; k_pod_prep's OR of the group's class bits against the
+            // wave's list-path classes), one scalar branch per group instead of one
+            // per pod, and the 8 list lookups run straight through (MINISCHED_K1_GROUP=0: off).
+            if (group_test && (gcur & ~w.fast) == 0u) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     if constexpr (K == 3)
@@ -581,7 +594,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
     // W == 1: each lane reads only its own LDS entries, no barrier needed
     sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags,
-                                 fast_mask >> 31);
+                                 fast_mask >> 31, reinterpret_cast<const uint32_t *>(ps + n_pods + kPodStreamPad));
 }
 
 // K1 v8: the same sweep as a persistent grid with a work queue. One workgroup
@@ -620,7 +633,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) voi
         const uint32_t pbeg = (it * W + wv) * chunk;
         const uint32_t pend = min(n_pods, pbeg + chunk);
         if (pbeg < pend) sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags,
-                                 fast_mask >> 31);
+                                 fast_mask >> 31, reinterpret_cast<const uint32_t *>(ps + n_pods + kPodStreamPad));
         __syncthreads();  // every wave has read s_item
         if (threadIdx.x == 0) s_item = nxt;
         __syncthreads();
@@ -1882,12 +1895,13 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
                              uint32_t *work, int num_cus, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     // pod stream + zeroed keys/flags (the sweep's atomicMax/atomicOr targets)
-    const uint32_t n_prep = n_pods + kPodStreamPad;
+    const uint32_t n_prep = n_pods + kPodStreamPad + 16u;  // + two groups of class masks past the stream
     const int var = k1_variant();
     const bool v8 = var == K1_V8 || (var == K1_AUTO && k1_columns(n_rows) >= kK1V8MinColumns);
     const uint32_t n_work = v8 ? k1_columns(n_rows) : 0u;
+    uint32_t *gmask = reinterpret_cast<uint32_t *>(pstream + n_pods + kPodStreamPad);
     hipLaunchKernelGGL(k_pod_prep, dim3(cdiv(std::max(n_prep, n_work), 256)), dim3(256), 0, s, pods, n_pods, seed32,
-                       pstream, keys, flags, work, n_work);
+                       pstream, keys, flags, work, n_work, gmask);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || n_rows == 0) return e;
     if (k1_variant() == K1_V0) {
