@@ -163,17 +163,26 @@ def main():
     # MINISCHED_PIPE_DEPTH / MINISCHED_PIPE_GROUP / MINISCHED_DECODE_STREAM=1 select
     # the other measured forms; MINISCHED_BENCH_PIPE=0 falls back to in-step pod
     # chunks (MINISCHED_BENCH_CHUNKS) whose reductions overlap the next chunk's sweep.
-    pipe = world > 1 and os.environ.get("MINISCHED_BENCH_PIPE", "1") != "0"
+    # N = 1 (MINISCHED_BENCH_PIPE1=1): the same pipeline with no collective, so
+    # decodes launch in groups too
+    pipe1 = world == 1 and os.environ.get("MINISCHED_BENCH_PIPE1", "0") == "1"
+    pipe = (world > 1 or pipe1) and os.environ.get("MINISCHED_BENCH_PIPE", "1") != "0"
     chunks = int(os.environ.get("MINISCHED_BENCH_CHUNKS", "4" if world > 1 else "1"))
     cyc = sharded.ShardedCycle(eng, N, P, pods, stream, want_flags=False, chunks=chunks, pipeline=pipe,
                                decode_stream=os.environ.get("MINISCHED_DECODE_STREAM", "0") == "1",
                                depth=int(os.environ.get("MINISCHED_PIPE_DEPTH", "4")),
-                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "4")))
+                               drain_group=int(os.environ.get("MINISCHED_PIPE_GROUP", "4")),
+                               collective=world > 1)
 
+    # Device time of the timed region: ONE event pair on the sweep stream around
+    # all K steps. Per-step event records sit inside the timed region and cost
+    # ~4 % of a step (profiles/r01z_n1_bench_forms_ab.jsonl);
+    # MINISCHED_BENCH_STEP_EVENTS=1 brings them back for per-step spreads.
+    per_step_events = os.environ.get("MINISCHED_BENCH_STEP_EVENTS", "0") == "1"
     sweep_events = []
 
     def step(timed):
-        if timed:
+        if timed and per_step_events:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
             cyc.step(world)
@@ -189,10 +198,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev_begin, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev_begin.record(stream)
     for _ in range(args.steps):
         step(True)
-    cyc.finish()  # pipelined: the last step's combine + decode
+    cyc.finish()  # pipelined: the last steps' combines + decodes
+    ev_end.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -202,7 +214,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    step_dev_ms = float(np.mean([a.elapsed_time(b) for a, b in sweep_events]))
+    if sweep_events:
+        step_dev_ms = float(np.mean([a.elapsed_time(b) for a, b in sweep_events]))
+    else:
+        step_dev_ms = ev_begin.elapsed_time(ev_end) / args.steps
     # kernel-only timing on the sweep's stream: separate timed launches after the run
     kev = []
     for _ in range(max(3, min(args.steps, 10))):

@@ -168,7 +168,7 @@ class ShardedCycle:
 
     def __init__(self, engine, n_nodes_global: int, n_pods: int, pods_dev, stream, want_flags: bool = False,
                  group=None, chunks: int = 1, pipeline: bool = False, decode_stream: bool = False,
-                 depth: int = 1, drain_group: int = 1):
+                 depth: int = 1, drain_group: int = 1, collective: bool = True):
         import torch
 
         self.eng = engine
@@ -193,6 +193,8 @@ class ShardedCycle:
         self._last = 0  # buffer of the most recently decoded batch
         self.chunks = chunk_bounds(n_pods, 1 if pipeline else chunks)
         self._pipe = None
+        # collective=False: one shard (N = 1) run through the same pipeline, decodes grouped
+        self._collective = collective
         # decode_stream=True (opt-in, MINISCHED_DECODE_STREAM=1 in bench.py): the
         # decode of step k waits for step k's combine on a stream of its own, so
         # the sweep stream never waits on another queue (a cross-queue wait idles
@@ -210,8 +212,8 @@ class ShardedCycle:
             self._dec_ev = [torch.cuda.Event() for _ in range(nbuf)]
         if pipeline:
             self._pipe = CrossStepPipeline(self._pipe_sweep,
-                                           lambda buf: combine_(self._keys[buf], self._flags[buf], self.group,
-                                                                async_op=True),
+                                           lambda buf: (combine_(self._keys[buf], self._flags[buf], self.group,
+                                                                 async_op=True) if collective else []),
                                            lambda buf, _b: self.decode(0, self.P, buf), depth=depth, nbuf=nbuf,
                                            group=drain_group, ordered=_ordered_backend(group),
                                            decode_many=self._decode_many if self._dstream is None else None)
@@ -261,7 +263,7 @@ class ShardedCycle:
         self._dec_live[buf] = True
 
     def step(self, world: int, on_sweep=None):
-        if self._pipe is not None and world > 1:
+        if self._pipe is not None and (world > 1 or not self._collective):
             self._pipe.step(drain_stream=self._dstream)
             return
         pending = []
