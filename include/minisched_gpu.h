@@ -202,6 +202,15 @@ int ms_decode_device_jobs(ms_ctx *ctx, uint32_t n_jobs, const ms_decode_job *job
                           void *stream);
 int ms_apply_binds_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
                           const ms_result *results_dev, void *stream);
+/* ms_select_batch_device: the stateless batched cycle (filter + score +
+ *   selectHost + decode) of a single-shard context on device-resident pods,
+ *   with no bind commit: results_dev[i] as ms_schedule_batch would return it
+ *   in MS_MODE_BATCHED. For NU+NN this is one fused kernel launch. Replaces
+ *   minisched.go:40-85 for pods whose placements do not interact (config D).
+ *   Node state the plugins read (NU, NN) is unchanged by binds, so for NU+NN
+ *   it also equals the queue-order loop (minisched.go:28-30). */
+int ms_select_batch_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
+                           void *stream);
 /* Whole exact sequential cycle on device-resident pods (single shard). */
 int ms_schedule_sequential_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
                                   ms_result *results_dev, void *stream);

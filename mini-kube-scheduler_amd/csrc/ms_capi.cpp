@@ -32,6 +32,10 @@ struct ms_ctx {
     std::vector<uint8_t> present;  // host mirror of presence, updated at enqueue
     uint32_t present_count = 0;
     uint32_t rows_used = 0;  // high-water mark of upserted rows (sweep extent)
+    // what the device table holds after the last flush: snapshots of the two
+    // counters above taken with the drained deltas (under delta_mu), read only
+    // by sched_mu holders
+    uint32_t rows_dev = 0, present_dev = 0;
 
     // one scheduling caller at a time (minisched.go:28-30 runs one goroutine)
     std::mutex sched_mu;
@@ -64,22 +68,26 @@ struct ms_ctx {
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
 
-    // NU+NN pod stream (k_pod_prep output), reused call after call; a call on
-    // another stream first waits for the previous user (pstream_ev)
+    // NU+NN pod stream of the class-indexed K1 forms (k_pod_prep output),
+    // reused call after call (ordered through the context stream like the table)
     uint2 *d_pstream = nullptr;
     uint32_t pstream_cap = 0;
-    uint32_t *d_work = nullptr;  // K1 work-queue counters (kK1MaxColumns), same ordering as d_pstream
-    hipStream_t pstream_last = nullptr;
-    hipEvent_t pstream_ev = nullptr;
+    uint32_t *d_work = nullptr;  // K1 v8 work-queue counters (kK1MaxColumns)
 
-    // Ordering of caller streams after the context stream (node deltas, binds):
-    // ctx_seq counts enqueues on the context stream; a caller stream that was
-    // ordered after it at ctx_seq needs no new cross-stream wait (each costs
-    // ~6 us of device time even when already signalled, tools/ubench/xstream)
+    // Ordering. Every piece of work that reads or writes the node table or the
+    // context's scratch is totally ordered through the context stream: a call
+    // on a caller stream first waits for the context stream (order_after_ctx_
+    // stream), and its work is then chained back into the context stream
+    // (chain_back), so later deltas, binds, read-backs and calls on any other
+    // stream wait for it. ctx_seq counts enqueues on the context stream that a
+    // caller stream has not necessarily seen; a caller stream ordered after it
+    // at ctx_seq needs no new cross-stream wait (each costs ~6-10 us of idle
+    // device time even when already signalled, tools/ubench/xstream).
     uint64_t ctx_seq = 0;
     hipStream_t ordered_stream = nullptr;
     uint64_t ordered_seq = 0;
     hipEvent_t ev_order = nullptr;
+    hipEvent_t ev_back = nullptr;
 
     std::string err;
 };
@@ -111,7 +119,7 @@ void free_all(ms_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *dev[] = {c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
+    void *dev[] = {c->t.planes, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream,
@@ -121,8 +129,8 @@ void free_all(ms_ctx *c) {
     if (c->h_pods) (void)hipHostFree(c->h_pods);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
-    if (c->pstream_ev) (void)hipEventDestroy(c->pstream_ev);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    if (c->ev_back) (void)hipEventDestroy(c->ev_back);
     for (int i = 0; i < 2; ++i) {
         if (c->ev_valid[i]) (void)hipEventDestroy(c->ev_valid[i]);
         if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
@@ -157,6 +165,8 @@ int flush_locked(ms_ctx *c) {
     {
         std::lock_guard<std::mutex> g(c->delta_mu);
         batch.swap(c->pending);
+        c->rows_dev = c->rows_used;
+        c->present_dev = c->present_count;
     }
     if (batch.empty()) return MS_OK;
     // later deltas to one row win: keep the last occurrence only
@@ -175,6 +185,7 @@ int flush_locked(ms_ctx *c) {
     MS_HIP(c, hipMemcpyAsync(c->d_deltas, c->h_deltas, sizeof(NodeDelta) * uniq.size(),
                              hipMemcpyHostToDevice, c->stream));
     MS_HIP(c, launch_apply_deltas(c->t, c->d_deltas, (uint32_t)uniq.size(), c->stream));
+    MS_HIP(c, launch_build_planes(c->t, c->d_deltas, (uint32_t)uniq.size(), c->stream));
     ++c->ctx_seq;
     return MS_OK;
 }
@@ -191,6 +202,25 @@ int order_after_ctx_stream(ms_ctx *c, hipStream_t s) {
     if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("stream ordering: ") + hipGetErrorString(e));
     c->ordered_stream = s;
     c->ordered_seq = c->ctx_seq;
+    return MS_OK;
+}
+
+// After a call's last launch on caller stream s: the context stream waits for
+// it, so later deltas, binds, read-backs and calls on other streams (which
+// order after the context stream) come after this call's table and scratch
+// accesses. s itself needs no new wait (ordered_seq is kept), another stream
+// does (ordered_stream differs).
+int chain_back(ms_ctx *c, hipStream_t s) {
+    if (s == c->stream) return MS_OK;
+    if (!c->ev_back) MS_HIP(c, hipEventCreateWithFlags(&c->ev_back, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(c->ev_back, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_back, 0);
+    if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("stream ordering: ") + hipGetErrorString(e));
+    if (c->ordered_stream != s) {  // the ctx stream now holds s's work: other streams must wait for it
+        ++c->ctx_seq;
+        c->ordered_stream = s;
+        c->ordered_seq = c->ctx_seq;
+    }
     return MS_OK;
 }
 
@@ -243,7 +273,7 @@ uint32_t seq_batch(const ms_ctx *) {
 // Exact sequential engine: speculative per-tile top-K sweep + in-order
 // validation, batch after batch on one stream.
 int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s) {
-    const uint32_t rows = c->rows_used;
+    const uint32_t rows = c->rows_dev;
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     if (rows == 0) {  // no node listed: every pod is a FitError with an empty mask
         for (uint32_t s0 = 0; s0 < n_pods; s0 += c->batch_cap) {
@@ -290,13 +320,6 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
                                       c->d_prev + (SB + 1) * par, d_res + s0, c->d_overflow, s));
         MS_HIP(c, hipEventRecord(c->ev_valid[par], s));
     }
-    // later deltas and calls (on any stream) order after the context stream:
-    // chain it after this call's last validation
-    if (s != c->stream) {
-        MS_HIP(c, hipEventRecord(c->ev_seq, s));
-        MS_HIP(c, hipStreamWaitEvent(c->stream, c->ev_seq, 0));
-        ++c->ctx_seq;
-    }
     return MS_OK;
 }
 
@@ -319,23 +342,51 @@ int ensure_pstream(ms_ctx *c, uint32_t n_pods) {
     return MS_OK;
 }
 
+// K1 choice for NU+NN, read at each call so A/B runs can interleave forms in
+// one process: the per-pair "pp" kernel (default, MINISCHED_K1 unset or "pp"),
+// or the round-1 class-indexed forms "v7" / "v8" and the plain "v0"
+// (ms_kernels.hip), kept as labelled alternatives and cross-checks.
+bool k1_pp() {
+    const char *e = getenv("MINISCHED_K1");
+    return !e || !e[0] || (e[0] == 'p' && e[1] == 'p');
+}
+
+// This shard's keys (and filter flags for the resource-aware set) for a batch.
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
                  hipStream_t s) {
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NN) {
+        if (k1_pp()) {
+            MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
+                                      c->num_cus, s));
+            return MS_OK;
+        }
         int rc = ensure_pstream(c, n_pods);
         if (rc) return rc;
-        if (!c->pstream_ev) MS_HIP(c, hipEventCreateWithFlags(&c->pstream_ev, hipEventDisableTiming));
-        if (c->pstream_last && c->pstream_last != s) MS_HIP(c, hipStreamWaitEvent(s, c->pstream_ev, 0));
-        MS_HIP(c, launch_sweep_nunn(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->d_pstream,
-                                    c->d_work, c->num_cus, s));
-        MS_HIP(c, hipEventRecord(c->pstream_ev, s));
-        c->pstream_last = s;
+        MS_HIP(c, launch_sweep_nunn(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->d_pstream, c->d_work,
+                                    c->num_cus, s));
     } else {
         MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
         if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
-        MS_HIP(c, launch_sweep_full(c->t, c->rows_used, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
+        MS_HIP(c, launch_sweep_full(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
     }
+    return MS_OK;
+}
+
+// The stateless cycle of one batch (n_pods <= batch_cap) on a single-shard
+// context: filter + score + selectHost + decode into results, no bind commit.
+// NU+NN with K1 pp is one fused launch; otherwise sweep into the context's
+// key/flag scratch, then decode.
+int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s) {
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN && k1_pp()) {
+        MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), c->d_keys, d_res,
+                                  c->present_dev, c->num_cus, s));
+        return MS_OK;
+    }
+    const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
+    int rc = sweep_locked(c, n_pods, d_pods, c->d_keys, want_flags ? c->d_flags : nullptr, s);
+    if (rc) return rc;
+    MS_HIP(c, launch_decode(d_pods, n_pods, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev, d_res, s));
     return MS_OK;
 }
 
@@ -403,6 +454,8 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
               hipMalloc((void **)&t.req_mem, n * 8) == hipSuccess &&
               hipMalloc((void **)&t.nz_cpu, n * 8) == hipSuccess &&
               hipMalloc((void **)&t.nz_mem, n * 8) == hipSuccess;
+    t.gcap = (uint32_t)((n + kGroupRows - 1) / kGroupRows);
+    ok = ok && hipMalloc((void **)&t.planes, sizeof(uint32_t) * kPlanes * t.gcap) == hipSuccess;
     if (!ok) return bail(MS_E_OOM, "node table allocation");
     const size_t b = c->batch_cap;
     ok = hipHostMalloc((void **)&c->h_pods, b * sizeof(ms_pod_rec)) == hipSuccess &&
@@ -414,7 +467,8 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
          hipMalloc((void **)&c->d_one, sizeof(ms_pod_rec)) == hipSuccess &&
          hipMalloc((void **)&c->d_overflow, kStatsBytes) == hipSuccess;
     if (!ok) return bail(MS_E_OOM, "staging allocation");
-    if (launch_init_table(t, c->stream) != hipSuccess) return bail(MS_E_HIP, "table init launch");
+    if (launch_init_table(t, c->stream) != hipSuccess || launch_build_planes(t, nullptr, 0, c->stream) != hipSuccess)
+        return bail(MS_E_HIP, "table init launch");
     if (hipMemsetAsync(c->d_overflow, 0, kStatsBytes, c->stream) != hipSuccess) return bail(MS_E_HIP, "memset");
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(MS_E_HIP, "table init");
     *out = c;
@@ -547,7 +601,7 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     int rc = flush_locked(c);
     if (rc) return rc;
     const hipStream_t s = c->stream;
-    ++c->ctx_seq;
+    ++c->ctx_seq;  // binds below write the table on the context stream
     const uint32_t B = c->batch_cap;
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
@@ -561,11 +615,8 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
         } else {
             // NU+NN keys never read mutable node state, so the queue-order
             // loop equals the batched sweep; binds are committed after it.
-            const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
-            rc = sweep_locked(c, nb, c->d_pods, c->d_keys, want_flags ? c->d_flags : nullptr, s);
+            rc = select_locked(c, nb, c->d_pods, c->d_res, s);
             if (rc) return rc;
-            MS_HIP(c, launch_decode(c->d_pods, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_count,
-                                    c->d_res, s));
             MS_HIP(c, launch_apply_binds(c->t, c->d_pods, nb, c->d_res, s));
         }
         MS_HIP(c, hipMemcpyAsync(c->h_res, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
@@ -583,6 +634,7 @@ static int bind_common(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod, int s
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
+    // the context stream already waits for earlier caller-stream work (chain_back)
     MS_HIP(c, hipMemcpyAsync(c->d_one, pod, sizeof(ms_pod_rec), hipMemcpyHostToDevice, c->stream));
     MS_HIP(c, launch_bind_one(c->t, ordinal - c->cfg.node_base, c->d_one, sign, c->stream));
     ++c->ctx_seq;
@@ -606,7 +658,28 @@ int ms_sweep_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
     if (rc) return rc;
-    return sweep_locked(c, n_pods, pods_dev, reinterpret_cast<unsigned long long *>(keys_dev), flags_dev, s);
+    rc = sweep_locked(c, n_pods, pods_dev, reinterpret_cast<unsigned long long *>(keys_dev), flags_dev, s);
+    if (rc) return rc;
+    return chain_back(c, s);
+}
+
+int ms_select_batch_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
+                           void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);
+    if (rc) return rc;
+    const uint32_t B = c->batch_cap;  // key/flag scratch (the fused NU+NN kernel needs none below 122,880 rows)
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        rc = select_locked(c, std::min(B, n_pods - s0), pods_dev + s0, results_dev + s0, s);
+        if (rc) return rc;
+    }
+    return chain_back(c, s);
 }
 
 int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, const uint64_t *keys_dev,
@@ -632,11 +705,18 @@ int ms_decode_device_jobs(ms_ctx *c, uint32_t n_jobs, const ms_decode_job *jobs,
 int ms_apply_binds_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, const ms_result *results_dev,
                           void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
     MS_HIP(c, hipSetDevice(c->cfg.device));
     const hipStream_t s = pick_stream(c, stream);
+    int rc = order_after_ctx_stream(c, s);  // after earlier sweeps and deltas
+    if (rc) return rc;
     MS_HIP(c, launch_apply_binds(c->t, pods_dev, n_pods, results_dev, s));
-    if (s == c->stream) ++c->ctx_seq;  // table writes on the context stream
-    return MS_OK;
+    if (s == c->stream) {
+        ++c->ctx_seq;  // table writes on the context stream
+        return MS_OK;
+    }
+    return chain_back(c, s);
 }
 
 int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
@@ -650,18 +730,26 @@ int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
     if (rc) return rc;
-    if (s == c->stream) ++c->ctx_seq;  // binds below write the table on the context stream
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA) return run_sequential(c, n_pods, pods_dev, results_dev, s);
-    // NU+NN: keys are independent of mutable state -> batched sweep + commit
-    const uint32_t B = c->batch_cap;
-    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
-        const uint32_t nb = std::min(B, n_pods - s0);
-        rc = sweep_locked(c, nb, pods_dev + s0, c->d_keys, nullptr, s);
-        if (rc) return rc;
-        MS_HIP(c, launch_decode(pods_dev + s0, nb, c->d_keys, nullptr, c->present_count, results_dev + s0, s));
-        MS_HIP(c, launch_apply_binds(c->t, pods_dev + s0, nb, results_dev + s0, s));
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA) {
+        rc = run_sequential(c, n_pods, pods_dev, results_dev, s);
+    } else {
+        // NU+NN: keys are independent of mutable state -> batched cycle + commit
+        const uint32_t B = c->batch_cap;
+        for (uint32_t s0 = 0; s0 < n_pods && !rc; s0 += B) {
+            const uint32_t nb = std::min(B, n_pods - s0);
+            rc = select_locked(c, nb, pods_dev + s0, results_dev + s0, s);
+            if (!rc) {
+                hipError_t e = launch_apply_binds(c->t, pods_dev + s0, nb, results_dev + s0, s);
+                if (e != hipSuccess) rc = fail(c, MS_E_HIP, std::string("apply binds: ") + hipGetErrorString(e));
+            }
+        }
     }
-    return MS_OK;
+    if (rc) return rc;
+    if (s == c->stream) {
+        ++c->ctx_seq;  // binds wrote the table on the context stream
+        return MS_OK;
+    }
+    return chain_back(c, s);
 }
 
 }  // extern "C"

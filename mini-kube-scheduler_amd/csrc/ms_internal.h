@@ -44,6 +44,22 @@ struct NodeTable {
     int64_t *nz_cpu, *nz_mem;
     uint32_t cap;   // rows allocated
     uint32_t base;  // global ordinal of row 0
+    // K1 "pp" bit planes, derived from flags/digit (k_build_planes after every
+    // delta batch): planes[p * gcap + g], p = kPlane*, one u32 per group g of
+    // kGroupRows consecutive rows (bit s = row g*kGroupRows + s).
+    uint32_t *planes;
+    uint32_t gcap;  // groups allocated = cdiv(cap, kGroupRows)
+};
+
+constexpr uint32_t kGroupRows = 30;
+enum : uint32_t {
+    kPlaneD0 = 0,   // name digit bit 0 (15 = no digit)
+    kPlaneD1,
+    kPlaneD2,
+    kPlaneD3,
+    kPlaneSched,    // present && !Spec.Unschedulable
+    kPlanePresent,  // present (not tombstoned)
+    kPlanes
 };
 
 // One queued node delta (upsert or delete) as it travels to the device.
@@ -110,6 +126,15 @@ constexpr uint32_t kK1MaxColumns = (MS_MAX_ORDINAL + 1) / 64 + 1;
 hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
                              uint32_t *work, int num_cus, hipStream_t s);
+// K1 "pp" (ms_sweep_pp.hip): every (pod, node) pair through NU + NN + selectHost.
+// results != nullptr: decoded ms_result per pod (single-shard cycle; keys is
+// scratch, needed only above 122,880 rows); else keys[i] = this shard's max
+// packed key (0 = none), overwritten. present: global present-node count (decode).
+hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
+                           int num_cus, hipStream_t s);
+// Rebuilds the bit planes of the groups touched by deltas (or all groups when d_deltas is null).
+hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s);

@@ -1,0 +1,360 @@
+// ms_sweep_pp.hip — K1 "pp", the production NU+NN sweep: for every (pod, node)
+// pair it evaluates NodeUnschedulable and NodeNumber, and selectHost's argmax
+// with the deterministic tie-break.
+//
+// Reference path (/root/reference/minisched/minisched.go):
+//   RunFilterPlugins :115-151 -> NodeUnschedulable.Filter (k8s@v1.22.0, restated)
+//   RunScorePlugins  :164-199 -> NodeNumber.Score (plugins/score/nodenumber/nodenumber.go:73-95)
+//   unweighted sum   :187-196
+//   selectHost       :304-325 (rand.Intn tie-break -> rule r3, minisched_gpu.h)
+//
+// Bit-sliced evaluation. The node table keeps, per group of 30 consecutive
+// rows, six bit planes (ms_internal.h kPlane*): the four bits of each row's
+// name digit (15 = no digit), "present and schedulable" and "present". A lane
+// holds up to kPpWords groups in registers. For one pod and one group:
+//   F = tolerates ? present : schedulable                     (NodeUnschedulable, 30 rows)
+//   m = F & XNOR(d0, pod bit 0) & .. & XNOR(d3, pod bit 3)    (NodeNumber's 10, 30 rows)
+// five v_bitop3 in all, each computing one boolean term for each of the 30
+// (pod, row) pairs of the group: every pair's filter and score comes from its
+// own row's bits and the pod's own bits. The rows set in m are the pairs that
+// pass the filter with score 10; their tie-break hashes (mix32 of A + ordinal *
+// kG24, rule r3) are the candidates of selectHost's max. A group of 30
+// consecutive names holds at most 3 rows of one digit when the digits cycle, so
+// three v_ffbl slots cover it with no lane-divergent loop; a tile where some
+// lane has more (the wave-uniform `gen` flag, computed when the tile is
+// loaded) takes a bit-scan loop instead. Rows scoring 0 matter only when no
+// feasible row of the wave scores 10: the wave's maximum is then 0 and the pod
+// is redone by the exact slow path (every feasible row hashed, explicit
+// found flags), which also covers non-digit pods.
+//
+// Grid: a workgroup holds ALL of the context's rows (up to 16 waves x 64 lanes
+// x kPpWords groups = 122,880 rows; more rows split over grid.y and combine
+// with atomicMax) and sweeps a chunk of pods through them, 8 pods at a time.
+// The 8 lane maxima are reduced by one transposed butterfly (reduce8), the
+// waves combine in LDS (ds_max_u64 of level<<32 | hash), and after one barrier
+// the workgroup unhashes each pod's winner (tb_unhash) and writes either the
+// packed key (ms_sweep_device: one plain store per pod, no zeroing, no
+// atomics) or the decoded ms_result directly (the fused single-shard cycle).
+#include <algorithm>
+#include <cstdlib>
+
+#include "ms_device.h"
+
+namespace msgpu {
+
+namespace {
+
+template <typename F>
+constexpr uint32_t truth3(F f) {  // v_bitop3 table, S0 the most significant index bit
+    uint32_t t = 0;
+    for (int i = 0; i < 8; ++i)
+        if (f((i >> 2) & 1, (i >> 1) & 1, i & 1)) t |= 1u << i;
+    return t;
+}
+constexpr uint32_t kXnorAnd = truth3([](int a, int b, int c) { return c && a == b; });  // c & ~(a ^ b)
+constexpr uint32_t kSelect = truth3([](int a, int b, int c) { return c ? a : b; });     // c ? a : b
+
+constexpr int kPpWords = 4;      // 30-row groups per lane
+constexpr int kPpMaxWaves = 16;  // 1024-thread workgroups
+constexpr uint32_t kPpWaveGroups = 64u * kPpWords;
+
+struct Word {
+    uint32_t d0, d1, d2, d3;  // digit bit planes
+    uint32_t sched, pres;     // present & schedulable, present
+    uint32_t hb;              // (ordinal of the group's row 0) * kG24
+};
+
+// One pod as the wave sees it (all wave-uniform, SGPRs).
+struct Pod {
+    uint32_t A;               // tb_pod(seed32, ordinal)
+    uint32_t s0, s1, s2, s3;  // digit bit i as 0 / ~0 (non-digit pods: 14, which no node has)
+    uint32_t tol;             // tolerates node.kubernetes.io/unschedulable: 0 / ~0
+};
+
+#define MS_BITOP3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
+
+__device__ __forceinline__ uint32_t feasible(const Word &w, const Pod &q) {
+    return MS_BITOP3(w.pres, w.sched, q.tol, kSelect);
+}
+
+// Rows of the group that pass NodeUnschedulable and score NodeNumber's 10.
+__device__ __forceinline__ uint32_t match10(const Word &w, const Pod &q) {
+    uint32_t m = MS_BITOP3(w.d0, q.s0, feasible(w, q), kXnorAnd);
+    m = MS_BITOP3(w.d1, q.s1, m, kXnorAnd);
+    m = MS_BITOP3(w.d2, q.s2, m, kXnorAnd);
+    return MS_BITOP3(w.d3, q.s3, m, kXnorAnd);
+}
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t slot, uint32_t hbA) {
+    return mix32(__umul24(slot, kG24) + hbA);  // A + (row0 + slot) * kG24, rule r3
+}
+
+// Lane maximum hash over the group's score-10 rows, at most 3 of them (the
+// tile's `gen` flag is clear). Slots 2 and 3 fall back to the previous slot when
+// the mask runs out (a duplicate leaves the max unchanged); an empty mask gives 0.
+__device__ __forceinline__ uint32_t word_fast(const Word &w, const Pod &q) {
+    const uint32_t m = match10(w, q);
+    const uint32_t hbA = w.hb + q.A;
+    const uint32_t m1 = m & (m - 1u), m2 = m1 & (m1 - 1u);
+    const int i0 = (int)first_slot(m);
+    const int i1 = max((int)first_slot(m1), i0);
+    const int i2 = max((int)first_slot(m2), i1);
+    const uint32_t h = max(max(hash_slot((uint32_t)i0, hbA), hash_slot((uint32_t)i1, hbA)),
+                           hash_slot((uint32_t)i2, hbA));
+    return m ? h : 0u;
+}
+
+// Any number of score-10 rows per lane: a bit-scan loop (lane-divergent trip count).
+__device__ __forceinline__ uint32_t word_scan(uint32_t m, uint32_t hbA) {
+    uint32_t h = 0;
+    while (m) {
+        const uint32_t s = first_slot(m);
+        m &= m - 1u;
+        h = max(h, hash_slot(s, hbA));
+    }
+    return h;
+}
+
+__device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
+    Pod q;
+    q.A = A;
+    q.s0 = (info & 1u) ? ~0u : 0u;
+    q.s1 = (info & 2u) ? ~0u : 0u;
+    q.s2 = (info & 4u) ? ~0u : 0u;
+    q.s3 = (info & 8u) ? ~0u : 0u;
+    q.tol = (info & 16u) ? ~0u : 0u;
+    return q;
+}
+
+// Exact evaluation of one pod over the wave's NW groups, with explicit found
+// flags: level 11 (score 10 + 1) over the score-10 rows, else level 1 over
+// every feasible row (all score 0). Returns level<<32 | max hash (wave-uniform),
+// 0 when no row of the wave is feasible.
+template <int NW>
+__device__ __forceinline__ u64 pod_slow(const Word (&W)[kPpWords], const Pod &q) {
+    uint32_t h = 0;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint32_t m = match10(W[k], q);
+        found = found || m != 0;
+        h = max(h, word_scan(m, W[k].hb + q.A));
+    }
+    if (__ballot(found) != 0) return (11ull << 32) | wave_max_u32_dpp(h);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint32_t m = feasible(W[k], q);
+        found = found || m != 0;
+        h = max(h, word_scan(m, W[k].hb + q.A));
+    }
+    if (__ballot(found) != 0) return (1ull << 32) | wave_max_u32_dpp(h);
+    return 0;
+}
+
+// One wave sweeps pods [pbeg, pend) through its NW groups into lds[p - pbeg].
+template <int NW, bool GEN>
+__device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const ms_pod_rec *__restrict__ pods,
+                                            uint32_t pbeg, uint32_t pend, uint32_t seed32, uint32_t lane,
+                                            u64 *lds) {
+    for (uint32_t pb = pbeg; pb < pend; pb += 64) {
+        const uint32_t nblk = min(64u, pend - pb);
+        // the block's pods, one per lane: A and digit | tolerates << 4
+        uint32_t a_l = 0, info_l = 14u;
+        if (lane < nblk) {
+            const uint2 pr = *reinterpret_cast<const uint2 *>(pods + pb + lane);  // ordinal, digit, tolerates
+            const int dig = (int)(int8_t)(pr.y & 0xFFu);
+            a_l = tb_pod(seed32, pr.x);
+            info_l = ((uint32_t)dig <= 9u ? (uint32_t)dig : 14u) | (((pr.y >> 8) & 0xFFu) ? 16u : 0u);
+        }
+        for (uint32_t j = 0; j < nblk; j += 8) {
+            Pod q[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                q[t] = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
+                                (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
+            uint32_t r[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                uint32_t h = 0;
+#pragma unroll
+                for (int k = 0; k < NW; ++k)
+                    h = max(h, GEN ? word_scan(match10(W[k], q[t]), W[k].hb + q[t].A) : word_fast(W[k], q[t]));
+                r[t] = h;
+            }
+            const uint32_t u = reduce8(r, lane);
+            const uint32_t pi = j + rev3(lane >> 3);  // lanes 8k: pod pi of the block
+            const bool mine = (lane & 7u) == 0u && pi < nblk;
+            if (mine && u != 0u) atomicMax(&lds[pb - pbeg + pi], (11ull << 32) | u);
+            // a zero maximum: no score-10 row in this wave (or one whose hash is 0);
+            // redo those pods exactly
+            u64 redo = __ballot(mine && u == 0u);
+            while (redo) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(redo);
+                redo &= redo - 1ull;
+                const uint32_t t = rev3(l >> 3);
+                const Pod qs = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
+                                        (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
+                const u64 v = pod_slow<NW>(W, qs);
+                if (lane == 0 && v) atomicMax(&lds[pb - pbeg + j + t], v);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
+    const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
+    const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
+    int atomic_keys, ms_result *__restrict__ results, uint32_t present) {
+    extern __shared__ u64 lds[];  // one combine slot per pod of the chunk
+    const uint32_t lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t pbeg = blockIdx.x * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lds[i] = 0;
+
+    // the wave's groups: word k of lane l is group g0 + 64k + l
+    const uint32_t g0 = (blockIdx.y * (blockDim.x >> 6) + wv) * kPpWaveGroups;
+    Word W[kPpWords];
+    int nw = 0;
+    bool over = false;
+#pragma unroll
+    for (int k = 0; k < kPpWords; ++k) {
+        const uint32_t g = g0 + 64u * k + lane;
+        const bool in = g < n_groups;
+        if (g0 + 64u * k < n_groups) nw = k + 1;  // wave-uniform
+        W[k].d0 = in ? planes[kPlaneD0 * gstride + g] : 0u;
+        W[k].d1 = in ? planes[kPlaneD1 * gstride + g] : 0u;
+        W[k].d2 = in ? planes[kPlaneD2 * gstride + g] : 0u;
+        W[k].d3 = in ? planes[kPlaneD3 * gstride + g] : 0u;
+        W[k].sched = in ? planes[kPlaneSched * gstride + g] : 0u;
+        W[k].pres = in ? planes[kPlanePresent * gstride + g] : 0u;
+        W[k].hb = (node_base + g * kGroupRows) * kG24;
+        // more than 3 present rows of one digit in a group: the fast slots cannot hold them
+#pragma unroll
+        for (int d = 0; d < 10; ++d) {
+            const uint32_t m = W[k].pres & ((d & 1) ? W[k].d0 : ~W[k].d0) & ((d & 2) ? W[k].d1 : ~W[k].d1) &
+                               ((d & 4) ? W[k].d2 : ~W[k].d2) & ((d & 8) ? W[k].d3 : ~W[k].d3);
+            over = over || __popc(m) > 3;
+        }
+    }
+    const bool gen = __ballot(over) != 0;
+    __syncthreads();
+    if (np) {
+        switch (nw * 2 + (gen ? 1 : 0)) {  // wave-uniform
+#define MS_PP_CASE(N)                                                                     \
+    case 2 * N:                                                                           \
+        sweep_range<N, false>(W, pods, pbeg, pend, seed32, lane, lds);                    \
+        break;                                                                            \
+    case 2 * N + 1:                                                                       \
+        sweep_range<N, true>(W, pods, pbeg, pend, seed32, lane, lds);                     \
+        break;
+            MS_PP_CASE(1)
+            MS_PP_CASE(2)
+            MS_PP_CASE(3)
+            MS_PP_CASE(4)
+#undef MS_PP_CASE
+            default:
+                break;  // no groups in this wave
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+        const u64 v = lds[i];
+        const uint2 pr = *reinterpret_cast<const uint2 *>(pods + pbeg + i);
+        u64 key = 0;
+        if (v) {
+            const uint32_t h = (uint32_t)v;
+            key = make_key((uint32_t)(v >> 32) - 1u, h, tb_unhash(tb_pod(seed32, pr.x), h));
+        }
+        if (keys) {
+            if (!atomic_keys) keys[pbeg + i] = key;
+            else if (key) atomicMax(&keys[pbeg + i], key);
+        }
+        if (results) results[pbeg + i] = decode_key(key, (int8_t)(pr.y & 0xFFu), nullptr, 0, present);
+    }
+}
+
+// Bit planes of one 30-row group from the SoA columns (flags, digit).
+__device__ __forceinline__ void build_group(const NodeTable &t, uint32_t g) {
+    uint32_t d[4] = {0, 0, 0, 0}, sched = 0, pres = 0;
+    for (uint32_t s = 0; s < kGroupRows; ++s) {
+        const uint32_t r = g * kGroupRows + s;
+        if (r >= t.cap) break;
+        const uint32_t f = t.flags[r], dg = t.digit[r];
+        const uint32_t v = dg <= 9u ? dg : 15u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) d[b] |= ((v >> b) & 1u) << s;
+        if (!(f & kNodeAbsent)) {
+            pres |= 1u << s;
+            if (!(f & kNodeUnschedulable)) sched |= 1u << s;
+        }
+    }
+    const uint32_t st = t.gcap;
+    t.planes[kPlaneD0 * st + g] = d[0];
+    t.planes[kPlaneD1 * st + g] = d[1];
+    t.planes[kPlaneD2 * st + g] = d[2];
+    t.planes[kPlaneD3 * st + g] = d[3];
+    t.planes[kPlaneSched * st + g] = sched;
+    t.planes[kPlanePresent * st + g] = pres;
+}
+
+// deltas != nullptr: the groups of the applied deltas (a group rebuilt twice gets the
+// same bits: the deltas' column writes finished in the previous launch); else all groups.
+__global__ void k_build_planes(NodeTable t, const NodeDelta *__restrict__ deltas, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = deltas ? deltas[i].local / kGroupRows : i;
+    if (g < t.gcap) build_group(t, g);
+}
+
+inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s) {
+    if (!t.planes) return hipSuccess;
+    if (!d_deltas) n = t.gcap;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_build_planes, dim3(cdiv(n, 256)), dim3(256), 0, s, t, d_deltas, n);
+    return hipGetLastError();
+}
+
+// Geometry: W = the fewest waves (<= 16) whose 256 groups each hold the rows
+// (more rows: grid.y workgroups per chunk); pods per workgroup sized for one
+// round of resident workgroups (32 waves per CU) in multiples of 8, at most
+// kPpMaxChunk (LDS). MINISCHED_PP_CHUNK overrides the chunk (tuning).
+constexpr uint32_t kPpMaxChunk = 4096;
+
+hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
+                           int num_cus, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    if (!t.planes) return hipErrorInvalidValue;
+    const uint32_t n_groups = cdiv(n_rows, kGroupRows);
+    const uint32_t waves_needed = std::max(1u, cdiv(n_groups, kPpWaveGroups));
+    const uint32_t W = std::min<uint32_t>(kPpMaxWaves, waves_needed);
+    const uint32_t gy = cdiv(waves_needed, W);
+    const uint32_t per_cu = std::max(1u, 32u / W);
+    const uint32_t resident = per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256) / gy;
+    uint32_t chunk = cdiv(cdiv(n_pods, std::max(1u, resident)), 8) * 8;
+    if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
+    chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
+    const dim3 grid(cdiv(n_pods, chunk), gy);
+    if (gy > 1) {
+        // several workgroups per chunk: combine keys with atomicMax, then decode
+        if (!keys) return hipErrorInvalidValue;
+        hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * sizeof(u64), s, t.planes, t.gcap, n_groups,
+                           t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present);
+        e = hipGetLastError();
+        if (e != hipSuccess || !results) return e;
+        return launch_decode(pods, n_pods, keys, nullptr, present, results, s);
+    }
+    hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * sizeof(u64), s, t.planes, t.gcap, n_groups, t.base,
+                       pods, n_pods, chunk, seed32, results ? nullptr : keys, 0, results, present);
+    return hipGetLastError();
+}
+
+}  // namespace msgpu

@@ -123,6 +123,7 @@ SIGNATURES = {
     "ms_decode_device_jobs": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp]),
     "ms_apply_binds_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_schedule_sequential_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_select_batch_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
 }
 
 DECODE_MAX_JOBS = 8  # MS_DECODE_MAX_JOBS
@@ -290,6 +291,13 @@ class Engine:
         self._check(
             "ms_apply_binds_device",
             self.lib.ms_apply_binds_device(self.h, n_pods, pods_dev, results_dev, stream or None),
+        )
+
+    def select_batch_device(self, n_pods, pods_dev, results_dev, stream=0):
+        """Stateless batched cycle on a single-shard context (no bind commit)."""
+        self._check(
+            "ms_select_batch_device",
+            self.lib.ms_select_batch_device(self.h, n_pods, pods_dev, results_dev, stream or None),
         )
 
     def schedule_sequential_device(self, n_pods, pods_dev, results_dev, stream=0):

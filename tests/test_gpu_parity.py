@@ -68,11 +68,12 @@ def test_readme_scenario_gpu(oracle):
         assert e.read(9, 1)["pod_count"][0] == 1  # assume-on-select
 
 
-@pytest.fixture(params=["v7", "v7w2", "v7w4", "v7w4-gen", "v8", "v0"])
+@pytest.fixture(params=["pp", "v7", "v7w2", "v7w4", "v7w4-gen", "v8", "v0"])
 def k1_variant(request, monkeypatch):
-    # every NU+NN sweep form stays bit-exact: v7 with 1, 2 or 4 waves per workgroup sharing
-    # one tile build (and with tolerating pods on the general path: -gen), the persistent v8,
-    # and v0 (hash every pair), the plain cross-check
+    # every NU+NN sweep form stays bit-exact: pp (the per-pair bit-sliced production kernel),
+    # the class-indexed v7 with 1, 2 or 4 waves per workgroup sharing one tile build (and with
+    # tolerating pods on the general path: -gen), the persistent v8, and v0 (hash every pair),
+    # the plain cross-check
     v = request.param
     monkeypatch.setenv("MINISCHED_K1", v[:2])
     monkeypatch.setenv("MINISCHED_K1_WAVES", v[3] if "w" in v else "1")
