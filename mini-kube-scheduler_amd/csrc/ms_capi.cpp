@@ -373,20 +373,32 @@ int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned 
     return MS_OK;
 }
 
-// The stateless cycle of one batch (n_pods <= batch_cap) on a single-shard
-// context: filter + score + selectHost + decode into results, no bind commit.
-// NU+NN with K1 pp is one fused launch; otherwise sweep into the context's
-// key/flag scratch, then decode.
+// The stateless cycle of a batch on a single-shard context: filter + score +
+// selectHost + decode into results, no bind commit. NU+NN with K1 pp is one
+// fused launch for the whole batch (it needs key scratch only above
+// kPpMaxFusedRows rows); otherwise batch_cap chunks are swept into the
+// context's key/flag scratch, then decoded.
 int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s) {
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN && k1_pp()) {
-        MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), c->d_keys, d_res,
+    const uint32_t B = c->batch_cap;
+    const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN && k1_pp();
+    if (fused && c->rows_dev <= kPpMaxFusedRows) {
+        MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), nullptr, d_res,
                                   c->present_dev, c->num_cus, s));
         return MS_OK;
     }
-    const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
-    int rc = sweep_locked(c, n_pods, d_pods, c->d_keys, want_flags ? c->d_flags : nullptr, s);
-    if (rc) return rc;
-    MS_HIP(c, launch_decode(d_pods, n_pods, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev, d_res, s));
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        if (fused) {
+            MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods + s0, nb, seed32_of(c->cfg.seed), c->d_keys,
+                                      d_res + s0, c->present_dev, c->num_cus, s));
+            continue;
+        }
+        const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
+        int rc = sweep_locked(c, nb, d_pods + s0, c->d_keys, want_flags ? c->d_flags : nullptr, s);
+        if (rc) return rc;
+        MS_HIP(c, launch_decode(d_pods + s0, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev,
+                                d_res + s0, s));
+    }
     return MS_OK;
 }
 
@@ -674,11 +686,8 @@ int ms_select_batch_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_de
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);
     if (rc) return rc;
-    const uint32_t B = c->batch_cap;  // key/flag scratch (the fused NU+NN kernel needs none below 122,880 rows)
-    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
-        rc = select_locked(c, std::min(B, n_pods - s0), pods_dev + s0, results_dev + s0, s);
-        if (rc) return rc;
-    }
+    rc = select_locked(c, n_pods, pods_dev, results_dev, s);
+    if (rc) return rc;
     return chain_back(c, s);
 }
 
@@ -734,14 +743,10 @@ int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *
         rc = run_sequential(c, n_pods, pods_dev, results_dev, s);
     } else {
         // NU+NN: keys are independent of mutable state -> batched cycle + commit
-        const uint32_t B = c->batch_cap;
-        for (uint32_t s0 = 0; s0 < n_pods && !rc; s0 += B) {
-            const uint32_t nb = std::min(B, n_pods - s0);
-            rc = select_locked(c, nb, pods_dev + s0, results_dev + s0, s);
-            if (!rc) {
-                hipError_t e = launch_apply_binds(c->t, pods_dev + s0, nb, results_dev + s0, s);
-                if (e != hipSuccess) rc = fail(c, MS_E_HIP, std::string("apply binds: ") + hipGetErrorString(e));
-            }
+        rc = select_locked(c, n_pods, pods_dev, results_dev, s);
+        if (!rc) {
+            hipError_t e = launch_apply_binds(c->t, pods_dev, n_pods, results_dev, s);
+            if (e != hipSuccess) rc = fail(c, MS_E_HIP, std::string("apply binds: ") + hipGetErrorString(e));
         }
     }
     if (rc) return rc;

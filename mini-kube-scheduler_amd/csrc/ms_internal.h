@@ -133,6 +133,9 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
                            int num_cus, hipStream_t s);
+// Rows one K1 pp workgroup holds (16 waves x 64 lanes x 4 groups of 30):
+// up to here the single-shard cycle is one launch with no key scratch.
+constexpr uint32_t kPpMaxFusedRows = 16u * 64u * 4u * kGroupRows;
 // Rebuilds the bit planes of the groups touched by deltas (or all groups when d_deltas is null).
 hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,

@@ -85,20 +85,27 @@ __device__ __forceinline__ uint32_t match10(const Word &w, const Pod &q) {
     return MS_BITOP3(w.d3, q.s3, m, kXnorAnd);
 }
 
+// Leading zeros (v_ffbh_u32; 0xFFFFFFFF for an empty mask).
+__device__ __forceinline__ uint32_t last_lz(uint32_t m) {
+    uint32_t s;
+    asm("v_ffbh_u32 %0, %1" : "=v"(s) : "v"(m));
+    return s;
+}
+
 __device__ __forceinline__ uint32_t hash_slot(uint32_t slot, uint32_t hbA) {
     return mix32(__umul24(slot, kG24) + hbA);  // A + (row0 + slot) * kG24, rule r3
 }
 
 // Lane maximum hash over the group's score-10 rows, at most 3 of them (the
-// tile's `gen` flag is clear). Slots 2 and 3 fall back to the previous slot when
-// the mask runs out (a duplicate leaves the max unchanged); an empty mask gives 0.
+// tile's `gen` flag is clear): the lowest (v_ffbl), the highest (v_ffbh) and
+// the lowest of the rest, which falls back to the lowest when fewer than 3
+// (a duplicate leaves the max unchanged); an empty mask gives 0.
 __device__ __forceinline__ uint32_t word_fast(const Word &w, const Pod &q) {
     const uint32_t m = match10(w, q);
     const uint32_t hbA = w.hb + q.A;
-    const uint32_t m1 = m & (m - 1u), m2 = m1 & (m1 - 1u);
     const int i0 = (int)first_slot(m);
-    const int i1 = max((int)first_slot(m1), i0);
-    const int i2 = max((int)first_slot(m2), i1);
+    const int i2 = 31 - (int)last_lz(m);
+    const int i1 = max((int)first_slot(m & (m - 1u)), i0);
     const uint32_t h = max(max(hash_slot((uint32_t)i0, hbA), hash_slot((uint32_t)i1, hbA)),
                            hash_slot((uint32_t)i2, hbA));
     return m ? h : 0u;
@@ -213,16 +220,20 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lds[i] = 0;
 
-    // the wave's groups: word k of lane l is group g0 + 64k + l
-    const uint32_t g0 = (blockIdx.y * (blockDim.x >> 6) + wv) * kPpWaveGroups;
+    // the wave's groups, dealt round-robin over the workgroup's waves so their
+    // word counts differ by at most one: word k of lane l is group
+    // g0 + (k * waves + wv) * 64 + l
+    const uint32_t waves = blockDim.x >> 6;
+    const uint32_t g0 = blockIdx.y * waves * kPpWaveGroups;
     Word W[kPpWords];
     int nw = 0;
     bool over = false;
 #pragma unroll
     for (int k = 0; k < kPpWords; ++k) {
-        const uint32_t g = g0 + 64u * k + lane;
+        const uint32_t gw = g0 + (k * waves + wv) * 64u;
+        const uint32_t g = gw + lane;
         const bool in = g < n_groups;
-        if (g0 + 64u * k < n_groups) nw = k + 1;  // wave-uniform
+        if (gw < n_groups) nw = k + 1;  // wave-uniform
         W[k].d0 = in ? planes[kPlaneD0 * gstride + g] : 0u;
         W[k].d1 = in ? planes[kPlaneD1 * gstride + g] : 0u;
         W[k].d2 = in ? planes[kPlaneD2 * gstride + g] : 0u;
@@ -320,8 +331,8 @@ hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, ui
     return hipGetLastError();
 }
 
-// Geometry: W = the fewest waves (<= 16) whose 256 groups each hold the rows
-// (more rows: grid.y workgroups per chunk); pods per workgroup sized for one
+// Geometry: W waves (<= 16) of up to 256 groups each hold the rows (more
+// rows: grid.y workgroups per chunk); pods per workgroup sized for one
 // round of resident workgroups (32 waves per CU) in multiples of 8, at most
 // kPpMaxChunk (LDS). MINISCHED_PP_CHUNK overrides the chunk (tuning).
 constexpr uint32_t kPpMaxChunk = 4096;
@@ -333,8 +344,13 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
     const uint32_t waves_needed = std::max(1u, cdiv(n_groups, kPpWaveGroups));
-    const uint32_t W = std::min<uint32_t>(kPpMaxWaves, waves_needed);
-    const uint32_t gy = cdiv(waves_needed, W);
+    // large shards: 16-wave workgroups (2 per CU = 8 waves per SIMD; the groups
+    // are dealt round-robin, so every wave holds 3 or 4 words); small shards:
+    // the fewest waves that hold the rows (profiles/r02c_ab.json)
+    uint32_t W = waves_needed >= 9 ? kPpMaxWaves : waves_needed;
+    if (const char *w = getenv("MINISCHED_PP_WAVES")) W = (uint32_t)std::min(16, std::max(1, atoi(w)));
+    if (!keys) W = std::max(W, std::min<uint32_t>(kPpMaxWaves, waves_needed));  // no scratch: one workgroup per chunk
+    const uint32_t gy = std::max(1u, cdiv(n_groups, W * kPpWaveGroups));
     const uint32_t per_cu = std::max(1u, 32u / W);
     const uint32_t resident = per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256) / gy;
     uint32_t chunk = cdiv(cdiv(n_pods, std::max(1u, resident)), 8) * 8;

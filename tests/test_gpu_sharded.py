@@ -1,9 +1,10 @@
 """N > 1 bench path on one GPU: two ranks (gloo, both on cuda:0) run
 sharded.ShardedCycle exactly as bench.py does — the HIP sweep of each node
-shard, the cross-shard MAX combine, the decode — in both the pipelined
-(cross-step at depth 1 and 2, with and without its own decode stream) and the in-step chunked
-forms, and every rank's decoded results must equal the oracle's over the
-whole cluster.
+shard, the cross-shard MAX reduce-scatter, the decode of each rank's pod
+slice (pipelined at depth 1 and 2), and the pod-split replicas — and every
+rank's decoded slice must equal the oracle's over the whole cluster. A 1-rank
+RCCL group drives the same pipeline through torch's "nccl" backend
+(reduce_scatter_tensor, ordered drains, grouped decodes).
 """
 import os
 import socket
@@ -16,7 +17,7 @@ from minisched_amd import synth
 
 pytestmark = pytest.mark.gpu
 
-N_NODES, N_PODS, SEED = 30_000, 5_000, 3
+N_NODES, N_PODS, SEED = 30_000, 5_001, 3
 
 
 def _free_port():
@@ -27,7 +28,12 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, pipeline, chunks, dstream, depth, q):
+def _same(res, o, a, b, tag):
+    for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
+        assert np.array_equal(res[k_res], o[k_or][a:b]), f"{tag} {k_res}"
+
+
+def _worker(rank, world, port, split, depth, group, q):
     import torch
     import torch.distributed as dist
 
@@ -39,50 +45,53 @@ def _worker(rank, world, port, pipeline, chunks, dstream, depth, q):
         torch.cuda.set_device(0)
         dev = torch.device("cuda:0")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        lo, hi = sharded.shard_bounds(N_NODES, rank, world)
+        lo, hi = sharded.shard_bounds(N_NODES, rank, world) if split == "nodes" else (0, N_NODES)
         eng = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NN, node_base=lo, seed=SEED)
         eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=SEED, start=lo))
         eng.flush()
+        present = sharded.present_total(eng) if split == "nodes" else None
         pods = torch.from_numpy(synth.pods(N_PODS, seed=SEED).view(np.uint8).copy()).to(dev)
         stream = torch.cuda.Stream(device=dev)
         torch.cuda.set_stream(stream)
-        cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, chunks=chunks, pipeline=pipeline,
-                                   decode_stream=dstream, depth=depth)
-        for _ in range(5):  # both key buffers reused after their decodes
-            cyc.step(world)
+        cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, split=split, depth=depth,
+                                   drain_group=group, rank=rank, world=world, present_total=present)
+        for _ in range(5):  # key buffers reused after their decodes
+            cyc.step()
         cyc.finish()
         torch.cuda.synchronize()
-        res = cyc.results.cpu().numpy().view(_lib.RESULT).copy()
+        res = cyc.results.cpu().numpy().view(_lib.RESULT)[: cyc.b - cyc.a].copy()
         eng.close()
         dist.destroy_process_group()
-        q.put((rank, res, None))
+        q.put((rank, cyc.a, cyc.b, res, present, None))
     except Exception as e:  # reported to the parent, which fails the test
-        q.put((rank, None, repr(e)))
+        q.put((rank, 0, 0, None, None, repr(e)))
 
 
-@pytest.mark.parametrize("pipeline,chunks,dstream,depth",
-                         [(True, 1, False, 1), (True, 1, False, 2), (True, 1, True, 1), (True, 1, True, 2),
-                          (False, 3, False, 1)])
-def test_two_rank_sharded_cycle_on_gpu(oracle, pipeline, chunks, dstream, depth):
+@pytest.mark.parametrize("split,depth,group", [("nodes", 1, 1), ("nodes", 2, 2), ("nodes", 3, 1), ("pods", 1, 1)])
+def test_two_rank_cycle_on_gpu(oracle, split, depth, group):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, pipeline, chunks, dstream, depth, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, split, depth, group, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=110) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    errs = [e for _, _, e in got if e]
+    errs = [e for *_, e in got if e]
     assert not errs, errs
     o = oracle.schedule(synth.nodes(N_NODES, seed=SEED), synth.pods(N_PODS, seed=SEED), seed=SEED)
-    for rank, res, _ in got:
-        for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
-            assert np.array_equal(res[k_res], o[k_or]), f"rank {rank} {k_res}"
+    covered = 0
+    for rank, a, b, res, present, _ in got:
+        _same(res, o, a, b, f"rank {rank}")
+        covered += b - a
+        if split == "nodes":
+            assert present == N_NODES  # summed over the shards
+    assert covered == N_PODS
 
 
-def _rccl_worker(port, depth, group, dstream, q):
+def _rccl_worker(port, depth, group, q):
     import torch
     import torch.distributed as dist
 
@@ -100,37 +109,33 @@ def _rccl_worker(port, depth, group, dstream, q):
         pods = torch.from_numpy(synth.pods(N_PODS, seed=SEED).view(np.uint8).copy()).to(dev)
         stream = torch.cuda.Stream(device=dev)
         torch.cuda.set_stream(stream)
-        cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, pipeline=True, decode_stream=dstream,
-                                   depth=depth, drain_group=group)
+        cyc = sharded.ShardedCycle(eng, N_NODES, N_PODS, pods, stream, depth=depth, drain_group=group,
+                                   collective=True, present_total=sharded.present_total(eng))
         ordered = cyc._pipe.ordered
-        outs = []
-        for k in range(7):  # world > 1 form: RCCL all-reduce per step, grouped drains
-            cyc.step(2)
+        for _ in range(7):  # the world > 1 form: RCCL reduce-scatter per step, grouped drains
+            cyc.step()
         cyc.finish()
         torch.cuda.synchronize()
-        outs.append(cyc.results.cpu().numpy().view(_lib.RESULT).copy())
+        res = cyc.results.cpu().numpy().view(_lib.RESULT).copy()
         eng.close()
         dist.destroy_process_group()
-        q.put((ordered, outs, None))
+        q.put((ordered, res, None))
     except Exception as e:
         q.put((None, None, repr(e)))
 
 
-@pytest.mark.parametrize("depth,group,dstream", [(2, 2, False), (3, 3, False), (2, 2, True)])
-def test_rccl_grouped_drain(oracle, depth, group, dstream):
-    # the RCCL backend takes the ordered path (one wait per drained group)
+@pytest.mark.parametrize("depth,group", [(2, 2), (4, 4), (3, 1)])
+def test_rccl_pipeline(oracle, depth, group):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_rccl_worker, args=(_free_port(), depth, group, dstream, q))
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), depth, group, q))
     p.start()
-    ordered, outs, err = q.get(timeout=110)
+    ordered, res, err = q.get(timeout=110)
     p.join(timeout=60)
     assert err is None, err
     assert ordered
     o = oracle.schedule(synth.nodes(N_NODES, seed=SEED), synth.pods(N_PODS, seed=SEED), seed=SEED)
-    for res in outs:
-        for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
-            assert np.array_equal(res[k_res], o[k_or]), k_res
+    _same(res, o, 0, N_PODS, "rccl")
 
 
 def test_decode_device_jobs_matches_oracle(oracle):
@@ -163,8 +168,7 @@ def test_decode_device_jobs_matches_oracle(oracle):
         for k, (pr, _pods, _keys, res) in enumerate(batches):
             got = res.cpu().numpy().view(_lib.RESULT)
             o = oracle.schedule(nr, pr, seed=SEED)
-            for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
-                assert np.array_equal(got[k_res], o[k_or]), f"batch {k} {k_res}"
+            _same(got, o, 0, len(pr), f"batch {k}")
         with pytest.raises(RuntimeError):
             eng.decode_device_jobs(jobs * 3, n_nodes, stream.cuda_stream)  # > MS_DECODE_MAX_JOBS
     finally:

@@ -1,9 +1,11 @@
 """N > 1 path on CPU: node-sharded shards combined over torch.distributed (gloo).
 
 Each rank evaluates its own node shard with the oracle (standing in for the
-HIP sweep, which needs a GPU), then the product's combine_ all-reduces the
-packed keys and filter flags; every rank must end with exactly the keys and
-FitError masks of the single-process run over the whole cluster.
+HIP sweep, which needs a GPU), then the product's combine_scatter_
+reduce-scatters the packed keys and filter flags (MAX); every rank must end
+with exactly the keys and FitError masks of the single-process run over the
+whole cluster for its own pod slice. The pod-split partition (replicas, no
+collective) is checked the same way.
 """
 import os
 import socket
@@ -48,25 +50,30 @@ def _worker(rank, world, port, n_nodes, n_pods, plugin_set, q, chunks=1):
         nr["pod_count"][::5] = 110
     lo, hi = sharded.shard_bounds(n_nodes, rank, world)
     o = _oracle.schedule(nr[lo:hi], pr, plugin_set=plugin_set, seed=11, node_base=lo)
-    keys = torch.from_numpy(o["key"].view(np.int64).copy())
+    pp = sharded.padded_pods(n_pods, world)
+    keys = torch.zeros(pp, dtype=torch.int64)
+    keys[:n_pods] = torch.from_numpy(o["key"].view(np.int64).copy())
     # per-shard flags: a shard with no feasible node reports its own FitError mask
     m = o["mask"].astype(np.uint32)
-    flags = torch.from_numpy(((m & 1) | ((m >> 1) & 1) << 8).astype(np.int32))
+    flags = torch.zeros(pp, dtype=torch.int32)
+    flags[:n_pods] = torch.from_numpy(((m & 1) | ((m >> 1) & 1) << 8).astype(np.int32))
+    kout = torch.zeros(pp // world, dtype=torch.int64)
+    fout = torch.zeros(pp // world, dtype=torch.int32)
     if chunks == 1:
-        sharded.combine_(keys, flags if plugin_set == 1 else None)
-    else:  # pipelined form used by ShardedCycle.step: async per chunk, wait at the end
-        works = []
-        for a, b in sharded.chunk_bounds(n_pods, chunks):
-            works += sharded.combine_(keys[a:b], flags[a:b] if plugin_set == 1 else None, async_op=True)
+        sharded.combine_scatter_(keys, kout, flags if plugin_set == 1 else None, fout if plugin_set == 1 else None)
+    else:  # async form used by the pipelined step: wait later
+        works = sharded.combine_scatter_(keys, kout, flags if plugin_set == 1 else None,
+                                         fout if plugin_set == 1 else None, async_op=True)
         for w in works:
             w.wait()
-    q.put((rank, keys.numpy().view(np.uint64).copy(), flags.numpy().astype(np.uint32).copy()))
+    a, b = sharded.pod_slice(n_pods, rank, world)
+    q.put((rank, a, b, kout.numpy().view(np.uint64)[: b - a].copy(), fout.numpy().astype(np.uint32)[: b - a].copy()))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,chunks", [(2, 1), (3, 1), (2, 3)])
 @pytest.mark.parametrize("plugin_set", [0, 1])
-def test_node_sharded_combine_gloo(oracle, world, chunks, plugin_set):
+def test_node_sharded_reduce_scatter_gloo(oracle, world, chunks, plugin_set):
     n_nodes, n_pods = 997, 300
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -88,14 +95,72 @@ def test_node_sharded_combine_gloo(oracle, world, chunks, plugin_set):
         nr["req_milli_cpu"] = nr["alloc_milli_cpu"] * 3 // 4
         nr["pod_count"][::5] = 110
     full = oracle.schedule(nr, pr, plugin_set=plugin_set, seed=11)
-    for rank, keys, flags in got:
-        assert np.array_equal(keys, full["key"]), f"rank {rank}"
+    covered = np.zeros(n_pods, dtype=bool)
+    for rank, a, b, keys, flags in got:
+        assert np.array_equal(keys, full["key"][a:b]), f"rank {rank}"
+        covered[a:b] = True
         if plugin_set == 1:
-            assert np.array_equal(_decode_mask(keys, flags), full["mask"]), f"rank {rank}"
+            assert np.array_equal(_decode_mask(keys, flags), full["mask"][a:b]), f"rank {rank}"
         # decoded winners: the global ordinal sits in the low 20 bits of the key
-        won = full["code"] == 0
-        assert np.array_equal((0xFFFFF - (keys[won] & 0xFFFFF)).astype(np.int64), full["node"][won].astype(np.int64))
-        assert np.array_equal((keys[won] >> 52).astype(np.int64), full["score"][won])
+        won = full["code"][a:b] == 0
+        assert np.array_equal((0xFFFFF - (keys[won] & 0xFFFFF)).astype(np.int64),
+                              full["node"][a:b][won].astype(np.int64))
+        assert np.array_equal((keys[won] >> 52).astype(np.int64), full["score"][a:b][won])
+    assert covered.all()
+
+
+def _podsplit_worker(rank, world, port, n_nodes, n_pods, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import _oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nr = synth.nodes(n_nodes, seed=13)  # every rank holds the whole table (replica)
+    pr = synth.pods(n_pods, seed=13)
+    a, b = sharded.pod_slice(n_pods, rank, world)
+    o = _oracle.schedule(nr, pr[a:b], seed=13)  # stands in for ms_select_batch_device on the slice
+    # gather the slices to rank 0 the way a caller would (not part of the step: no collective there)
+    parts = [None] * world
+    dist.all_gather_object(parts, (a, b, o["key"].copy()))
+    q.put((rank, parts))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pod_split_replicas_gloo(oracle, world):
+    # config D's pod split: replicated nodes, disjoint pod slices, no combine; the union of
+    # the slices equals the single-process run (the tie-break hash depends on the pod's
+    # ordinal, not its position in the batch)
+    n_nodes, n_pods = 1200, 401
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_podsplit_worker, args=(r, world, port, n_nodes, n_pods, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = oracle.schedule(synth.nodes(n_nodes, seed=13), synth.pods(n_pods, seed=13), seed=13)
+    for rank, parts in got:
+        keys = np.concatenate([k for _a, _b, k in sorted(parts, key=lambda t: t[0])])
+        assert np.array_equal(keys, full["key"]), f"rank {rank}"
+
+
+def test_pod_slices_cover_everything():
+    for n in (0, 1, 7, 100_000, 1_000_000):
+        for w in (1, 2, 3, 8):
+            spans = [sharded.pod_slice(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            per = (n + w - 1) // w
+            assert all(b - a <= per for a, b in spans)
+            assert sharded.padded_pods(n, w) == per * w
 
 
 def test_shard_bounds_cover_everything():
@@ -107,16 +172,6 @@ def test_shard_bounds_cover_everything():
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
     with pytest.raises(ValueError):
         sharded.shard_bounds(10, 3, 3)
-
-
-def test_chunk_bounds():
-    for n in (1, 63, 64, 65, 1000, 100_000):
-        for c in (1, 2, 4, 7):
-            spans = sharded.chunk_bounds(n, c)
-            assert spans[0][0] == 0 and spans[-1][1] == n
-            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
-            assert all(a % 64 == 0 for a, _ in spans)
-            assert len(spans) <= c
 
 
 def _pipe_worker(rank, world, port, n_nodes, batches, depth, group, q):
@@ -132,19 +187,23 @@ def _pipe_worker(rank, world, port, n_nodes, batches, depth, group, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     nr = synth.nodes(n_nodes, seed=21)
     lo, hi = sharded.shard_bounds(n_nodes, rank, world)
-    keys = [torch.zeros(batches[0], dtype=torch.int64) for _ in range(depth + 1)]
+    pp = sharded.padded_pods(max(batches), world)
+    keys = [torch.zeros(pp, dtype=torch.int64) for _ in range(depth + 1)]
+    mine = [torch.zeros(pp // world, dtype=torch.int64) for _ in range(depth + 1)]
     out = {}
 
     def sweep(buf, k):  # this rank's shard of batch k (the oracle stands in for the HIP sweep)
         pr = synth.pods(batches[k], seed=100 + k)
         o = _oracle.schedule(nr[lo:hi], pr, seed=21, node_base=lo)
+        keys[buf].zero_()
         keys[buf][: batches[k]] = torch.from_numpy(o["key"].view(np.int64).copy())
 
     def combine(buf):
-        return sharded.combine_(keys[buf], None, async_op=True)
+        return sharded.combine_scatter_(keys[buf], mine[buf], async_op=True)
 
     def decode(buf, k):
-        out[k] = keys[buf][: batches[k]].numpy().view(np.uint64).copy()
+        a, b = sharded.pod_slice(pp, rank, world)
+        out[k] = (a, mine[buf].numpy().view(np.uint64).copy())
 
     pipe = sharded.CrossStepPipeline(sweep, combine, decode, depth=depth, group=group)
     for k in range(len(batches)):
@@ -174,5 +233,8 @@ def test_cross_step_pipeline_gloo(oracle, depth, group):
     nr = synth.nodes(n_nodes, seed=21)
     for k, n in enumerate(batches):
         full = oracle.schedule(nr, synth.pods(n, seed=100 + k), seed=21)
+        ref = np.zeros(sharded.padded_pods(max(batches), world), dtype=np.uint64)
+        ref[:n] = full["key"]
         for rank, out in got:
-            assert np.array_equal(out[k], full["key"]), f"rank {rank} batch {k}"
+            a, keys = out[k]
+            assert np.array_equal(keys, ref[a:a + len(keys)]), f"rank {rank} batch {k}"

@@ -26,6 +26,60 @@ KERNEL(k_xor, "v_xor_b32")
 KERNEL(k_mullo, "v_mul_lo_u32")
 KERNEL(k_mul24, "v_mul_u32_u24")
 KERNEL(k_mulhi, "v_mul_hi_u32")
+#define CHAIN8_1(INSN)                                                                                   \
+    for (int i = 0; i < ITERS; ++i) {                                                                    \
+        asm volatile(INSN " %0, %0\n\t" INSN " %1, %1\n\t" INSN " %2, %2\n\t" INSN " %3, %3\n\t" INSN       \
+                     " %4, %4\n\t" INSN " %5, %5\n\t" INSN " %6, %6\n\t" INSN " %7, %7"                          \
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));     \
+    }
+__global__ void k_ffbl(unsigned *out, unsigned k) {
+    unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    CHAIN8_1("v_ffbl_b32")
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ k;
+}
+KERNEL(k_max, "v_max_u32")
+
+// three-operand forms: dst = op(dst, dst, k)
+#define CHAIN8_3(INSN, SUFFIX)                                                                                   \
+    for (int i = 0; i < ITERS; ++i) {                                                                            \
+        asm volatile(INSN " %0, %0, %0, %8" SUFFIX "\n\t" INSN " %1, %1, %1, %8" SUFFIX "\n\t" INSN            \
+                     " %2, %2, %2, %8" SUFFIX "\n\t" INSN " %3, %3, %3, %8" SUFFIX "\n\t" INSN " %4, %4, %4, %8" \
+                     SUFFIX "\n\t" INSN " %5, %5, %5, %8" SUFFIX "\n\t" INSN " %6, %6, %6, %8" SUFFIX "\n\t"     \
+                     INSN " %7, %7, %7, %8" SUFFIX                                                               \
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)            \
+                     : "s"(k));                                                                                  \
+    }
+#define KERNEL3(NAME, INSN, SUFFIX)                                                       \
+    __global__ void NAME(unsigned *out, unsigned k) {                                     \
+        unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,    \
+                 a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                                   \
+        CHAIN8_3(INSN, SUFFIX)                                                            \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7; \
+    }
+KERNEL3(k_bitop3, "v_bitop3_b32", " bitop3:0x82")
+KERNEL3(k_mad24, "v_mad_u32_u24", "")
+KERNEL3(k_max3, "v_max3_u32", "")
+KERNEL3(k_fmaf3, "v_fma_f32", "")
+
+// v_xor_b32 with SDWA src0 = WORD_1 (x ^= x >> 16)
+#define CHAIN8_SDWA()                                                                                           \
+    for (int i = 0; i < ITERS; ++i) {                                                                           \
+        asm volatile(                                                                                           \
+            "v_xor_b32_sdwa %0, %0, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %1, %1, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %2, %2, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %3, %3, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %4, %4, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %5, %5, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %6, %6, %6 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n\t"  \
+            "v_xor_b32_sdwa %7, %7, %7 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"        \
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));                 \
+    }
+__global__ void k_xsdwa(unsigned *out, unsigned k) {
+    unsigned a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    CHAIN8_SDWA()
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ k;
+}
 
 int main() {
     int cus = 0;
@@ -35,7 +89,9 @@ int main() {
     hipMalloc(&out, blocks * threads * 4);
     struct { const char *n; void (*f)(unsigned *, unsigned); } ks[] = {
         {"v_add_u32", k_add}, {"v_xor_b32", k_xor}, {"v_mul_lo_u32", k_mullo}, {"v_mul_u32_u24", k_mul24},
-        {"v_mul_hi_u32", k_mulhi}};
+        {"v_mul_hi_u32", k_mulhi}, {"v_ffbl_b32", k_ffbl}, {"v_max_u32", k_max},
+        {"v_bitop3_b32", k_bitop3}, {"v_mad_u32_u24", k_mad24}, {"v_max3_u32", k_max3}, {"v_fma_f32", k_fmaf3},
+        {"v_xor_b32_sdwa", k_xsdwa}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
