@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 1
+#define MS_ABI_VERSION 2
 
 /* ---- return codes -------------------------------------------------------- */
 #define MS_OK 0
@@ -55,6 +55,10 @@ extern "C" {
 /* ---- plugin sets (minisched/initialize.go:80-138 hard-codes the first) --- */
 #define MS_PLUGINS_NU_NN 0        /* Filter[NodeUnschedulable]; Score[NodeNumber]            */
 #define MS_PLUGINS_NU_NRF_NN_LA 1 /* Filter[NU, NodeResourcesFit]; Score[NN, LeastAllocated] */
+/* Filter[NU]; Score[NN (weight w0), NodeAffinity preferred (weight w1) with
+ * ScoreExtensions = DefaultNormalizeScore(MaxNodeScore, reverse=false), run by
+ * RunScorePlugins' in-loop hook (minisched.go:178-183) exactly as written]. */
+#define MS_PLUGINS_NU_NN_NA 2
 
 /* ---- modes --------------------------------------------------------------- */
 #define MS_MODE_BATCHED 0    /* all pods of the call see the same node state               */
@@ -79,7 +83,9 @@ extern "C" {
 typedef struct ms_node_rec {
     uint8_t unschedulable; /* node.Spec.Unschedulable                              */
     uint8_t name_digit;    /* last char of node name as 0..9; 0xFF = not a digit     */
-    uint8_t _pad0[2];
+    uint8_t zone;          /* value id of the node's topology.kubernetes.io/zone
+                              label, 0 = unlabelled (MS_PLUGINS_NU_NN_NA)           */
+    uint8_t _pad0;
     int32_t allowed_pods;  /* NodeInfo.Allocatable.AllowedPodNumber                 */
     int32_t pod_count;     /* len(NodeInfo.Pods)                                    */
     int32_t _pad1;
@@ -93,7 +99,10 @@ typedef struct ms_pod_rec {
     uint32_t ordinal;                /* stable pod id fed to the tie-break           */
     int8_t name_digit;               /* last char of pod name as 0..9; -1 = not     */
     uint8_t tolerates_unschedulable; /* TolerationsTolerateTaint(unschedulable:NoSchedule) */
-    uint8_t _pad[2];
+    /* MS_PLUGINS_NU_NN_NA: one PreferredSchedulingTerm {weight, zone In [pref_zone]}
+     * (NodeAffinity.Score = weight when the node's zone label matches); 0 = none */
+    uint8_t pref_zone;
+    uint8_t pref_weight;             /* 1..100 (API validation of the term weight)  */
     int64_t req_milli_cpu, req_memory;         /* Fit PreFilter request              */
     int64_t nonzero_milli_cpu, nonzero_memory; /* GetNonzeroRequests sum            */
 } ms_pod_rec;
@@ -113,7 +122,10 @@ typedef struct ms_config {
     uint32_t max_nodes;  /* node capacity of this context                       */
     uint32_t node_base;  /* global ordinal of local node 0 (shard offset)       */
     uint32_t max_batch;  /* pods per internal chunk of ms_schedule_batch        */
-    uint32_t _reserved;
+    /* score plugin weights (MS_PLUGINS_NU_NN_NA only; 0 means 1): [0] NodeNumber,
+     * [1] NodeAffinity. The reference sums unweighted ("TODO: plugin weight",
+     * minisched.go:186); weights 1/1 reproduce it. w0*10 + w1*100 < 2048. */
+    uint16_t score_weight[2];
     uint64_t seed;       /* tie-break seed                                      */
 } ms_config;
 
@@ -175,7 +187,11 @@ int ms_uncommit_bind(ms_ctx *ctx, uint32_t ordinal, const ms_pod_rec *pod);
  *              byte 1: some node here rejected by NodeResourcesFit  (0/1)
  *   Both arrays are overwritten. flags may be NULL for MS_PLUGINS_NU_NN.
  *   Shards combine keys with an element-wise uint64 MAX and flags with a
- *   byte-wise uint8 MAX (= OR of 0/1 bytes): one all-reduce each.
+ *   byte-wise uint8 MAX (= OR of 0/1 bytes): one reduction each.
+ *   MS_PLUGINS_NU_NN_NA: keys use raw NodeAffinity scores and flags[i] is the
+ *   normalise anchor, ((0xFFFFF - ordinal) << 1 | NodeNumber match) + 1 of this
+ *   shard's first feasible node with a non-zero NodeAffinity score (0 = none);
+ *   shards combine it with an element-wise uint32 MAX.
  * ms_decode_device: combined keys/flags -> ms_result. present_nodes is the
  *   global count of present nodes (used when flags is NULL).
  * ms_apply_binds_device: NodeInfo.AddPod on this shard for every SUCCESS

@@ -47,7 +47,8 @@ struct ms_ctx {
     ms_pod_rec *d_pods = nullptr;
     ms_result *d_res = nullptr;
     unsigned long long *d_keys = nullptr;
-    uint32_t *d_flags = nullptr;
+    uint32_t *d_flags = nullptr;  // per-pod filter flags (set 1) / NodeAffinity anchors (set 2)
+    uint32_t w_nn = 1, w_na = 1;  // score weights (MS_PLUGINS_NU_NN_NA)
     NodeDelta *h_deltas = nullptr;
     NodeDelta *d_deltas = nullptr;
     uint32_t delta_cap = 0;
@@ -119,7 +120,7 @@ void free_all(ms_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *dev[] = {c->t.planes, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
+    void *dev[] = {c->t.planes, c->t.zone, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream,
@@ -365,12 +366,25 @@ int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned 
         if (rc) return rc;
         MS_HIP(c, launch_sweep_nunn(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->d_pstream, c->d_work,
                                     c->num_cus, s));
+    } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
+        MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
+        MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
+        MS_HIP(c, launch_sweep_na(c->t, c->rows_dev, d_pods, n_pods, seed32, c->w_nn, c->w_na, keys, flags,
+                                  c->num_cus, s));
     } else {
         MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
         if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
         MS_HIP(c, launch_sweep_full(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
     }
     return MS_OK;
+}
+
+// Combined keys (+ flags / anchors) -> ms_result for this context's plugin set.
+hipError_t decode_for(const ms_ctx *c, const ms_pod_rec *pods, uint32_t n, const unsigned long long *keys,
+                      const uint32_t *flags, uint32_t present, ms_result *out, hipStream_t s) {
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA)
+        return launch_decode_na(pods, n, keys, flags, present, seed32_of(c->cfg.seed), c->w_nn, c->w_na, out, s);
+    return launch_decode(pods, n, keys, flags, present, out, s);
 }
 
 // The stateless cycle of a batch on a single-shard context: filter + score +
@@ -396,8 +410,8 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
         const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
         int rc = sweep_locked(c, nb, d_pods + s0, c->d_keys, want_flags ? c->d_flags : nullptr, s);
         if (rc) return rc;
-        MS_HIP(c, launch_decode(d_pods + s0, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev,
-                                d_res + s0, s));
+        MS_HIP(c, decode_for(c, d_pods + s0, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev,
+                             d_res + s0, s));
     }
     return MS_OK;
 }
@@ -421,8 +435,15 @@ int ms_device_count(int *out) {
 int ms_create(const ms_config *cfg, ms_ctx **out) {
     if (!cfg || !out) return fail(nullptr, MS_E_INVAL, "ms_create: null argument");
     *out = nullptr;
-    if (cfg->plugin_set != MS_PLUGINS_NU_NN && cfg->plugin_set != MS_PLUGINS_NU_NRF_NN_LA)
+    if (cfg->plugin_set != MS_PLUGINS_NU_NN && cfg->plugin_set != MS_PLUGINS_NU_NRF_NN_LA &&
+        cfg->plugin_set != MS_PLUGINS_NU_NN_NA)
         return fail(nullptr, MS_E_INVAL, "ms_create: unknown plugin_set");
+    const uint32_t w0 = cfg->score_weight[0] ? cfg->score_weight[0] : 1u;
+    const uint32_t w1 = cfg->score_weight[1] ? cfg->score_weight[1] : 1u;
+    if (cfg->plugin_set != MS_PLUGINS_NU_NN_NA && (w0 != 1 || w1 != 1))
+        return fail(nullptr, MS_E_INVAL, "ms_create: score weights apply to MS_PLUGINS_NU_NN_NA only");
+    if (w0 * 10u + w1 * 100u >= 2048u)
+        return fail(nullptr, MS_E_INVAL, "ms_create: weighted score must stay below 2048 (packed key)");
     if (cfg->max_nodes == 0 || (uint64_t)cfg->node_base + cfg->max_nodes > (uint64_t)MS_MAX_ORDINAL + 1)
         return fail(nullptr, MS_E_INVAL, "ms_create: node range must be non-empty and end at or below 0xFFFFF");
     int ndev = 0;
@@ -440,6 +461,8 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     c->cfg = *cfg;
     if (c->cfg.max_batch == 0) c->cfg.max_batch = 1u << 16;
     c->num_cus = prop.multiProcessorCount;
+    c->w_nn = w0;
+    c->w_na = w1;
     c->batch_cap = c->cfg.max_batch;
     c->present.assign(cfg->max_nodes, 0);
 
@@ -458,6 +481,7 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     t.base = cfg->node_base;
     bool ok = hipMalloc((void **)&t.flags, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.digit, n + kColumnPad) == hipSuccess &&
+              hipMalloc((void **)&t.zone, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.alloc_cpu, n * 8) == hipSuccess &&
@@ -661,7 +685,7 @@ int ms_sweep_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint
                     void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !keys_dev))) return MS_E_INVAL;
     if (c->cfg.plugin_set != MS_PLUGINS_NU_NN && n_pods && !flags_dev)
-        return fail(c, MS_E_INVAL, "ms_sweep_device: flags required for the resource-aware plugin set");
+        return fail(c, MS_E_INVAL, "ms_sweep_device: flags required for the resource-aware / NodeAffinity plugin sets");
     if (n_pods == 0) return MS_OK;
     std::lock_guard<std::mutex> g(c->sched_mu);
     MS_HIP(c, hipSetDevice(c->cfg.device));
@@ -695,8 +719,10 @@ int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, con
                      const uint32_t *flags_dev, uint32_t present_nodes, ms_result *results_dev, void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !keys_dev || !results_dev))) return MS_E_INVAL;
     MS_HIP(c, hipSetDevice(c->cfg.device));
-    MS_HIP(c, launch_decode(pods_dev, n_pods, reinterpret_cast<const unsigned long long *>(keys_dev), flags_dev,
-                            present_nodes, results_dev, pick_stream(c, stream)));
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA && n_pods && !flags_dev)
+        return fail(c, MS_E_INVAL, "ms_decode_device: the NodeAffinity anchors (flags) are required for this plugin set");
+    MS_HIP(c, decode_for(c, pods_dev, n_pods, reinterpret_cast<const unsigned long long *>(keys_dev), flags_dev,
+                         present_nodes, results_dev, pick_stream(c, stream)));
     return MS_OK;
 }
 
@@ -707,6 +733,14 @@ int ms_decode_device_jobs(ms_ctx *c, uint32_t n_jobs, const ms_decode_job *jobs,
         if (jobs[i].n_pods && (!jobs[i].pods || !jobs[i].keys || !jobs[i].results)) return MS_E_INVAL;
     if (n_jobs == 0) return MS_OK;
     MS_HIP(c, hipSetDevice(c->cfg.device));
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {  // one launch per job
+        for (uint32_t i = 0; i < n_jobs; ++i) {
+            if (jobs[i].n_pods && !jobs[i].flags) return fail(c, MS_E_INVAL, "ms_decode_device_jobs: anchors required");
+            MS_HIP(c, decode_for(c, jobs[i].pods, jobs[i].n_pods, reinterpret_cast<const unsigned long long *>(jobs[i].keys),
+                                 jobs[i].flags, present_nodes, jobs[i].results, pick_stream(c, stream)));
+        }
+        return MS_OK;
+    }
     MS_HIP(c, launch_decode_jobs(jobs, n_jobs, present_nodes, pick_stream(c, stream)));
     return MS_OK;
 }

@@ -37,6 +37,7 @@ constexpr uint32_t kColumnPad = 64;
 struct NodeTable {
     uint8_t *flags;
     uint8_t *digit;
+    uint8_t *zone;  // zone label value id (MS_PLUGINS_NU_NN_NA), 0 = none
     int32_t *allowed_pods;
     int32_t *pod_count;
     int64_t *alloc_cpu, *alloc_mem;
@@ -59,6 +60,7 @@ enum : uint32_t {
     kPlaneD3,
     kPlaneSched,    // present && !Spec.Unschedulable
     kPlanePresent,  // present (not tombstoned)
+    kPlaneOver,     // 1 if the group holds more than 3 present rows of one digit (K1 pp's scan path)
     kPlanes
 };
 
@@ -138,6 +140,18 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
 constexpr uint32_t kPpMaxFusedRows = 16u * 64u * 4u * kGroupRows;
 // Rebuilds the bit planes of the groups touched by deltas (or all groups when d_deltas is null).
 hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
+// MS_PLUGINS_NU_NN_NA sweep (one pair per lane-slot): keys[i] = max packed key
+// with raw NodeAffinity scores, fkeys[i] = max over this shard's feasible nodes
+// with a non-zero raw NodeAffinity score of ((0xFFFFF - ordinal) << 1 | NN
+// match) + 1, i.e. the normalise hook's anchor (the first such node in LIST
+// order); both atomicMax targets, zeroed by the caller. w: score weights.
+hipError_t launch_sweep_na(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           uint32_t seed32, uint32_t w_nn, uint32_t w_na, unsigned long long *keys, uint32_t *fkeys,
+                           int num_cus, hipStream_t s);
+// decode of the NU+NN+NA set: the anchor's score becomes w_na * 100
+hipError_t launch_decode_na(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
+                            const uint32_t *fkeys, uint32_t present_nodes, uint32_t seed32, uint32_t w_nn,
+                            uint32_t w_na, ms_result *out, hipStream_t s);
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s);

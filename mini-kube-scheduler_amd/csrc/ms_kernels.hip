@@ -1595,6 +1595,7 @@ __global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uin
     if (x.absent) {
         t.flags[r] = kNodeAbsent;
         t.digit[r] = 0xFF;
+        t.zone[r] = 0;
         t.allowed_pods[r] = 0;
         t.pod_count[r] = 0;
         t.alloc_cpu[r] = t.alloc_mem[r] = 0;
@@ -1604,6 +1605,7 @@ __global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uin
     }
     t.flags[r] = x.rec.unschedulable ? kNodeUnschedulable : 0;
     t.digit[r] = x.rec.name_digit <= 9 ? x.rec.name_digit : 0xFF;
+    t.zone[r] = x.rec.zone;
     t.allowed_pods[r] = x.rec.allowed_pods;
     t.pod_count[r] = x.rec.pod_count;
     t.alloc_cpu[r] = x.rec.alloc_milli_cpu;
@@ -1619,6 +1621,7 @@ __global__ void k_init_table(NodeTable t) {
     if (r >= t.cap) return;
     t.flags[r] = kNodeAbsent;
     t.digit[r] = 0xFF;
+    t.zone[r] = 0;
     t.allowed_pods[r] = 0;
     t.pod_count[r] = 0;
     t.alloc_cpu[r] = t.alloc_mem[r] = 0;
@@ -1634,6 +1637,7 @@ __global__ void k_read_rows(NodeTable t, uint32_t first, uint32_t n, ms_node_rec
     const uint8_t f = t.flags[r];
     x.unschedulable = (f & kNodeUnschedulable) ? 1 : 0;
     x.name_digit = t.digit[r];
+    x.zone = t.zone[r];
     x.allowed_pods = (f & kNodeAbsent) ? -1 : t.allowed_pods[r];
     x.pod_count = t.pod_count[r];
     x.alloc_milli_cpu = t.alloc_cpu[r];
@@ -1643,6 +1647,78 @@ __global__ void k_read_rows(NodeTable t, uint32_t first, uint32_t n, ms_node_rec
     x.nonzero_milli_cpu = t.nz_cpu[r];
     x.nonzero_memory = t.nz_mem[r];
     out[i] = x;
+}
+
+// ----------------------------------------------------------------------------
+// MS_PLUGINS_NU_NN_NA: Filter[NU]; Score[NodeNumber, NodeAffinity preferred term]
+// with NodeAffinity's DefaultNormalizeScore(100, reverse=false) run by
+// RunScorePlugins after every node on the whole, partially filled list
+// (minisched.go:164-185). For raw scores <= 100 that in-loop hook leaves every
+// entry at its raw score except the first feasible node in LIST order with a
+// non-zero raw score (the anchor), which ends at 100: after the first non-zero
+// entry the list maximum is 100 and every later normalisation is the
+// identity (oracle/ms_oracle.c msor_schedule_na checks the closed form against
+// the loop as written). So per pod the sweep keeps (a) the max packed key with
+// raw NodeAffinity scores and (b) the anchor as a min-ordinal reduction; the
+// decode takes max(a, key of the anchor scored w_nn*NN + w_na*100). The
+// anchor's raw key never beats its boosted key, so including it in (a) is
+// harmless. One pair per lane-slot, plain per-pair evaluation.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(kNunnThreads) void k_sweep_na(
+    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, const uint8_t *__restrict__ nzone,
+    uint32_t n_rows, uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
+    uint32_t seed32, uint32_t w_nn, uint32_t w_na, u64 *__restrict__ keys, uint32_t *__restrict__ fkeys) {
+    const uint32_t row0 = blockIdx.x * kNunnTile + threadIdx.x * kNunnSlots;
+    uint8_t fl[kNunnSlots], dg[kNunnSlots], zn[kNunnSlots];
+#pragma unroll
+    for (int i = 0; i < kNunnSlots; ++i) {
+        const uint32_t r = row0 + i;
+        fl[i] = r < n_rows ? nflags[r] : kNodeAbsent;
+        dg[i] = r < n_rows ? ndigit[r] : 0xFF;
+        zn[i] = r < n_rows ? nzone[r] : 0;
+    }
+    const uint32_t pbeg = blockIdx.y * chunk;
+    const uint32_t pend = min(n_pods, pbeg + chunk);
+    for (uint32_t p = pbeg; p < pend; ++p) {
+        const ms_pod_rec pr = pods[p];  // wave-uniform
+        const uint32_t A = tb_pod(seed32, pr.ordinal);
+        u64 best = 0;
+        uint32_t anchor = 0;
+#pragma unroll
+        for (int i = 0; i < kNunnSlots; ++i) {
+            const bool feas = !(fl[i] & kNodeAbsent) && !((fl[i] & kNodeUnschedulable) && !pr.tolerates_unschedulable);
+            const uint32_t ord = node_base + row0 + i;
+            const uint32_t nn = ((int)dg[i] == (int)pr.name_digit) ? 1u : 0u;
+            const uint32_t raw = (pr.pref_zone != 0 && zn[i] == pr.pref_zone) ? pr.pref_weight : 0u;
+            const u64 key = make_key(w_nn * 10u * nn + w_na * raw, tb_hash(A, ord), ord);
+            best = feas ? umax64(best, key) : best;
+            const uint32_t a = (((0xFFFFFu - ord) << 1) | nn) + 1u;
+            anchor = (feas && raw) ? max(anchor, a) : anchor;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            best = umax64(best, __shfl_xor(best, off, 64));
+            anchor = max(anchor, (uint32_t)__shfl_xor(anchor, off, 64));
+        }
+        if ((threadIdx.x & 63u) == 0u) {
+            if (best) atomicMax(&keys[p], best);
+            if (anchor) atomicMax(&fkeys[p], anchor);
+        }
+    }
+}
+
+__global__ void k_decode_na(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const u64 *__restrict__ keys,
+                            const uint32_t *__restrict__ fkeys, uint32_t present, uint32_t seed32, uint32_t w_nn,
+                            uint32_t w_na, ms_result *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pods) return;
+    u64 k = keys[i];
+    const uint32_t a = fkeys[i];
+    if (a) {  // the normalise anchor, scored w_nn * NN + w_na * 100
+        const uint32_t ord = 0xFFFFFu - ((a - 1u) >> 1), nn = (a - 1u) & 1u;
+        k = umax64(k, make_key(w_nn * 10u * nn + w_na * 100u, tb_hash(tb_pod(seed32, pods[i].ordinal), ord), ord));
+    }
+    out[i] = decode_key(k, pods[i].name_digit, nullptr, 0, present);
 }
 
 inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -1786,7 +1862,11 @@ static hipError_t launch_v8(const NodeTable &t, uint32_t n_rows, uint32_t rpl, c
     // resident workgroups: 8 waves per SIMD, 4 SIMDs per CU (the occupancy API
     // under-reports kernels with scratch; MINISCHED_K1_DEBUG prints both)
     const uint32_t per_cu = std::max<uint32_t>((uint32_t)bpc, 32u / W);
-    const uint32_t blocks = std::min(items, per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256));
+    // at least one workgroup per column: workgroup b serves column b % n_cols only, so
+    // fewer blocks than columns would leave columns unswept (small CU counts, many rows)
+    uint32_t blocks = std::min(items, per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256));
+    if (const char *c = getenv("MINISCHED_K1_V8_BLOCKS")) blocks = (uint32_t)std::max(1, atoi(c));  // tests
+    blocks = std::max(blocks, std::min(items, n_cols));
     if (getenv("MINISCHED_K1_DEBUG"))
         fprintf(stderr, "k1 v8: api blocks/CU %d, used %u, cols %u, items %u, blocks %u, chunk %u\n", bpc, per_cu,
                 n_cols, items, blocks, chunk);
@@ -1836,6 +1916,26 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
                      : launch_v8_rows<false>(t, n_rows, pstream, n_pods, keys, flags, work, num_cus, s);
     return flags ? launch_v7_rows<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
                  : launch_v7_rows<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
+}
+
+hipError_t launch_sweep_na(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           uint32_t seed32, uint32_t w_nn, uint32_t w_na, unsigned long long *keys, uint32_t *fkeys,
+                           int num_cus, hipStream_t s) {
+    if (n_pods == 0 || n_rows == 0) return hipSuccess;
+    const uint32_t gx = cdiv(n_rows, kNunnTile);
+    const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
+    hipLaunchKernelGGL(k_sweep_na, dim3(gx, cdiv(n_pods, chunk)), dim3(kNunnThreads), 0, s, t.flags, t.digit, t.zone,
+                       n_rows, t.base, pods, n_pods, chunk, seed32, w_nn, w_na, keys, fkeys);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_na(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
+                            const uint32_t *fkeys, uint32_t present_nodes, uint32_t seed32, uint32_t w_nn,
+                            uint32_t w_na, ms_result *out, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_na, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, pods, n_pods, keys, fkeys,
+                       present_nodes, seed32, w_nn, w_na, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,

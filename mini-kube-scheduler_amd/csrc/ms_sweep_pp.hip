@@ -242,12 +242,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
         W[k].pres = in ? planes[kPlanePresent * gstride + g] : 0u;
         W[k].hb = (node_base + g * kGroupRows) * kG24;
         // more than 3 present rows of one digit in a group: the fast slots cannot hold them
-#pragma unroll
-        for (int d = 0; d < 10; ++d) {
-            const uint32_t m = W[k].pres & ((d & 1) ? W[k].d0 : ~W[k].d0) & ((d & 2) ? W[k].d1 : ~W[k].d1) &
-                               ((d & 4) ? W[k].d2 : ~W[k].d2) & ((d & 8) ? W[k].d3 : ~W[k].d3);
-            over = over || __popc(m) > 3;
-        }
+        over = over || (in && planes[kPlaneOver * gstride + g] != 0u);
     }
     const bool gen = __ballot(over) != 0;
     __syncthreads();
@@ -301,7 +296,15 @@ __device__ __forceinline__ void build_group(const NodeTable &t, uint32_t g) {
             if (!(f & kNodeUnschedulable)) sched |= 1u << s;
         }
     }
+    uint32_t over = 0;
+#pragma unroll
+    for (int v = 0; v < 10; ++v) {
+        const uint32_t m = pres & ((v & 1) ? d[0] : ~d[0]) & ((v & 2) ? d[1] : ~d[1]) & ((v & 4) ? d[2] : ~d[2]) &
+                           ((v & 8) ? d[3] : ~d[3]);
+        over |= __popc(m) > 3 ? 1u : 0u;
+    }
     const uint32_t st = t.gcap;
+    t.planes[kPlaneOver * st + g] = over;
     t.planes[kPlaneD0 * st + g] = d[0];
     t.planes[kPlaneD1 * st + g] = d[1];
     t.planes[kPlaneD2 * st + g] = d[2];

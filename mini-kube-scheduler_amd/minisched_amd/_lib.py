@@ -23,6 +23,7 @@ MS_OK = 0
 MS_E_INVAL, MS_E_HIP, MS_E_RCCL, MS_E_OOM, MS_E_CAPACITY, MS_E_NODEV = -1, -2, -3, -4, -5, -6
 PLUGINS_NU_NN = 0
 PLUGINS_NU_NRF_NN_LA = 1
+PLUGINS_NU_NN_NA = 2
 MODE_BATCHED = 0
 MODE_SEQUENTIAL = 1
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE = 0, 1, 2
@@ -44,7 +45,8 @@ NODE_REC = np.dtype(
     [
         ("unschedulable", "u1"),
         ("name_digit", "u1"),
-        ("_pad0", "u1", (2,)),
+        ("zone", "u1"),
+        ("_pad0", "u1"),
         ("allowed_pods", "<i4"),
         ("pod_count", "<i4"),
         ("_pad1", "<i4"),
@@ -61,7 +63,8 @@ POD_REC = np.dtype(
         ("ordinal", "<u4"),
         ("name_digit", "i1"),
         ("tolerates_unschedulable", "u1"),
-        ("_pad", "u1", (2,)),
+        ("pref_zone", "u1"),
+        ("pref_weight", "u1"),
         ("req_milli_cpu", "<i8"),
         ("req_memory", "<i8"),
         ("nonzero_milli_cpu", "<i8"),
@@ -81,7 +84,7 @@ class ms_config(ctypes.Structure):
         ("max_nodes", ctypes.c_uint32),
         ("node_base", ctypes.c_uint32),
         ("max_batch", ctypes.c_uint32),
-        ("_reserved", ctypes.c_uint32),
+        ("score_weight", ctypes.c_uint16 * 2),
         ("seed", ctypes.c_uint64),
     ]
 
@@ -195,9 +198,10 @@ class Engine:
         seed: int = 1,
         device: int = 0,
         max_batch: int = 1 << 16,
+        score_weights=(0, 0),
     ):
         self.lib = load()
-        cfg = ms_config(device, plugin_set, max_nodes, node_base, max_batch, 0, seed)
+        cfg = ms_config(device, plugin_set, max_nodes, node_base, max_batch, (ctypes.c_uint16 * 2)(*score_weights), seed)
         h = ctypes.c_void_p()
         rc = self.lib.ms_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != MS_OK:

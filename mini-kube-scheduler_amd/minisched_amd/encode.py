@@ -8,18 +8,23 @@ Only the fields the in-scope plugins read cross the boundary:
                   (k8s@v1.22.0 nodeunschedulable, restated).
   * requests    — Fit PreFilter computePodResourceRequest and
                   NodeInfo.calculateResource / GetNonzeroRequests (k8s@v1.22.0).
+  * zone / pref_zone, pref_weight — MS_PLUGINS_NU_NN_NA: the node's
+                  topology.kubernetes.io/zone label and the pod's one preferred
+                  NodeAffinity term {weight, zone In [value]}, as value ids that
+                  one ZoneIds table assigns on both sides (0 = none).
 Quantities are already integers here: cpu in millicores, memory in bytes.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
 from ._lib import NODE_REC, POD_REC
 
 TAINT_NODE_UNSCHEDULABLE = "node.kubernetes.io/unschedulable"
+ZONE_LABEL = "topology.kubernetes.io/zone"
 TAINT_EFFECT_NO_SCHEDULE = "NoSchedule"
 DEFAULT_MILLI_CPU_REQUEST = 100
 DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
@@ -73,6 +78,8 @@ class Pod:
     containers: List[Container] = field(default_factory=list)
     init_containers: List[Container] = field(default_factory=list)
     overhead: Optional[Dict[str, int]] = None
+    # one PreferredSchedulingTerm: (zone label value, weight 1..100)
+    preferred_zone: Optional[Tuple[str, int]] = None
 
 
 @dataclass
@@ -80,6 +87,23 @@ class Node:
     name: str
     unschedulable: bool = False
     allocatable: Dict[str, int] = field(default_factory=dict)  # cpu (milli), memory (bytes), pods
+    labels: Dict[str, str] = field(default_factory=dict)
+
+
+class ZoneIds:
+    """Label value -> id 1..255, shared by node and pod encoding (the shim's map)."""
+
+    def __init__(self):
+        self.ids: Dict[str, int] = {}
+
+    def __call__(self, value: Optional[str]) -> int:
+        if value is None:
+            return 0
+        if value not in self.ids:
+            if len(self.ids) >= 255:
+                raise ValueError("more than 255 zone label values")
+            self.ids[value] = len(self.ids) + 1
+        return self.ids[value]
 
 
 def pod_requests(p: Pod):
@@ -107,9 +131,15 @@ def pod_requests(p: Pod):
     return rc, rm, nc, nm
 
 
-def pod_records(pods: List[Pod]) -> np.ndarray:
+def pod_records(pods: List[Pod], zone_ids: Optional[ZoneIds] = None) -> np.ndarray:
     rec = np.zeros(len(pods), dtype=POD_REC)
     for i, p in enumerate(pods):
+        if p.preferred_zone is not None:
+            zone, weight = p.preferred_zone
+            if not 1 <= weight <= 100:
+                raise ValueError("PreferredSchedulingTerm weight must be in 1..100 (API validation)")
+            rec[i]["pref_zone"] = (zone_ids or ZoneIds())(zone)
+            rec[i]["pref_weight"] = weight
         rc, rm, nc, nm = pod_requests(p)
         rec[i]["ordinal"] = p.ordinal
         rec[i]["name_digit"] = name_digit(p.name)
@@ -119,9 +149,11 @@ def pod_records(pods: List[Pod]) -> np.ndarray:
     return rec
 
 
-def node_records(nodes: List[Node]) -> np.ndarray:
+def node_records(nodes: List[Node], zone_ids: Optional[ZoneIds] = None) -> np.ndarray:
     rec = np.zeros(len(nodes), dtype=NODE_REC)
     for i, n in enumerate(nodes):
+        if ZONE_LABEL in n.labels:
+            rec[i]["zone"] = (zone_ids or ZoneIds())(n.labels[ZONE_LABEL])
         d = name_digit(n.name)
         rec[i]["unschedulable"] = 1 if n.unschedulable else 0
         rec[i]["name_digit"] = d if d >= 0 else 0xFF

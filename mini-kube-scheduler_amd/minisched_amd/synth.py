@@ -25,6 +25,8 @@ GiB = 1 << 30
 
 # column streams
 S_NODE_UNSCHED, S_POD_TOL, S_NODE_CPU, S_NODE_MEM, S_POD_NOREQ, S_POD_CPU, S_POD_MEM = 1, 2, 3, 4, 5, 6, 7
+S_NODE_ZONE, S_POD_ZONE, S_POD_ZWEIGHT = 8, 9, 10
+N_ZONES = 8
 
 DEFAULT_MILLI_CPU_REQUEST = 100  # k8s@v1.22.0 pkg/scheduler/util/non_zero.go
 DEFAULT_MEMORY_REQUEST = 200 * MiB
@@ -44,8 +46,9 @@ def stream_u64(seed: int, stream: int, start: int, n: int) -> np.ndarray:
         return mix64(state + k * GOLDEN)
 
 
-def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False) -> np.ndarray:
-    """Node records for ordinals [start, start+n)."""
+def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False) -> np.ndarray:
+    """Node records for ordinals [start, start+n). zones: topology zone labels
+    for MS_PLUGINS_NU_NN_NA (value ids 1..8, 5 % of nodes unlabelled)."""
     rec = np.zeros(n, dtype=NODE_REC)
     i = np.arange(start, start + n, dtype=np.int64)
     rec["name_digit"] = (i % 10).astype(np.uint8)
@@ -58,11 +61,15 @@ def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False) -> np.
         mem = np.array([2, 4, 8, 16], dtype=np.int64) * GiB
         rec["alloc_milli_cpu"] = cpu[(stream_u64(seed, S_NODE_CPU, start, n) % np.uint64(4)).astype(np.int64)]
         rec["alloc_memory"] = mem[(stream_u64(seed, S_NODE_MEM, start, n) % np.uint64(4)).astype(np.int64)]
+    if zones:
+        u = stream_u64(seed, S_NODE_ZONE, start, n)
+        rec["zone"] = np.where(u % np.uint64(100) < np.uint64(5), 0, 1 + (u >> np.uint64(8)) % np.uint64(N_ZONES))
     return rec
 
 
-def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False) -> np.ndarray:
-    """Pod records for ordinals [start, start+n)."""
+def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False) -> np.ndarray:
+    """Pod records for ordinals [start, start+n). zones: 70 % of pods carry one
+    preferred zone term (zone 1..8, weight 1..100) for MS_PLUGINS_NU_NN_NA."""
     rec = np.zeros(n, dtype=POD_REC)
     j = np.arange(start, start + n, dtype=np.int64)
     rec["ordinal"] = j.astype(np.uint32)
@@ -78,6 +85,11 @@ def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False) -> np.n
         rec["req_memory"] = np.where(noreq, 0, mem)
         rec["nonzero_milli_cpu"] = np.where(noreq, DEFAULT_MILLI_CPU_REQUEST, cpu)
         rec["nonzero_memory"] = np.where(noreq, DEFAULT_MEMORY_REQUEST, mem)
+    if zones:
+        u = stream_u64(seed, S_POD_ZONE, start, n)
+        w = stream_u64(seed, S_POD_ZWEIGHT, start, n)
+        rec["pref_zone"] = np.where(u % np.uint64(10) < np.uint64(7), 1 + (u >> np.uint64(8)) % np.uint64(N_ZONES), 0)
+        rec["pref_weight"] = np.where(rec["pref_zone"] > 0, 1 + w % np.uint64(100), 0)
     return rec
 
 

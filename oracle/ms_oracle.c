@@ -302,3 +302,103 @@ int msor_schedule_nunn_names(const char *const *node_names, const uint8_t *node_
     free(list);
     return 0;
 }
+
+/* ---- NodeAffinity (preferred terms) + the in-loop normalise hook ---------- */
+
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/helper/normalize_score.go
+ * DefaultNormalizeScore: maxCount = max score; 0 -> (reverse: all maxPriority)
+ * unchanged; else score = maxPriority * score / maxCount, reversed as
+ * maxPriority - score. */
+void msor_default_normalize(int64_t max_priority, int reverse, int64_t *scores, uint32_t n) {
+    int64_t max_count = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (scores[i] > max_count) max_count = scores[i];
+    if (max_count == 0) {
+        if (reverse)
+            for (uint32_t i = 0; i < n; ++i) scores[i] = max_priority;
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        int64_t sc = max_priority * scores[i] / max_count;
+        if (reverse) sc = max_priority - sc;
+        scores[i] = sc;
+    }
+}
+
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/nodeaffinity/node_affinity.go
+ * Score: the sum of the weights of the pod's PreferredSchedulingTerms whose
+ * selector matches the node; here one term {weight, zone In [pref_zone]}. */
+static int64_t na_raw(const msor_nodes *nd, uint32_t i, const msor_pods *pd, uint32_t j) {
+    const uint8_t z = pd->pref_zone[j];
+    return (z != 0 && nd->zone[i] == z) ? (int64_t)pd->pref_weight[j] : 0;
+}
+
+int msor_schedule_na(const msor_nodes *nd, const msor_pods *pd, int64_t w_nn, int64_t w_na, int literal,
+                     uint64_t seed, uint32_t node_base, int32_t *out_node, int64_t *out_score,
+                     int32_t *out_code, uint32_t *out_mask, uint64_t *out_key) {
+    if (!nd || !pd || !nd->flags || !nd->digit || !nd->zone || !pd->ordinal || !pd->digit || !pd->tol ||
+        !pd->pref_zone || !pd->pref_weight)
+        return -1;
+    if ((uint64_t)node_base + nd->n >= 0xFFFFFu) return -1;
+    uint32_t *feas = (uint32_t *)malloc(sizeof(uint32_t) * (nd->n ? nd->n : 1));
+    int64_t *nn = (int64_t *)malloc(sizeof(int64_t) * (nd->n ? nd->n : 1));
+    int64_t *na = (int64_t *)malloc(sizeof(int64_t) * (nd->n ? nd->n : 1));
+    if (!feas || !nn || !na) { free(feas); free(nn); free(na); return -1; }
+    for (uint32_t j = 0; j < pd->n; ++j) {
+        /* RunFilterPlugins (minisched.go:115-151): NodeUnschedulable only */
+        uint32_t F = 0, mask = 0;
+        for (uint32_t i = 0; i < nd->n; ++i) {
+            if (nd->flags[i] & MSOR_NODE_ABSENT) continue;
+            if (nu_rejects(nd->flags[i], pd->tol[j])) { mask |= MSOR_MASK_NU; continue; }
+            feas[F++] = i;
+        }
+        int32_t node = -1, code;
+        int64_t score = 0;
+        uint64_t best = 0;
+        if (F == 0) {
+            code = MSOR_CODE_UNSCHEDULABLE;
+        } else if (pd->digit[j] < 0) { /* NodeNumber.Score fails at the first node (:170-172) */
+            code = MSOR_CODE_ERROR;
+            mask = 0;
+            best = 1; /* any non-zero key: F > 0 */
+        } else {
+            /* RunScorePlugins (minisched.go:164-185): createPluginToNodeScores
+             * zero-fills both lists (:327-334); for each feasible node in order,
+             * NodeNumber then NodeAffinity score it, and NodeAffinity's
+             * NormalizeScore runs on its whole list right away (:178-183). */
+            memset(na, 0, sizeof(int64_t) * F);
+            int first = -1;
+            for (uint32_t k = 0; k < F; ++k) {
+                nn[k] = nn_score(pd->digit[j], nd->digit[feas[k]]);
+                na[k] = na_raw(nd, feas[k], pd, j);
+                if (literal) {
+                    msor_default_normalize(100, 0, na, k + 1); /* entries > k are still 0 */
+                } else if (first < 0 && na[k] > 0) {
+                    first = (int)k;
+                }
+            }
+            if (!literal && first >= 0) na[first] = 100;
+            /* sum (:187-196), weights applied; selectHost (:304-325) */
+            const uint32_t ph = msor_pod_hash(seed, pd->ordinal[j]);
+            for (uint32_t k = 0; k < F; ++k) {
+                const uint32_t ord = node_base + feas[k];
+                const uint64_t key = msor_key(w_nn * nn[k] + w_na * na[k], msor_tb_hash(ph, ord), ord);
+                if (key > best) best = key;
+            }
+            code = MSOR_CODE_SUCCESS;
+            mask = 0;
+            node = (int32_t)(0xFFFFFu - (uint32_t)(best & 0xFFFFFu));
+            score = (int64_t)(best >> 52);
+        }
+        if (code == MSOR_CODE_ERROR) best = 0, node = -1;
+        if (out_node) out_node[j] = node;
+        if (out_score) out_score[j] = score;
+        if (out_code) out_code[j] = code;
+        if (out_mask) out_mask[j] = code == MSOR_CODE_UNSCHEDULABLE ? mask : 0;
+        if (out_key) out_key[j] = best;
+    }
+    free(feas);
+    free(nn);
+    free(na);
+    return 0;
+}

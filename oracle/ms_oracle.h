@@ -26,6 +26,7 @@ extern "C" {
 /* plugin sets (same numbering as include/minisched_gpu.h) */
 #define MSOR_PLUGINS_NU_NN 0        /* Filter[NodeUnschedulable], Score[NodeNumber]          */
 #define MSOR_PLUGINS_NU_NRF_NN_LA 1 /* Filter[NU, NodeResourcesFit], Score[NN, LeastAllocated] */
+#define MSOR_PLUGINS_NU_NN_NA 2     /* Filter[NU], Score[NN, NodeAffinity + DefaultNormalizeScore] */
 
 #define MSOR_MODE_BATCHED 0    /* every pod against the same node state          */
 #define MSOR_MODE_SEQUENTIAL 1 /* queue order, assume-on-select NodeInfo.AddPod   */
@@ -49,6 +50,7 @@ typedef struct {
     int64_t *alloc_cpu, *alloc_mem; /* Allocatable.MilliCPU / .Memory              */
     int64_t *req_cpu, *req_mem;     /* Requested.MilliCPU / .Memory                */
     int64_t *nz_cpu, *nz_mem;       /* NonZeroRequested.MilliCPU / .Memory         */
+    const uint8_t *zone;            /* zone label value id, 0 = none (NU_NN_NA)   */
 } msor_nodes;
 
 typedef struct {
@@ -57,6 +59,7 @@ typedef struct {
     const int8_t *digit;     /* last char of pod name as 0..9, -1 = non-digit     */
     const uint8_t *tol;      /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
     const int64_t *req_cpu, *req_mem, *nz_cpu, *nz_mem; /* may be NULL for NU_NN */
+    const uint8_t *pref_zone, *pref_weight; /* one preferred zone term (NU_NN_NA)  */
 } msor_pods;
 
 uint32_t msor_fmix32(uint32_t h);
@@ -98,6 +101,23 @@ int msor_schedule_nunn_names(const char *const *node_names, const uint8_t *node_
                              const uint8_t *pod_tol, const uint32_t *pod_ordinal,
                              uint32_t n_pods, uint64_t seed, int32_t *out_node,
                              int64_t *out_score, int32_t *out_code, uint32_t *out_mask);
+
+/* MSOR_PLUGINS_NU_NN_NA, batched (no mutable state: sequential is the same).
+ * Score plugins in order [NodeNumber (weight w_nn), NodeAffinity preferred
+ * term (weight w_na)]; NodeAffinity's ScoreExtensions is upstream
+ * DefaultNormalizeScore(MaxNodeScore=100, reverse=false), which
+ * RunScorePlugins calls on the WHOLE, partially filled list after every node
+ * (minisched.go:164-185). literal=1 runs that loop as written (O(F^2) per
+ * pod); literal=0 uses its closed form for raw scores <= 100: every entry
+ * keeps its raw score except the first feasible node (LIST order) with a
+ * non-zero raw score, which ends at 100. Weights: total = w_nn*NN + w_na*NA
+ * (the reference's sum is unweighted, minisched.go:186; 1/1 reproduces it). */
+int msor_schedule_na(const msor_nodes *nodes, const msor_pods *pods, int64_t w_nn, int64_t w_na, int literal,
+                     uint64_t seed, uint32_t node_base, int32_t *out_node, int64_t *out_score,
+                     int32_t *out_code, uint32_t *out_mask, uint64_t *out_key);
+
+/* upstream k8s@v1.22.0 pkg/scheduler/framework/plugins/helper/normalize_score.go */
+void msor_default_normalize(int64_t max_priority, int reverse, int64_t *scores, uint32_t n);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "libmsoracle.so")
 
-PLUGINS_NU_NN, PLUGINS_NU_NRF_NN_LA = 0, 1
+PLUGINS_NU_NN, PLUGINS_NU_NRF_NN_LA, PLUGINS_NU_NN_NA = 0, 1, 2
 MODE_BATCHED, MODE_SEQUENTIAL = 0, 1
 
 
@@ -33,13 +33,15 @@ class msor_nodes(ctypes.Structure):
             "req_mem",
             "nz_cpu",
             "nz_mem",
+            "zone",
         )
     ]
 
 
 class msor_pods(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32)] + [
-        (f, ctypes.c_void_p) for f in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem")
+        (f, ctypes.c_void_p)
+        for f in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem", "pref_zone", "pref_weight")
     ]
 
 
@@ -81,6 +83,18 @@ def lib():
             ctypes.c_uint32,
             ctypes.c_int,
         ] + [ctypes.c_void_p] * 5
+        L.msor_schedule_na.restype = ctypes.c_int
+        L.msor_schedule_na.argtypes = [
+            ctypes.POINTER(msor_nodes),
+            ctypes.POINTER(msor_pods),
+            ctypes.c_int64,
+            ctypes.c_int64,
+            ctypes.c_int,
+            ctypes.c_uint64,
+            ctypes.c_uint32,
+        ] + [ctypes.c_void_p] * 5
+        L.msor_default_normalize.restype = None
+        L.msor_default_normalize.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32]
         L.msor_schedule_nunn_names.restype = ctypes.c_int
         L.msor_schedule_nunn_names.argtypes = [
             ctypes.POINTER(ctypes.c_char_p),
@@ -120,6 +134,7 @@ class NodeCols:
         self.req_mem = _col(recs["req_memory"], np.int64)
         self.nz_cpu = _col(recs["nonzero_milli_cpu"], np.int64)
         self.nz_mem = _col(recs["nonzero_memory"], np.int64)
+        self.zone = _col(recs["zone"], np.uint8)
 
     def struct(self):
         return msor_nodes(
@@ -137,6 +152,7 @@ class NodeCols:
                     "req_mem",
                     "nz_cpu",
                     "nz_mem",
+                    "zone",
                 )
             ],
         )
@@ -151,8 +167,11 @@ def _pod_cols(pods):
         req_mem=_col(pods["req_memory"], np.int64),
         nz_cpu=_col(pods["nonzero_milli_cpu"], np.int64),
         nz_mem=_col(pods["nonzero_memory"], np.int64),
+        pref_zone=_col(pods["pref_zone"], np.uint8),
+        pref_weight=_col(pods["pref_weight"], np.uint8),
     )
-    st = msor_pods(len(pods), *[_p(cols[k]) for k in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem")])
+    st = msor_pods(len(pods), *[_p(cols[k]) for k in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem",
+                                                      "pref_zone", "pref_weight")])
     return cols, st
 
 
@@ -180,6 +199,28 @@ def schedule(node_recs, pods, plugin_set=PLUGINS_NU_NN, mode=MODE_BATCHED, seed=
     assert rc == 0, "oracle rejected its arguments"
     o["cols"] = cols
     return o
+
+
+def schedule_na(node_recs, pods, weights=(1, 1), literal=True, seed=1, node_base=0):
+    """MSOR_PLUGINS_NU_NN_NA (batched): literal=True runs RunScorePlugins' in-loop
+    NormalizeScore as written (O(F^2) per pod), False its closed form."""
+    L = lib()
+    cols = NodeCols(node_recs)
+    nst = cols.struct()
+    pc, pst = _pod_cols(pods)
+    o = _outs(len(pods))
+    rc = L.msor_schedule_na(
+        ctypes.byref(nst), ctypes.byref(pst), int(weights[0]), int(weights[1]), 1 if literal else 0, seed, node_base,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),
+    )
+    assert rc == 0, "oracle rejected its arguments"
+    return o
+
+
+def default_normalize(scores, max_priority=100, reverse=False):
+    a = np.ascontiguousarray(scores, dtype=np.int64).copy()
+    lib().msor_default_normalize(max_priority, 1 if reverse else 0, _p(a), len(a))
+    return a
 
 
 def schedule_batched_commit(node_recs, pods, plugin_set, seed=1, node_base=0):

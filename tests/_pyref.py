@@ -7,7 +7,7 @@ Test infrastructure, never product code.
 """
 from __future__ import annotations
 
-from minisched_amd.encode import name_digit, pod_requests, tolerates_unschedulable
+from minisched_amd.encode import ZONE_LABEL, name_digit, pod_requests, tolerates_unschedulable
 
 MASK_NU, MASK_NRF = 1, 2
 
@@ -126,4 +126,57 @@ def schedule(nodes, pods, resources=False, sequential=False, seed=1):
             st.nz_cpu += nc
             st.nz_mem += nm
             st.pods += 1
+    return out
+
+
+def default_normalize_score(max_priority, reverse, scores):
+    """k8s@v1.22.0 pkg/scheduler/framework/plugins/helper/normalize_score.go, in place."""
+    max_count = max([s for s in scores] + [0])
+    if max_count == 0:
+        if reverse:
+            for i in range(len(scores)):
+                scores[i] = max_priority
+        return
+    for i in range(len(scores)):
+        sc = max_priority * scores[i] // max_count
+        scores[i] = max_priority - sc if reverse else sc
+
+
+def schedule_na(nodes, pods, weights=(1, 1), seed=1):
+    """MS_PLUGINS_NU_NN_NA on v1-style objects, minisched.go:164-199 as written:
+    createPluginToNodeScores zero-fills one list per plugin; for each feasible
+    node, NodeNumber then NodeAffinity score it and NodeAffinity's
+    NormalizeScore (DefaultNormalizeScore(100, false)) runs on its whole list
+    right away; then the (here weighted) sum and selectHost."""
+    out = []
+    for pod in pods:
+        tol = tolerates_unschedulable(pod.tolerations)
+        feasible, plugins = [], 0
+        for i, n in enumerate(nodes):
+            if n.unschedulable and not tol:
+                plugins |= MASK_NU
+                continue
+            feasible.append(i)
+        if not feasible:
+            out.append((2, -1, 0, plugins))
+            continue
+        podnum = name_digit(pod.name)
+        if podnum < 0:
+            out.append((1, -1, 0, 0))
+            continue
+        nn = [0] * len(feasible)
+        na = [0] * len(feasible)
+        for k, i in enumerate(feasible):
+            d = name_digit(nodes[i].name)
+            nn[k] = 10 if (d >= 0 and d == podnum) else 0
+            pz = pod.preferred_zone
+            na[k] = pz[1] if (pz is not None and nodes[i].labels.get(ZONE_LABEL) == pz[0]) else 0
+            default_normalize_score(100, False, na)
+        total = [weights[0] * a + weights[1] * b for a, b in zip(nn, na)]
+        best, best_k = -1, -1
+        for k, i in enumerate(feasible):
+            kk = key(total[k], h32(seed, pod.ordinal, i), i)
+            if kk > best:
+                best, best_k = kk, k
+        out.append((0, feasible[best_k], total[best_k], 0))
     return out

@@ -55,16 +55,16 @@ def test_struct_sizes_match_header():
 
 def test_abi_version_and_no_device_error_path():
     lib = _lib.load()
-    assert lib.ms_abi_version() == 1
+    assert lib.ms_abi_version() == 2
     if _lib.device_count() > 0:
         pytest.skip("a device is visible; the no-device path is exercised on CPU hosts")
-    cfg = _lib.ms_config(0, 0, 16, 0, 64, 0, 1)
+    cfg = _lib.ms_config(0, 0, 16, 0, 64, (ctypes.c_uint16 * 2)(), 1)
     h = ctypes.c_void_p()
     rc = lib.ms_create(ctypes.byref(cfg), ctypes.byref(h))
     assert rc == _lib.MS_E_NODEV
     assert b"device" in lib.ms_last_error(None)
     # argument validation happens before any device work
-    bad = _lib.ms_config(0, 7, 16, 0, 64, 0, 1)
+    bad = _lib.ms_config(0, 7, 16, 0, 64, (ctypes.c_uint16 * 2)(), 1)
     assert lib.ms_create(ctypes.byref(bad), ctypes.byref(h)) == _lib.MS_E_INVAL
     assert lib.ms_create(None, ctypes.byref(h)) == _lib.MS_E_INVAL
     assert lib.ms_destroy(None) == _lib.MS_E_INVAL

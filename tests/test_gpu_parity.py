@@ -328,3 +328,173 @@ def test_resource_sequential_tile_counts(oracle, n_nodes):
     with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=5) as e:
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
         assert_table_equal(e, o["cols"], n_nodes)
+
+
+def _pods_with_zero_hash(seed, n_nodes, want=4):
+    # pods j for which some node ordinal r < n_nodes has tie-break hash exactly 0:
+    # mix32(A + r * kG24) == 0 <=> A + r * kG24 == 0 (mix32 is a bijection fixing 0),
+    # so r = -A * kG24^-1 mod 2^32 (ms_internal.h tb_unhash(A, 0)); distinct digits r % 10
+    import _pyref
+
+    M = np.uint64(0xFFFFFFFF)
+
+    def fmix32(h):
+        h = h ^ (h >> np.uint64(16))
+        h = (h * np.uint64(0x85EBCA6B)) & M
+        h = h ^ (h >> np.uint64(13))
+        h = (h * np.uint64(0xC2B2AE35)) & M
+        return h ^ (h >> np.uint64(16))
+
+    out, digits, j = [], set(), 0
+    with np.errstate(over="ignore"):
+        while len(out) < want:
+            js = np.arange(j, j + 1 << 20, dtype=np.uint64)
+            j += 1 << 20
+            a = fmix32(js ^ np.uint64(_pyref.seed32(seed)))
+            r = (((M + np.uint64(1) - a) & M) * np.uint64(0xF2B382C9)) & M
+            for x in np.nonzero(r < np.uint64(n_nodes))[0]:
+                rr = int(r[x])
+                if rr % 10 not in digits and len(out) < want:
+                    assert _pyref.h32(seed, int(js[x]), rr) == 0
+                    digits.add(rr % 10)
+                    out.append((int(js[x]), rr))
+    return out
+
+
+def test_pp_zero_hash_winner(oracle):
+    # K1 pp treats a wave maximum of 0 as "no score-10 row here" and redoes the pod
+    # exactly: a pod whose only feasible score-10 node hashes to exactly 0 must still
+    # land on it, and with other score-10 nodes present the 0 must lose
+    seed, n = 4, 1 << 15
+    cases = _pods_with_zero_hash(seed, n, want=4)
+    nr = synth.nodes(n, seed=seed)
+    nr["unschedulable"] = 0
+    pr = synth.pods(len(cases) * 2, seed=seed)
+    for k, (j, r) in enumerate(cases):
+        for t in (0, 1):
+            p = pr[2 * k + t]
+            p["ordinal"] = j
+            p["name_digit"] = r % 10
+            p["tolerates_unschedulable"] = t
+    lone = nr.copy()
+    for j, r in cases:  # every other node of that digit unschedulable
+        same = (np.arange(n) % 10 == r % 10) & (np.arange(n) != r)
+        lone["unschedulable"][same] = 1
+    for table, tag in ((lone, "lone"), (nr, "crowded")):
+        o = oracle.schedule(table, pr, seed=seed)
+        with engine_with(table, seed=seed) as e:
+            res = e.schedule(pr, MODE_BATCHED)
+        assert_same(res, o)
+        if tag == "lone":
+            for k, (j, r) in enumerate(cases):
+                assert res["node"][2 * k] == r and res["score"][2 * k] == 10, (j, r)
+
+
+def test_stream_ordering_deltas_binds_reads(oracle):
+    # work queued on a caller stream and the context stream's delta /
+    # bind / read-back work must be ordered both ways. Rounds of select + bind
+    # commit on a caller stream with informer upserts in between and no host sync:
+    # each round must see exactly the table its call found, and the read-back at
+    # the end must include every bind.
+    import torch
+
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    n, p, rounds = 40_000, 4000, 5
+    nr = synth.nodes(n, seed=12)
+    pr = synth.pods(p, seed=12)
+    pods_d = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    outs = [torch.empty(p * 24, dtype=torch.uint8, device=dev) for _ in range(rounds)]
+    tables, touched = [], np.zeros(n, dtype=bool)
+    rng = np.random.default_rng(3)
+    with engine_with(nr, seed=12) as e:
+        cur = nr.copy()
+        for k in range(rounds):
+            tables.append(cur.copy())
+            e.select_batch_device(p, pods_d.data_ptr(), outs[k].data_ptr(), s.cuda_stream)
+            e.apply_binds_device(p, pods_d.data_ptr(), outs[k].data_ptr(), s.cuda_stream)
+            idx = rng.choice(n, 3000, replace=False)  # an informer Update, mid-flight
+            cur["unschedulable"][idx] = 1 - cur["unschedulable"][idx]
+            e.upsert(idx, cur[idx])
+            touched[idx] = True
+        t = e.read(0, n)  # context stream: after every caller-stream bind
+        s.synchronize()
+    placed = np.zeros(n, dtype=np.int64)
+    for k in range(rounds):
+        res = outs[k].cpu().numpy().view(_lib.RESULT)
+        assert_same(res, oracle.schedule(tables[k], pr, seed=12))
+        ok = res["code"] == 0
+        placed += np.bincount(res["node"][ok], minlength=n)
+    # rows an upsert never replaced carry every round's binds
+    keep = ~touched
+    assert np.array_equal(t["pod_count"][keep], placed[keep])
+
+
+def test_v8_covers_every_column_with_few_blocks(oracle, monkeypatch):
+    # K1 v8 serves column b % n_cols from workgroup b; a launch capped below
+    # the column count (few CUs, many rows) must still sweep every column
+    monkeypatch.setenv("MINISCHED_K1", "v8")
+    monkeypatch.setenv("MINISCHED_K1_V8_BLOCKS", "7")
+    n = 60_000  # 32 columns of 1920 rows
+    nr = synth.nodes(n, seed=14)
+    pr = synth.pods(900, seed=14)
+    o = oracle.schedule(nr, pr, seed=14)
+    with engine_with(nr, seed=14) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+
+
+# ---- MS_PLUGINS_NU_NN_NA: weights + the in-loop NormalizeScore hook ----
+
+@pytest.mark.parametrize("weights", [(1, 1), (2, 3), (10, 10)])
+@pytest.mark.parametrize("n_nodes,n_pods", [(1, 5), (17, 64), (300, 200), (5000, 700), (40_000, 300)])
+def test_na_batched(oracle, weights, n_nodes, n_pods):
+    seed = n_nodes + 3 * n_pods + weights[1]
+    nr = synth.nodes(n_nodes, seed=seed, zones=True)
+    pr = synth.pods(n_pods, seed=seed, zones=True)
+    pr["tolerates_unschedulable"][::6] = 1
+    pr["name_digit"][::17] = -1
+    nr["name_digit"][::9] = 0xFF
+    literal = n_nodes <= 300  # the loop as written is O(F^2) per pod
+    o = oracle.schedule_na(nr, pr, weights=weights, literal=literal, seed=seed)
+    with Engine(max_nodes=n_nodes, plugin_set=_lib.PLUGINS_NU_NN_NA, seed=seed, score_weights=weights) as e:
+        e.upsert(np.arange(n_nodes), nr)
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+        assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)  # no mutable state: queue order changes nothing
+
+
+def test_na_two_shards_combine(oracle):
+    # node-sharded NA: keys combine with a u64 MAX and the normalise anchors with a u32 MAX
+    import torch
+
+    n, p, seed = 9000, 800, 21
+    nr = synth.nodes(n, seed=seed, zones=True)
+    pr = synth.pods(p, seed=seed, zones=True)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pods_d = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    keys, anchors, engines = [], [], []
+    for a, b in ((0, 4321), (4321, n)):
+        e = Engine(max_nodes=b - a, plugin_set=_lib.PLUGINS_NU_NN_NA, node_base=a, seed=seed, score_weights=(2, 1))
+        e.upsert(np.arange(a, b), nr[a:b])
+        k = torch.empty(p, dtype=torch.int64, device=dev)
+        f = torch.empty(p, dtype=torch.int32, device=dev)
+        e.sweep_device(p, pods_d.data_ptr(), k.data_ptr(), f.data_ptr(), s.cuda_stream)
+        keys.append(k)
+        anchors.append(f)
+        engines.append(e)
+    with torch.cuda.stream(s):
+        kc = torch.maximum(keys[0], keys[1])
+        fc = torch.maximum(anchors[0], anchors[1])  # anchors < 2^21: the int32 max is the u32 max
+    res = torch.empty(p * 24, dtype=torch.uint8, device=dev)
+    engines[0].decode_device(p, pods_d.data_ptr(), kc.data_ptr(), fc.data_ptr(), n, res.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert_same(res.cpu().numpy().view(_lib.RESULT), oracle.schedule_na(nr, pr, weights=(2, 1), literal=False, seed=seed))
+    for e in engines:
+        e.close()
+
+
+def test_na_weight_validation():
+    with pytest.raises(_lib.MSError):
+        Engine(max_nodes=4, plugin_set=_lib.PLUGINS_NU_NN_NA, score_weights=(5, 20))  # 5*10 + 20*100 >= 2048
+    with pytest.raises(_lib.MSError):
+        Engine(max_nodes=4, plugin_set=PLUGINS_NU_NN, score_weights=(2, 1))  # weights are NA-only
