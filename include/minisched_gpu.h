@@ -227,6 +227,39 @@ int ms_apply_binds_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_d
  *   it also equals the queue-order loop (minisched.go:28-30). */
 int ms_select_batch_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
                            void *stream);
+/* ---- node-sharded exact sequential mode (MS_PLUGINS_NU_NRF_NN_LA) ---------
+ * Queue order with assume-on-select over nodes split across contexts (one per
+ * GPU), batch after batch; every shard s runs, for pods [a, a + n):
+ *   1. ms_seq_candidates_device: flushes deltas, then this shard's speculative
+ *      top-4 per pod against its current table: cands[p*4 + r] (key 0 = none)
+ *      with the node's record, and flags[p] = OR over this shard's nodes of
+ *      the filter plugins rejecting them (byte 0 NU, byte 1 NRF).
+ *   2. the caller all-gathers cands and flags over the shards (shard-major:
+ *      cands_all[s][p][4], flags_all[s][p]) — one collective each;
+ *   3. ms_seq_validate_device (identical on every shard): merges the shards'
+ *      lists into each pod's global speculative top-4, walks the pods in queue
+ *      order against them — a node bound earlier in the batch is re-evaluated
+ *      from its record plus those binds, the first untouched entry is exact —
+ *      and stops before the first pod the lists cannot decide (its four
+ *      candidates all bound earlier, more nodes below them). Writes
+ *      results[0, *n_done) and *n_done (>= 1 when n > 0), and commits the
+ *      binds that land on this shard's own nodes (NodeInfo.AddPod), so every
+ *      bind reaches its owner and no other shard. The caller continues at
+ *      a + *n_done. No deltas are drained between 1 and 3. */
+typedef struct ms_seq_cand {
+    uint64_t key; /* packed key at speculation; 0 = no candidate */
+    int64_t alloc_milli_cpu, alloc_memory, req_milli_cpu, req_memory, nonzero_milli_cpu, nonzero_memory;
+    int32_t allowed_pods, pod_count;
+    uint32_t flags_digit; /* bit0 unschedulable, bit7 absent | name digit << 8 */
+    uint32_t _pad;
+} ms_seq_cand; /* 72 bytes */
+#define MS_SEQ_SHARD_BATCH_MAX 256u
+#define MS_SEQ_MAX_SHARDS 16u
+int ms_seq_candidates_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_seq_cand *cands_dev,
+                             uint32_t *flags_dev, void *stream);
+int ms_seq_validate_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                           const ms_seq_cand *cands_all_dev, const uint32_t *flags_all_dev, ms_result *results_dev,
+                           uint32_t *n_done_dev, void *stream);
 /* Whole exact sequential cycle on device-resident pods (single shard). */
 int ms_schedule_sequential_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
                                   ms_result *results_dev, void *stream);

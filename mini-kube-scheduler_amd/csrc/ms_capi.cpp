@@ -68,6 +68,9 @@ struct ms_ctx {
     hipEvent_t ev_valid[2] = {nullptr, nullptr}, ev_swept[2] = {nullptr, nullptr}, ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
+    // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
+    ms_seq_cand *d_merged = nullptr;
+    uint32_t *d_merged_flags = nullptr;
 
     // NU+NN pod stream of the class-indexed K1 forms (k_pod_prep output),
     // reused call after call (ordered through the context stream like the table)
@@ -116,6 +119,8 @@ int fail(ms_ctx *c, int code, const std::string &msg) {
 
 uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
+constexpr uint32_t kTopKCands = 4;  // ms_seq_cand entries per pod and shard (the validator's top-K)
+
 void free_all(ms_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
@@ -124,7 +129,7 @@ void free_all(ms_ctx *c) {
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream,
-                   c->d_work};
+                   c->d_work, c->d_merged, c->d_merged_flags};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -786,6 +791,72 @@ int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *
     if (rc) return rc;
     if (s == c->stream) {
         ++c->ctx_seq;  // binds wrote the table on the context stream
+        return MS_OK;
+    }
+    return chain_back(c, s);
+}
+
+int ms_seq_candidates_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_seq_cand *cands_dev,
+                             uint32_t *flags_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !cands_dev || !flags_dev))) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NRF_NN_LA)
+        return fail(c, MS_E_INVAL, "ms_seq_candidates_device: the resource-aware plugin set only");
+    if (n_pods > MS_SEQ_SHARD_BATCH_MAX) return fail(c, MS_E_INVAL, "ms_seq_candidates_device: batch too large");
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);
+    if (rc) return rc;
+    const uint32_t rows = c->rows_dev;
+    if (rows == 0) {  // no node listed: no candidates, no rejections
+        MS_HIP(c, hipMemsetAsync(cands_dev, 0, sizeof(ms_seq_cand) * kTopKCands * n_pods, s));
+        MS_HIP(c, hipMemsetAsync(flags_dev, 0, sizeof(uint32_t) * n_pods, s));
+        return chain_back(c, s);
+    }
+    if (rows > seq_max_rows())
+        return fail(c, MS_E_CAPACITY, "ms_seq_candidates_device: at most " + std::to_string(seq_max_rows()) +
+                                          " rows per context");
+    const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
+    rc = ensure_tiles(c, n_tiles);
+    if (rc) return rc;
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    MS_HIP(c, launch_sweep_full_tiles(c->t, rows, pods_dev, n_pods, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
+    MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, n_pods, n_tiles, c->d_top4, c->d_spec,
+                                c->d_spec_flags, s));
+    MS_HIP(c, launch_seq_pack_cands(c->t, c->d_top4, c->d_tile_flags, n_tiles, n_pods, cands_dev, flags_dev, s));
+    return chain_back(c, s);
+}
+
+int ms_seq_validate_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                           const ms_seq_cand *cands_all_dev, const uint32_t *flags_all_dev, ms_result *results_dev,
+                           uint32_t *n_done_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !cands_all_dev || !flags_all_dev || !results_dev || !n_done_dev)))
+        return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NRF_NN_LA)
+        return fail(c, MS_E_INVAL, "ms_seq_validate_device: the resource-aware plugin set only");
+    if (n_pods > MS_SEQ_SHARD_BATCH_MAX || n_shards == 0 || n_shards > MS_SEQ_MAX_SHARDS)
+        return fail(c, MS_E_INVAL, "ms_seq_validate_device: batch or shard count out of range");
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    hipStream_t s = pick_stream(c, stream);
+    if (n_pods == 0) {
+        MS_HIP(c, hipMemsetAsync(n_done_dev, 0, sizeof(uint32_t), s));
+        return MS_OK;
+    }
+    int rc = order_after_ctx_stream(c, s);  // (deltas are not drained here: the candidates' records must stay current)
+    if (rc) return rc;
+    if (!c->d_merged) {
+        if (hipMalloc((void **)&c->d_merged, sizeof(ms_seq_cand) * kTopKCands * MS_SEQ_SHARD_BATCH_MAX) != hipSuccess ||
+            hipMalloc((void **)&c->d_merged_flags, sizeof(uint32_t) * MS_SEQ_SHARD_BATCH_MAX) != hipSuccess)
+            return fail(c, MS_E_OOM, "sharded validator scratch");
+    }
+    MS_HIP(c, launch_seq_validate_rep(c->t, n_pods, pods_dev, seed32_of(c->cfg.seed), n_shards, cands_all_dev,
+                                      flags_all_dev, c->d_merged, c->d_merged_flags, results_dev, n_done_dev, s));
+    if (s == c->stream) {
+        ++c->ctx_seq;
         return MS_OK;
     }
     return chain_back(c, s);

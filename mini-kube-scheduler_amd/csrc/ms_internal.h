@@ -178,6 +178,16 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
                                uint32_t seed32, const unsigned long long *tile_keys,
                                const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
                                const unsigned long long *top4, uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out, ms_result *results, uint32_t *stats, hipStream_t s);
+// Node-sharded sequential mode (minisched_gpu.h ms_seq_*): this shard's top-4
+// candidates with records + all-tile filter flags per pod, from the top-4 merge
+// output; and the replicated validation over the shards' gathered lists
+// (merged / merged_flags: n_pods * 4 / n_pods scratch).
+hipError_t launch_seq_pack_cands(const NodeTable &t, const unsigned long long *top4, const uint32_t *tile_flags,
+                                 uint32_t n_tiles, uint32_t n_pods, ms_seq_cand *cands, uint32_t *flags, hipStream_t s);
+hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms_pod_rec *pods, uint32_t seed32,
+                                   uint32_t n_shards, const ms_seq_cand *cands_all, const uint32_t *flags_all,
+                                   ms_seq_cand *merged, uint32_t *merged_flags, ms_result *results, uint32_t *n_done,
+                                   hipStream_t s);
 // Rows the sequential engine's validator supports (tile lists held in registers).
 uint32_t seq_max_rows();
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,

@@ -1537,6 +1537,205 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
 }
 
 // ----------------------------------------------------------------------------
+// Node-sharded exact sequential mode (minisched_gpu.h ms_seq_*): every shard
+// publishes its speculative top-4 per pod with the nodes' records; after an
+// all-gather every shard runs the same replicated in-order validation on the
+// merged lists and commits the binds that land on its own nodes.
+// ----------------------------------------------------------------------------
+static_assert(sizeof(ms_seq_cand) == 72, "ms_seq_cand layout");
+
+// One wave per pod: this shard's top-4 (k_topk_merge output) with records, and
+// the OR over every tile of the shard of the filter flags (plugins rejecting
+// at least one node: NU rejections are static and NRF ones only grow with
+// binds, so the OR stays a valid part of the FitError mask later in the batch).
+__global__ __launch_bounds__(64) void k_seq_pack_cands(NodeTable t, const u64 *__restrict__ top4,
+                                                       const uint32_t *__restrict__ tile_flags, uint32_t n_tiles,
+                                                       uint32_t n_pods, ms_seq_cand *__restrict__ cands,
+                                                       uint32_t *__restrict__ flags) {
+    const uint32_t p = blockIdx.x, lane = threadIdx.x;
+    if (p >= n_pods) return;
+    uint32_t fl = 0;
+    for (uint32_t tt = lane; tt < n_tiles; tt += 64) fl |= tile_flags[(size_t)p * n_tiles + tt];
+    const uint32_t f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+    if (lane == 0) flags[p] = f;
+    if (lane < (uint32_t)kTopK) {
+        const u64 e = top4[(size_t)p * kTopK + lane];
+        ms_seq_cand c = {};
+        c.key = e;
+        if (e) {
+            const uint32_t r = row_of_key(e, t.base);
+            c.alloc_milli_cpu = t.alloc_cpu[r];
+            c.alloc_memory = t.alloc_mem[r];
+            c.req_milli_cpu = t.req_cpu[r];
+            c.req_memory = t.req_mem[r];
+            c.nonzero_milli_cpu = t.nz_cpu[r];
+            c.nonzero_memory = t.nz_mem[r];
+            c.allowed_pods = t.allowed_pods[r];
+            c.pod_count = t.pod_count[r];
+            c.flags_digit = (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8);
+        }
+        cands[(size_t)p * kTopK + lane] = c;
+    }
+}
+
+// One wave per pod: the global speculative top-4 from the shards' lists (the
+// global rank-r entry, r < 4, is within its shard's top r+1), and the OR of
+// the shards' flags.
+__global__ __launch_bounds__(64) void k_seq_merge_shards(uint32_t n_pods, uint32_t n_shards,
+                                                         const ms_seq_cand *__restrict__ cands_all,
+                                                         const uint32_t *__restrict__ flags_all,
+                                                         ms_seq_cand *__restrict__ merged,
+                                                         uint32_t *__restrict__ merged_flags) {
+    const uint32_t p = blockIdx.x, lane = threadIdx.x;
+    if (p >= n_pods) return;
+    const bool in = lane < n_shards * kTopK;
+    const size_t src = (size_t)(lane / kTopK) * n_pods * kTopK + (size_t)p * kTopK + lane % kTopK;
+    u64 k = in ? cands_all[src].key : 0ull;
+    for (int r = 0; r < kTopK; ++r) {
+        const u64 m = wave_max_u64_dpp(k);
+        const u64 own = __ballot(m != 0 && k == m);  // keys embed the global ordinal: one owner
+        const uint32_t ol = own ? (uint32_t)__builtin_ctzll(own) : 0u;
+        if (own ? lane == ol : lane == 0) {
+            ms_seq_cand c = {};
+            if (own) c = cands_all[src];
+            merged[(size_t)p * kTopK + r] = c;
+        }
+        if (own && lane == ol) k = 0;
+    }
+    uint32_t f = lane < n_shards ? flags_all[(size_t)lane * n_pods + p] : 0u;
+    f = (__ballot((f & 0xFFu) != 0) ? 1u : 0u) | (__ballot((f & 0xFF00u) != 0) ? 0x100u : 0u);
+    if (lane == 0) merged_flags[p] = f;
+}
+
+constexpr int kRepMapBits = 11;
+constexpr int kRepMapCap = 1 << kRepMapBits;  // >= 2 x the nodes a batch binds (<= 256)
+
+struct RepShared {
+    ms_seq_cand c[MS_SEQ_SHARD_BATCH_MAX * kTopK];  // the merged candidates; a bound node's slot is its live record
+    uint32_t map[kRepMapCap];                       // ((ordinal + 1) << 10) | slot; 0 = empty
+    uint16_t bound_slot[MS_SEQ_SHARD_BATCH_MAX];    // live slots in bind order (write-back)
+    uint32_t n_bound;
+};
+static_assert(sizeof(RepShared) <= 100 * 1024, "replicated validator LDS");
+
+__device__ __forceinline__ uint32_t rep_hash(uint32_t ord) { return (ord * kGolden32) >> (32 - kRepMapBits); }
+
+__device__ __forceinline__ int rep_find(const RepShared &S, uint32_t ord) {
+    uint32_t h = rep_hash(ord);
+    for (;;) {
+        const uint32_t v = S.map[h];
+        if (v == 0) return -1;
+        if ((v >> 10) == ord + 1) return (int)(v & 1023u);
+        h = (h + 1) & (kRepMapCap - 1);
+    }
+}
+
+__device__ __forceinline__ FullRow cand_row(const ms_seq_cand &c) {
+    return make_row(c.alloc_milli_cpu, c.alloc_memory, c.req_milli_cpu, c.req_memory, c.nonzero_milli_cpu,
+                    c.nonzero_memory, c.allowed_pods - c.pod_count, c.flags_digit);
+}
+
+// The replicated in-order validation (one wave; identical on every shard).
+// Lanes 0..3 take a pod's four merged candidates: entries bound earlier in the
+// batch are re-evaluated from their live record, the first untouched one is
+// exact and bounds everything below it (binds only lower the keys of the node
+// they land on; unlisted nodes are below the 4th entry). A pod whose four
+// entries are all touched while the list is full cannot be decided from the
+// lists: the batch ends before it.
+__global__ __launch_bounds__(64) void k_seq_validate_rep(NodeTable t, uint32_t n_pods,
+                                                         const ms_pod_rec *__restrict__ pods, uint32_t seed32,
+                                                         const ms_seq_cand *__restrict__ merged,
+                                                         const uint32_t *__restrict__ merged_flags,
+                                                         ms_result *__restrict__ results,
+                                                         uint32_t *__restrict__ n_done) {
+    __shared__ RepShared S;
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t i = lane; i < n_pods * kTopK; i += 64) S.c[i] = merged[i];
+    for (uint32_t i = lane; i < (uint32_t)kRepMapCap; i += 64) S.map[i] = 0;
+    if (lane == 0) S.n_bound = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    uint32_t p = 0;
+    for (; p < n_pods; ++p) {
+        const ms_pod_rec pr = pods[p];
+        const PodFull q = load_pod(pr, seed32);
+        const uint32_t slot = p * kTopK + (lane & 3u);
+        const u64 e = lane < (uint32_t)kTopK ? S.c[slot].key : 0ull;
+        const uint32_t ord = e ? 0xFFFFFu - (uint32_t)(e & 0xFFFFFu) : 0u;
+        const int live = e ? rep_find(S, ord) : -1;
+        const u64 untouched = __ballot(e != 0 && live < 0);
+        const u64 listed = __ballot(e != 0);
+        if (!untouched && __builtin_popcountll(listed) == kTopK) break;  // undecidable from the lists
+        const uint32_t f = untouched ? (uint32_t)__builtin_ctzll(untouched) : (uint32_t)kTopK;
+        u64 v = 0;
+        if (lane < f && e != 0) {
+            uint32_t nu, nrf;
+            v = eval_full(cand_row(S.c[live]), ord, q, nu, nrf);
+        } else if (lane == f) {
+            v = e;
+        }
+        const u64 b = wave_max_u64_dpp(v);
+        const u64 own = __ballot(b != 0 && v == b);
+        ms_result r;
+        r._pad = 0;
+        r.plugin_mask = 0;
+        if (b == 0) {  // FitError: nothing feasible at speculation, or every listed node bound full since
+            const uint32_t fm = merged_flags[p] | (listed ? 0x100u : 0u);
+            r.code = MS_CODE_UNSCHEDULABLE;
+            r.node = -1;
+            r.score = 0;
+            r.plugin_mask = ((fm & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
+                            ((fm & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u);
+        } else if (pr.name_digit < 0) {
+            r.code = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
+            r.node = -1;
+            r.score = 0;
+        } else {
+            r.code = MS_CODE_SUCCESS;
+            r.node = (int32_t)(0xFFFFFu - (uint32_t)(b & 0xFFFFFu));
+            r.score = (int64_t)(b >> 52);
+            // assume-on-select: NodeInfo.AddPod on the winner's live record
+            const uint32_t wl = (uint32_t)__builtin_ctzll(own);
+            const int wlive = __builtin_amdgcn_readlane(live, (int)wl);
+            if (lane == 0) {
+                int sl = wlive;
+                if (sl < 0) {  // first bind on this node in the batch: its candidate slot becomes live
+                    sl = (int)(p * kTopK + wl);
+                    uint32_t h = rep_hash((uint32_t)r.node);
+                    while (S.map[h] != 0) h = (h + 1) & (kRepMapCap - 1);
+                    S.map[h] = (((uint32_t)r.node + 1) << 10) | (uint32_t)sl;
+                    S.bound_slot[S.n_bound++] = (uint16_t)sl;
+                }
+                ms_seq_cand &c = S.c[sl];
+                c.req_milli_cpu += pr.req_milli_cpu;
+                c.req_memory += pr.req_memory;
+                c.nonzero_milli_cpu += pr.nonzero_milli_cpu;
+                c.nonzero_memory += pr.nonzero_memory;
+                c.pod_count += 1;
+            }
+        }
+        if (lane == 0) results[p] = r;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+    }
+    // this shard's own bound nodes go back to its table (absolute values: the
+    // candidates were read from this table and nothing else wrote it since)
+    const uint32_t nb = S.n_bound;
+    for (uint32_t i = lane; i < nb; i += 64) {
+        const ms_seq_cand &c = S.c[S.bound_slot[i]];
+        const uint32_t ord = 0xFFFFFu - (uint32_t)(c.key & 0xFFFFFu);
+        if (ord < t.base || ord - t.base >= t.cap) continue;  // another shard's node
+        const uint32_t row = ord - t.base;
+        t.req_cpu[row] = c.req_milli_cpu;
+        t.req_mem[row] = c.req_memory;
+        t.nz_cpu[row] = c.nonzero_milli_cpu;
+        t.nz_mem[row] = c.nonzero_memory;
+        t.pod_count[row] = c.pod_count;
+    }
+    if (lane == 0) *n_done = p;
+}
+
+// ----------------------------------------------------------------------------
 // decode / bind commit / deltas
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ void decode_one(const ms_pod_rec *__restrict__ pods, const u64 *__restrict__ keys,
@@ -2050,6 +2249,29 @@ hipError_t launch_init_table(const NodeTable &t, hipStream_t s) {
 hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_node_rec *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_read_rows, dim3(cdiv(n, 256)), dim3(256), 0, s, t, first, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_pack_cands(const NodeTable &t, const unsigned long long *top4, const uint32_t *tile_flags,
+                                 uint32_t n_tiles, uint32_t n_pods, ms_seq_cand *cands, uint32_t *flags, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seq_pack_cands, dim3(n_pods), dim3(64), 0, s, t, top4, tile_flags, n_tiles, n_pods, cands,
+                       flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms_pod_rec *pods, uint32_t seed32,
+                                   uint32_t n_shards, const ms_seq_cand *cands_all, const uint32_t *flags_all,
+                                   ms_seq_cand *merged, uint32_t *merged_flags, ms_result *results, uint32_t *n_done,
+                                   hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    if (n_pods > MS_SEQ_SHARD_BATCH_MAX || n_shards == 0 || n_shards > MS_SEQ_MAX_SHARDS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_seq_merge_shards, dim3(n_pods), dim3(64), 0, s, n_pods, n_shards, cands_all, flags_all, merged,
+                       merged_flags);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seq_validate_rep, dim3(1), dim3(64), 0, s, t, n_pods, pods, seed32, merged, merged_flags,
+                       results, n_done);
     return hipGetLastError();
 }
 

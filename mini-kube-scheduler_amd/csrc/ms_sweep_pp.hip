@@ -158,20 +158,28 @@ __device__ __forceinline__ u64 pod_slow(const Word (&W)[kPpWords], const Pod &q)
     return 0;
 }
 
-// One wave sweeps pods [pbeg, pend) through its NW groups into lds[p - pbeg].
+// Pod p of a workgroup's chunk as the prologue leaves it in LDS: x = A =
+// tb_pod(seed32, ordinal), y = class bits (digit, 14 for a non-digit name, |
+// tolerates << 4) | name digit byte << 8.
+__device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, uint32_t p, uint32_t seed32) {
+    const uint2 pr = *reinterpret_cast<const uint2 *>(pods + p);  // ordinal, digit, tolerates
+    const int dig = (int)(int8_t)(pr.y & 0xFFu);
+    const uint32_t info = ((uint32_t)dig <= 9u ? (uint32_t)dig : 14u) | (((pr.y >> 8) & 0xFFu) ? 16u : 0u);
+    return make_uint2(tb_pod(seed32, pr.x), info | ((pr.y & 0xFFu) << 8));
+}
+
+// One wave sweeps the chunk's pods [0, np) through its NW groups into lds[p].
 template <int NW, bool GEN>
-__device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const ms_pod_rec *__restrict__ pods,
-                                            uint32_t pbeg, uint32_t pend, uint32_t seed32, uint32_t lane,
-                                            u64 *lds) {
-    for (uint32_t pb = pbeg; pb < pend; pb += 64) {
-        const uint32_t nblk = min(64u, pend - pb);
+__device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const uint2 *pinfo, uint32_t np,
+                                            uint32_t lane, u64 *lds) {
+    for (uint32_t pb = 0; pb < np; pb += 64) {
+        const uint32_t nblk = min(64u, np - pb);
         // the block's pods, one per lane: A and digit | tolerates << 4
         uint32_t a_l = 0, info_l = 14u;
         if (lane < nblk) {
-            const uint2 pr = *reinterpret_cast<const uint2 *>(pods + pb + lane);  // ordinal, digit, tolerates
-            const int dig = (int)(int8_t)(pr.y & 0xFFu);
-            a_l = tb_pod(seed32, pr.x);
-            info_l = ((uint32_t)dig <= 9u ? (uint32_t)dig : 14u) | (((pr.y >> 8) & 0xFFu) ? 16u : 0u);
+            const uint2 e = pinfo[pb + lane];
+            a_l = e.x;
+            info_l = e.y & 0xFFu;
         }
         for (uint32_t j = 0; j < nblk; j += 8) {
             Pod q[8];
@@ -191,7 +199,7 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const ms_
             const uint32_t u = reduce8(r, lane);
             const uint32_t pi = j + rev3(lane >> 3);  // lanes 8k: pod pi of the block
             const bool mine = (lane & 7u) == 0u && pi < nblk;
-            if (mine && u != 0u) atomicMax(&lds[pb - pbeg + pi], (11ull << 32) | u);
+            if (mine && u != 0u) atomicMax(&lds[pb + pi], (11ull << 32) | u);
             // a zero maximum: no score-10 row in this wave (or one whose hash is 0);
             // redo those pods exactly
             u64 redo = __ballot(mine && u == 0u);
@@ -202,7 +210,7 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const ms_
                 const Pod qs = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
                                         (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
                 const u64 v = pod_slow<NW>(W, qs);
-                if (lane == 0 && v) atomicMax(&lds[pb - pbeg + j + t], v);
+                if (lane == 0 && v) atomicMax(&lds[pb + j + t], v);
             }
         }
     }
@@ -212,13 +220,18 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
     int atomic_keys, ms_result *__restrict__ results, uint32_t present) {
-    extern __shared__ u64 lds[];  // one combine slot per pod of the chunk
+    // LDS: one combine slot per pod of the chunk, then the chunk's pod entries
+    extern __shared__ u64 lds[];
+    uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk);
     const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t pbeg = blockIdx.x * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
     const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
-    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) lds[i] = 0;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+        lds[i] = 0;
+        pinfo[i] = pod_entry(pods, pbeg + i, seed32);
+    }
 
     // the wave's groups, dealt round-robin over the workgroup's waves so their
     // word counts differ by at most one: word k of lane l is group
@@ -250,10 +263,10 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
         switch (nw * 2 + (gen ? 1 : 0)) {  // wave-uniform
 #define MS_PP_CASE(N)                                                                     \
     case 2 * N:                                                                           \
-        sweep_range<N, false>(W, pods, pbeg, pend, seed32, lane, lds);                    \
+        sweep_range<N, false>(W, pinfo, np, lane, lds);                                   \
         break;                                                                            \
     case 2 * N + 1:                                                                       \
-        sweep_range<N, true>(W, pods, pbeg, pend, seed32, lane, lds);                     \
+        sweep_range<N, true>(W, pinfo, np, lane, lds);                                    \
         break;
             MS_PP_CASE(1)
             MS_PP_CASE(2)
@@ -267,17 +280,17 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
         const u64 v = lds[i];
-        const uint2 pr = *reinterpret_cast<const uint2 *>(pods + pbeg + i);
+        const uint2 pe = pinfo[i];
         u64 key = 0;
         if (v) {
             const uint32_t h = (uint32_t)v;
-            key = make_key((uint32_t)(v >> 32) - 1u, h, tb_unhash(tb_pod(seed32, pr.x), h));
+            key = make_key((uint32_t)(v >> 32) - 1u, h, tb_unhash(pe.x, h));
         }
         if (keys) {
             if (!atomic_keys) keys[pbeg + i] = key;
             else if (key) atomicMax(&keys[pbeg + i], key);
         }
-        if (results) results[pbeg + i] = decode_key(key, (int8_t)(pr.y & 0xFFu), nullptr, 0, present);
+        if (results) results[pbeg + i] = decode_key(key, (int8_t)(pe.y >> 8), nullptr, 0, present);
     }
 }
 
@@ -338,7 +351,7 @@ hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, ui
 // rows: grid.y workgroups per chunk); pods per workgroup sized for one
 // round of resident workgroups (32 waves per CU) in multiples of 8, at most
 // kPpMaxChunk (LDS). MINISCHED_PP_CHUNK overrides the chunk (tuning).
-constexpr uint32_t kPpMaxChunk = 4096;
+constexpr uint32_t kPpMaxChunk = 2048;
 
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
@@ -365,14 +378,14 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
         if (!keys) return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * sizeof(u64), s, t.planes, t.gcap, n_groups,
-                           t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present);
+        hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
+                           t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present);
         e = hipGetLastError();
         if (e != hipSuccess || !results) return e;
         return launch_decode(pods, n_pods, keys, nullptr, present, results, s);
     }
-    hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * sizeof(u64), s, t.planes, t.gcap, n_groups, t.base,
-                       pods, n_pods, chunk, seed32, results ? nullptr : keys, 0, results, present);
+    hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes, t.gcap,
+                       n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0, results, present);
     return hipGetLastError();
 }
 

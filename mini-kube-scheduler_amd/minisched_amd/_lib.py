@@ -74,7 +74,26 @@ POD_REC = np.dtype(
 RESULT = np.dtype(
     [("node", "<i4"), ("code", "<i4"), ("score", "<i8"), ("plugin_mask", "<u4"), ("_pad", "<u4")]
 )
-assert NODE_REC.itemsize == 64 and POD_REC.itemsize == 40 and RESULT.itemsize == 24
+# ms_seq_cand: a shard's speculative candidate with the node's record (node-sharded sequential mode)
+SEQ_CAND = np.dtype(
+    [
+        ("key", "<u8"),
+        ("alloc_milli_cpu", "<i8"),
+        ("alloc_memory", "<i8"),
+        ("req_milli_cpu", "<i8"),
+        ("req_memory", "<i8"),
+        ("nonzero_milli_cpu", "<i8"),
+        ("nonzero_memory", "<i8"),
+        ("allowed_pods", "<i4"),
+        ("pod_count", "<i4"),
+        ("flags_digit", "<u4"),
+        ("_pad", "<u4"),
+    ]
+)
+SEQ_TOPK = 4
+SEQ_SHARD_BATCH_MAX = 256
+SEQ_MAX_SHARDS = 16
+assert NODE_REC.itemsize == 64 and POD_REC.itemsize == 40 and RESULT.itemsize == 24 and SEQ_CAND.itemsize == 72
 
 
 class ms_config(ctypes.Structure):
@@ -127,6 +146,8 @@ SIGNATURES = {
     "ms_apply_binds_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_schedule_sequential_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_select_batch_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_seq_candidates_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp]),
+    "ms_seq_validate_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
 }
 
 DECODE_MAX_JOBS = 8  # MS_DECODE_MAX_JOBS
@@ -303,6 +324,18 @@ class Engine:
             "ms_select_batch_device",
             self.lib.ms_select_batch_device(self.h, n_pods, pods_dev, results_dev, stream or None),
         )
+
+    def seq_candidates_device(self, n_pods, pods_dev, cands_dev, flags_dev, stream=0):
+        """Node-sharded sequential mode, step 1: this shard's top-4 candidates + flags."""
+        self._check("ms_seq_candidates_device",
+                    self.lib.ms_seq_candidates_device(self.h, n_pods, pods_dev, cands_dev, flags_dev, stream or None))
+
+    def seq_validate_device(self, n_pods, pods_dev, n_shards, cands_all_dev, flags_all_dev, results_dev, n_done_dev,
+                            stream=0):
+        """Node-sharded sequential mode, step 3: replicated in-order validation + owned binds."""
+        self._check("ms_seq_validate_device",
+                    self.lib.ms_seq_validate_device(self.h, n_pods, pods_dev, n_shards, cands_all_dev, flags_all_dev,
+                                                    results_dev, n_done_dev, stream or None))
 
     def schedule_sequential_device(self, n_pods, pods_dev, results_dev, stream=0):
         self._check(

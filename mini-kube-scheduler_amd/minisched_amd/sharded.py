@@ -278,6 +278,77 @@ class ShardedCycle:
             self._pipe.finish()
 
 
+class ShardedSequential:
+    """Node-sharded exact sequential cycle (config E over G GPUs).
+
+    Queue order with assume-on-select over nodes split across ranks. Per batch
+    of at most `batch` pods starting at pod a:
+      1. ms_seq_candidates_device: this shard's speculative top-4 per pod with
+         the nodes' records, and its filter flags;
+      2. all-gather of both over the ranks (two collectives);
+      3. ms_seq_validate_device, the same on every rank: the merged global
+         top-4 walked in queue order (nodes bound earlier in the batch are
+         re-evaluated from their records), up to the first pod the lists
+         cannot decide; each rank commits the binds on its own nodes only.
+    The next batch starts at a + n_done (n_done >= 1; a host read per batch).
+    Every rank ends with every pod's result.
+    """
+
+    def __init__(self, engine, n_pods: int, pods_dev, stream, group=None, batch: int = 128):
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+
+        self.eng, self.P, self.pods, self.stream, self.group = engine, n_pods, pods_dev, stream, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if self.world > _lib.SEQ_MAX_SHARDS:
+            raise ValueError("too many shards for the replicated validator")
+        self.B = max(1, min(batch, _lib.SEQ_SHARD_BATCH_MAX))
+        dev = pods_dev.device
+        cb = _lib.SEQ_CAND.itemsize * _lib.SEQ_TOPK
+        self._cands = torch.zeros(self.B * cb, dtype=torch.uint8, device=dev)
+        self._flags = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self._cands_all = torch.zeros(self.world * self.B * cb, dtype=torch.uint8, device=dev)
+        self._flags_all = torch.zeros(self.world * self.B, dtype=torch.int32, device=dev)
+        self.results = torch.zeros(n_pods * 24, dtype=torch.uint8, device=dev)
+        self._n_done = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.batches = 0
+
+    def _gather(self, nb):
+        import torch.distributed as dist
+
+        from . import _lib
+
+        cb = _lib.SEQ_CAND.itemsize * _lib.SEQ_TOPK
+        if self.world == 1:
+            self._cands_all[: nb * cb].copy_(self._cands[: nb * cb])
+            self._flags_all[:nb].copy_(self._flags[:nb])
+            return
+        # shard-major [s][p]: gather the first nb pods' entries of every rank
+        dist.all_gather_into_tensor(self._cands_all[: self.world * nb * cb], self._cands[: nb * cb].contiguous(),
+                                    group=self.group)
+        dist.all_gather_into_tensor(self._flags_all[: self.world * nb], self._flags[:nb].contiguous(),
+                                    group=self.group)
+
+    def run(self):
+        sp = self.stream.cuda_stream
+        a = 0
+        while a < self.P:
+            nb = min(self.B, self.P - a)
+            pods = self.pods.data_ptr() + 40 * a
+            self.eng.seq_candidates_device(nb, pods, self._cands.data_ptr(), self._flags.data_ptr(), sp)
+            self._gather(nb)
+            self.eng.seq_validate_device(nb, pods, self.world, self._cands_all.data_ptr(), self._flags_all.data_ptr(),
+                                         self.results.data_ptr() + 24 * a, self._n_done.data_ptr(), sp)
+            done = int(self._n_done.item())  # (syncs the current stream)
+            if done < 1:
+                raise RuntimeError("replicated validator made no progress")
+            a += done
+            self.batches += 1
+        return self.results
+
+
 def present_total(engine, group=None) -> int:
     """Present nodes over every shard (decode's FitError mask for NU+NN needs the
     cluster's count, not this shard's): one all-reduce at setup / after deltas."""

@@ -173,3 +173,108 @@ def test_decode_device_jobs_matches_oracle(oracle):
             eng.decode_device_jobs(jobs * 3, n_nodes, stream.cuda_stream)  # > MS_DECODE_MAX_JOBS
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("cuts,n_pods,batch", [((0, 23, 60), 700, 64), ((0, 700, 1400, 2000), 12_000, 128),
+                                              ((0, 9000, 20_000), 30_000, 256), ((0, 3, 7), 300, 16)])
+def test_node_sharded_sequential_contexts(oracle, cuts, n_pods, batch):
+    # config E over node shards on one GPU: one context per shard, the all-gather done by
+    # concatenation; every shard's replicated validation must agree, the results equal the
+    # 1-context sequential oracle, and the shards' tables after the binds its columns
+    import torch
+
+    from minisched_amd import _lib
+
+    n_nodes = cuts[-1]
+    seed = 40 + n_nodes
+    nr = synth.nodes(n_nodes, seed=seed, resources=True)
+    pr = synth.pods(n_pods, seed=seed, resources=True)
+    pr["name_digit"][::19] = -1
+    o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    sp = s.cuda_stream
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    G = len(cuts) - 1
+    engines = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        e = _lib.Engine(max_nodes=b - a, plugin_set=_lib.PLUGINS_NU_NRF_NN_LA, node_base=a, seed=seed)
+        e.upsert(np.arange(a, b), nr[a:b])
+        engines.append(e)
+    cb = _lib.SEQ_CAND.itemsize * _lib.SEQ_TOPK
+    cands = [torch.zeros(batch * cb, dtype=torch.uint8, device=dev) for _ in range(G)]
+    flags = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in range(G)]
+    res = [torch.zeros(n_pods * 24, dtype=torch.uint8, device=dev) for _ in range(G)]
+    done = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(G)]
+    a, batches = 0, 0
+    try:
+        while a < n_pods:
+            nb = min(batch, n_pods - a)
+            for g, e in enumerate(engines):
+                e.seq_candidates_device(nb, pods.data_ptr() + 40 * a, cands[g].data_ptr(), flags[g].data_ptr(), sp)
+            with torch.cuda.stream(s):
+                call = torch.cat([c[: nb * cb] for c in cands])
+                fall = torch.cat([f[:nb] for f in flags])
+            for g, e in enumerate(engines):
+                e.seq_validate_device(nb, pods.data_ptr() + 40 * a, G, call.data_ptr(), fall.data_ptr(),
+                                      res[g].data_ptr() + 24 * a, done[g].data_ptr(), sp)
+            s.synchronize()
+            nd = [int(d.item()) for d in done]
+            assert len(set(nd)) == 1 and nd[0] >= 1, nd
+            a += nd[0]
+            batches += 1
+        tables = [e.read(lo, hi - lo) for e, lo, hi in zip(engines, cuts[:-1], cuts[1:])]
+    finally:
+        for e in engines:
+            e.close()
+    for g in range(G):
+        _same(res[g].cpu().numpy().view(_lib.RESULT), o, 0, n_pods, f"shard {g}")
+    t = np.concatenate(tables)
+    cols = o["cols"]
+    for k_dev, k_or in (("pod_count", "pod_count"), ("req_milli_cpu", "req_cpu"), ("req_memory", "req_mem"),
+                        ("nonzero_milli_cpu", "nz_cpu"), ("nonzero_memory", "nz_mem")):
+        assert np.array_equal(t[k_dev], getattr(cols, k_or)), k_dev
+    assert batches >= (n_pods + batch - 1) // batch
+
+
+def _seq_rccl_worker(port, q):
+    import torch
+    import torch.distributed as dist
+
+    from minisched_amd import _lib, sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        n, p = 3000, 9000
+        eng = _lib.Engine(max_nodes=n, plugin_set=_lib.PLUGINS_NU_NRF_NN_LA, seed=5)
+        eng.upsert(np.arange(n), synth.nodes(n, seed=5, resources=True))
+        pods = torch.from_numpy(synth.pods(p, seed=5, resources=True).view(np.uint8).copy()).to(dev)
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
+        cyc = sharded.ShardedSequential(eng, p, pods, stream, batch=128)
+        res = cyc.run().cpu().numpy().view(_lib.RESULT).copy()
+        t = eng.read(0, n)
+        eng.close()
+        dist.destroy_process_group()
+        q.put((res, t["pod_count"].copy(), None))
+    except Exception as e:
+        q.put((None, None, repr(e)))
+
+
+def test_sharded_sequential_class_rccl(oracle):
+    # sharded.ShardedSequential through a 1-rank RCCL group (the world-1 gather path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr_ = ctx.Process(target=_seq_rccl_worker, args=(_free_port(), q))
+    pr_.start()
+    res, cnt, err = q.get(timeout=110)
+    pr_.join(timeout=60)
+    assert err is None, err
+    o = oracle.schedule(synth.nodes(3000, seed=5, resources=True), synth.pods(9000, seed=5, resources=True),
+                        plugin_set=1, mode=1, seed=5)
+    _same(res, o, 0, 9000, "rccl seq")
+    assert np.array_equal(cnt, o["cols"].pod_count)

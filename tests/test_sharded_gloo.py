@@ -238,3 +238,75 @@ def test_cross_step_pipeline_gloo(oracle, depth, group):
         for rank, out in got:
             a, keys = out[k]
             assert np.array_equal(keys, ref[a:a + len(keys)]), f"rank {rank} batch {k}"
+
+
+def _seqshard_worker(rank, world, port, n_nodes, n_pods, batch, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import _seq_shard_ref as ref
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nr = synth.nodes(n_nodes, seed=31, resources=True)
+    pr = synth.pods(n_pods, seed=31, resources=True)
+    pr["name_digit"][::23] = -1
+    lo, hi = sharded.shard_bounds(n_nodes, rank, world)
+    shard = ref.Shard(nr[lo:hi], lo)
+    results, a, batches = [], 0, 0
+    while a < n_pods:
+        nb = min(batch, n_pods - a)
+        c, f = shard.candidates(pr[a:a + nb], seed=31)
+        call = torch.zeros((world,) + c.shape, dtype=torch.int64)
+        fall = torch.zeros((world, nb), dtype=torch.int64)
+        dist.all_gather_into_tensor(call, torch.from_numpy(c).unsqueeze(0))  # shard-major, like the GPU path
+        dist.all_gather_into_tensor(fall, torch.from_numpy(f).unsqueeze(0))
+        done, out, live = ref.validate(pr[a:a + nb], call.numpy(), fall.numpy(), seed=31)
+        assert done >= 1
+        results += out
+        for o, rec in live.items():  # every bind reaches its owner and no other shard
+            shard.commit(o, (rec[3], rec[4], rec[5], rec[6], rec[8]))
+        a += done
+        batches += 1
+    q.put((rank, results, batches, shard.cnt.copy(), shard.req_cpu.copy(), shard.nz_mem.copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_nodes,n_pods,batch", [(2, 60, 700, 64), (3, 200, 1200, 128), (2, 7, 300, 16)])
+def test_node_sharded_sequential_protocol_gloo(oracle, world, n_nodes, n_pods, batch):
+    # config E over node shards: per-shard top-4 + records, all-gather,
+    # replicated in-order validation with truncation, binds to their owner only. Every
+    # rank's results and the shards' tables after the binds equal the 1-process oracle.
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seqshard_worker, args=(r, world, port, n_nodes, n_pods, batch, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nr = synth.nodes(n_nodes, seed=31, resources=True)
+    pr = synth.pods(n_pods, seed=31, resources=True)
+    pr["name_digit"][::23] = -1
+    o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=31)
+    assert (o["code"] == 2).sum() > 0  # saturated: FitErrors and re-evaluations happen
+    for rank, results, batches, *_ in got:
+        codes = np.array([r[0] for r in results])
+        nodes = np.array([r[1] for r in results])
+        scores = np.array([r[2] for r in results])
+        masks = np.array([r[3] for r in results])
+        assert np.array_equal(codes, o["code"]), rank
+        assert np.array_equal(nodes, o["node"]), rank
+        assert np.array_equal(scores, o["score"]), rank
+        assert np.array_equal(masks, o["mask"]), rank
+        assert batches >= (n_pods + batch - 1) // batch
+    cols = o["cols"]
+    cnt = np.concatenate([g[3] for g in got])
+    req = np.concatenate([g[4] for g in got])
+    nzm = np.concatenate([g[5] for g in got])
+    assert np.array_equal(cnt, cols.pod_count) and np.array_equal(req, cols.req_cpu) and np.array_equal(nzm, cols.nz_mem)

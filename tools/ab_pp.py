@@ -5,7 +5,9 @@ interleaved rounds on one device).
 AB_VARIANTS = "name:K=V,K=V;name2:K=V" — each variant sets those env vars
 (read by the library at each launch) on top of the base environment.
 AB_MODE = select (ms_select_batch_device: the fused single-shard cycle, default)
-        | sweep  (ms_sweep_device: this shard's keys only).
+        | sweep  (ms_sweep_device: this shard's keys only)
+        | sweepdec (ms_sweep_device + ms_decode_device: the unfused cycle);
+a variant may set MODE=... itself (results of different modes are not compared).
 Prints per-variant kernel ms (HIP events on the launch stream), median and
 min over rounds, and whether all variants produced identical bytes."""
 import json
@@ -53,12 +55,15 @@ def main():
     eng.upsert(np.arange(base_ord, base_ord + N), synth.nodes(N, seed=1, start=base_ord))
     eng.flush()
     pods = torch.from_numpy(synth.pods(P, seed=1).view(np.uint8).copy()).to(dev)
-    width = 24 if mode == "select" else 8
-    outs = {n: torch.empty(P * width, dtype=torch.uint8, device=dev) for n, _ in variants}
+    outs = {n: torch.empty(P * 24, dtype=torch.uint8, device=dev) for n, _ in variants}
+    keys = torch.empty(P, dtype=torch.int64, device=dev)
     times = {n: [] for n, _ in variants}
     for r in range(rounds + 1):
         for name, env in variants:
+            vmode = env.get("MODE", mode)
             for k in touched:
+                if k == "MODE":
+                    continue
                 if k in env:
                     os.environ[k] = env[k]
                 elif base_env[k] is None:
@@ -67,8 +72,11 @@ def main():
                     os.environ[k] = base_env[k]
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
-            if mode == "select":
+            if vmode == "select":
                 eng.select_batch_device(P, pods.data_ptr(), outs[name].data_ptr(), s.cuda_stream)
+            elif vmode == "sweepdec":
+                eng.sweep_device(P, pods.data_ptr(), keys.data_ptr(), 0, s.cuda_stream)
+                eng.decode_device(P, pods.data_ptr(), keys.data_ptr(), 0, N, outs[name].data_ptr(), s.cuda_stream)
             else:
                 eng.sweep_device(P, pods.data_ptr(), outs[name].data_ptr(), 0, s.cuda_stream)
             b.record(s)
@@ -76,7 +84,8 @@ def main():
             if r:
                 times[name].append(a.elapsed_time(b))
     names = [n for n, _ in variants]
-    same = all(torch.equal(outs[names[0]], outs[n]) for n in names[1:])
+    mode_of = {n: {"sweepdec": "select"}.get(env.get("MODE", mode), env.get("MODE", mode)) for n, env in variants}
+    same = all(torch.equal(outs[names[0]], outs[n]) for n in names[1:] if mode_of[n] == mode_of[names[0]])
     out = {n: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                "evals_per_s": N * P / (np.median(t) * 1e-3)} for n, t in times.items()}
     out["identical"] = bool(same)

@@ -3,7 +3,7 @@
 
   B  5k x 10k   NU+NN  exact sequential      device-resident (ms_schedule_sequential_device)
   C  100k x 100k NU+NN batched, host API     PCIe-inclusive (ms_schedule_batch, host arrays)
-  D  50k x 1M   NU+NN  batched                device-resident sweep+decode
+  D  50k x 1M   NU+NN  batched                device-resident fused cycle (ms_select_batch_device)
   E  50k x 200k NU+NRF+NN+LA exact sequential device-resident (speculative sweep + in-order validator)
 
 Each line: evals/s (P*N/time), pods/s, median of --reps after one warm-up.
@@ -96,11 +96,10 @@ def main():
             eng.flush()
 
             def run():
-                eng.sweep_device(P, pods.data_ptr(), keys.data_ptr(), 0, sp)
-                eng.decode_device(P, pods.data_ptr(), keys.data_ptr(), 0, N, results.data_ptr(), sp)
+                eng.select_batch_device(P, pods.data_ptr(), results.data_ptr(), sp)
 
             med, mn = timed(run, args.reps, s.synchronize)
-            mode = "batched (device-resident sweep+decode)"
+            mode = "batched (device-resident fused cycle, one launch)"
         line = dict(config=c, nodes=N, pods=P, plugins=cfg["plugins"], mode=mode, median_s=med, min_s=mn,
                     evals_per_s=N * P / med, pods_per_s=P / med, **extra)
         print(json.dumps(line), flush=True)
