@@ -260,8 +260,67 @@ static void gpu_tests() {
     });
 }
 
+// ------------------------------------------------------------- GPU replay
+// ms_host_test replay <cluster.txt> <out.txt> <seed> <plugin_set>: feeds a
+// cluster through the informer handlers (OnNodeAdd in file order, then
+// OnPodAdd), runs ScheduleOne until the queue is empty and writes one line per
+// cycle: "pod kind node score mask" (mask: bit0 NodeUnschedulable, bit1
+// NodeResourcesFit). tests/test_host_cpp.py compares that with the CPU oracle
+// on the same inputs: the host mirror's queue order, ordinals, encoders and
+// ErrorFunc against an independent restatement, not against itself.
+//   N <name> <unschedulable 0/1> <cpu milli> <memory bytes> <pods>
+//   P <name> <cpu milli or -1> <memory bytes or -1> <tolerates 0/1>
+static int replay(const char *in_path, const char *out_path, uint64_t seed, int plugin_set) {
+    FILE *f = std::fopen(in_path, "r");
+    if (!f) return 2;
+    Scheduler::Options o;
+    o.seed = seed;
+    o.plugins = plugin_set ? Scheduler::PluginSet::NU_NRF_NN_LA : Scheduler::PluginSet::NU_NN;
+    o.binder = [](const v1::Pod &, const std::string &) { return true; };
+    std::vector<v1::Node> nodes;
+    std::vector<v1::Pod> pods;
+    char kind[4], name[128];
+    while (std::fscanf(f, "%3s %127s", kind, name) == 2) {
+        if (kind[0] == 'N') {
+            int uns;
+            long long cpu, mem, np;
+            if (std::fscanf(f, "%d %lld %lld %lld", &uns, &cpu, &mem, &np) != 4) return 3;
+            v1::Node n = node(name, uns != 0, cpu, mem);
+            n.allocatable.pods = np;
+            nodes.push_back(n);
+        } else {
+            long long cpu, mem;
+            int tol;
+            if (std::fscanf(f, "%lld %lld %d", &cpu, &mem, &tol) != 3) return 3;
+            v1::Pod p = pod(name, cpu, mem);
+            if (tol) p.tolerations.push_back({v1::kTaintNodeUnschedulable, "Exists", "", ""});
+            pods.push_back(p);
+        }
+    }
+    std::fclose(f);
+    o.max_nodes = (uint32_t)std::max<size_t>(1, nodes.size());
+    Scheduler s(o);
+    for (const auto &n : nodes) s.OnNodeAdd(n);
+    for (const auto &p : pods) s.OnPodAdd(p);
+    FILE *out = std::fopen(out_path, "w");
+    if (!out) return 2;
+    for (;;) {
+        const ScheduleResult r = s.ScheduleOne();
+        if (r.kind == ScheduleResult::NoPod) break;
+        unsigned mask = 0;
+        for (const auto &pl : r.error.diagnosis.UnschedulablePlugins)
+            mask |= pl == "NodeUnschedulable" ? 1u : pl == "NodeResourcesFit" ? 2u : 0u;
+        std::fprintf(out, "%s %d %s %lld %u\n", r.pod.c_str(), (int)r.kind, r.node.empty() ? "-" : r.node.c_str(),
+                     (long long)r.score, mask);
+    }
+    std::fclose(out);
+    std::printf("replayed %zu pods on %zu nodes\n", pods.size(), nodes.size());
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
+    if (mode == "replay" && argc == 6) return replay(argv[2], argv[3], std::strtoull(argv[4], nullptr, 10), std::atoi(argv[5]));
     if (mode == "cpu" || mode == "all") cpu_tests();
     if (mode == "gpu" || mode == "all") gpu_tests();
     std::printf("%d passed, %d failed\n", g_pass, g_fail);

@@ -50,3 +50,50 @@ def test_oracle_asan():
 def test_host_mirror_gpu():
     out = _run([_ensure("host", HOST_TEST), "gpu"])
     assert "0 failed" in out, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plugin_set,n_nodes,n_pods", [(1, 300, 1500), (0, 2000, 800)])
+def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes, n_pods):
+    # the host mirror checked against the oracle, not against itself.
+    # v1 objects go through the informer handlers, the queue (FIFO), the encoders, ScheduleOne,
+    # the binder and ErrorFunc; every cycle's outcome must equal the sequential oracle's
+    # for the same cluster, with pod ordinals in queue order and node ordinals in Add order.
+    import numpy as np
+
+    from minisched_amd import synth
+
+    seed = 17 + plugin_set
+    nr = synth.nodes(n_nodes, seed=seed, resources=True)
+    pr = synth.pods(n_pods, seed=seed, resources=True)
+    pr["tolerates_unschedulable"][::9] = 1
+    names = [f"pod{j}" if j % 37 else f"pod{j}x" for j in range(n_pods)]  # some names end in a letter
+    pr["name_digit"] = [int(n[-1]) if n[-1].isdigit() else -1 for n in names]
+    lines = []
+    for i in range(n_nodes):
+        lines.append(f"N node{i} {int(nr['unschedulable'][i])} {int(nr['alloc_milli_cpu'][i])} "
+                     f"{int(nr['alloc_memory'][i])} {int(nr['allowed_pods'][i])}")
+    for j in range(n_pods):
+        none = pr["req_milli_cpu"][j] == 0 and pr["req_memory"][j] == 0
+        cpu = -1 if none else int(pr["req_milli_cpu"][j])
+        mem = -1 if none else int(pr["req_memory"][j])
+        lines.append(f"P {names[j]} {cpu} {mem} {int(pr['tolerates_unschedulable'][j])}")
+    cluster = tmp_path / "cluster.txt"
+    cluster.write_text("\n".join(lines) + "\n")
+    out = tmp_path / "out.txt"
+    _run([_ensure("host", HOST_TEST), "replay", str(cluster), str(out), str(seed), str(plugin_set)])
+    rows = [l.split() for l in out.read_text().splitlines()]
+    assert [r[0] for r in rows] == names  # one cycle per pod, in queue order
+    code = np.array([{1: 0, 2: 2, 3: 1}[int(r[1])] for r in rows])
+    node = np.array([-1 if r[2] == "-" else int(r[2][4:]) for r in rows])
+    score = np.array([int(r[3]) for r in rows])
+    mask = np.array([int(r[4]) for r in rows])
+    if plugin_set == 0:  # NU+NN reads no resources: the oracle's records need none
+        nr["alloc_milli_cpu"] = nr["alloc_memory"] = 0
+    o = oracle.schedule(nr, pr, plugin_set=plugin_set, mode=1, seed=seed)
+    assert np.array_equal(code, o["code"])
+    assert np.array_equal(node, o["node"])
+    assert np.array_equal(score, o["score"])
+    assert np.array_equal(mask, o["mask"])
+    if plugin_set == 1:
+        assert (o["code"] == 2).sum() > 0 and (o["code"] == 1).sum() > 0
