@@ -60,12 +60,15 @@ struct ms_ctx {
     unsigned long long *d_spec = nullptr;  // per-pod speculative winner key (atomicMax target)
     uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
     unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
+    int64_t *d_top4_rec = nullptr;         // their batch-start node records (validator layout)
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
+    int64_t *d_prev_rec = nullptr;         // and their final records (x2)
     // pipelined sequential engine: batch k+1's speculation (seq_stream) runs
     // while batch k validates (caller stream); every buffer above is double-
     // buffered by batch parity
     hipStream_t seq_stream = nullptr;
-    hipEvent_t ev_valid[2] = {nullptr, nullptr}, ev_swept[2] = {nullptr, nullptr}, ev_seq = nullptr;
+    hipEvent_t ev_valid[3] = {nullptr, nullptr, nullptr}, ev_swept[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
     // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
@@ -120,6 +123,7 @@ int fail(ms_ctx *c, int code, const std::string &msg) {
 uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
 constexpr uint32_t kTopKCands = 4;  // ms_seq_cand entries per pod and shard (the validator's top-K)
+constexpr int kSeqBufs = 3;         // sequential-engine batch buffer sets (pipeline depth <= 3)
 
 void free_all(ms_ctx *c) {
     if (!c) return;
@@ -128,7 +132,7 @@ void free_all(ms_ctx *c) {
     void *dev[] = {c->t.planes, c->t.zone, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev, c->d_overflow, c->d_pstream,
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow, c->d_pstream,
                    c->d_work, c->d_merged, c->d_merged_flags};
     for (void *p : dev)
         if (p) (void)hipFree(p);
@@ -137,7 +141,7 @@ void free_all(ms_ctx *c) {
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_back) (void)hipEventDestroy(c->ev_back);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kSeqBufs; ++i) {
         if (c->ev_valid[i]) (void)hipEventDestroy(c->ev_valid[i]);
         if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
     }
@@ -230,11 +234,11 @@ int chain_back(ms_ctx *c, hipStream_t s) {
     return MS_OK;
 }
 
-// Sequential-engine scratch for n_tiles tiles, two batches deep (pipelining).
+// Sequential-engine scratch for n_tiles tiles, kSeqBufs batches deep (pipelining).
 int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (!c->seq_stream) {
         MS_HIP(c, hipStreamCreateWithFlags(&c->seq_stream, hipStreamNonBlocking));
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < kSeqBufs; ++i) {
             MS_HIP(c, hipEventCreateWithFlags(&c->ev_valid[i], hipEventDisableTiming));
             MS_HIP(c, hipEventCreateWithFlags(&c->ev_swept[i], hipEventDisableTiming));
         }
@@ -242,7 +246,8 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     }
     if (n_tiles <= c->tile_cap) return MS_OK;
     MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
-    void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_prev};
+    void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev,
+                   c->d_prev_rec};
     for (void *q : old)
         if (q) (void)hipFree(q);
     c->d_tile_keys = nullptr;
@@ -250,18 +255,23 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     c->d_spec = nullptr;
     c->d_spec_flags = nullptr;
     c->d_top4 = nullptr;
+    c->d_top4_rec = nullptr;
     c->d_prev = nullptr;
+    c->d_prev_rec = nullptr;
     c->tile_cap = 0;
-    const size_t B = seq_batch_limit(), n = 2 * B * n_tiles;
+    // (ms_seq_candidates_device uses the same buffers for up to kSeqBufs * B pods)
+    const size_t B = seq_batch_limit(), NB = kSeqBufs * B, n = NB * n_tiles;
     if (hipMalloc((void **)&c->d_tile_keys, n * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&c->d_tile_flags, n * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&c->d_spec, 2 * B * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void **)&c->d_spec_flags, 2 * B * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&c->d_top4, 2 * B * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void **)&c->d_prev, 2 * (B + 1) * sizeof(uint32_t)) != hipSuccess)
+        hipMalloc((void **)&c->d_spec, NB * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&c->d_spec_flags, NB * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_top4, NB * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&c->d_top4_rec, NB * seq_topk() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_prev, 2 * (2 + seq_prev_cap()) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_prev_rec, 2 * seq_prev_cap() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential-engine scratch");
-    MS_HIP(c, hipMemsetAsync(c->d_spec, 0, 2 * B * sizeof(unsigned long long), c->stream));
-    MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, 2 * B * sizeof(uint32_t), c->stream));
+    MS_HIP(c, hipMemsetAsync(c->d_spec, 0, NB * sizeof(unsigned long long), c->stream));
+    MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, NB * sizeof(uint32_t), c->stream));
     MS_HIP(c, hipStreamSynchronize(c->stream));
     c->tile_cap = n_tiles;
     return MS_OK;
@@ -295,36 +305,80 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
     int rc = ensure_tiles(c, n_tiles);
     if (rc) return rc;
-    // Batch k: speculative sweep + top-4 merge on seq_stream into buffer k&1, after
-    // validation k-2 (which last read that buffer, and whose binds the sweep must
-    // see); validation k on s after merge k (stream events only: a device-side
-    // wait would stall wherever dispatches are serialised, e.g. under counter
-    // profiling; an event costs ~6 us when already signalled, ~11 us otherwise,
-    // tools/ubench/xstream). Validation k marks the nodes batch k-1 bound as
-    // touched (prev rows): sweep k may have run concurrently with it.
+    // Batch k: speculative sweep + top-4 merge on seq_stream into buffer set
+    // k % kSeqBufs, after validation k-D (D = the pipeline depth: every bind up
+    // to batch k-D is in the table the sweep reads; validations k-D+1 .. k-1,
+    // which may be running, read the other buffer sets); validation k on s
+    // after merge k (stream events only: a device-side wait would stall
+    // wherever dispatches are serialised, e.g. under counter profiling; an
+    // event costs ~6 us when already signalled, ~11 us otherwise,
+    // tools/ubench/xstream). Validation k treats the nodes batches k-D+1 .. k-1
+    // bound as stale (their prev lists): its sweep may predate those binds.
+    // D = 3 (default) keeps the sweep of batch k+1 off validation k-1's
+    // critical path: each chain then runs back to back instead of paying a
+    // cross-stream event per batch (profiles/r02j_e_timeline*.json).
+    const uint32_t B = seq_batch(c), SB = seq_batch_limit();
+    const size_t prev_words = 2 + seq_prev_cap(), prev_fields = (size_t)seq_prev_cap() * seq_rec_fields();
+    const size_t cells_per_set = (size_t)SB * n_tiles, recs_per_set = (size_t)SB * seq_topk() * seq_rec_fields();
+    const char *pipe_env = getenv("MINISCHED_SEQ_PIPE");
+    if (!pipe_env || std::string(pipe_env) == "fused") {
+        // Single stream (default): step k = one launch validating batch k while
+        // sweeping batch k+1 (launch_seq_step), then batch k+1's top-4 merge.
+        // No cross-stream hand-off (each cost ~12 us per batch, and a
+        // validation launched beside a sweep waited for a SIMD to drain);
+        // batch k+1 treats batch k's binds as stale.
+        const uint32_t nb0 = std::min(B, n_pods);
+        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
+        MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, nb0, n_tiles, c->d_top4, c->d_spec,
+                                    c->d_spec_flags, c->t, c->d_top4_rec, s));
+        uint32_t k = 0;
+        for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
+            const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
+            const uint32_t s1 = s0 + B, nn = s1 < n_pods ? std::min(B, n_pods - s1) : 0u;
+            unsigned long long *tk = c->d_tile_keys + cells_per_set * seq_topk() * cur;
+            unsigned long long *tk1 = c->d_tile_keys + cells_per_set * seq_topk() * nxt;
+            uint32_t *tf = c->d_tile_flags + cells_per_set * cur, *tf1 = c->d_tile_flags + cells_per_set * nxt;
+            MS_HIP(c, launch_seq_step(c->t, rows, n_tiles, seed32, d_pods + s0, nb, tk, tf, c->d_spec + SB * cur,
+                                      c->d_spec_flags + SB * cur, c->d_top4 + (size_t)SB * seq_topk() * cur,
+                                      c->d_top4_rec + recs_per_set * cur,
+                                      k ? c->d_prev + prev_words * nxt : nullptr,
+                                      k ? c->d_prev_rec + prev_fields * nxt : nullptr, c->d_prev + prev_words * cur,
+                                      c->d_prev_rec + prev_fields * cur, d_res + s0, c->d_overflow,
+                                      nn ? d_pods + s1 : nullptr, nn, tk1, tf1, c->num_cus, s));
+            if (nn)
+                MS_HIP(c, launch_topk_merge(tk1, tf1, nn, n_tiles, c->d_top4 + (size_t)SB * seq_topk() * nxt,
+                                            c->d_spec + SB * nxt, c->d_spec_flags + SB * nxt, c->t,
+                                            c->d_top4_rec + recs_per_set * nxt, s));
+        }
+        return MS_OK;
+    }
+    // Two streams (MINISCHED_SEQ_PIPE = 0: no overlap, 1: one stale batch, 2:
+    // two), handing off by stream events (measured slower than the single
+    // stream: profiles/r02j_e_modes.txt)
     MS_HIP(c, hipEventRecord(c->ev_seq, s));
     MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_seq, 0));
-    const uint32_t B = seq_batch(c), SB = seq_batch_limit();
-    const char *pipe_env = getenv("MINISCHED_SEQ_PIPE");  // 0: no overlap (diagnostics)
-    const bool pipe = !pipe_env || atoi(pipe_env) != 0;
+    const uint32_t D = 1u + (uint32_t)std::min(2, std::max(0, atoi(pipe_env)));
     uint32_t k = 0;
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
-        const uint32_t nb = std::min(B, n_pods - s0), par = k & 1u;
-        const size_t cells = (size_t)SB * n_tiles * par;
+        const uint32_t nb = std::min(B, n_pods - s0), slot = k % kSeqBufs, par = k & 1u;
+        const size_t cells = cells_per_set * slot;
         unsigned long long *tk = c->d_tile_keys + cells * seq_topk();
         uint32_t *tf = c->d_tile_flags + cells;
-        unsigned long long *sp = c->d_spec + SB * par, *top = c->d_top4 + (size_t)SB * seq_topk() * par;
-        uint32_t *sf = c->d_spec_flags + SB * par;
-        if (k >= (pipe ? 2u : 1u)) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[pipe ? par : par ^ 1u], 0));
+        unsigned long long *sp = c->d_spec + SB * slot, *top = c->d_top4 + (size_t)SB * seq_topk() * slot;
+        uint32_t *sf = c->d_spec_flags + SB * slot;
+        int64_t *trec = c->d_top4_rec + recs_per_set * slot;
+        if (k >= D) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[(k - D) % kSeqBufs], 0));
         MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, tk, tf, n_tiles, c->seq_stream));
-        MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->seq_stream));
-        MS_HIP(c, hipEventRecord(c->ev_swept[par], c->seq_stream));
-        MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[par], 0));
-        const uint32_t *prev_in = (pipe && k) ? c->d_prev + (SB + 1) * (par ^ 1u) : nullptr;
-        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, n_tiles,
-                                      prev_in,
-                                      c->d_prev + (SB + 1) * par, d_res + s0, c->d_overflow, s));
-        MS_HIP(c, hipEventRecord(c->ev_valid[par], s));
+        MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->t, trec, c->seq_stream));
+        MS_HIP(c, hipEventRecord(c->ev_swept[slot], c->seq_stream));
+        MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[slot], 0));
+        const bool has_prev = D > 1 && k;
+        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, trec, n_tiles,
+                                      has_prev ? c->d_prev + prev_words * (par ^ 1u) : nullptr,
+                                      has_prev ? c->d_prev_rec + prev_fields * (par ^ 1u) : nullptr,
+                                      c->d_prev + prev_words * par, c->d_prev_rec + prev_fields * par, D > 2 ? 1 : 0,
+                                      d_res + s0, c->d_overflow, s));
+        MS_HIP(c, hipEventRecord(c->ev_valid[slot], s));
     }
     return MS_OK;
 }
@@ -527,10 +581,10 @@ int ms_destroy(ms_ctx *c) {
             const uint64_t *cy = reinterpret_cast<const uint64_t *>(st + 8);
             std::fprintf(stderr,
                          "MS_VSTAMPS pods=%u slow=%u tile_scans=%u misses=%u recomputes=%u resweeps=%u cycles: prologue=%llu "
-                         "fast_check=%llu scan=%llu commit=%llu loop=%llu epilogue=%llu\n",
+                         "group=%llu prologue_loads=%llu slow=%llu rounds=%llu epilogue=%llu first_slow=%llu\n",
                          st[3], st[5], st[6], st[4], st[2], st[1], (unsigned long long)cy[0], (unsigned long long)cy[1],
                          (unsigned long long)cy[2], (unsigned long long)cy[3], (unsigned long long)cy[4],
-                         (unsigned long long)cy[5]);
+                         (unsigned long long)cy[5], (unsigned long long)cy[6]);
         }
     }
 #endif
@@ -825,7 +879,7 @@ int ms_seq_candidates_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     MS_HIP(c, launch_sweep_full_tiles(c->t, rows, pods_dev, n_pods, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
     MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, n_pods, n_tiles, c->d_top4, c->d_spec,
-                                c->d_spec_flags, s));
+                                c->d_spec_flags, c->t, nullptr, s));
     MS_HIP(c, launch_seq_pack_cands(c->t, c->d_top4, c->d_tile_flags, n_tiles, n_pods, cands_dev, flags_dev, s));
     return chain_back(c, s);
 }

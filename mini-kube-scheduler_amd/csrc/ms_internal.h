@@ -164,20 +164,40 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
                                    uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s);
-// In-order validation of a speculative batch; writes results and commits
-// binds to the table. Single workgroup.
-// Global speculative top-4 keys per pod (top[p*4 + r]) from the per-tile lists.
-// Per pod: global speculative top-4 from the tile lists, the speculative
-// winner (rank 0) and the filters of tiles with no feasible row.
+// Per pod: global speculative top-4 from the tile lists (top[p*4 + r]), the
+// speculative winner (rank 0) and the filters of tiles with no feasible row;
+// recs (optional, n_pods * 4 * seq_rec_fields() i64) gets the four entries'
+// batch-start node records for the in-order validator.
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
                              uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
-                             hipStream_t s);
+                             const NodeTable &t, int64_t *recs, hipStream_t s);
+// In-order validation of a speculative batch (single workgroup); writes
+// results and commits binds to the table. prev_in / prev_recs_in: the stale
+// nodes (bound by the previous one or two batches) with their final records
+// ({n_own, n_carried, rows} of 2 + seq_prev_cap() words;
+// seq_prev_cap() * seq_rec_fields() i64), written by the previous batch's
+// validator into its prev_out / prev_recs_out; carry != 0 also carries the
+// previous batch's own binds into prev_out (the next sweep overlaps two
+// validations).
 // stats: u32[6] = overflow flags, re-swept tiles, recomputed entries, pods,
 // speculation misses, pods whose speculative winner was touched.
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                               uint32_t seed32, const unsigned long long *tile_keys,
-                               const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
-                               const unsigned long long *top4, uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out, ms_result *results, uint32_t *stats, hipStream_t s);
+                               uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
+                               const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
+                               const int64_t *top4_recs, uint32_t n_tiles, const uint32_t *prev_in,
+                               const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
+                               ms_result *results, uint32_t *stats, hipStream_t s);
+// One single-stream step: validate batch k (n_pods, carry 0: batch k's sweep
+// ran beside batch k-1's validation) while sweeping batch k+1 (n_next pods,
+// tile lists only; launch_topk_merge follows). Either count may be 0.
+hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles, uint32_t seed32,
+                           const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *tile_keys,
+                           const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
+                           const unsigned long long *top4, const int64_t *top4_recs, const uint32_t *prev_in,
+                           const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
+                           ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
+                           unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
+                           hipStream_t s);
 // Node-sharded sequential mode (minisched_gpu.h ms_seq_*): this shard's top-4
 // candidates with records + all-tile filter flags per pod, from the top-4 merge
 // output; and the replicated validation over the shards' gathered lists
@@ -201,6 +221,9 @@ hipError_t launch_bind_one(const NodeTable &t, uint32_t local, const ms_pod_rec 
 hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_node_rec *out, hipStream_t s);
 // Largest speculative batch the sequential validator accepts.
 uint32_t seq_batch_limit();
+// i64 fields per validator node record; stale nodes per prev list.
+uint32_t seq_rec_fields();
+uint32_t seq_prev_cap();
 // Entries per (pod, tile) speculative list: tile_keys has n_pods * n_tiles * seq_topk() u64.
 uint32_t seq_topk();
 

@@ -858,24 +858,37 @@ __device__ __forceinline__ void sweep_topk_pods(const FullRow *x, uint32_t ord0,
     }
 }
 
-__global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, uint32_t n_rows,
-                                                                  const ms_pod_rec *__restrict__ pods,
-                                                                  uint32_t n_pods, uint32_t chunk, uint32_t seed32,
-                                                                  u64 *__restrict__ tile_keys,
-                                                                  uint32_t *__restrict__ tile_flags, uint32_t n_tiles) {
-    const uint32_t lane = lane_id();
-    const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
-    if (tile >= n_tiles) return;  // wave-uniform; no block barriers in this kernel
+struct SweepArgs {
+    NodeTable t;
+    uint32_t n_rows;
+    const ms_pod_rec *pods;
+    uint32_t n_pods;
+    uint32_t chunk;  // pods per task, <= 64
+    uint32_t seed32;
+    u64 *tile_keys;
+    uint32_t *tile_flags;
+    uint32_t n_tiles;
+};
+
+// One wave: tile `tile`'s top-4 lists and filter flags for the pods of chunk cidx.
+__device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t tile, uint32_t cidx, uint32_t lane) {
     const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
     FullRow x[kFullSlots];
 #pragma unroll
-    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(t, row0 + s, n_rows);
-    const uint32_t ord0 = t.base + row0;
-    const uint32_t pbeg = blockIdx.y * chunk;
-    const uint32_t cnt = min(min(chunk, 64u), n_pods - pbeg);  // host: chunk <= 64
-    const PodLanes m = stage_pods(pods, pbeg, cnt, lane, seed32);
-    if (rows_huge(x)) sweep_topk_pods<true>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags);
-    else sweep_topk_pods<false>(x, ord0, m, pbeg, cnt, lane, tile, n_tiles, tile_keys, tile_flags);
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
+    const uint32_t ord0 = a.t.base + row0;
+    const uint32_t pbeg = cidx * a.chunk;
+    if (pbeg >= a.n_pods) return;
+    const uint32_t cnt = min(min(a.chunk, 64u), a.n_pods - pbeg);
+    const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
+    if (rows_huge(x)) sweep_topk_pods<true>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+    else sweep_topk_pods<false>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+}
+
+__global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(SweepArgs a) {
+    const uint32_t tile = blockIdx.x * (kFullThreads / 64) + (threadIdx.x >> 6);
+    if (tile >= a.n_tiles) return;  // wave-uniform; no block barriers in this kernel
+    sweep_topk_task(a, tile, blockIdx.y, lane_id());
 }
 
 // ----------------------------------------------------------------------------
@@ -883,11 +896,61 @@ __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(NodeTable t, u
 // wave per pod). Exact: the global rank-r entry (r < 4) is within its tile's
 // top r+1, so it is in its tile's list.
 // ----------------------------------------------------------------------------
+// Record of a touched node in the in-order validator, one i64 per field
+// (F_INV_*: f32 bits of 100 / Allocatable); kSpecF fields come from the table.
+constexpr int kRecF = 12;
+constexpr int kSpecF = 9;
+enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALLOC_MEM, F_CNT, F_ALLOWED, F_FD,
+                F_ROW, F_INV_CPU, F_INV_MEM };
+
+__device__ __forceinline__ uint32_t row_of_key(u64 k, uint32_t base) {
+    return (0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) - base;
+}
+
+// Field f (< kSpecF) of node row r's current device record.
+__device__ __forceinline__ int64_t rec_field(const NodeTable &t, uint32_t r, uint32_t f) {
+    switch (f) {
+        case F_REQ_CPU: return t.req_cpu[r];
+        case F_REQ_MEM: return t.req_mem[r];
+        case F_NZ_CPU: return t.nz_cpu[r];
+        case F_NZ_MEM: return t.nz_mem[r];
+        case F_ALLOC_CPU: return t.alloc_cpu[r];
+        case F_ALLOC_MEM: return t.alloc_mem[r];
+        case F_CNT: return t.pod_count[r];
+        case F_ALLOWED: return t.allowed_pods[r];
+        default: return (int64_t)((uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8));  // F_FD
+    }
+}
+
+// The validator's record of key k's node (F_ROW = -1 for an empty entry),
+// written with 16-byte stores so the validator copies it as is.
+__device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int64_t *dst) {
+    int64_t v[kRecF];
+#pragma unroll
+    for (int f = 0; f < kRecF; ++f) v[f] = 0;
+    v[F_ROW] = -1;
+    if (k) {
+        const uint32_t r = row_of_key(k, t.base);
+#pragma unroll
+        for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) v[f] = rec_field(t, r, f);
+        v[F_ROW] = r;
+        v[F_INV_CPU] = __float_as_uint(r100(v[F_ALLOC_CPU]));
+        v[F_INV_MEM] = __float_as_uint(r100(v[F_ALLOC_MEM]));
+    }
+    longlong2 *d = reinterpret_cast<longlong2 *>(dst);
+#pragma unroll
+    for (int f = 0; f < kRecF; f += 2) d[f / 2] = make_longlong2(v[f], v[f + 1]);
+}
+
+// Per pod (one wave): merge the tiles' top-4 lists into the global top-4, the
+// speculative winner and the no-feasible-row filter flags; recs (optional)
+// gets the batch-start records of the four entries for the in-order validator.
 template <int J>
 __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
                                                    const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
                                                    uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
-                                                   uint32_t *__restrict__ spec_flags) {
+                                                   uint32_t *__restrict__ spec_flags, NodeTable t,
+                                                   int64_t *__restrict__ recs) {
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_pods) return;
     u64 e[J][kTopK];
@@ -927,6 +990,7 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
+    if (recs && lane < (uint32_t)kTopK) store_merged_rec(t, out, recs + ((size_t)p * kTopK + lane) * kRecF);
     // the speculative winner (rank 0) and, when no row is feasible, the filters
     const uint32_t f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
     if (lane == 0) {
@@ -957,31 +1021,29 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
 //  - the bind (NodeInfo.AddPod) updates that LDS record, one field per lane.
 // Results and records stay in LDS until the batch ends.
 // ----------------------------------------------------------------------------
-constexpr int kSeqBatch = 256;  // pods per speculative batch (host clamps)
+constexpr int kSeqBatch = 128;  // pods per speculative batch (host clamps)
 constexpr int kMapBits = 11;
 constexpr int kMapCap = 1 << kMapBits;  // >= 4 x the nodes a batch and its predecessor bind
 constexpr int kSeqMaxJ = 16;            // tile lists per lane in registers: n_tiles <= 1024 (262k rows)
-constexpr int kRecF = 12;               // record fields per slot (see RecField)
-constexpr int kSpecF = 9;               // fields loaded from the node table (F_REQ_CPU .. F_FD)
 constexpr int kClaimBits = 12;          // claim table: 64 lanes in 4096 buckets, ~0.8% false conflicts
 constexpr int kClaimCap = 1 << kClaimBits;
 constexpr uint32_t kForceSlow = 0xFFFFu;  // spec_slot: speculation could not be re-resolved
+constexpr int kPrevCap = 2 * kSeqBatch;              // stale nodes: the two previous batches' binds
+constexpr int kPrevSlot0 = kTopK * kSeqBatch;         // first slot of the stale nodes
+constexpr int kSeqSlots = kPrevSlot0 + kPrevCap;      // < 1024 (the map's slot field)
+constexpr int kPrevWords = 2 + kPrevCap;              // prev lists: {n_own, n_carried, rows...}
+static_assert(kSeqSlots <= 1024, "map entries hold a 10-bit slot");
 
-// LDS record of a touched node, one i64 per field (F_INV_*: f32 bits of 100 / Allocatable)
-enum RecField { F_REQ_CPU = 0, F_REQ_MEM, F_NZ_CPU, F_NZ_MEM, F_ALLOC_CPU, F_ALLOC_MEM, F_CNT, F_ALLOWED, F_FD,
-                F_ROW, F_INV_CPU, F_INV_MEM };
-
-// Slots: rec[p] for p < kSeqBatch is pod p's speculative winner's record,
-// loaded at batch start (it becomes that node's live record when pod p binds
-// there first); rec[kSeqBatch + p] is pod p's next candidate (prefetched at
-// batch start; reloaded if pod p binds elsewhere off its speculation);
-// rec[2*kSeqBatch + i] are the nodes the previous batch bound (pipelined
-// mode: this batch's speculation may predate those binds). A node has at most
-// one live slot: the map's.
+// Record slots: rec[4p + r] is the batch-start record of pod p's top-4 entry
+// r (k_topk_merge wrote it; it becomes that node's live record when pod p
+// binds there first, and is dead otherwise); rec[kPrevSlot0 + i] are the
+// stale nodes: those the previous one or two batches bound (pipelined mode:
+// this batch's speculation may predate those binds), as the previous batch's
+// validator left them. A node has at most one live slot: the map's.
 struct SeqShared {
     uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
-    int64_t rec[3 * kSeqBatch][kRecF];
-    uint8_t bound[3 * kSeqBatch];  // slot was bound in this batch
+    int64_t rec[kSeqSlots][kRecF];
+    uint8_t bound[kSeqSlots];  // slot was bound in this batch
     uint32_t n_out;
     ms_pod_rec pods[kSeqBatch];
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
@@ -1021,33 +1083,33 @@ __device__ __forceinline__ FullRow slot_row(const SeqShared &S, int sl) {
     return x;
 }
 
-// Field f (< kSpecF) of node row r's current device record.
-__device__ __forceinline__ int64_t rec_field(const NodeTable &t, uint32_t r, uint32_t f) {
-    switch (f) {
-        case F_REQ_CPU: return t.req_cpu[r];
-        case F_REQ_MEM: return t.req_mem[r];
-        case F_NZ_CPU: return t.nz_cpu[r];
-        case F_NZ_MEM: return t.nz_mem[r];
-        case F_ALLOC_CPU: return t.alloc_cpu[r];
-        case F_ALLOC_MEM: return t.alloc_mem[r];
-        case F_CNT: return t.pod_count[r];
-        case F_ALLOWED: return t.allowed_pods[r];
-        default: return (int64_t)((uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8));  // F_FD
-    }
-}
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void global_void_t;
 
-// Node row r's current device record into LDS slot sl (one lane).
-__device__ __forceinline__ void load_rec(SeqShared &S, const NodeTable &t, uint32_t sl, uint32_t r) {
-    int64_t *rec = S.rec[sl];
+// n16 16-byte units global src -> LDS dst (contiguous), straight to LDS with
+// global_load_lds_dwordx4 (64 lanes x 16 B per instruction, no registers);
+// the caller waits (s_waitcnt vmcnt(0)) before reading dst. U = units per
+// lane at most; sources clamped to valid units.
+template <int U>
+__device__ __forceinline__ void lds_dma16(void *dst, const void *src, uint32_t n16, uint32_t lane) {
+    if (n16 == 0) return;
+    const uint4 *g = reinterpret_cast<const uint4 *>(src);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+#ifdef MS_NO_LDS_DMA
 #pragma unroll
-    for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) rec[f] = rec_field(t, r, f);
-    rec[F_ROW] = r;
-    rec[F_INV_CPU] = __float_as_uint(r100(rec[F_ALLOC_CPU]));
-    rec[F_INV_MEM] = __float_as_uint(r100(rec[F_ALLOC_MEM]));
+    for (int k = 0; k < U; ++k) d[lane + 64 * k] = g[min(lane + 64u * k, n16 - 1)];
+#else
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+        __builtin_amdgcn_global_load_lds((global_void_t *)(g + min(lane + 64u * k, n16 - 1)), (lds_void_t *)(d + 64 * k),
+                                         16, 0, 0);
+#endif
 }
 
-__device__ __forceinline__ uint32_t row_of_key(u64 k, uint32_t base) {
-    return (0xFFFFFu - (uint32_t)(k & 0xFFFFFu)) - base;
+// Entry k (wave-divergent) of a register-held top-4 list, without the dynamic
+// register indexing that would put the list in scratch.
+__device__ __forceinline__ u64 pick4(const u64 (&e)[kTopK], int k) {
+    return k == 0 ? e[0] : k == 1 ? e[1] : k == 2 ? e[2] : e[3];
 }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
@@ -1123,7 +1185,7 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
         }
         // walk the list: touched entries are re-evaluated, the first untouched one ends it
         for (int k = 0;;) {
-            const uint32_t row = row_of_key(B.e[j][k], t.base);
+            const uint32_t row = row_of_key(pick4(B.e[j], k), t.base);
             uint32_t nu, nrf;
             const u64 r = eval_full(slot_row(S, sl), t.base + row, q, nu, nrf);
             ++ctr.recompute;
@@ -1135,7 +1197,7 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
                 need |= 1u << j;  // K touched entries: the tile's next row is unknown, re-sweep it
                 break;
             }
-            const u64 e2 = B.e[j][k];
+            const u64 e2 = pick4(B.e[j], k);
             if (e2 == 0) break;  // list ended: the remaining rows were infeasible and stay so
             sl = map_find(S, row_of_key(e2, t.base));
             if (sl < 0) {
@@ -1217,9 +1279,9 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, uint32_t l) {
 // over the batch, land in stats[8..] (u64), printed at ms_destroy.
 #ifdef MS_VSTAMPS
 struct VStamps {
-    u64 prev, acc[6];
+    u64 prev, acc[7];
 };
-#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0}};
+#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0, 0}};
 #define MS_VST(i)                                               \
     do {                                                        \
         __builtin_amdgcn_sched_barrier(0);                      \
@@ -1235,56 +1297,147 @@ struct VStamps {
     } while (0)
 #endif
 
+// Stale-node list entry o: row and record (16-byte stores).
+__device__ __forceinline__ void put_stale(uint32_t *rows, int64_t *recs, uint32_t o, uint32_t row, const int64_t *r) {
+    rows[2 + o] = row;
+    longlong2 *d = reinterpret_cast<longlong2 *>(recs + (size_t)o * kRecF);
+#pragma unroll
+    for (int f = 0; f < kRecF; f += 2) d[f / 2] = make_longlong2(r[f], r[f + 1]);
+}
+
+// One speculative batch's in-order validation (k_validate_seq, k_seq_step).
+// stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
+//        [4] speculation misses (records loaded), [5] slow pods, [6] slow pods that scanned the tile lists
+// top4/top4_recs: k_topk_merge's per-pod top-4 keys and their batch-start records
+// prev_in/prev_out: {n_own, n_carried, rows...} of the stale nodes this batch
+// sees / the next one will: rows [0, n_own) bound by the writing batch, then
+// rows [n_own, n_own + n_carried) bound by its predecessor only (carry != 0:
+// the next batch's speculation may predate both); prev_recs_in/out: their
+// final records. prev_in null when this batch's sweep saw every earlier bind.
+struct SeqArgs {
+    NodeTable t;
+    uint32_t n_rows;
+    const ms_pod_rec *pods;
+    uint32_t n_pods;
+    uint32_t seed32;
+    const u64 *tile_keys;
+    const uint32_t *tile_flags;
+    const u64 *spec;
+    const uint32_t *spec_flags;
+    const u64 *top4;
+    const int64_t *top4_recs;
+    uint32_t n_tiles;
+    const uint32_t *prev_in;
+    const int64_t *prev_recs_in;
+    uint32_t *prev_out;
+    int64_t *prev_recs_out;
+    int carry;
+    ms_result *results;
+    uint32_t *stats;
+};
+
 template <int J>  // tile lists per lane: n_tiles <= 64 * J
-__global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_rows,
-                                                     const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
-                                                     uint32_t seed32, const u64 *__restrict__ tile_keys,
-                                                     const uint32_t *__restrict__ tile_flags, const u64 *__restrict__ spec,
-                                                     const uint32_t *__restrict__ spec_flags, const u64 *__restrict__ top4,
-                                                     uint32_t n_tiles,
-                                                     const uint32_t *__restrict__ prev_in,
-                                                     uint32_t *__restrict__ prev_out, ms_result *__restrict__ results,
-                                                     uint32_t *__restrict__ stats) {
-    // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
-    //        [4] speculation misses (records loaded), [5] slow pods, [6] slow pods that scanned the tile lists
-    // prev_in/prev_out: {count, rows...} of the nodes the previous / this batch bound
-    // (prev_in null when the sweep of this batch saw every earlier bind).
-    __shared__ SeqShared S;
-    const uint32_t lane = threadIdx.x;
+__device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, uint32_t lane) {
+    const NodeTable &t = va.t;
+    const uint32_t n_rows = va.n_rows, n_pods = va.n_pods, seed32 = va.seed32, n_tiles = va.n_tiles;
+    const ms_pod_rec *__restrict__ pods = va.pods;
+    const u64 *__restrict__ tile_keys = va.tile_keys;
+    const uint32_t *__restrict__ tile_flags = va.tile_flags;
+    const u64 *__restrict__ spec = va.spec;
+    const uint32_t *__restrict__ spec_flags = va.spec_flags;
+    const u64 *__restrict__ top4 = va.top4;
+    const int64_t *__restrict__ top4_recs = va.top4_recs;
+    const uint32_t *__restrict__ prev_in = va.prev_in;
+    const int64_t *__restrict__ prev_recs_in = va.prev_recs_in;
+    uint32_t *__restrict__ prev_out = va.prev_out;
+    int64_t *__restrict__ prev_recs_out = va.prev_recs_out;
+    const int carry = va.carry;
+    ms_result *__restrict__ results = va.results;
+    uint32_t *__restrict__ stats = va.stats;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
         if (lane == 0) atomicOr(&stats[0], 1u);
         return;
     }
     MS_VST_DECL
-    // prologue: touched map, pods, speculative winners and their batch-start records (slot p)
+    // prologue, one memory round trip: every load below is issued (from clamped,
+    // always valid addresses; no branches) before the first wait. The records
+    // go global -> LDS directly (no registers); stores past the batch stay
+    // inside the LDS arrays and are never read.
+    constexpr int kPodU = (kSeqBatch * (int)sizeof(ms_pod_rec) / 8) / 64;  // uint2 per lane
+    constexpr int kTopU = (kSeqBatch * kTopK * 8 / 16) / 64;                // uint4 per lane
+    constexpr int kRecU = (kSeqBatch * kTopK * kRecF * 8 / 16) / 64;
+    constexpr int kPrevU = (kPrevCap * kRecF * 8 / 16) / 64;
+    constexpr int kPrevW = (kPrevWords + 63) / 64;  // prev_in words per lane
+    constexpr int kSpecU = kSeqBatch / 64;
+    static_assert(kPodU * 64 * 8 == kSeqBatch * (int)sizeof(ms_pod_rec) && kTopU * 64 * 16 == kSeqBatch * kTopK * 8 &&
+                      kRecU * 64 * 16 == kPrevSlot0 * kRecF * 8 && kPrevU * 64 * 16 == kPrevCap * kRecF * 8 &&
+                      kSpecU * 64 == kSeqBatch,
+                  "prologue copies tile the LDS arrays exactly");
+    lds_dma16<kRecU>(&S.rec[0][0], top4_recs, n_pods * kTopK * kRecF / 2, lane);
+    if (prev_in) lds_dma16<kPrevU>(&S.rec[kPrevSlot0][0], prev_recs_in, kPrevCap * kRecF / 2, lane);
+    const uint32_t n_pod_u = n_pods * (uint32_t)sizeof(ms_pod_rec) / 8, n_top_u = n_pods * kTopK / 2;
+    uint2 vpod[kPodU];
+    uint4 vtop[kTopU];
+    u64 vspec[kSpecU];
+    uint32_t vflag[kSpecU], vprow[kPrevW];
+    {
+        const uint2 *sp = reinterpret_cast<const uint2 *>(pods);
+        const uint4 *st = reinterpret_cast<const uint4 *>(top4);
+#pragma unroll
+        for (int k = 0; k < kPodU; ++k) vpod[k] = sp[min(lane + 64u * k, n_pod_u - 1)];
+#pragma unroll
+        for (int k = 0; k < kTopU; ++k) vtop[k] = st[min(lane + 64u * k, n_top_u - 1)];
+#pragma unroll
+        for (int k = 0; k < kSpecU; ++k) {
+            vspec[k] = spec[min(lane + 64u * k, n_pods - 1)];
+            vflag[k] = spec_flags[min(lane + 64u * k, n_pods - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < kPrevW; ++k) vprow[k] = prev_in ? prev_in[min(lane + 64u * k, (uint32_t)kPrevWords - 1)] : 0u;
+    }
     for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map[i] = 0;
-    for (uint32_t i = lane; i < 3u * kSeqBatch; i += 64) S.bound[i] = 0;
+    for (uint32_t i = lane; i < (uint32_t)kSeqSlots; i += 64) S.bound[i] = 0;
     for (uint32_t i = lane; i < (uint32_t)kClaimCap; i += 64) S.claim[i] = ~0u;
     if (lane == 0) S.n_out = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // nodes the previous batch bound are "touched" here: this batch's speculation
-    // may have read them before or during that batch's write-back
-    const uint32_t n_prev = prev_in ? min(prev_in[0], (uint32_t)kSeqBatch) : 0u;
-    for (uint32_t i = lane; i < n_prev; i += 64) {
-        const uint32_t r = prev_in[1 + i];
-        const uint32_t sl = 2u * kSeqBatch + i;
-        load_rec(S, t, sl, r);
-        uint32_t h = map_hash(r);
-        while (atomicCAS(&S.map[h], 0u, ((r + 1) << 10) | sl) != 0u) h = (h + 1) & (kMapCap - 1);
-    }
-    for (uint32_t i = lane; i < n_pods; i += 64) {
-        S.pods[i] = pods[i];
-        S.spec_key[i] = spec[i];
-        S.spec_flags[i] = spec_flags[i];
+    {
+        uint2 *dp = reinterpret_cast<uint2 *>(S.pods);
+        uint4 *dt = reinterpret_cast<uint4 *>(&S.top4[0][0]);
 #pragma unroll
-        for (int k = 0; k < kTopK; ++k) S.top4[i][k] = top4[(size_t)i * kTopK + k];
+        for (int k = 0; k < kPodU; ++k) dp[lane + 64u * k] = vpod[k];
+#pragma unroll
+        for (int k = 0; k < kTopU; ++k) dt[lane + 64u * k] = vtop[k];
+#pragma unroll
+        for (int k = 0; k < kSpecU; ++k) {
+            S.spec_key[lane + 64u * k] = vspec[k];
+            S.spec_flags[lane + 64u * k] = vflag[k];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the LDS DMA above has landed
+    MS_VST(2);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // the stale nodes are "touched" here: this batch's speculation may have read
+    // them before or during their batches' write-back. Word a >= 2 of prev_in
+    // is stale node a - 2 (the two lists hold distinct rows).
+    const uint32_t n_own_in = prev_in ? (uint32_t)__builtin_amdgcn_readfirstlane((int)vprow[0]) : 0u;
+    const uint32_t n_prev =
+        prev_in ? min(n_own_in + (uint32_t)__builtin_amdgcn_readlane((int)vprow[0], 1), (uint32_t)kPrevCap) : 0u;
+#pragma unroll
+    for (int k = 0; k < kPrevW; ++k) {
+        const uint32_t a = lane + 64u * k;
+        if (a >= 2 && a < n_prev + 2) {
+            const uint32_t r = vprow[k];
+            uint32_t h = map_hash(r);
+            while (atomicCAS(&S.map[h], 0u, ((r + 1) << 10) | (uint32_t)(kPrevSlot0 + a - 2)) != 0u)
+                h = (h + 1) & (kMapCap - 1);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    // each pod's speculative winner slot: its own top-4 record (normally entry 0)
     for (uint32_t i = lane; i < n_pods; i += 64) {
         u64 sk = S.spec_key[i];
-        uint32_t sslot = i;
+        uint32_t sslot = kTopK * i;
         if (sk && n_prev && map_find(S, row_of_key(sk, t.base)) >= 0) {
             // Pipelined: the winner is a node the previous batch bound, so its key
             // is stale. Re-resolve against the current state (nothing of this
@@ -1305,7 +1458,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                 if (es < 0) {
                     if (e > best) {
                         best = e;
-                        bslot = -1;
+                        bslot = (int)(kTopK * i) + k;
                     }
                     done = true;
                     break;
@@ -1319,28 +1472,13 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
             }
             if (done && best != 0) {
                 sk = best;
-                sslot = bslot >= 0 ? (uint32_t)bslot : i;
+                sslot = (uint32_t)bslot;
                 S.spec_key[i] = sk;
             } else {
                 sslot = kForceSlow;  // all four stale (or none feasible now): resolved in order
             }
         }
         S.spec_slot[i] = (uint16_t)sslot;
-        const uint32_t wrow = sk ? row_of_key(sk, t.base) : 0xFFFFFFFFu;
-        if (sk && sslot == i) load_rec(S, t, i, wrow);
-        // the pod's next candidate: first other top-4 entry on a node without a live record
-        uint32_t prow = 0xFFFFFFFFu;
-        for (int k = 0; k < kTopK; ++k) {
-            const u64 e = S.top4[i][k];
-            if (e == 0) break;
-            const uint32_t r = row_of_key(e, t.base);
-            if (r != wrow && map_find(S, r) < 0) {
-                prow = r;
-                break;
-            }
-        }
-        if (prow != 0xFFFFFFFFu) load_rec(S, t, kSeqBatch + i, prow);
-        else S.rec[kSeqBatch + i][F_ROW] = -1;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1381,7 +1519,7 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                 // touched: bound earlier in the batch (a previous batch's node
                 // whose record is in the map is touched only once bound again)
                 const int sl = map_find(S, srow_l);
-                conflict = ss_l == kForceSlow || (sl >= 0 && (sl < 2 * kSeqBatch || S.bound[sl]));
+                conflict = ss_l == kForceSlow || (sl >= 0 && (sl < kPrevSlot0 || S.bound[sl]));
                 if (binds_l) atomicMin(&S.claim[ch], lane);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1402,9 +1540,9 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                     rinfo = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
                 } else {
                     rinfo = MS_CODE_SUCCESS;
-                    if (ss_l == pl) {  // first bind on this node in the batch: its record is slot pl
+                    if (ss_l < (uint32_t)kPrevSlot0) {  // first bind on this node in the batch: pod pl's own record
                         prow = srow_l;
-                        pslot = pl;
+                        pslot = ss_l;
                     }
                     padd = (int)ss_l;
                 }
@@ -1468,16 +1606,19 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                 // assume-on-select: NodeInfo.AddPod on the winner's LDS record
                 const uint32_t row = row_of_key(b, t.base);
                 int sl = wslot;
-                if (sl < 0) {  // untouched winner: its batch-start record (prefetched, or from the table)
-                    sl = kSeqBatch + (int)p;
-                    if ((uint32_t)S.rec[sl][F_ROW] != row) {
-                    ++ctr.miss;
-                    int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
-                    const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
-                    if (lane == (uint32_t)F_ROW) v = row;
-                    if (lane == (uint32_t)F_INV_CPU) v = __float_as_uint(r100(capc));
-                    if (lane == (uint32_t)F_INV_MEM) v = __float_as_uint(r100(capm));
-                    if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
+                if (sl < 0) {  // untouched winner: its batch-start record (pod p's top-4, or from the table)
+                    const u64 hit = __ballot(lane < (uint32_t)kTopK && e == b);
+                    sl = (int)(kTopK * p);
+                    if (hit) {
+                        sl += (int)__builtin_ctzll(hit);
+                    } else {  // (a list scan's winner) into slot 4p: pod p binds elsewhere than its top-4
+                        ++ctr.miss;
+                        int64_t v = lane < (uint32_t)kSpecF ? rec_field(t, row, lane) : 0;
+                        const int64_t capc = readlane64(v, F_ALLOC_CPU), capm = readlane64(v, F_ALLOC_MEM);
+                        if (lane == (uint32_t)F_ROW) v = row;
+                        if (lane == (uint32_t)F_INV_CPU) v = __float_as_uint(r100(capc));
+                        if (lane == (uint32_t)F_INV_MEM) v = __float_as_uint(r100(capm));
+                        if (lane < (uint32_t)kRecF) S.rec[sl][lane] = v;
                     }
                     if (lane == s) {
                         prow = row;
@@ -1491,7 +1632,10 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
                 rinfo = info;
             }
             flush_pending(S, prow, pslot, padd, mypod);
-            MS_VST(3);
+#ifdef MS_VSTAMPS
+            if (ctr.slow == 1) MS_VST(6);  // the batch's first slow pod (cold caches)
+            else MS_VST(3);
+#endif
             i0 = s + 1;
         }
         if (mine) {  // this lane's pod result
@@ -1515,8 +1659,8 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         atomicAdd(&stats[5], ctr.slow);
         atomicAdd(&stats[6], ctr.scan);
     }
-    for (uint32_t sl = lane; sl < 3u * kSeqBatch; sl += 64) {
-        if (!S.bound[sl]) continue;  // not bound in this batch (a prefetch, a previous batch's node)
+    for (uint32_t sl = lane; sl < (uint32_t)kSeqSlots; sl += 64) {
+        if (!S.bound[sl]) continue;  // not bound in this batch (a dead copy, a stale node)
         const int64_t *r = S.rec[sl];
         const uint32_t row = (uint32_t)r[F_ROW];
         t.req_cpu[row] = r[F_REQ_CPU];
@@ -1524,16 +1668,55 @@ __global__ __launch_bounds__(64) void k_validate_seq(NodeTable t, uint32_t n_row
         t.nz_cpu[row] = r[F_NZ_CPU];
         t.nz_mem[row] = r[F_NZ_MEM];
         t.pod_count[row] = (int32_t)r[F_CNT];
-        if (prev_out) prev_out[1 + atomicAdd(&S.n_out, 1u)] = row;
+        if (prev_out) put_stale(prev_out, prev_recs_out, atomicAdd(&S.n_out, 1u), row, r);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (prev_out && lane == 0) prev_out[0] = S.n_out;
+    if (prev_out) {
+        // carried: the previous batch's own binds that this batch did not bind again
+        const uint32_t n_own = S.n_out;
+        if (carry)
+            for (uint32_t i = lane; i < min(n_own_in, (uint32_t)kSeqBatch); i += 64) {
+                const uint32_t sl = kPrevSlot0 + i;
+                if (!S.bound[sl]) put_stale(prev_out, prev_recs_out, atomicAdd(&S.n_out, 1u), (uint32_t)S.rec[sl][F_ROW], S.rec[sl]);
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            prev_out[0] = n_own;
+            prev_out[1] = S.n_out - n_own;
+        }
+    }
 #ifdef MS_VSTAMPS
     MS_VST(5);
     if (lane == 0)
-        for (int i = 0; i < 6; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i, vst.acc[i]);
+        for (int i = 0; i < 7; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i, vst.acc[i]);
 #endif
+}
+
+template <int J>
+__global__ __launch_bounds__(64) void k_validate_seq(SeqArgs va) {
+    __shared__ SeqShared S;
+    validate_batch<J>(S, va, threadIdx.x);
+}
+
+// One step of the single-stream sequential engine: workgroup 0 validates
+// batch k (one wave; the workgroup's LDS is the validator's, so it has a CU to
+// itself) while the other workgroups sweep batch k+1 (a (tile, pod chunk)
+// task per wave, k_sweep_full_topk's work). One launch per batch and no
+// cross-stream hand-off: batch k+1's speculation may predate batch k's binds,
+// which its validation treats as stale (prev lists). W waves per workgroup:
+// the most that fit the validator's VGPRs at one workgroup per CU.
+template <int J, int W>
+__global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks) {
+    __shared__ SeqShared S;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x);
+        return;
+    }
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    for (uint32_t task = (blockIdx.x - 1) * W + wave; task < n_tasks; task += (gridDim.x - 1) * W)
+        sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
 }
 
 // ----------------------------------------------------------------------------
@@ -2158,21 +2341,25 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
     if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::min(64, std::max(1, atoi(e)));
     const dim3 grid(gx, cdiv(n_pods, chunk));
-    hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, t, n_rows, pods, n_pods, chunk, seed32,
-                       tile_keys, tile_flags, n_tiles);
+    const SweepArgs a = {t, n_rows, pods, n_pods, chunk, seed32, tile_keys, tile_flags, n_tiles};
+    hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
                                const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
-                               uint32_t n_tiles, const uint32_t *prev_in, uint32_t *prev_out,
+                               const int64_t *top4_recs, uint32_t n_tiles, const uint32_t *prev_in,
+                               const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
                                ms_result *results, uint32_t *stats, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
-    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
-#define MS_VAL(J)                                                                                          \
-    hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, t, n_rows, pods, n_pods, seed32, tile_keys, \
-                       tile_flags, spec, spec_flags, top4, n_tiles, prev_in, prev_out, results, stats)
+    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || !top4_recs || (prev_in && !prev_recs_in) ||
+        (prev_out && !prev_recs_out))
+        return hipErrorInvalidValue;
+    const SeqArgs va = {t,        n_rows,       pods,     n_pods,        seed32, tile_keys, tile_flags,
+                        spec,     spec_flags,   top4,     top4_recs,     n_tiles, prev_in,  prev_recs_in,
+                        prev_out, prev_recs_out, carry,   results,       stats};
+#define MS_VAL(J) hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, va)
     if (n_tiles <= 64) MS_VAL(1);
     else if (n_tiles <= 128) MS_VAL(2);
     else if (n_tiles <= 256) MS_VAL(4);
@@ -2182,14 +2369,49 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
     return hipGetLastError();
 }
 
+hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles, uint32_t seed32,
+                           const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *tile_keys,
+                           const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
+                           const unsigned long long *top4, const int64_t *top4_recs, const uint32_t *prev_in,
+                           const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
+                           ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
+                           unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
+                           hipStream_t s) {
+    if (n_pods == 0 && n_next == 0) return hipSuccess;
+    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
+        (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
+        return hipErrorInvalidValue;
+    const SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
+                        spec,     spec_flags,   top4,    top4_recs,  n_tiles, prev_in, prev_recs_in,
+                        prev_out, prev_recs_out, 0,      results,    stats};
+    // tasks: (tile, chunk of next pods) pairs, sized to fit one pass of the
+    // sweep workgroups (one per CU beside the validator's)
+    const uint32_t cus = (uint32_t)(num_cus > 1 ? num_cus : 256);
+    const int J = n_tiles <= 64 ? 1 : n_tiles <= 128 ? 2 : n_tiles <= 256 ? 4 : n_tiles <= 512 ? 8 : 16;
+    const uint32_t W = J <= 4 ? 12u : J == 8 ? 8u : 4u;
+    uint32_t chunk = 8;
+    if (n_next) chunk = std::min(64u, std::max(8u, cdiv(n_tiles * n_next, (cus - 1) * W)));
+    const SweepArgs sw = {t, n_rows, next_pods, n_next, chunk, seed32, next_tile_keys, next_tile_flags, n_tiles};
+    const uint32_t n_tasks = n_next ? n_tiles * cdiv(n_next, chunk) : 0u;
+    const uint32_t grid = 1u + std::min(cus - 1, cdiv(n_tasks, W));
+#define MS_STEP(JJ, WW) hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks)
+    if (J == 1) MS_STEP(1, 12);
+    else if (J == 2) MS_STEP(2, 12);
+    else if (J == 4) MS_STEP(4, 12);
+    else if (J == 8) MS_STEP(8, 8);
+    else MS_STEP(16, 4);
+#undef MS_STEP
+    return hipGetLastError();
+}
+
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
                              uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
-                             hipStream_t s) {
+                             const NodeTable &t, int64_t *recs, hipStream_t s) {
     if (n_pods == 0 || n_tiles == 0) return hipSuccess;
     if (n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
 #define MS_MERGE(J)                                                                                           \
     hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, tile_flags, n_pods, n_tiles, top, \
-                       spec, spec_flags)
+                       spec, spec_flags, t, recs)
     if (n_tiles <= 64) MS_MERGE(1);
     else if (n_tiles <= 128) MS_MERGE(2);
     else if (n_tiles <= 256) MS_MERGE(4);
@@ -2276,6 +2498,8 @@ hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms
 }
 
 uint32_t seq_batch_limit() { return (uint32_t)kSeqBatch; }
+uint32_t seq_rec_fields() { return (uint32_t)kRecF; }
+uint32_t seq_prev_cap() { return (uint32_t)kPrevCap; }
 uint32_t seq_topk() { return (uint32_t)kTopK; }
 
 }  // namespace msgpu

@@ -360,10 +360,14 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
     const uint32_t waves_needed = std::max(1u, cdiv(n_groups, kPpWaveGroups));
-    // large shards: 16-wave workgroups (2 per CU = 8 waves per SIMD; the groups
-    // are dealt round-robin, so every wave holds 3 or 4 words); small shards:
-    // the fewest waves that hold the rows (profiles/r02c_ab.json)
-    uint32_t W = waves_needed >= 9 ? kPpMaxWaves : waves_needed;
+    // W a power of two (32 / W workgroups per CU fill all 8 wave slots per
+    // SIMD; W = 7 leaves one idle and was 9% slower at 50k rows): large shards
+    // 16-wave workgroups (the groups are dealt round-robin, so every wave holds
+    // 3 or 4 words), shards of 257..2048 groups at least 4 waves
+    // (profiles/r02c_ab.json, r02j_ab_shard_waves.jsonl)
+    uint32_t W = 1;
+    if (waves_needed > 1)
+        while (W < std::max(4u, waves_needed) && W < (uint32_t)kPpMaxWaves) W *= 2;
     if (const char *w = getenv("MINISCHED_PP_WAVES")) W = (uint32_t)std::min(16, std::max(1, atoi(w)));
     if (!keys) W = std::max(W, std::min<uint32_t>(kPpMaxWaves, waves_needed));  // no scratch: one workgroup per chunk
     const uint32_t gy = std::max(1u, cdiv(n_groups, W * kPpWaveGroups));

@@ -300,12 +300,14 @@ def test_chunked_batches(oracle):
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
 
 
-@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("pipe", ["fused", "2", "1", "0"])
 @pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
 def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch, pipe):
     # speculative batch boundaries must not change placements: 50 nodes (one
-    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted); with and
-    # without the next batch's speculation overlapping validation
+    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted); the
+    # default single-stream steps (validation k beside the sweep of k+1), and
+    # two streams with the speculation overlapping two validations (2), one
+    # (1) or none (0); 256 is clamped to the validator's 128
     monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
     monkeypatch.setenv("MINISCHED_SEQ_PIPE", pipe)
     for n_nodes, n_pods in ((50, 600), (2500, 3000)):

@@ -40,6 +40,30 @@ int main(int argc, char **argv) {
     CK(hipExtMallocWithFlags((void **)&sig, 8, hipMallocSignalMemory));
     CK(hipMemset(sig, 0, 8));
     CK(hipDeviceSynchronize());
+    if (mode == 3) {  // the same pattern captured into a graph (fork/join through events), launched per iteration
+        hipEvent_t fork;
+        CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        hipGraphExec_t ge[2];
+        for (int odd = 0; odd < 2; ++odd) {
+            hipGraph_t g;
+            CK(hipStreamBeginCapture(s2, hipStreamCaptureModeGlobal));
+            CK(hipEventRecord(fork, s2));
+            CK(hipStreamWaitEvent(s1, fork, 0));
+            k_busy<<<1, 64, 0, s2>>>(odd ? 100000u : 12000u, nullptr, 0);
+            k_busy<<<1, 64, 0, s1>>>(50000u, nullptr, 0);
+            CK(hipEventRecord(ev, s1));
+            CK(hipStreamWaitEvent(s2, ev, 0));
+            k_busy<<<1, 64, 0, s2>>>(2000u, nullptr, 0);
+            CK(hipStreamEndCapture(s2, &g));
+            CK(hipGraphInstantiate(&ge[odd], g, nullptr, nullptr, 0));
+        }
+        for (int it = 1; it <= 200; ++it) {
+            CK(hipGraphLaunch(ge[it & 1], s2));
+            CK(hipDeviceSynchronize());
+        }
+        std::printf("mode %d done\n", mode);
+        return 0;
+    }
     for (int it = 1; it <= 200; ++it) {
         // C on s2: ~40 us (odd) or ~5 us (even); A on s1: ~20 us; then B on s2 after the hand-off
         k_busy<<<1, 64, 0, s2>>>(it & 1 ? 100000u : 12000u, nullptr, 0);

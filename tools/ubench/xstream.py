@@ -1,25 +1,20 @@
-"""Gap between kernel A's end (stream 1) and kernel B's start (stream 2) in a
-rocprofv3 kernel trace of tools/ubench/xstream (python tools/ubench/xstream.py trace.csv)."""
+"""Gap between kernel B's start and the end of the kernels it waits for, in a
+rocprofv3 kernel trace of tools/ubench/xstream (python tools/ubench/xstream.py trace.csv).
+Per iteration the dispatches are C (s2), A (s1), B (s2, after A via the hand-off);
+kernels are matched by dispatch order (the trace's stream ids are not reliable)."""
 import csv
 import statistics
 import sys
 
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-# per iteration: C (s2), A (s1), B (s2), dispatched in that order
-ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Stream_Id"])) for r in rows]
-by_stream = {}
-for s, e, q in ks:
-    by_stream.setdefault(q, []).append((s, e))
-qs = sorted(by_stream, key=lambda q: len(by_stream[q]))
-a_list = by_stream[qs[0]]  # stream 1: A only
-cb = by_stream[qs[-1]]  # stream 2: C, B alternating
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Dispatch_Id"]))
+ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
 gaps_after_a, gaps_after_c = [], []
-for i, (a_s, a_e) in enumerate(a_list[5:], start=5):
-    c_s, c_e = cb[2 * i]
-    b_s, b_e = cb[2 * i + 1]
+for i in range(5, len(ks) // 3):
+    (c_s, c_e), (a_s, a_e), (b_s, b_e) = ks[3 * i], ks[3 * i + 1], ks[3 * i + 2]
     if c_e > a_e:
         gaps_after_c.append((b_s - c_e) / 1e3)
     else:
         gaps_after_a.append((b_s - a_e) / 1e3)
-print(f"B start after A end (A last):  median {statistics.median(gaps_after_a):.2f} us  n={len(gaps_after_a)}")
-print(f"B start after C end (C last):  median {statistics.median(gaps_after_c):.2f} us  n={len(gaps_after_c)}")
+for name, g in (("A last (waiting on the hand-off)", gaps_after_a), ("C last (hand-off already signalled)", gaps_after_c)):
+    if g:
+        print(f"B start - end of {name}: median {statistics.median(g):.2f} us  n={len(g)}")
