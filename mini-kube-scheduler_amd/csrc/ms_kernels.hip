@@ -1041,7 +1041,7 @@ static_assert(kSeqSlots <= 1024, "map entries hold a 10-bit slot");
 // this batch's speculation may predate those binds), as the previous batch's
 // validator left them. A node has at most one live slot: the map's.
 struct SeqShared {
-    uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
+    alignas(16) uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
     int64_t rec[kSeqSlots][kRecF];
     uint8_t bound[kSeqSlots];  // slot was bound in this batch
     uint32_t n_out;
@@ -1049,7 +1049,7 @@ struct SeqShared {
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
     uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
     u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
-    uint32_t claim[kClaimCap];       // per round: lowest lane whose speculative winner hashes here
+    alignas(16) uint32_t claim[kClaimCap];  // per round: lowest lane whose speculative winner hashes here
     uint16_t spec_slot[kSeqBatch];   // slot of the speculative winner's record (kForceSlow: unresolved)
 };
 static_assert(sizeof(SeqShared) <= 160 * 1024, "validator LDS");
@@ -1374,7 +1374,10 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                       kSpecU * 64 == kSeqBatch,
                   "prologue copies tile the LDS arrays exactly");
     lds_dma16<kRecU>(&S.rec[0][0], top4_recs, n_pods * kTopK * kRecF / 2, lane);
-    if (prev_in) lds_dma16<kPrevU>(&S.rec[kPrevSlot0][0], prev_recs_in, kPrevCap * kRecF / 2, lane);
+    if (prev_in) {  // (a writer without carry left at most kSeqBatch entries)
+        if (carry) lds_dma16<kPrevU>(&S.rec[kPrevSlot0][0], prev_recs_in, kPrevCap * kRecF / 2, lane);
+        else lds_dma16<kPrevU / 2>(&S.rec[kPrevSlot0][0], prev_recs_in, kSeqBatch * kRecF / 2, lane);
+    }
     const uint32_t n_pod_u = n_pods * (uint32_t)sizeof(ms_pod_rec) / 8, n_top_u = n_pods * kTopK / 2;
     uint2 vpod[kPodU];
     uint4 vtop[kTopU];
@@ -1395,9 +1398,10 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 #pragma unroll
         for (int k = 0; k < kPrevW; ++k) vprow[k] = prev_in ? prev_in[min(lane + 64u * k, (uint32_t)kPrevWords - 1)] : 0u;
     }
-    for (uint32_t i = lane; i < (uint32_t)kMapCap; i += 64) S.map[i] = 0;
+    for (uint32_t i = lane; i < (uint32_t)kMapCap / 4; i += 64) reinterpret_cast<uint4 *>(S.map)[i] = make_uint4(0, 0, 0, 0);
     for (uint32_t i = lane; i < (uint32_t)kSeqSlots; i += 64) S.bound[i] = 0;
-    for (uint32_t i = lane; i < (uint32_t)kClaimCap; i += 64) S.claim[i] = ~0u;
+    for (uint32_t i = lane; i < (uint32_t)kClaimCap / 4; i += 64)
+        reinterpret_cast<uint4 *>(S.claim)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     if (lane == 0) S.n_out = 0;
     {
         uint2 *dp = reinterpret_cast<uint2 *>(S.pods);
