@@ -373,6 +373,8 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     const uint32_t gy = std::max(1u, cdiv(n_groups, W * kPpWaveGroups));
     const uint32_t per_cu = std::max(1u, 32u / W);
     const uint32_t resident = per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256) / gy;
+    // (multiples of 8: a wave takes pods 8 at a time, and a part-filled 8 costs
+    // a full one -- exact chunks ran 11% slower at 25k rows, r02k_ab_chunk.txt)
     uint32_t chunk = cdiv(cdiv(n_pods, std::max(1u, resident)), 8) * 8;
     if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
