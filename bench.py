@@ -58,8 +58,8 @@ PP_KERNEL = "k_sweep_nunn_pp"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)  # (N = 8: ~65 us a step; amortises pipeline fill and barriers)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C", choices=["B", "C", "D"])
     ap.add_argument("--split", default=None, choices=["nodes", "pods"],
                     help="N > 1 partition (default: nodes for B/C, pods for D)")

@@ -942,17 +942,13 @@ __device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int6
     for (int f = 0; f < kRecF; f += 2) d[f / 2] = make_longlong2(v[f], v[f + 1]);
 }
 
-// Per pod (one wave): merge the tiles' top-4 lists into the global top-4, the
-// speculative winner and the no-feasible-row filter flags; recs (optional)
-// gets the batch-start records of the four entries for the in-order validator.
+// One wave merges pod p's tile lists: lane r < 4 gets the global rank-r key
+// (out, 0 past the feasible rows), f the filters of the tiles with no feasible
+// row (bit0 NodeUnschedulable, bit8 NodeResourcesFit; wave-uniform).
 template <int J>
-__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
-                                                   const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
-                                                   uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
-                                                   uint32_t *__restrict__ spec_flags, NodeTable t,
-                                                   int64_t *__restrict__ recs) {
-    const uint32_t p = blockIdx.x, lane = threadIdx.x;
-    if (p >= n_pods) return;
+__device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_keys,
+                                                const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
+                                                uint32_t lane, u64 &out, uint32_t &f) {
     u64 e[J][kTopK];
     uint32_t pos[J];
     uint32_t fl = 0;  // filters of this lane's tiles that have no feasible row
@@ -970,7 +966,7 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         e[j][3] = ((u64)b.w << 32) | b.z;
         if (tt < n_tiles && e[j][0] == 0) fl |= tf;
     }
-    u64 out = 0;
+    out = 0;
 #pragma unroll
     for (int r = 0; r < kTopK; ++r) {
         u64 head = 0;  // this lane's best list head
@@ -989,10 +985,26 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         if (lane == (uint32_t)r) out = m;
         if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
     }
+    f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+}
+
+// Per pod (one wave): merge the tiles' top-4 lists into the global top-4, the
+// speculative winner and the no-feasible-row filter flags; recs (optional)
+// gets the batch-start records of the four entries for the in-order validator.
+template <int J>
+__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
+                                                   const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
+                                                   uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
+                                                   uint32_t *__restrict__ spec_flags, NodeTable t,
+                                                   int64_t *__restrict__ recs) {
+    const uint32_t p = blockIdx.x, lane = threadIdx.x;
+    if (p >= n_pods) return;
+    u64 out;
+    uint32_t f;
+    merge_pod_lists<J>(tile_keys, tile_flags, p, n_tiles, lane, out, f);
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
     if (recs && lane < (uint32_t)kTopK) store_merged_rec(t, out, recs + ((size_t)p * kTopK + lane) * kRecF);
     // the speculative winner (rank 0) and, when no row is feasible, the filters
-    const uint32_t f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
     if (lane == 0) {
         spec[p] = out;
         spec_flags[p] = f;
@@ -1493,13 +1505,19 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     MS_VST(0);
 
     // Pods go in groups of 64, lane i <-> pod g+i, decided in rounds. A round
-    // takes the group's undecided pods i0.. in parallel: the first one whose
-    // speculative winner is touched (in the map: bound earlier in the batch) or
-    // is claimed by an earlier undecided pod (hash claim; collisions only make
-    // false conflicts) is the round's slow pod s. Pods i0..s-1 take their
-    // speculative outcome, exact (current keys never exceed speculative ones and
-    // their winners are distinct and untouched) and bind at once; pod s is
-    // resolved alone against current state; the next round starts at s+1.
+    // takes the group's undecided pods i0.. in parallel, each with its winner
+    // against the state at the round's start: the speculative winner while its
+    // node is untouched (not bound in this batch; current keys never exceed
+    // speculative ones), else re-resolved from its top-4 on the lane itself
+    // (touched entries re-evaluated from their LDS records, the first untouched
+    // one exact and bounding every row below it). The first pod whose winner is
+    // claimed by an earlier undecided pod (hash claim; collisions only make
+    // false conflicts) or that needs its tile lists (four touched entries in a
+    // full list, or no feasible node left) is the round's stop s. Pods i0..s-1
+    // take their winners and bind at once: their winners are distinct, and a
+    // bind only lowers its own node's keys. A claimed pod s is re-resolved in the
+    // next round, which starts at s; a pod that needs its lists is resolved
+    // alone (below) and the next round starts at s+1.
     for (uint32_t g = 0; g < n_pods; g += 64) {
         const uint32_t gn = min(64u, n_pods - g);
         const bool mine = lane < gn;
@@ -1507,9 +1525,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         const u64 sk_l = mine ? S.spec_key[pl] : 0ull;
         const uint32_t srow_l = sk_l ? row_of_key(sk_l, t.base) : 0xFFFFFFFEu;
         const int dig_l = mine ? (int)S.pods[pl].name_digit : 0;
-        const bool binds_l = sk_l != 0 && dig_l >= 0;  // binds at its speculative winner if that is exact
         const uint32_t ss_l = mine ? (uint32_t)S.spec_slot[pl] : 0u;
-        const uint32_t ch = claim_hash(srow_l);
         const ms_pod_rec &mypod = S.pods[pl];
         uint32_t prow = 0xFFFFFFFFu, pslot = 0;  // this lane's pending map insert
         int padd = -1;                           // and pending AddPod (flush_pending)
@@ -1518,23 +1534,64 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         MS_VST(1);
         for (uint32_t i0 = 0; i0 < gn;) {
             const bool act = mine && lane >= i0 && sk_l != 0;
-            bool conflict = false;
+            u64 ck = 0;                          // winner key against the round-start state
+            uint32_t cslot = 0, crow = 0xFFFFFFFEu;
+            bool cins = false, need = false;     // first bind on an untouched node / needs the lists
             if (act) {
                 // touched: bound earlier in the batch (a previous batch's node
                 // whose record is in the map is touched only once bound again)
                 const int sl = map_find(S, srow_l);
-                conflict = ss_l == kForceSlow || (sl >= 0 && (sl < kPrevSlot0 || S.bound[sl]));
-                if (binds_l) atomicMin(&S.claim[ch], lane);
+                if (ss_l != kForceSlow && !(sl >= 0 && (sl < kPrevSlot0 || S.bound[sl]))) {
+                    ck = sk_l;
+                    cslot = ss_l;
+                    crow = srow_l;
+                    cins = ss_l < (uint32_t)kPrevSlot0;  // pod pl's own record of an untouched node
+                } else {
+                    const PodFull q = load_pod(mypod, seed32);
+                    bool untouched = false, listend = false;
+                    for (int r = 0; r < kTopK; ++r) {
+                        const u64 e = S.top4[pl][r];
+                        if (e == 0) {  // list ended: every feasible row was listed
+                            listend = true;
+                            break;
+                        }
+                        const uint32_t er = row_of_key(e, t.base);
+                        const int es = map_find(S, er);
+                        if (es < 0) {
+                            if (e > ck) {
+                                ck = e;
+                                cslot = kTopK * pl + (uint32_t)r;
+                                cins = true;
+                            }
+                            untouched = true;
+                            break;
+                        }
+                        uint32_t nu, nrf;
+                        const u64 v = eval_full(slot_row(S, es), er + t.base, q, nu, nrf);
+                        ++ctr.recompute;
+                        if (v > ck) {
+                            ck = v;
+                            cslot = (uint32_t)es;
+                            cins = false;
+                        }
+                    }
+                    need = (!untouched && !listend) || ck == 0;
+                    crow = ck ? row_of_key(ck, t.base) : 0xFFFFFFFEu;
+                }
             }
+            const bool claims = act && !need && dig_l >= 0;  // binds at ck if decided this round
+            const uint32_t ch = claim_hash(crow);
+            if (claims) atomicMin(&S.claim[ch], lane);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (act) conflict = conflict || S.claim[ch] < lane;
-            const u64 bad = __ballot(act && conflict);
+            const bool conflict = act && (need || (claims && S.claim[ch] < lane));
+            const u64 bad = __ballot(conflict);
             const uint32_t s = bad ? (uint32_t)__builtin_ctzll(bad) : gn;
+            const bool serial = bad && ((__ballot(need) >> s) & 1ull);
             __builtin_amdgcn_wave_barrier();
-            if (act && binds_l) S.claim[ch] = ~0u;  // (every lane read its bucket above)
-            if (mine && lane >= i0 && lane < s) {  // speculative outcome, exact
-                rk = sk_l;
+            if (claims) S.claim[ch] = ~0u;  // (every lane read its bucket above)
+            if (mine && lane >= i0 && lane < s) {  // decided: exact against the round-start state
+                rk = ck;
                 if (sk_l == 0) {  // no feasible row at speculation: none now either
                     const uint32_t fm = S.spec_flags[pl];
                     rinfo = MS_CODE_UNSCHEDULABLE | ((((fm & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
@@ -1544,16 +1601,20 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                     rinfo = MS_CODE_ERROR;  // NodeNumber.Score fails (nodenumber.go:74-77); nothing binds
                 } else {
                     rinfo = MS_CODE_SUCCESS;
-                    if (ss_l < (uint32_t)kPrevSlot0) {  // first bind on this node in the batch: pod pl's own record
-                        prow = srow_l;
-                        pslot = ss_l;
+                    if (cins) {  // first bind on this node in the batch: pod pl's own record
+                        prow = crow;
+                        pslot = cslot;
                     }
-                    padd = (int)ss_l;
+                    padd = (int)cslot;
                 }
             }
             flush_pending(S, prow, pslot, padd, mypod);
             MS_VST(4);
             if (s == gn) break;
+            if (!serial) {  // claimed: re-resolved next round (then first, so unclaimed)
+                i0 = s;
+                continue;
+            }
             // ---- slow pod p: resolved against current state
             const uint32_t p = g + s;
             ++ctr.slow;
