@@ -802,6 +802,19 @@ __device__ __forceinline__ u64 wave_max_u64_dpp(u64 v) {
     return ((u64)hmax << 32) | lmax;
 }
 
+// Max over each quad of lanes (4i .. 4i+3), every lane of the quad gets it.
+template <int CTRL>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ u64 quad_max_u64(u64 v) {
+    v = umax64(v, dpp_u64<0xB1>(v));     // quad_perm [1,0,3,2]
+    return umax64(v, dpp_u64<0x4E>(v));  // quad_perm [2,3,0,1]
+}
+
 __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
     const u64 hi = umax64(a, b), lo = a > b ? b : a;
     a = hi;
@@ -817,45 +830,65 @@ __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
 constexpr int kTopK = 4;
 static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
 
+// NP pods at a time: their evaluations, sorts and wave reductions are
+// independent, so the DPP chains of one hide the latency of the other's (3
+// waves per SIMD leave little else to hide it).
+template <bool kHuge, int NP>
+__device__ __forceinline__ void sweep_topk_group(const FullRow *x, uint32_t ord0, const PodLanes &m, uint32_t pbeg,
+                                                 uint32_t i, uint32_t lane, uint32_t tile, uint32_t n_tiles,
+                                                 u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
+    u64 k[NP][kFullSlots], out[NP];
+    uint32_t nu_any[NP], nrf_any[NP];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        const PodFull q = pod_of_lane(m, i + n);
+        nu_any[n] = nrf_any[n] = 0;
+#pragma unroll
+        for (int s = 0; s < kFullSlots; ++s) {
+            uint32_t nu, nrf;
+            k[n][s] = eval_full<kHuge>(x[s], ord0 + s, q, nu, nrf);
+            nu_any[n] |= nu;
+            nrf_any[n] |= nrf;
+        }
+        // descending sort of the lane's 4 keys (keys are unique unless 0)
+        cswap_desc(k[n][0], k[n][1]);
+        cswap_desc(k[n][2], k[n][3]);
+        cswap_desc(k[n][0], k[n][2]);
+        cswap_desc(k[n][1], k[n][3]);
+        cswap_desc(k[n][1], k[n][2]);
+        out[n] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kTopK; ++j) {
+#pragma unroll
+        for (int n = 0; n < NP; ++n) {
+            const u64 mx = wave_max_u64_dpp(k[n][0]);
+            if (lane == (uint32_t)j) out[n] = mx;
+            if (mx != 0 && k[n][0] == mx) {  // the owning lane pops its head
+                k[n][0] = k[n][1];
+                k[n][1] = k[n][2];
+                k[n][2] = k[n][3];
+                k[n][3] = 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+        const uint32_t f = (__ballot(nu_any[n] != 0) ? 1u : 0u) | (__ballot(nrf_any[n] != 0) ? 0x100u : 0u);
+        const size_t cell = (size_t)(pbeg + i + n) * n_tiles + tile;
+        if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out[n];
+        if (lane == 0) tile_flags[cell] = f;
+    }
+}
+
 template <bool kHuge>
 __device__ __forceinline__ void sweep_topk_pods(const FullRow *x, uint32_t ord0, const PodLanes &m, uint32_t pbeg,
                                                 uint32_t cnt, uint32_t lane, uint32_t tile, uint32_t n_tiles,
                                                 u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
-    for (uint32_t i = 0; i < cnt; ++i) {
-        const uint32_t p = pbeg + i;
-        const PodFull q = pod_of_lane(m, i);
-        u64 k[kFullSlots];
-        uint32_t nu_any = 0, nrf_any = 0;
-#pragma unroll
-        for (int s = 0; s < kFullSlots; ++s) {
-            uint32_t nu, nrf;
-            k[s] = eval_full<kHuge>(x[s], ord0 + s, q, nu, nrf);
-            nu_any |= nu;
-            nrf_any |= nrf;
-        }
-        // descending sort of the lane's 4 keys (keys are unique unless 0)
-        cswap_desc(k[0], k[1]);
-        cswap_desc(k[2], k[3]);
-        cswap_desc(k[0], k[2]);
-        cswap_desc(k[1], k[3]);
-        cswap_desc(k[1], k[2]);
-        u64 out = 0;
-#pragma unroll
-        for (int j = 0; j < kTopK; ++j) {
-            const u64 mx = wave_max_u64_dpp(k[0]);
-            if (lane == (uint32_t)j) out = mx;
-            if (mx != 0 && k[0] == mx) {  // the owning lane pops its head
-                k[0] = k[1];
-                k[1] = k[2];
-                k[2] = k[3];
-                k[3] = 0;
-            }
-        }
-        const uint32_t f = (__ballot(nu_any != 0) ? 1u : 0u) | (__ballot(nrf_any != 0) ? 0x100u : 0u);
-        const size_t cell = (size_t)p * n_tiles + tile;
-        if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out;
-        if (lane == 0) tile_flags[cell] = f;
-    }
+    uint32_t i = 0;
+    for (; i + 2 <= cnt; i += 2)
+        sweep_topk_group<kHuge, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
+    if (i < cnt) sweep_topk_group<kHuge, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
 }
 
 struct SweepArgs {
@@ -1052,10 +1085,16 @@ static_assert(kSeqSlots <= 1024, "map entries hold a 10-bit slot");
 // stale nodes: those the previous one or two batches bound (pipelined mode:
 // this batch's speculation may predate those binds), as the previous batch's
 // validator left them. A node has at most one live slot: the map's.
+struct WalkResult {
+    u64 key;        // winner against the current state (0: none feasible among the listed)
+    uint32_t slot;  // its record slot
+    uint32_t flags; // bit0: untouched node (first bind inserts the map entry), bit1: needs the tile lists
+};
+
 struct SeqShared {
     alignas(16) uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
     int64_t rec[kSeqSlots][kRecF];
-    uint8_t bound[kSeqSlots];  // slot was bound in this batch
+    alignas(16) uint8_t bound[kSeqSlots];  // binds on the slot in this batch (<= 128: no wrap)
     uint32_t n_out;
     ms_pod_rec pods[kSeqBatch];
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
@@ -1063,6 +1102,9 @@ struct SeqShared {
     u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
     alignas(16) uint32_t claim[kClaimCap];  // per round: lowest lane whose speculative winner hashes here
     uint16_t spec_slot[kSeqBatch];   // slot of the speculative winner's record (kForceSlow: unresolved)
+    uint32_t walk[16];               // a round's re-resolution pass: lanes whose pod walks its top-4
+    uint16_t bl[kSeqBatch];          // write-back: the slots bound in this batch (one per binding pod at most)
+    WalkResult walkres[16];          // and each one's winner
 };
 static_assert(sizeof(SeqShared) <= 160 * 1024, "validator LDS");
 
@@ -1161,7 +1203,7 @@ __device__ __forceinline__ void load_lists(TileLists<J> &B, const u64 *__restric
 }
 
 struct SeqCounters {
-    uint32_t recompute, resweep, miss, slow, scan;
+    uint32_t recompute, resweep, miss, slow, scan, rounds;
 };
 
 
@@ -1254,6 +1296,71 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
     wslot_out = own ? __builtin_amdgcn_readlane(best_slot, (int)__builtin_ctzll(own)) : -1;
 }
 
+// Re-resolution of the pods of the lanes with `walk` set (pod index `pod`),
+// 16 pods per pass with lane 4i + r on entry r of the pass's pod i: touched
+// entries (in the map) are re-evaluated from their LDS records, the first
+// untouched one is exact and bounds every row below it. Out, per walking lane:
+// ck (0: no listed node feasible now), its slot, cins (untouched: the pod's
+// own record slot, whose first bind inserts the map entry) and need (four
+// touched entries in a full list, or none feasible: the tile lists decide).
+// Called by the whole wave (wave-uniform passes); clears `walk`.
+__device__ __forceinline__ void walk_top4(SeqShared &S, const NodeTable &t, uint32_t seed32, bool &walk, uint32_t pod,
+                                          u64 &ck, uint32_t &cslot, bool &cins, bool &need, SeqCounters &ctr) {
+    const uint32_t lane = lane_id();
+    for (u64 wm = __ballot(walk); wm;) {
+        const uint32_t nw = min(16u, (uint32_t)__builtin_popcountll(wm));
+        const uint32_t rank = (uint32_t)__builtin_popcountll(wm & ((1ull << lane) - 1ull));
+        if (walk && rank < 16u) S.walk[rank] = pod;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t qi = lane >> 2, r = lane & 3u;
+        u64 v = 0;
+        uint32_t vs = 0;
+        bool unt = false, end = false;
+        if (qi < nw) {
+            const uint32_t pw = S.walk[qi];
+            const u64 e = S.top4[pw][r];
+            if (e == 0) {
+                end = true;  // list ended: every feasible row was listed
+            } else {
+                const uint32_t er = row_of_key(e, t.base);
+                const int es = map_find(S, er);
+                if (es < 0) {
+                    unt = true;
+                    v = e;
+                    vs = kTopK * pw + r;
+                } else {
+                    uint32_t nu, nrf;
+                    v = eval_full(slot_row(S, es), er + t.base, load_pod(S.pods[pw], seed32), nu, nrf);
+                    vs = (uint32_t)es;
+                    ++ctr.recompute;
+                }
+            }
+        }
+        // entries past the quad's first untouched-or-end entry do not count
+        const uint32_t qb = (uint32_t)(__ballot(unt || end) >> (4u * qi)) & 0xFu;
+        const uint32_t f = qb ? (uint32_t)__builtin_ctz(qb) : 4u;
+        const bool valid = qi < nw && !end && (r < f || (r == f && unt));
+        const u64 ve = valid ? v : 0ull;
+        const u64 m = quad_max_u64(ve);
+        const uint32_t own = (uint32_t)(__ballot(valid && m != 0 && ve == m) >> (4u * qi)) & 0xFu;
+        if (qi < nw && r == (own ? (uint32_t)__builtin_ctz(own) : 0u))
+            S.walkres[qi] = {m, vs, (unt && m != 0 ? 1u : 0u) | ((f == 4u || m == 0) ? 2u : 0u)};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (walk && rank < 16u) {
+            const WalkResult w = S.walkres[rank];
+            ck = w.key;
+            cslot = w.slot;
+            cins = (w.flags & 1u) != 0;
+            need = (w.flags & 2u) != 0;
+            walk = false;
+        }
+        __builtin_amdgcn_wave_barrier();
+        wm = __ballot(walk);
+    }
+}
+
 // Deferred bind effects of a 64-pod group, lane i <-> pod i of the group:
 //  prow/pslot: the (row, slot) map entry of a node pod i bound first in the batch;
 //  padd: the slot pod i bound to, whose record still lacks pod i's NodeInfo.AddPod.
@@ -1274,7 +1381,7 @@ __device__ __forceinline__ void flush_pending(SeqShared &S, uint32_t &prow, uint
         atomicAdd(&r[F_NZ_CPU], (unsigned long long)mypod.nonzero_milli_cpu);
         atomicAdd(&r[F_NZ_MEM], (unsigned long long)mypod.nonzero_memory);
         atomicAdd(&r[F_CNT], 1ull);
-        S.bound[padd] = 1;
+        S.bound[padd] = (uint8_t)(S.bound[padd] + 1u);  // (decided lanes bind distinct slots)
         padd = -1;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1291,9 +1398,9 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, uint32_t l) {
 // over the batch, land in stats[8..] (u64), printed at ms_destroy.
 #ifdef MS_VSTAMPS
 struct VStamps {
-    u64 prev, acc[7];
+    u64 prev, acc[9];
 };
-#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0, 0}};
+#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0, 0, 0, 0}};
 #define MS_VST(i)                                               \
     do {                                                        \
         __builtin_amdgcn_sched_barrier(0);                      \
@@ -1411,7 +1518,8 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         for (int k = 0; k < kPrevW; ++k) vprow[k] = prev_in ? prev_in[min(lane + 64u * k, (uint32_t)kPrevWords - 1)] : 0u;
     }
     for (uint32_t i = lane; i < (uint32_t)kMapCap / 4; i += 64) reinterpret_cast<uint4 *>(S.map)[i] = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = lane; i < (uint32_t)kSeqSlots; i += 64) S.bound[i] = 0;
+    static_assert(kSeqSlots % 16 == 0, "bound[] is cleared 16 slots per lane");
+    for (uint32_t i = lane; i < (uint32_t)kSeqSlots / 16; i += 64) reinterpret_cast<uint4 *>(S.bound)[i] = make_uint4(0, 0, 0, 0);
     for (uint32_t i = lane; i < (uint32_t)kClaimCap / 4; i += 64)
         reinterpret_cast<uint4 *>(S.claim)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     if (lane == 0) S.n_out = 0;
@@ -1450,58 +1558,39 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // each pod's speculative winner slot: its own top-4 record (normally entry 0)
-    for (uint32_t i = lane; i < n_pods; i += 64) {
-        u64 sk = S.spec_key[i];
-        uint32_t sslot = kTopK * i;
-        if (sk && n_prev && map_find(S, row_of_key(sk, t.base)) >= 0) {
-            // Pipelined: the winner is a node the previous batch bound, so its key
-            // is stale. Re-resolve against the current state (nothing of this
-            // batch is bound yet) from the top-4: previous-batch entries are
-            // re-evaluated from their records, the first other entry is exact
-            // and bounds every row below it.
-            const PodFull q = load_pod(S.pods[i], seed32);
-            u64 best = 0;
-            int bslot = -1;
-            bool done = false;
-            for (int k = 0; k < kTopK && !done; ++k) {
-                const u64 e = S.top4[i][k];
-                if (e == 0) {  // list ended: every feasible row was listed
-                    done = true;
-                    break;
-                }
-                const int es = map_find(S, row_of_key(e, t.base));
-                if (es < 0) {
-                    if (e > best) {
-                        best = e;
-                        bslot = (int)(kTopK * i) + k;
-                    }
-                    done = true;
-                    break;
-                }
-                uint32_t nu, nrf;
-                const u64 v = eval_full(slot_row(S, es), row_of_key(e, t.base) + t.base, q, nu, nrf);
-                if (v > best) {
-                    best = v;
-                    bslot = es;
+    // each pod's speculative winner slot: its own top-4 record (normally entry 0).
+    // Pipelined: a winner that is a stale node (bound by a previous batch after
+    // this batch's speculation may have read it) is re-resolved against the
+    // current state, nothing of this batch being bound yet (walk_top4); all
+    // four entries stale, or none feasible now: resolved in order (kForceSlow).
+    SeqCounters ctr = {0, 0, 0, 0, 0, 0};
+    for (uint32_t i0 = 0; i0 < (uint32_t)kSeqBatch; i0 += 64) {  // (wave-uniform trip count)
+        const uint32_t i = i0 + lane;
+        const u64 sk = i < n_pods ? S.spec_key[i] : 0ull;
+        bool walk = sk && n_prev && map_find(S, row_of_key(sk, t.base)) >= 0;
+        u64 ck = 0;
+        uint32_t cslot = 0;
+        bool cins = false, need = false;
+        const bool stale = walk;
+        walk_top4(S, t, seed32, walk, i, ck, cslot, cins, need, ctr);
+        if (i < n_pods) {
+            uint32_t sslot = kTopK * i;
+            if (stale) {
+                if (!need) {
+                    S.spec_key[i] = ck;
+                    sslot = cslot;
+                } else {
+                    sslot = kForceSlow;
                 }
             }
-            if (done && best != 0) {
-                sk = best;
-                sslot = (uint32_t)bslot;
-                S.spec_key[i] = sk;
-            } else {
-                sslot = kForceSlow;  // all four stale (or none feasible now): resolved in order
-            }
+            S.spec_slot[i] = (uint16_t)sslot;
         }
-        S.spec_slot[i] = (uint16_t)sslot;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     uint32_t tiles = 0;  // tiles: bit j <=> this lane owns tile lane + 64 j
 #pragma unroll
     for (int j = 0; j < J; ++j) tiles |= (lane + 64u * j < n_tiles) ? 1u << j : 0u;
-    SeqCounters ctr = {0, 0, 0, 0, 0};
     MS_VST(0);
 
     // Pods go in groups of 64, lane i <-> pod g+i, decided in rounds. A round
@@ -1532,12 +1621,23 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         u64 rk = 0;                              // this lane's pod: winner key
         uint32_t rinfo = 0;                      // and code | plugin mask << 8
         MS_VST(1);
+        // this lane's winner against the state at the start of the round that
+        // computed it; kept while its node is not bound again (a bind only
+        // lowers its own node's keys, so no other bind can change the max).
+        // Every bind is a decided claimant's (or the serial pod's), so a lane
+        // whose claim lost to an earlier lane, or whose node the serial pod
+        // took, recomputes; collisions in the claim hash only recompute early.
+        u64 ck = 0;
+        uint32_t cslot = 0, crow = 0xFFFFFFFEu;
+        bool cins = false, need = false, cvalid = false;  // first bind on an untouched node / needs the lists
         for (uint32_t i0 = 0; i0 < gn;) {
             const bool act = mine && lane >= i0 && sk_l != 0;
-            u64 ck = 0;                          // winner key against the round-start state
-            uint32_t cslot = 0, crow = 0xFFFFFFFEu;
-            bool cins = false, need = false;     // first bind on an untouched node / needs the lists
-            if (act) {
+            bool walk = false;  // re-resolve from the top-4 (below, four lanes per pod)
+            if (act && !cvalid) {
+                cvalid = true;
+                ck = 0;
+                cins = false;
+                need = false;
                 // touched: bound earlier in the batch (a previous batch's node
                 // whose record is in the map is touched only once bound again)
                 const int sl = map_find(S, srow_l);
@@ -1547,49 +1647,28 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                     crow = srow_l;
                     cins = ss_l < (uint32_t)kPrevSlot0;  // pod pl's own record of an untouched node
                 } else {
-                    const PodFull q = load_pod(mypod, seed32);
-                    bool untouched = false, listend = false;
-                    for (int r = 0; r < kTopK; ++r) {
-                        const u64 e = S.top4[pl][r];
-                        if (e == 0) {  // list ended: every feasible row was listed
-                            listend = true;
-                            break;
-                        }
-                        const uint32_t er = row_of_key(e, t.base);
-                        const int es = map_find(S, er);
-                        if (es < 0) {
-                            if (e > ck) {
-                                ck = e;
-                                cslot = kTopK * pl + (uint32_t)r;
-                                cins = true;
-                            }
-                            untouched = true;
-                            break;
-                        }
-                        uint32_t nu, nrf;
-                        const u64 v = eval_full(slot_row(S, es), er + t.base, q, nu, nrf);
-                        ++ctr.recompute;
-                        if (v > ck) {
-                            ck = v;
-                            cslot = (uint32_t)es;
-                            cins = false;
-                        }
-                    }
-                    need = (!untouched && !listend) || ck == 0;
-                    crow = ck ? row_of_key(ck, t.base) : 0xFFFFFFFEu;
+                    walk = true;
                 }
             }
+            walk_top4(S, t, seed32, walk, pl, ck, cslot, cins, need, ctr);
+            if (act && cvalid) crow = ck ? row_of_key(ck, t.base) : 0xFFFFFFFEu;
+            MS_VST(7);
             const bool claims = act && !need && dig_l >= 0;  // binds at ck if decided this round
             const uint32_t ch = claim_hash(crow);
             if (claims) atomicMin(&S.claim[ch], lane);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            const bool conflict = act && (need || (claims && S.claim[ch] < lane));
+            // (a pod that cannot bind -- no NodeNumber digit -- still watches its
+            // winner's bucket: a bind there can leave it with no feasible node)
+            const bool lost = act && !need && S.claim[ch] < lane;
+            const bool conflict = act && (need || lost);
+            if (lost) cvalid = false;
             const u64 bad = __ballot(conflict);
             const uint32_t s = bad ? (uint32_t)__builtin_ctzll(bad) : gn;
             const bool serial = bad && ((__ballot(need) >> s) & 1ull);
             __builtin_amdgcn_wave_barrier();
             if (claims) S.claim[ch] = ~0u;  // (every lane read its bucket above)
+            MS_VST(8);
             if (mine && lane >= i0 && lane < s) {  // decided: exact against the round-start state
                 rk = ck;
                 if (sk_l == 0) {  // no feasible row at speculation: none now either
@@ -1609,6 +1688,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                 }
             }
             flush_pending(S, prow, pslot, padd, mypod);
+            ++ctr.rounds;
             MS_VST(4);
             if (s == gn) break;
             if (!serial) {  // claimed: re-resolved next round (then first, so unclaimed)
@@ -1691,6 +1771,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                     }
                 }
                 if (lane == s) padd = sl;
+                if (crow == row) cvalid = false;  // the serial pod took this lane's winner
             }
             if (lane == s) {
                 rk = b;
@@ -1723,18 +1804,39 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         atomicAdd(&stats[4], ctr.miss);
         atomicAdd(&stats[5], ctr.slow);
         atomicAdd(&stats[6], ctr.scan);
+#ifdef MS_VSTAMPS
+        atomicAdd(&stats[7], ctr.rounds);
+#endif
     }
-    for (uint32_t sl = lane; sl < (uint32_t)kSeqSlots; sl += 64) {
-        if (!S.bound[sl]) continue;  // not bound in this batch (a dead copy, a stale node)
-        const int64_t *r = S.rec[sl];
+    // the bound slots (not a dead copy or an untouched stale node), compacted
+    // with ballots into bl[], then written back one slot per lane
+    uint32_t n_bl = 0;
+    {
+        constexpr int kChunks = kSeqSlots / 64;
+        static_assert(kSeqSlots % 64 == 0, "bound[] scanned 64 slots at a time");
+        uint32_t bv[kChunks];
+#pragma unroll
+        for (int c = 0; c < kChunks; ++c) bv[c] = S.bound[c * 64 + lane];
+#pragma unroll
+        for (int c = 0; c < kChunks; ++c) {
+            const u64 m = __ballot(bv[c] != 0u);
+            if (bv[c]) S.bl[n_bl + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint16_t)(c * 64 + lane);
+            n_bl += (uint32_t)__builtin_popcountll(m);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t o = lane; o < n_bl; o += 64) {
+        const int64_t *r = S.rec[S.bl[o]];
         const uint32_t row = (uint32_t)r[F_ROW];
         t.req_cpu[row] = r[F_REQ_CPU];
         t.req_mem[row] = r[F_REQ_MEM];
         t.nz_cpu[row] = r[F_NZ_CPU];
         t.nz_mem[row] = r[F_NZ_MEM];
         t.pod_count[row] = (int32_t)r[F_CNT];
-        if (prev_out) put_stale(prev_out, prev_recs_out, atomicAdd(&S.n_out, 1u), row, r);
+        if (prev_out) put_stale(prev_out, prev_recs_out, o, row, r);
     }
+    if (lane == 0) S.n_out = n_bl;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (prev_out) {
@@ -1755,7 +1857,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 #ifdef MS_VSTAMPS
     MS_VST(5);
     if (lane == 0)
-        for (int i = 0; i < 7; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i, vst.acc[i]);
+        for (int i = 0; i < 9; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i, vst.acc[i]);
 #endif
 }
 
