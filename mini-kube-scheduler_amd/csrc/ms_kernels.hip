@@ -803,6 +803,18 @@ __device__ __forceinline__ u64 wave_max_u64_dpp(u64 v) {
 }
 
 // Max over each quad of lanes (4i .. 4i+3), every lane of the quad gets it.
+// wave_max_u64_dpp where one lane usually holds the high-word maximum (the
+// sweep's packed keys): that lane supplies the low word by one readlane
+// instead of a second reduction.
+__device__ __forceinline__ u64 wave_max_u64_unique(u64 v) {
+    const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+    const uint32_t hmax = wave_max_u32_dpp(hi);
+    const u64 tie = __ballot(hi == hmax);
+    if ((tie & (tie - 1ull)) == 0ull)
+        return ((u64)hmax << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)__builtin_ctzll(tie));
+    return ((u64)hmax << 32) | wave_max_u32_dpp(hi == hmax ? lo : 0u);
+}
+
 template <int CTRL>
 __device__ __forceinline__ u64 dpp_u64(u64 v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, false);
@@ -830,6 +842,9 @@ __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
 constexpr int kTopK = 4;
 static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
 
+#ifndef MS_SWEEP_WMAX
+#define MS_SWEEP_WMAX wave_max_u64_unique
+#endif
 // NP pods at a time: their evaluations, sorts and wave reductions are
 // independent, so the DPP chains of one hide the latency of the other's (3
 // waves per SIMD leave little else to hide it).
@@ -862,7 +877,7 @@ __device__ __forceinline__ void sweep_topk_group(const FullRow *x, uint32_t ord0
     for (int j = 0; j < kTopK; ++j) {
 #pragma unroll
         for (int n = 0; n < NP; ++n) {
-            const u64 mx = wave_max_u64_dpp(k[n][0]);
+            const u64 mx = MS_SWEEP_WMAX(k[n][0]);
             if (lane == (uint32_t)j) out[n] = mx;
             if (mx != 0 && k[n][0] == mx) {  // the owning lane pops its head
                 k[n][0] = k[n][1];
@@ -977,7 +992,9 @@ __device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int6
 
 // One wave merges pod p's tile lists: lane r < 4 gets the global rank-r key
 // (out, 0 past the feasible rows), f the filters of the tiles with no feasible
-// row (bit0 NodeUnschedulable, bit8 NodeResourcesFit; wave-uniform).
+// row (bit0 NodeUnschedulable, bit8 NodeResourcesFit; wave-uniform) and, in
+// bits 16 / 24, those of all tiles with NodeResourcesFit for a tile that had a
+// feasible row: the FitError mask once binds have filled every feasible row.
 template <int J>
 __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_keys,
                                                 const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
@@ -985,6 +1002,7 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
     u64 e[J][kTopK];
     uint32_t pos[J];
     uint32_t fl = 0;  // filters of this lane's tiles that have no feasible row
+    uint32_t fa = 0;  // filters of all its tiles, + NRF for a tile with feasible rows
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const uint32_t tt = lane + 64u * j;
@@ -998,6 +1016,7 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
         e[j][2] = ((u64)b.y << 32) | b.x;
         e[j][3] = ((u64)b.w << 32) | b.z;
         if (tt < n_tiles && e[j][0] == 0) fl |= tf;
+        if (tt < n_tiles) fa |= tf | (e[j][0] != 0 ? 0x100u : 0u);
     }
     out = 0;
 #pragma unroll
@@ -1018,7 +1037,8 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
         if (lane == (uint32_t)r) out = m;
         if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
     }
-    f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+    f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u) |
+        (__ballot((fa & 0xFFu) != 0) ? 0x10000u : 0u) | (__ballot((fa & 0xFF00u) != 0) ? 0x1000000u : 0u);
 }
 
 // Per pod (one wave): merge the tiles' top-4 lists into the global top-4, the
@@ -1300,9 +1320,10 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
 // 16 pods per pass with lane 4i + r on entry r of the pass's pod i: touched
 // entries (in the map) are re-evaluated from their LDS records, the first
 // untouched one is exact and bounds every row below it. Out, per walking lane:
-// ck (0: no listed node feasible now), its slot, cins (untouched: the pod's
-// own record slot, whose first bind inserts the map entry) and need (four
-// touched entries in a full list, or none feasible: the tile lists decide).
+// ck, its slot, cins (untouched: the pod's own record slot, whose first bind
+// inserts the map entry) and need (four touched entries in a full list: the
+// tile lists decide). ck == 0 without need: the list ended and none of its
+// nodes is feasible now, so no node is (a FitError).
 // Called by the whole wave (wave-uniform passes); clears `walk`.
 __device__ __forceinline__ void walk_top4(SeqShared &S, const NodeTable &t, uint32_t seed32, bool &walk, uint32_t pod,
                                           u64 &ck, uint32_t &cslot, bool &cins, bool &need, SeqCounters &ctr) {
@@ -1345,7 +1366,7 @@ __device__ __forceinline__ void walk_top4(SeqShared &S, const NodeTable &t, uint
         const u64 m = quad_max_u64(ve);
         const uint32_t own = (uint32_t)(__ballot(valid && m != 0 && ve == m) >> (4u * qi)) & 0xFu;
         if (qi < nw && r == (own ? (uint32_t)__builtin_ctz(own) : 0u))
-            S.walkres[qi] = {m, vs, (unt && m != 0 ? 1u : 0u) | ((f == 4u || m == 0) ? 2u : 0u)};
+            S.walkres[qi] = {m, vs, (unt && m != 0 ? 1u : 0u) | (f == 4u ? 2u : 0u)};
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         if (walk && rank < 16u) {
@@ -1576,7 +1597,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         if (i < n_pods) {
             uint32_t sslot = kTopK * i;
             if (stale) {
-                if (!need) {
+                if (!need && ck != 0) {
                     S.spec_key[i] = ck;
                     sslot = cslot;
                 } else {
@@ -1653,14 +1674,14 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
             walk_top4(S, t, seed32, walk, pl, ck, cslot, cins, need, ctr);
             if (act && cvalid) crow = ck ? row_of_key(ck, t.base) : 0xFFFFFFFEu;
             MS_VST(7);
-            const bool claims = act && !need && dig_l >= 0;  // binds at ck if decided this round
+            const bool claims = act && !need && ck != 0 && dig_l >= 0;  // binds at ck if decided this round
             const uint32_t ch = claim_hash(crow);
             if (claims) atomicMin(&S.claim[ch], lane);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             // (a pod that cannot bind -- no NodeNumber digit -- still watches its
             // winner's bucket: a bind there can leave it with no feasible node)
-            const bool lost = act && !need && S.claim[ch] < lane;
+            const bool lost = act && !need && ck != 0 && S.claim[ch] < lane;
             const bool conflict = act && (need || lost);
             if (lost) cvalid = false;
             const u64 bad = __ballot(conflict);
@@ -1671,8 +1692,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
             MS_VST(8);
             if (mine && lane >= i0 && lane < s) {  // decided: exact against the round-start state
                 rk = ck;
-                if (sk_l == 0) {  // no feasible row at speculation: none now either
-                    const uint32_t fm = S.spec_flags[pl];
+                if (ck == 0) {  // no feasible node: none at speculation (the empty tiles' filters)
+                    // or binds filled every listed one (all tiles' filters, + NRF)
+                    const uint32_t fm = sk_l == 0 ? S.spec_flags[pl] : S.spec_flags[pl] >> 16;
                     rinfo = MS_CODE_UNSCHEDULABLE | ((((fm & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
                                                       ((fm & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u))
                                                      << 8);
@@ -1877,13 +1899,26 @@ __global__ __launch_bounds__(64) void k_validate_seq(SeqArgs va) {
 template <int J, int W>
 __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks) {
     __shared__ SeqShared S;
+#ifdef MS_VSTAMPS  // wave durations (s_memrealtime, 100 MHz): u64 stats[8+9] validator, [8+10] sweep waves, [8+11] their count
+    const u64 t_begin = __builtin_amdgcn_s_memrealtime();
+#endif
     if (blockIdx.x == 0) {
         if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x);
+#ifdef MS_VSTAMPS
+        if (threadIdx.x == 0 && va.n_pods)
+            atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 9, __builtin_amdgcn_s_memrealtime() - t_begin);
+#endif
         return;
     }
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     for (uint32_t task = (blockIdx.x - 1) * W + wave; task < n_tasks; task += (gridDim.x - 1) * W)
         sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
+#ifdef MS_VSTAMPS
+    if (lane == 0 && (blockIdx.x - 1) * W + wave < n_tasks) {
+        atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 10, __builtin_amdgcn_s_memrealtime() - t_begin);
+        atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 11, 1ull);
+    }
+#endif
 }
 
 // ----------------------------------------------------------------------------
