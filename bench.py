@@ -19,6 +19,13 @@ One step = the whole pod batch through the hot path with inputs resident in HBM:
          the fused cycle on its P/G pods; no collective.
 value = P * N / step time (max over ranks): whole-job evals/s.
 
+Scaling (--scaling, default weak): every GPU brings config C's 100k-pod batch,
+so at N GPUs one step schedules N x 100k pods against the same 100k nodes (each
+rank sweeps all N x 100k pods against its 100k/N rows and decodes its 100k;
+per-GPU evaluations stay 1e10). --scaling strong keeps the job at 100k pods
+split over the GPUs (at N = 8 a rank's step is ~60 us and fixed launch /
+collective latencies dominate).
+
 Extra fields (rank 0): the end-to-end pods/s of ms_schedule_batch with host
 arrays (pinned staging, H2D, the cycle, bind commit, D2H; 1 warm-up, median of
 5), the class-indexed K1 v8 (round 1, a separately labelled
@@ -63,6 +70,9 @@ def parse():
     ap.add_argument("--config", default="C", choices=["B", "C", "D"])
     ap.add_argument("--split", default=None, choices=["nodes", "pods"],
                     help="N > 1 partition (default: nodes for B/C, pods for D)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak (default): every GPU brings the config's pod batch, so the job schedules "
+                         "N x P pods against the same N nodes; strong: the config's P pods split over the GPUs")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -221,6 +231,8 @@ def main():
 
     cfg = synth.CONFIGS[args.config]
     N, P = cfg["nodes"], cfg["pods"]
+    if args.scaling == "weak":
+        P = P * world  # the job's pod batch: the config's batch per GPU, same node count
     plugins = cfg["plugins"]
     split = args.split or ("pods" if args.config == "D" else "nodes")
     lo, hi = sharded.shard_bounds(N, rank, world) if split == "nodes" else (0, N)
@@ -345,15 +357,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u32",
             "data": f"synthetic (splitmix64 seed {args.seed}, BASELINE.md §3)",
             "config": {
-                "workload": f"{args.config}: {N} nodes x {P} pods, {plugins}, batched, every pair evaluated, "
+                "workload": f"{args.config}: {N} nodes x {P} pods ({P // world} per GPU), {plugins}, batched, "
+                            "every pair evaluated, "
                             + (f"node-sharded over {world} GPU" if split == "nodes" else f"pods split over {world} GPU"),
                 "nodes": N,
                 "pods": P,
+                "pods_per_gpu": P // world,
                 "plugins": plugins,
                 "parallelism": f"{'node' if split == 'nodes' else 'pod'}-shard{world}",
             },
