@@ -749,6 +749,123 @@ __device__ __forceinline__ bool rows_huge(const FullRow *x) {
     return __ballot(h) != 0;
 }
 
+// ---- binary64 LeastAllocated (the config-E sweep's fast form) --------------
+// floor(100 (av - n) / cap) as ONE fma + a saturating conversion per resource:
+//   r = RN(100 / cap), a = RN(RN(av * r) + 2^-43), x = RN(-n * r + a) (fma),
+//   score = x <= 0 ? 0 : trunc(x)                               (v_cvt_u32_f64)
+// |x - (X + 2^-43)| <= 402 u (u = 2^-53) for X = 100 (av - n) / cap <= 100, so
+// trunc(x) = floor(X) whenever 2^-43 > 402 u and 2^-43 + 402 u < 1 / cap, i.e.
+// for 0 < cap < 2^41 (cap <= 0: r = 0, score 0 as leastRequestedScore gives);
+// negative X (requested > capacity) lands below 0 and saturates to 0.
+// Exact by the bound and by tests/c/la_f64_exact.c (boundary cases around every
+// k * cap / 100; the window of working epsilons is 2^-46 .. 2^-42). Needs
+// NonZeroRequested >= 0 (av <= cap) and 0 <= pod non-zero request < 2^53; a
+// wave whose rows or pods fall outside takes the general path (eval_full).
+constexpr int64_t kFastCap = 1ll << 41;
+constexpr int64_t kFastReq = 1ll << 53;
+constexpr double kLaEps = 0x1p-43;
+
+struct FastRow {
+    int64_t fr_cpu, fr_mem;  // Allocatable - Requested (NodeResourcesFit)
+    double r_cpu, r_mem;     // RN(100 / Allocatable), 0 when Allocatable <= 0
+    double a_cpu, a_mem;     // RN(RN((Allocatable - NonZeroRequested) * r) + 2^-43)
+    int32_t room;            // AllowedPodNumber - len(Pods)
+    uint32_t fd;             // flags | digit << 8
+    bool ok;                 // the fast form is exact for this row
+};
+
+__device__ __forceinline__ double la_r(int64_t cap) { return cap > 0 ? __ddiv_rn(100.0, (double)cap) : 0.0; }
+
+__device__ __forceinline__ double la_a(int64_t cap, int64_t nz, double r) {
+    const int64_t av = (int64_t)((uint64_t)cap - (uint64_t)nz);  // (wraps only where r == 0 or av < 0 anyway)
+    return __dadd_rn(__dmul_rn((double)av, r), kLaEps);
+}
+
+__device__ __forceinline__ FastRow load_fast_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
+    FastRow x;
+    if (r >= n_rows) {
+        x.fr_cpu = x.fr_mem = 0;
+        x.r_cpu = x.r_mem = x.a_cpu = x.a_mem = 0.0;
+        x.room = 0;
+        x.fd = kNodeAbsent | (0xFFu << 8);
+        x.ok = true;
+        return x;
+    }
+    const int64_t ac = t.alloc_cpu[r], am = t.alloc_mem[r], zc = t.nz_cpu[r], zm = t.nz_mem[r];
+    x.fr_cpu = ac - t.req_cpu[r];
+    x.fr_mem = am - t.req_mem[r];
+    x.r_cpu = la_r(ac);
+    x.r_mem = la_r(am);
+    x.a_cpu = la_a(ac, zc, x.r_cpu);
+    x.a_mem = la_a(am, zm, x.r_mem);
+    x.room = t.allowed_pods[r] - t.pod_count[r];
+    x.fd = (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8);
+    x.ok = ac < kFastCap && am < kFastCap && zc >= 0 && zm >= 0;
+    return x;
+}
+
+struct PodFast {
+    int64_t rc, rm;    // requests (Fit)
+    double nnc, nnm;   // -(double) non-zero requests (LeastAllocated)
+    uint32_t A;
+    uint32_t bits;     // digit (9 bits, sign-extended) | kPfTol | kPfZero | kPfOk
+};
+constexpr uint32_t kPfTol = 0x200u, kPfZero = 0x400u, kPfOk = 0x800u;
+
+__device__ __forceinline__ PodFast load_pod_fast(const ms_pod_rec &pr, uint32_t seed32) {
+    PodFast q;
+    q.rc = pr.req_milli_cpu;
+    q.rm = pr.req_memory;
+    q.nnc = -(double)pr.nonzero_milli_cpu;
+    q.nnm = -(double)pr.nonzero_memory;
+    q.A = tb_pod(seed32, pr.ordinal);
+    const bool ok = pr.nonzero_milli_cpu >= 0 && pr.nonzero_milli_cpu < kFastReq && pr.nonzero_memory >= 0 &&
+                    pr.nonzero_memory < kFastReq;
+    // the digit as 9 bits: a negative (non-digit) name never equals a node's digit byte
+    q.bits = ((uint32_t)(int32_t)pr.name_digit & 0x1FFu) | (pr.tolerates_unschedulable ? kPfTol : 0u) |
+             ((pr.req_milli_cpu == 0 && pr.req_memory == 0) ? kPfZero : 0u) | (ok ? kPfOk : 0u);
+    return q;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, uint32_t l) {
+    return __longlong_as_double(readlane_i64(__double_as_longlong(v), l));
+}
+
+__device__ __forceinline__ PodFast pod_fast_of_lane(const PodFast &m, uint32_t i) {
+    PodFast q;
+    q.rc = readlane_i64(m.rc, i);
+    q.rm = readlane_i64(m.rm, i);
+    q.nnc = readlane_f64(m.nnc, i);
+    q.nnm = readlane_f64(m.nnm, i);
+    q.A = (uint32_t)__builtin_amdgcn_readlane((int)m.A, (int)i);
+    q.bits = (uint32_t)__builtin_amdgcn_readlane((int)m.bits, (int)i);
+    return q;
+}
+
+__device__ __forceinline__ uint32_t cvt_u32_sat(double x) {  // negatives -> 0
+    uint32_t q;
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(q) : "v"(x));
+    return q;
+}
+
+// eval_full's key and first-failure flags through the binary64 LeastAllocated.
+__device__ __forceinline__ u64 eval_fast(const FastRow &x, uint32_t ord, const PodFast &q, uint32_t &nu,
+                                         uint32_t &nrf) {
+    const uint32_t fl = x.fd & 0xFFu;
+    const bool absent = (fl & kNodeAbsent) != 0;
+    const bool f_nu = !absent && (fl & kNodeUnschedulable) != 0 && !(q.bits & kPfTol);
+    bool bad = x.room < 1;
+    if (!(q.bits & kPfZero)) bad = bad || (q.rc > x.fr_cpu) || (q.rm > x.fr_mem);
+    const bool f_nrf = !absent && !f_nu && bad;
+    nu = f_nu ? 1u : 0u;
+    nrf = f_nrf ? 1u : 0u;
+    const uint32_t s_cpu = cvt_u32_sat(__builtin_fma(q.nnc, x.r_cpu, x.a_cpu));
+    const uint32_t s_mem = cvt_u32_sat(__builtin_fma(q.nnm, x.r_mem, x.a_mem));
+    const uint32_t nn = ((x.fd >> 8) == (q.bits & 0x1FFu)) ? 10u : 0u;
+    const u64 key = make_key(nn + ((s_cpu + s_mem) >> 1), tb_hash(q.A, ord), ord);
+    return (absent || f_nu || bad) ? 0ull : key;
+}
+
 // Batched resource-aware sweep: atomicMax into keys[P] / atomicOr into flags[P].
 __global__ __launch_bounds__(kFullThreads) void k_sweep_full(NodeTable t, uint32_t n_rows,
                                                              const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
@@ -845,23 +962,38 @@ static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort
 #ifndef MS_SWEEP_WMAX
 #define MS_SWEEP_WMAX wave_max_u64_unique
 #endif
+// Row forms of the sweep (F): 0 general int64/f32 LeastAllocated, 1 rows with
+// capacities >= 2^53, 2 the binary64 fast form.
+template <int F, typename Pod>
+__device__ __forceinline__ u64 sweep_eval(const FullRow &x, uint32_t ord, const Pod &q, uint32_t &nu, uint32_t &nrf) {
+    return eval_full<F == 1>(x, ord, q, nu, nrf);
+}
+template <int F, typename Pod>
+__device__ __forceinline__ u64 sweep_eval(const FastRow &x, uint32_t ord, const Pod &q, uint32_t &nu, uint32_t &nrf) {
+    return eval_fast(x, ord, q, nu, nrf);
+}
+
+__device__ __forceinline__ PodFull lane_pod(const PodLanes &m, uint32_t i) { return pod_of_lane(m, i); }
+__device__ __forceinline__ PodFast lane_pod(const PodFast &m, uint32_t i) { return pod_fast_of_lane(m, i); }
+
 // NP pods at a time: their evaluations, sorts and wave reductions are
 // independent, so the DPP chains of one hide the latency of the other's (3
-// waves per SIMD leave little else to hide it).
-template <bool kHuge, int NP>
-__device__ __forceinline__ void sweep_topk_group(const FullRow *x, uint32_t ord0, const PodLanes &m, uint32_t pbeg,
+// waves per SIMD leave little else to hide it). F: 0 general, 1 huge rows, 2
+// binary64 fast form (Row FastRow, Lanes PodFast).
+template <int F, int NP, typename Row, typename Lanes>
+__device__ __forceinline__ void sweep_topk_group(const Row *x, uint32_t ord0, const Lanes &m, uint32_t pbeg,
                                                  uint32_t i, uint32_t lane, uint32_t tile, uint32_t n_tiles,
                                                  u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
     u64 k[NP][kFullSlots], out[NP];
     uint32_t nu_any[NP], nrf_any[NP];
 #pragma unroll
     for (int n = 0; n < NP; ++n) {
-        const PodFull q = pod_of_lane(m, i + n);
+        const auto q = lane_pod(m, i + n);
         nu_any[n] = nrf_any[n] = 0;
 #pragma unroll
         for (int s = 0; s < kFullSlots; ++s) {
             uint32_t nu, nrf;
-            k[n][s] = eval_full<kHuge>(x[s], ord0 + s, q, nu, nrf);
+            k[n][s] = sweep_eval<F>(x[s], ord0 + s, q, nu, nrf);
             nu_any[n] |= nu;
             nrf_any[n] |= nrf;
         }
@@ -896,14 +1028,14 @@ __device__ __forceinline__ void sweep_topk_group(const FullRow *x, uint32_t ord0
     }
 }
 
-template <bool kHuge>
-__device__ __forceinline__ void sweep_topk_pods(const FullRow *x, uint32_t ord0, const PodLanes &m, uint32_t pbeg,
+template <int F, typename Row, typename Lanes>
+__device__ __forceinline__ void sweep_topk_pods(const Row *x, uint32_t ord0, const Lanes &m, uint32_t pbeg,
                                                 uint32_t cnt, uint32_t lane, uint32_t tile, uint32_t n_tiles,
                                                 u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
     uint32_t i = 0;
     for (; i + 2 <= cnt; i += 2)
-        sweep_topk_group<kHuge, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
-    if (i < cnt) sweep_topk_group<kHuge, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
+        sweep_topk_group<F, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
+    if (i < cnt) sweep_topk_group<F, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
 }
 
 struct SweepArgs {
@@ -916,21 +1048,40 @@ struct SweepArgs {
     u64 *tile_keys;
     uint32_t *tile_flags;
     uint32_t n_tiles;
+    uint32_t fast;  // binary64 LeastAllocated where exact (default 1)
 };
 
-// One wave: tile `tile`'s top-4 lists and filter flags for the pods of chunk cidx.
+// One wave: tile `tile`'s top-4 lists and filter flags for the pods of chunk
+// cidx. The binary64 fast form unless a row or pod of the task is outside its
+// exact range (MINISCHED_SEQ_FAST=0 forces the general form: fast == 0).
 __device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t tile, uint32_t cidx, uint32_t lane) {
     const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
-    FullRow x[kFullSlots];
-#pragma unroll
-    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
     const uint32_t ord0 = a.t.base + row0;
     const uint32_t pbeg = cidx * a.chunk;
     if (pbeg >= a.n_pods) return;
     const uint32_t cnt = min(min(a.chunk, 64u), a.n_pods - pbeg);
+    if (a.fast) {
+        FastRow x[kFullSlots];
+        bool ok = true;
+#pragma unroll
+        for (int s = 0; s < kFullSlots; ++s) {
+            x[s] = load_fast_row(a.t, row0 + s, a.n_rows);
+            ok = ok && x[s].ok;
+        }
+        ms_pod_rec z = {};
+        const PodFast m = load_pod_fast(lane < cnt ? a.pods[pbeg + lane] : z, a.seed32);
+        ok = ok && (lane >= cnt || (m.bits & kPfOk));
+        if (__ballot(!ok) == 0) {
+            sweep_topk_pods<2>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+            return;
+        }
+    }
+    FullRow x[kFullSlots];
+#pragma unroll
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
     const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
-    if (rows_huge(x)) sweep_topk_pods<true>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
-    else sweep_topk_pods<false>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+    if (rows_huge(x)) sweep_topk_pods<1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+    else sweep_topk_pods<0>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
 }
 
 __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(SweepArgs a) {
@@ -2534,6 +2685,13 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
     return hipGetLastError();
 }
 
+// The config-E sweep's binary64 LeastAllocated form (default on; MINISCHED_SEQ_FAST=0
+// keeps the general form everywhere, for A/B runs and parity cross-checks).
+static uint32_t seq_fast() {
+    const char *e = getenv("MINISCHED_SEQ_FAST");
+    return (e && e[0] == '0') ? 0u : 1u;
+}
+
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
                                    uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s) {
@@ -2543,7 +2701,7 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
     if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::min(64, std::max(1, atoi(e)));
     const dim3 grid(gx, cdiv(n_pods, chunk));
-    const SweepArgs a = {t, n_rows, pods, n_pods, chunk, seed32, tile_keys, tile_flags, n_tiles};
+    const SweepArgs a = {t, n_rows, pods, n_pods, chunk, seed32, tile_keys, tile_flags, n_tiles, seq_fast()};
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, a);
     return hipGetLastError();
 }
@@ -2593,7 +2751,8 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     const uint32_t W = J <= 4 ? 12u : J == 8 ? 8u : 4u;
     uint32_t chunk = 8;
     if (n_next) chunk = std::min(64u, std::max(8u, cdiv(n_tiles * n_next, (cus - 1) * W)));
-    const SweepArgs sw = {t, n_rows, next_pods, n_next, chunk, seed32, next_tile_keys, next_tile_flags, n_tiles};
+    const SweepArgs sw = {t,       n_rows,         next_pods,       n_next,  chunk,
+                          seed32,  next_tile_keys, next_tile_flags, n_tiles, seq_fast()};
     const uint32_t n_tasks = n_next ? n_tiles * cdiv(n_next, chunk) : 0u;
     const uint32_t grid = 1u + std::min(cus - 1, cdiv(n_tasks, W));
 #define MS_STEP(JJ, WW) hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks)

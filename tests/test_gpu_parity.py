@@ -332,6 +332,34 @@ def test_resource_sequential_tile_counts(oracle, n_nodes):
         assert_table_equal(e, o["cols"], n_nodes)
 
 
+@pytest.mark.parametrize("fast", ["1", "0"])
+@pytest.mark.parametrize("n_nodes,n_pods", [(3000, 4000), (40_000, 1500)])
+def test_resource_sequential_capacity_forms(oracle, monkeypatch, fast, n_nodes, n_pods):
+    # the sweep's binary64 LeastAllocated form (exact for Allocatable < 2^41,
+    # NonZeroRequested >= 0, pod requests < 2^53) beside tiles that must take the
+    # general form: 5 TiB and 2^60 capacities, zero capacities, overcommitted
+    # nodes, pods with non-zero requests >= 2^53; MINISCHED_SEQ_FAST=0 forces the
+    # general form everywhere. Placements and tables equal the oracle either way.
+    monkeypatch.setenv("MINISCHED_SEQ_FAST", fast)
+    seed = n_nodes + 17
+    nr = synth.nodes(n_nodes, seed=seed, resources=True)
+    pr = synth.pods(n_pods, seed=seed, resources=True)
+    nr["alloc_memory"][5::997] = 5 << 40
+    nr["alloc_memory"][7::2113] = 1 << 60
+    nr["alloc_milli_cpu"][3::89] = 0
+    over = slice(11, None, 53)
+    nr["nonzero_milli_cpu"][over] = nr["alloc_milli_cpu"][over] * 2 + 1
+    nr["req_milli_cpu"][over] = nr["alloc_milli_cpu"][over] // 4
+    pr["nonzero_memory"][13::701] = 1 << 54
+    pr["req_memory"][13::701] = 0
+    pr["req_milli_cpu"][13::701] = 0
+    o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed)
+    with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed) as e:
+        assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
+        assert_table_equal(e, o["cols"], n_nodes)
+        assert e.info()._pad == 0
+
+
 def _pods_with_zero_hash(seed, n_nodes, want=4):
     # pods j for which some node ordinal r < n_nodes has tie-break hash exactly 0:
     # mix32(A + r * kG24) == 0 <=> A + r * kG24 == 0 (mix32 is a bijection fixing 0),

@@ -1,0 +1,8 @@
+# rocprof passes of the bench kernel (profile_pp.sh) + config E validator/sweep wave stamps (MS_VSTAMPS build)
+set -o pipefail
+TAG=${1:-r02n}
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+MINISCHED_LIB=$PWD/mini-kube-scheduler_amd/minisched_amd/libminisched_gpu_vstamps.so timeout -k 10 200 python -u tools/bench_configs.py --configs E --reps 1 > gpurun_out/${TAG}_e_vst.jsonl 2> gpurun_out/${TAG}_e_vst.err || exit 1
+grep MS_VSTAMPS gpurun_out/${TAG}_e_vst.err
+bash tools/profile_pp.sh ${TAG} || exit 1

@@ -81,6 +81,58 @@ __global__ void k_xsdwa(unsigned *out, unsigned k) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ k;
 }
 
+
+// 64-bit forms: dst = op(dst, dst, k) on VGPR pairs (f64 FMA, u64 compare + select)
+#define KERNEL_F64(NAME, BODY)                                                                  \
+    __global__ void NAME(unsigned *out, unsigned k) {                                           \
+        double d0 = threadIdx.x, d1 = d0 + 1, d2 = d0 + 2, d3 = d0 + 3, d4 = d0 + 4, d5 = d0 + 5, \
+               d6 = d0 + 6, d7 = d0 + 7;                                                        \
+        const double kd = (double)k * 1e-12;                                                    \
+        for (int i = 0; i < ITERS; ++i) {                                                       \
+            asm volatile(BODY(0) BODY(1) BODY(2) BODY(3) BODY(4) BODY(5) BODY(6) BODY(7)        \
+                         : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), \
+                           "+v"(d7)                                                             \
+                         : "s"(kd));                                                            \
+        }                                                                                       \
+        out[blockIdx.x * blockDim.x + threadIdx.x] =                                            \
+            (unsigned)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7);                                  \
+    }
+#define FMA64(i) "v_fma_f64 %" #i ", %" #i ", %" #i ", %8\n\t"
+#define ADD64(i) "v_add_f64 %" #i ", %" #i ", %8\n\t"
+KERNEL_F64(k_fma64, FMA64)
+KERNEL_F64(k_add64, ADD64)
+// v_cvt_u32_f64 (saturating truncation), 8 independent chains through a u32 -> f64 round trip
+__global__ void k_cvt64(unsigned *out, unsigned k) {
+    double d0 = threadIdx.x, d1 = d0 + 1, d2 = d0 + 2, d3 = d0 + 3, d4 = d0 + 4, d5 = d0 + 5, d6 = d0 + 6, d7 = d0 + 7;
+    unsigned u0, u1, u2, u3, u4, u5, u6, u7;
+    for (int i = 0; i < ITERS / 2; ++i) {
+        asm volatile(
+            "v_cvt_u32_f64 %8, %0\n\tv_cvt_u32_f64 %9, %1\n\tv_cvt_u32_f64 %10, %2\n\tv_cvt_u32_f64 %11, %3\n\t"
+            "v_cvt_u32_f64 %12, %4\n\tv_cvt_u32_f64 %13, %5\n\tv_cvt_u32_f64 %14, %6\n\tv_cvt_u32_f64 %15, %7\n\t"
+            "v_cvt_f64_u32 %0, %8\n\tv_cvt_f64_u32 %1, %9\n\tv_cvt_f64_u32 %2, %10\n\tv_cvt_f64_u32 %3, %11\n\t"
+            "v_cvt_f64_u32 %4, %12\n\tv_cvt_f64_u32 %5, %13\n\tv_cvt_f64_u32 %6, %14\n\tv_cvt_f64_u32 %7, %15"
+            : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7), "=v"(u0), "=v"(u1),
+              "=v"(u2), "=v"(u3), "=v"(u4), "=v"(u5), "=v"(u6), "=v"(u7));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7) ^ k;
+}
+// v_mad_u64_u32 (32x32 + 64 -> 64)
+__global__ void k_mad64(unsigned *out, unsigned k) {
+    unsigned long long a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+                       a7 = a0 + 7;
+    for (int i = 0; i < ITERS; ++i) {
+        asm volatile(
+            "v_mad_u64_u32 %0, vcc, %8, %8, %0\n\tv_mad_u64_u32 %1, vcc, %8, %8, %1\n\t"
+            "v_mad_u64_u32 %2, vcc, %8, %8, %2\n\tv_mad_u64_u32 %3, vcc, %8, %8, %3\n\t"
+            "v_mad_u64_u32 %4, vcc, %8, %8, %4\n\tv_mad_u64_u32 %5, vcc, %8, %8, %5\n\t"
+            "v_mad_u64_u32 %6, vcc, %8, %8, %6\n\tv_mad_u64_u32 %7, vcc, %8, %8, %7"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "s"(k)
+            : "vcc");
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7);
+}
+
 int main() {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -91,7 +143,8 @@ int main() {
         {"v_add_u32", k_add}, {"v_xor_b32", k_xor}, {"v_mul_lo_u32", k_mullo}, {"v_mul_u32_u24", k_mul24},
         {"v_mul_hi_u32", k_mulhi}, {"v_ffbl_b32", k_ffbl}, {"v_max_u32", k_max},
         {"v_bitop3_b32", k_bitop3}, {"v_mad_u32_u24", k_mad24}, {"v_max3_u32", k_max3}, {"v_fma_f32", k_fmaf3},
-        {"v_xor_b32_sdwa", k_xsdwa}};
+        {"v_xor_b32_sdwa", k_xsdwa}, {"v_fma_f64", k_fma64}, {"v_add_f64", k_add64},
+        {"v_cvt_u32_f64+v_cvt_f64_u32", k_cvt64}, {"v_mad_u64_u32", k_mad64}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
