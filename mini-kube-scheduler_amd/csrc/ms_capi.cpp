@@ -63,6 +63,7 @@ struct ms_ctx {
     int64_t *d_top4_rec = nullptr;         // their batch-start node records (validator layout)
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
     int64_t *d_prev_rec = nullptr;         // and their final records (x2)
+    DRow *d_drow = nullptr;                // derived rows of the binary64 sweep (tile_cap * kFullWaveTile)
     // pipelined sequential engine: batch k+1's speculation (seq_stream) runs
     // while batch k validates (caller stream); every buffer above is double-
     // buffered by batch parity
@@ -133,7 +134,7 @@ void free_all(ms_ctx *c) {
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow, c->d_pstream,
-                   c->d_work, c->d_merged, c->d_merged_flags};
+                   c->d_work, c->d_merged, c->d_merged_flags, c->d_drow};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -247,7 +248,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (n_tiles <= c->tile_cap) return MS_OK;
     MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
     void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev,
-                   c->d_prev_rec};
+                   c->d_prev_rec, c->d_drow};
     for (void *q : old)
         if (q) (void)hipFree(q);
     c->d_tile_keys = nullptr;
@@ -258,6 +259,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     c->d_top4_rec = nullptr;
     c->d_prev = nullptr;
     c->d_prev_rec = nullptr;
+    c->d_drow = nullptr;
     c->tile_cap = 0;
     // (ms_seq_candidates_device uses the same buffers for up to kSeqBufs * B pods)
     const size_t B = seq_batch_limit(), NB = kSeqBufs * B, n = NB * n_tiles;
@@ -268,7 +270,8 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
         hipMalloc((void **)&c->d_top4, NB * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&c->d_top4_rec, NB * seq_topk() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess ||
         hipMalloc((void **)&c->d_prev, 2 * (2 + seq_prev_cap()) * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&c->d_prev_rec, 2 * seq_prev_cap() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess)
+        hipMalloc((void **)&c->d_prev_rec, 2 * seq_prev_cap() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_drow, (size_t)n_tiles * kFullWaveTile * sizeof(DRow)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential-engine scratch");
     MS_HIP(c, hipMemsetAsync(c->d_spec, 0, NB * sizeof(unsigned long long), c->stream));
     MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, NB * sizeof(uint32_t), c->stream));
@@ -305,6 +308,12 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
     int rc = ensure_tiles(c, n_tiles);
     if (rc) return rc;
+    // the engine's table copy carries the derived rows of the binary64 sweep,
+    // rebuilt here (deltas and binds since the last run) and kept current by
+    // the validator's write-back
+    NodeTable tq = c->t;
+    tq.drow = c->d_drow;
+    MS_HIP(c, launch_build_drows(tq, rows, n_tiles * kFullWaveTile, s));
     // Batch k: speculative sweep + top-4 merge on seq_stream into buffer set
     // k % kSeqBufs, after validation k-D (D = the pipeline depth: every bind up
     // to batch k-D is in the table the sweep reads; validations k-D+1 .. k-1,
@@ -328,9 +337,9 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         // validation launched beside a sweep waited for a SIMD to drain);
         // batch k+1 treats batch k's binds as stale.
         const uint32_t nb0 = std::min(B, n_pods);
-        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
+        MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
         MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, nb0, n_tiles, c->d_top4, c->d_spec,
-                                    c->d_spec_flags, c->t, c->d_top4_rec, s));
+                                    c->d_spec_flags, tq, c->d_top4_rec, s));
         uint32_t k = 0;
         for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
             const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
@@ -338,7 +347,7 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
             unsigned long long *tk = c->d_tile_keys + cells_per_set * seq_topk() * cur;
             unsigned long long *tk1 = c->d_tile_keys + cells_per_set * seq_topk() * nxt;
             uint32_t *tf = c->d_tile_flags + cells_per_set * cur, *tf1 = c->d_tile_flags + cells_per_set * nxt;
-            MS_HIP(c, launch_seq_step(c->t, rows, n_tiles, seed32, d_pods + s0, nb, tk, tf, c->d_spec + SB * cur,
+            MS_HIP(c, launch_seq_step(tq, rows, n_tiles, seed32, d_pods + s0, nb, tk, tf, c->d_spec + SB * cur,
                                       c->d_spec_flags + SB * cur, c->d_top4 + (size_t)SB * seq_topk() * cur,
                                       c->d_top4_rec + recs_per_set * cur,
                                       k ? c->d_prev + prev_words * nxt : nullptr,
@@ -368,12 +377,12 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         uint32_t *sf = c->d_spec_flags + SB * slot;
         int64_t *trec = c->d_top4_rec + recs_per_set * slot;
         if (k >= D) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[(k - D) % kSeqBufs], 0));
-        MS_HIP(c, launch_sweep_full_tiles(c->t, rows, d_pods + s0, nb, seed32, tk, tf, n_tiles, c->seq_stream));
+        MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods + s0, nb, seed32, tk, tf, n_tiles, c->seq_stream));
         MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->t, trec, c->seq_stream));
         MS_HIP(c, hipEventRecord(c->ev_swept[slot], c->seq_stream));
         MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[slot], 0));
         const bool has_prev = D > 1 && k;
-        MS_HIP(c, launch_validate_seq(c->t, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, trec, n_tiles,
+        MS_HIP(c, launch_validate_seq(tq, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, trec, n_tiles,
                                       has_prev ? c->d_prev + prev_words * (par ^ 1u) : nullptr,
                                       has_prev ? c->d_prev_rec + prev_fields * (par ^ 1u) : nullptr,
                                       c->d_prev + prev_words * par, c->d_prev_rec + prev_fields * par, D > 2 ? 1 : 0,

@@ -50,7 +50,25 @@ struct NodeTable {
     // kGroupRows consecutive rows (bit s = row g*kGroupRows + s).
     uint32_t *planes;
     uint32_t gcap;  // groups allocated = cdiv(cap, kGroupRows)
+    // Derived rows of the config-E sweep's binary64 form (DRow), set only in the
+    // table copy the sequential engine passes to its launches: rebuilt at the
+    // start of each run (k_build_drows) and kept current by the validator's
+    // write-back of the rows it binds. nullptr everywhere else.
+    struct DRow *drow;
 };
+
+// One node as the config-E sweep's binary64 LeastAllocated form reads it
+// (ms_kernels.hip make_drow; 64 B, one row per lane and load).
+struct DRow {
+    int64_t fr_cpu, fr_mem;  // Allocatable - Requested (NodeResourcesFit)
+    double r_cpu, r_mem;     // RN(100 / Allocatable), 0 when Allocatable <= 0
+    double a_cpu, a_mem;     // RN(RN((Allocatable - NonZeroRequested) * r) + 2^-43)
+    int32_t room;            // AllowedPodNumber - len(Pods)
+    uint32_t fd;             // flags | digit << 8
+    uint32_t ok;             // 1: the binary64 form is exact for this row
+    uint32_t pad;
+};
+static_assert(sizeof(DRow) == 64, "DRow layout");
 
 constexpr uint32_t kGroupRows = 30;
 enum : uint32_t {
@@ -208,6 +226,9 @@ hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms
                                    uint32_t n_shards, const ms_seq_cand *cands_all, const uint32_t *flags_all,
                                    ms_seq_cand *merged, uint32_t *merged_flags, ms_result *results, uint32_t *n_done,
                                    hipStream_t s);
+// Derived rows [0, n_total) of the sequential engine's table copy (t.drow): rows
+// at or past n_rows are absent.
+hipError_t launch_build_drows(const NodeTable &t, uint32_t n_rows, uint32_t n_total, hipStream_t s);
 // Rows the sequential engine's validator supports (tile lists held in registers).
 uint32_t seq_max_rows();
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,

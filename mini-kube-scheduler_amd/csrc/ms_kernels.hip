@@ -765,14 +765,7 @@ constexpr int64_t kFastCap = 1ll << 41;
 constexpr int64_t kFastReq = 1ll << 53;
 constexpr double kLaEps = 0x1p-43;
 
-struct FastRow {
-    int64_t fr_cpu, fr_mem;  // Allocatable - Requested (NodeResourcesFit)
-    double r_cpu, r_mem;     // RN(100 / Allocatable), 0 when Allocatable <= 0
-    double a_cpu, a_mem;     // RN(RN((Allocatable - NonZeroRequested) * r) + 2^-43)
-    int32_t room;            // AllowedPodNumber - len(Pods)
-    uint32_t fd;             // flags | digit << 8
-    bool ok;                 // the fast form is exact for this row
-};
+typedef DRow FastRow;  // (ms_internal.h)
 
 __device__ __forceinline__ double la_r(int64_t cap) { return cap > 0 ? __ddiv_rn(100.0, (double)cap) : 0.0; }
 
@@ -781,27 +774,42 @@ __device__ __forceinline__ double la_a(int64_t cap, int64_t nz, double r) {
     return __dadd_rn(__dmul_rn((double)av, r), kLaEps);
 }
 
-__device__ __forceinline__ FastRow load_fast_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
-    FastRow x;
-    if (r >= n_rows) {
-        x.fr_cpu = x.fr_mem = 0;
-        x.r_cpu = x.r_mem = x.a_cpu = x.a_mem = 0.0;
-        x.room = 0;
-        x.fd = kNodeAbsent | (0xFFu << 8);
-        x.ok = true;
-        return x;
-    }
-    const int64_t ac = t.alloc_cpu[r], am = t.alloc_mem[r], zc = t.nz_cpu[r], zm = t.nz_mem[r];
-    x.fr_cpu = ac - t.req_cpu[r];
-    x.fr_mem = am - t.req_mem[r];
+__device__ __forceinline__ DRow make_drow(int64_t ac, int64_t am, int64_t rqc, int64_t rqm, int64_t zc, int64_t zm,
+                                          int32_t room, uint32_t fd) {
+    DRow x;
+    x.fr_cpu = (int64_t)((uint64_t)ac - (uint64_t)rqc);
+    x.fr_mem = (int64_t)((uint64_t)am - (uint64_t)rqm);
     x.r_cpu = la_r(ac);
     x.r_mem = la_r(am);
     x.a_cpu = la_a(ac, zc, x.r_cpu);
     x.a_mem = la_a(am, zm, x.r_mem);
-    x.room = t.allowed_pods[r] - t.pod_count[r];
-    x.fd = (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8);
-    x.ok = ac < kFastCap && am < kFastCap && zc >= 0 && zm >= 0;
+    x.room = room;
+    x.fd = fd;
+    x.ok = (ac < kFastCap && am < kFastCap && zc >= 0 && zm >= 0) ? 1u : 0u;
+    x.pad = 0;
     return x;
+}
+
+__device__ __forceinline__ DRow absent_drow() {
+    DRow x;
+    x.fr_cpu = x.fr_mem = 0;
+    x.r_cpu = x.r_mem = x.a_cpu = x.a_mem = 0.0;
+    x.room = 0;
+    x.fd = kNodeAbsent | (0xFFu << 8);
+    x.ok = 1;
+    x.pad = 0;
+    return x;
+}
+
+__device__ __forceinline__ FastRow load_fast_row(const NodeTable &t, uint32_t r, uint32_t n_rows) {
+    if (r >= n_rows) return absent_drow();
+    return make_drow(t.alloc_cpu[r], t.alloc_mem[r], t.req_cpu[r], t.req_mem[r], t.nz_cpu[r], t.nz_mem[r],
+                     t.allowed_pods[r] - t.pod_count[r], (uint32_t)t.flags[r] | ((uint32_t)t.digit[r] << 8));
+}
+
+__global__ void k_build_drows(NodeTable t, uint32_t n_rows, uint32_t n_total) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n_total) t.drow[r] = load_fast_row(t, r, n_rows);
 }
 
 struct PodFast {
@@ -945,9 +953,13 @@ __device__ __forceinline__ u64 quad_max_u64(u64 v) {
 }
 
 __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
-    const u64 hi = umax64(a, b), lo = a > b ? b : a;
-    a = hi;
-    b = lo;
+    // one 64-bit compare, four 32-bit selects (selecting whole u64s lets the
+    // compiler re-derive min with a second compare)
+    const bool c = a > b;
+    const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+    const uint32_t hl = c ? al : bl, hh = c ? ah : bh, ll = c ? bl : al, lh = c ? bh : ah;
+    a = ((u64)hh << 32) | hl;
+    b = ((u64)lh << 32) | ll;
 }
 
 // ----------------------------------------------------------------------------
@@ -1028,14 +1040,15 @@ __device__ __forceinline__ void sweep_topk_group(const Row *x, uint32_t ord0, co
     }
 }
 
-template <int F, typename Row, typename Lanes>
+template <int F, typename Row, typename Lanes, int NPMAX = 2>
 __device__ __forceinline__ void sweep_topk_pods(const Row *x, uint32_t ord0, const Lanes &m, uint32_t pbeg,
                                                 uint32_t cnt, uint32_t lane, uint32_t tile, uint32_t n_tiles,
                                                 u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
     uint32_t i = 0;
-    for (; i + 2 <= cnt; i += 2)
-        sweep_topk_group<F, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
-    if (i < cnt) sweep_topk_group<F, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
+    if (NPMAX >= 2)
+        for (; i + 2 <= cnt; i += 2)
+            sweep_topk_group<F, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
+    for (; i < cnt; ++i) sweep_topk_group<F, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
 }
 
 struct SweepArgs {
@@ -1051,15 +1064,13 @@ struct SweepArgs {
     uint32_t fast;  // binary64 LeastAllocated where exact (default 1)
 };
 
-// One wave: tile `tile`'s top-4 lists and filter flags for the pods of chunk
-// cidx. The binary64 fast form unless a row or pod of the task is outside its
-// exact range (MINISCHED_SEQ_FAST=0 forces the general form: fast == 0).
-__device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t tile, uint32_t cidx, uint32_t lane) {
+// One wave, lane = row: tile `tile`'s top-4 lists and filter flags for pods
+// [pbeg, pbeg + cnt), cnt <= 64. The binary64 fast form unless a row or pod of
+// the task is outside its exact range (MINISCHED_SEQ_FAST=0: a.fast == 0).
+__device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t tile, uint32_t pbeg, uint32_t cnt,
+                                                uint32_t lane) {
     const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
     const uint32_t ord0 = a.t.base + row0;
-    const uint32_t pbeg = cidx * a.chunk;
-    if (pbeg >= a.n_pods) return;
-    const uint32_t cnt = min(min(a.chunk, 64u), a.n_pods - pbeg);
     if (a.fast) {
         FastRow x[kFullSlots];
         bool ok = true;
@@ -1082,6 +1093,167 @@ __device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t til
     const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
     if (rows_huge(x)) sweep_topk_pods<1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
     else sweep_topk_pods<0>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+}
+
+// The transposed form's fallback (a row or pod outside the binary64 range,
+// rare): the general int64 form one pod at a time, lean on registers.
+__device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_t tile, uint32_t pbeg, uint32_t cnt,
+                                                     uint32_t lane) {
+    const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
+    const uint32_t ord0 = a.t.base + row0;
+    FullRow x[kFullSlots];
+#pragma unroll
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
+    const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
+    if (rows_huge(x))
+        sweep_topk_pods<1, FullRow, PodLanes, 1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys,
+                                                 a.tile_flags);
+    else
+        sweep_topk_pods<0, FullRow, PodLanes, 1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys,
+                                                 a.tile_flags);
+}
+
+// ---- transposed sweep: lane = (pod, row part) ------------------------------
+// A workgroup stages one tile's 256 derived rows (t.drow, 16 KB) in LDS; each
+// wave then takes kTpPods pods of the batch: lane 4p + j evaluates pod p
+// against rows j, j+4, .., j+252 (the four lanes of a pod read 4 consecutive
+// rows, the 16 pods' lanes the same ones: LDS broadcasts), keeping its own
+// sorted top-4 (each 4 rows: a sorting network, then a bitonic merge), and
+// the pod's four lanes merge their lists over DPP quad permutations. No cross-lane reduction per row: 1.6x fewer VALU
+// than the lane = row form, whose per-(pod, tile) sort + four wave-wide max
+// extractions dominated.
+constexpr uint32_t kTpPods = 16;
+
+__device__ __forceinline__ void tile_keys_store(u64 *dst, uint32_t j, const u64 (&k)[4]) {
+    *dst = j == 0 ? k[0] : j == 1 ? k[1] : j == 2 ? k[2] : k[3];
+}
+
+__device__ __forceinline__ void sort4_desc(u64 (&x)[4]) {
+    cswap_desc(x[0], x[1]);
+    cswap_desc(x[2], x[3]);
+    cswap_desc(x[0], x[2]);
+    cswap_desc(x[1], x[3]);
+    cswap_desc(x[1], x[2]);
+}
+
+// k <- top 4 of k u s, both sorted descending (bitonic half-cleaner).
+__device__ __forceinline__ void merge4_desc(u64 (&k)[4], const u64 (&s)[4]) {
+    u64 c0 = umax64(k[0], s[3]), c1 = umax64(k[1], s[2]), c2 = umax64(k[2], s[1]), c3 = umax64(k[3], s[0]);
+    cswap_desc(c0, c2);
+    cswap_desc(c1, c3);
+    cswap_desc(c0, c1);
+    cswap_desc(c2, c3);
+    k[0] = c0;
+    k[1] = c1;
+    k[2] = c2;
+    k[3] = c3;
+}
+
+template <int CTRL>
+__device__ __forceinline__ void quad_merge4(u64 (&k)[4], uint32_t &f) {
+    u64 o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = dpp_u64<CTRL>(k[j]);
+    merge4_desc(k, o);
+    f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, CTRL, 0xF, 0xF, false);
+}
+
+// eval_fast for the transposed form, where the pod differs per lane: branch-
+// free filters (bitwise, not short-circuit: no exec-mask branches), the flags
+// OR-ed straight into the lane's accumulators.
+__device__ __forceinline__ u64 eval_tp(const DRow &x, uint32_t ord, const PodFast &q, uint32_t &nu_any,
+                                       uint32_t &nrf_any) {
+    const uint32_t fl = x.fd;
+    const bool absent = (fl & kNodeAbsent) != 0;
+    const bool f_nu = (fl & kNodeUnschedulable) & !absent & !(q.bits & kPfTol);
+    const bool fit_fail = (q.rc > x.fr_cpu) | (q.rm > x.fr_mem);
+    const bool bad = (x.room < 1) | (fit_fail & !(q.bits & kPfZero));
+    const bool reject = absent | f_nu | bad;
+    nu_any |= f_nu ? 1u : 0u;
+    nrf_any |= (bad & !absent & !f_nu) ? 1u : 0u;
+    const uint32_t s_cpu = cvt_u32_sat(__builtin_fma(q.nnc, x.r_cpu, x.a_cpu));
+    const uint32_t s_mem = cvt_u32_sat(__builtin_fma(q.nnm, x.r_mem, x.a_mem));
+    const uint32_t nn = ((fl >> 8) == (q.bits & 0x1FFu)) ? 10u : 0u;
+    const u64 key = make_key(nn + ((s_cpu + s_mem) >> 1), tb_hash(q.A, ord), ord);
+    return reject ? 0ull : key;
+}
+
+// false: a row or pod of the task is outside the binary64 form's exact range
+// and nothing was written (the caller runs the lane = row form instead).
+__device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile, uint32_t grp, uint32_t lane,
+                                              const DRow *rows) {
+    const uint32_t pbeg = grp * kTpPods;
+    if (pbeg >= a.n_pods) return true;  // wave-uniform
+    const uint32_t cnt = min(kTpPods, a.n_pods - pbeg);
+    const uint32_t pi = lane >> 2, part = lane & 3u;
+    ms_pod_rec z = {};
+    const PodFast q = load_pod_fast(pi < cnt ? a.pods[pbeg + pi] : z, a.seed32);
+    uint32_t ok = (pi >= cnt || (q.bits & kPfOk)) ? 1u : 0u;
+    const uint32_t row0 = tile * kFullWaveTile + part;
+    const uint32_t ord0 = a.t.base + row0;
+    const DRow *d = rows + part;  // the tile's rows, staged in LDS
+    u64 k[4] = {0ull, 0ull, 0ull, 0ull};
+    uint32_t nu_any = 0, nrf_any = 0;
+    // rows 4 at a time (LDS reads issued together at the top of each block)
+#pragma unroll 2
+    for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
+        u64 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const DRow &r = d[4 * (i + u)];
+            ok &= r.ok;
+            x[u] = eval_tp(r, ord0 + 4 * (i + u), q, nu_any, nrf_any);
+        }
+        sort4_desc(x);
+        merge4_desc(k, x);
+    }
+    uint32_t f = (nu_any ? 1u : 0u) | (nrf_any ? 0x100u : 0u);
+    quad_merge4<0xB1>(k, f);  // quad_perm [1,0,3,2]
+    quad_merge4<0x4E>(k, f);  // quad_perm [2,3,0,1]
+    if (__ballot(ok == 0u) != 0) return false;
+    if (pi < cnt) {
+        const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
+        tile_keys_store(a.tile_keys + cell * kTopK + part, part, k);
+        if (part == 0) a.tile_flags[cell] = f;
+    }
+    return true;
+}
+
+// One task of the lane = row sweep: (tile, pod chunk cidx of a.chunk pods).
+__device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t tile, uint32_t cidx, uint32_t lane) {
+    const uint32_t pbeg = cidx * a.chunk;
+    if (pbeg >= a.n_pods) return;
+    sweep_rows_task(a, tile, pbeg, min(min(a.chunk, 64u), a.n_pods - pbeg), lane);
+}
+
+// The transposed sweep of one tile by a workgroup of W waves: every thread
+// stages the tile's rows, then wave w takes pod groups w, w + W, ..
+// (block-uniform control flow: every wave reaches both barriers).
+template <int W>
+__device__ __forceinline__ void sweep_tp_tile(const SweepArgs &a, uint32_t tile, DRow *rows, uint32_t wave,
+                                              uint32_t lane) {
+    __syncthreads();  // the previous tile's readers are done
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.t.drow + (size_t)tile * kFullWaveTile);
+    uint4 *dst = reinterpret_cast<uint4 *>(rows);
+    constexpr uint32_t kVec = kFullWaveTile * sizeof(DRow) / sizeof(uint4);
+    for (uint32_t i = threadIdx.x; i < kVec; i += 64u * W) dst[i] = src[i];
+    __syncthreads();
+    uint32_t redo = 0;  // groups outside the binary64 form's range (bit i: the i-th of this wave)
+    for (uint32_t grp = wave, i = 0; grp * kTpPods < a.n_pods; grp += W, ++i)
+        if (!sweep_tp_task(a, tile, grp, lane, rows)) redo |= 1u << i;
+    // (a separate loop: the lane = row form's registers do not add to the transposed form's)
+    for (uint32_t grp = wave, i = 0; redo; grp += W, ++i)
+        if (redo & (1u << i)) {
+            redo &= ~(1u << i);
+            sweep_rows_task_lean(a, tile, grp * kTpPods, min(kTpPods, a.n_pods - grp * kTpPods), lane);
+        }
+}
+
+constexpr int kTpWaves = 8;  // standalone transposed sweep: 8 waves x 16 pods = a full batch per tile
+
+__global__ __launch_bounds__(64 * kTpWaves) void k_sweep_tp_topk(SweepArgs a) {
+    __shared__ DRow rows[kFullWaveTile];
+    sweep_tp_tile<kTpWaves>(a, blockIdx.x, rows, threadIdx.x >> 6, lane_id());
 }
 
 __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(SweepArgs a) {
@@ -1278,6 +1450,7 @@ struct SeqShared {
     WalkResult walkres[16];          // and each one's winner
 };
 static_assert(sizeof(SeqShared) <= 160 * 1024, "validator LDS");
+static_assert(sizeof(SeqShared) >= kFullWaveTile * sizeof(DRow), "a sweep workgroup stages a tile in it");
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
 __device__ __forceinline__ uint32_t claim_hash(uint32_t row) { return (row * 0x85EBCA6Bu) >> (32 - kClaimBits); }
@@ -2007,6 +2180,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         t.nz_cpu[row] = r[F_NZ_CPU];
         t.nz_mem[row] = r[F_NZ_MEM];
         t.pod_count[row] = (int32_t)r[F_CNT];
+        if (t.drow)  // the next sweep's derived row (a sweep reading it now treats the row as stale)
+            t.drow[row] = make_drow(r[F_ALLOC_CPU], r[F_ALLOC_MEM], r[F_REQ_CPU], r[F_REQ_MEM], r[F_NZ_CPU],
+                                    r[F_NZ_MEM], (int32_t)(r[F_ALLOWED] - r[F_CNT]), (uint32_t)r[F_FD]);
         if (prev_out) put_stale(prev_out, prev_recs_out, o, row, r);
     }
     if (lane == 0) S.n_out = n_bl;
@@ -2062,8 +2238,14 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         return;
     }
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    for (uint32_t task = (blockIdx.x - 1) * W + wave; task < n_tasks; task += (gridDim.x - 1) * W)
-        sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
+    if (sw.t.drow && sw.fast) {  // transposed form: a tile per workgroup, its rows in the validator's (idle) LDS
+        DRow *rows = reinterpret_cast<DRow *>(&S);
+        for (uint32_t tile = blockIdx.x - 1; tile < sw.n_tiles; tile += gridDim.x - 1)
+            sweep_tp_tile<W>(sw, tile, rows, wave, lane);
+    } else {
+        for (uint32_t task = (blockIdx.x - 1) * W + wave; task < n_tasks; task += (gridDim.x - 1) * W)
+            sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
+    }
 #ifdef MS_VSTAMPS
     if (lane == 0 && (blockIdx.x - 1) * W + wave < n_tasks) {
         atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 10, __builtin_amdgcn_s_memrealtime() - t_begin);
@@ -2700,6 +2882,11 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
     uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
     if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::min(64, std::max(1, atoi(e)));
+    if (t.drow && seq_fast()) {  // transposed form: one workgroup per tile
+        const SweepArgs a = {t, n_rows, pods, n_pods, kTpPods, seed32, tile_keys, tile_flags, n_tiles, 1u};
+        hipLaunchKernelGGL(k_sweep_tp_topk, dim3(n_tiles), dim3(64 * kTpWaves), 0, s, a);
+        return hipGetLastError();
+    }
     const dim3 grid(gx, cdiv(n_pods, chunk));
     const SweepArgs a = {t, n_rows, pods, n_pods, chunk, seed32, tile_keys, tile_flags, n_tiles, seq_fast()};
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, a);
@@ -2751,10 +2938,12 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     const uint32_t W = J <= 4 ? 12u : J == 8 ? 8u : 4u;
     uint32_t chunk = 8;
     if (n_next) chunk = std::min(64u, std::max(8u, cdiv(n_tiles * n_next, (cus - 1) * W)));
+    const bool tp = t.drow && seq_fast();
+    if (tp) chunk = kTpPods;  // transposed form: a tile per sweep workgroup
     const SweepArgs sw = {t,       n_rows,         next_pods,       n_next,  chunk,
                           seed32,  next_tile_keys, next_tile_flags, n_tiles, seq_fast()};
     const uint32_t n_tasks = n_next ? n_tiles * cdiv(n_next, chunk) : 0u;
-    const uint32_t grid = 1u + std::min(cus - 1, cdiv(n_tasks, W));
+    const uint32_t grid = n_tasks ? 1u + std::min(cus - 1, tp ? n_tiles : cdiv(n_tasks, W)) : 1u;
 #define MS_STEP(JJ, WW) hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks)
     if (J == 1) MS_STEP(1, 12);
     else if (J == 2) MS_STEP(2, 12);
@@ -2779,6 +2968,12 @@ hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t
     else if (n_tiles <= 512) MS_MERGE(8);
     else MS_MERGE(16);
 #undef MS_MERGE
+    return hipGetLastError();
+}
+
+hipError_t launch_build_drows(const NodeTable &t, uint32_t n_rows, uint32_t n_total, hipStream_t s) {
+    if (!t.drow || n_total == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_build_drows, dim3(cdiv(n_total, 256)), dim3(256), 0, s, t, n_rows, n_total);
     return hipGetLastError();
 }
 
