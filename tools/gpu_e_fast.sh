@@ -9,3 +9,6 @@ MINISCHED_SEQ_FAST=$f timeout -k 10 200 python -u tools/bench_configs.py --confi
 echo fast=$f; cut -c1-260 gpurun_out/${TAG}_e_fast$f.jsonl
 done
 bash tools/gpu_e_split.sh ${TAG} | grep -E "sweep_full_topk|validate_seq|topk_merge" | cut -c1-200
+OUT=gpurun_out/e_fused_${TAG}; mkdir -p $OUT
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-format csv -- python -u tools/bench_configs.py --configs E --reps 1 > $OUT/e.jsonl 2> $OUT/e.err || exit 1
+grep -E "seq_step|topk_merge|tp_topk" $OUT/run_kernel_stats.csv | cut -c1-200
