@@ -1119,9 +1119,10 @@ __device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_
 // against rows j, j+4, .., j+252 (the four lanes of a pod read 4 consecutive
 // rows, the 16 pods' lanes the same ones: LDS broadcasts), keeping its own
 // sorted top-4 (each 4 rows: a sorting network, then a bitonic merge), and
-// the pod's four lanes merge their lists over DPP quad permutations. No cross-lane reduction per row: 1.6x fewer VALU
-// than the lane = row form, whose per-(pod, tile) sort + four wave-wide max
-// extractions dominated.
+// the pod's four lanes merge their lists over DPP quad permutations. No
+// cross-lane reduction per (pod, row): ~52 VALU per pair in the inner loop,
+// where the lane = row form paid a sort plus four wave-wide max extractions
+// per (pod, tile) on top of its evaluations.
 constexpr uint32_t kTpPods = 16;
 
 __device__ __forceinline__ void tile_keys_store(u64 *dst, uint32_t j, const u64 (&k)[4]) {
@@ -1238,7 +1239,9 @@ __device__ __forceinline__ void sweep_tp_tile(const SweepArgs &a, uint32_t tile,
     constexpr uint32_t kVec = kFullWaveTile * sizeof(DRow) / sizeof(uint4);
     for (uint32_t i = threadIdx.x; i < kVec; i += 64u * W) dst[i] = src[i];
     __syncthreads();
-    uint32_t redo = 0;  // groups outside the binary64 form's range (bit i: the i-th of this wave)
+    // groups outside the binary64 form's range (bit i: the wave's i-th group;
+    // a batch holds at most kSeqBatch = 128 pods, i.e. 8 groups)
+    uint32_t redo = 0;
     for (uint32_t grp = wave, i = 0; grp * kTpPods < a.n_pods; grp += W, ++i)
         if (!sweep_tp_task(a, tile, grp, lane, rows)) redo |= 1u << i;
     // (a separate loop: the lane = row form's registers do not add to the transposed form's)
