@@ -27,7 +27,7 @@ split over the GPUs (at N = 8 a rank's step is ~60 us and fixed launch /
 collective latencies dominate).
 
 Extra fields (rank 0): the end-to-end pods/s of ms_schedule_batch with host
-arrays (pinned staging, H2D, the cycle, bind commit, D2H; 1 warm-up, median of
+arrays (H2D of the pods, the cycle, bind commit, D2H of the results; 1 warm-up, median of
 5), the class-indexed K1 v8 (round 1, a separately labelled
 shortcut, never `value`), the VALU-issue roofline of the timed kernel with its
 HBM figures, and the CPU baseline (oracle, OpenMP, on the box's host cores).
@@ -175,8 +175,8 @@ def timed(fn, stream, reps):
 
 
 def e2e_host(eng, pods_np, n_nodes):
-    """BASELINE.md §2 pods/s: ms_schedule_batch on host arrays (pinned staging,
-    H2D, the cycle, bind commit, D2H), 1 warm-up then the median of 5."""
+    """BASELINE.md §2 pods/s: ms_schedule_batch on host arrays (H2D of the pods,
+    the cycle, bind commit, D2H of the results), 1 warm-up then the median of 5."""
     from minisched_amd import _lib
 
     eng.schedule(pods_np, _lib.MODE_BATCHED)
@@ -189,8 +189,8 @@ def e2e_host(eng, pods_np, n_nodes):
     P = len(pods_np)
     return {"ms_median": ms, "pods_per_s": P / (ms * 1e-3), "evals_per_s": P * n_nodes / (ms * 1e-3),
             "runs": [t * 1e3 for t in ts],
-            "includes": "ms_schedule_batch: host->pinned copy, H2D pods, filter+score+selectHost+decode, "
-                        "bind commit, D2H results, pinned->host copy"}
+            "includes": "ms_schedule_batch: H2D pods (pageable host array), filter+score+selectHost+decode, "
+                        "bind commit, D2H results into the host array"}
 
 
 def load_profile(path, n_local, n_pods):

@@ -165,7 +165,8 @@ int ms_nodes_read(ms_ctx *ctx, uint32_t first, uint32_t n, ms_node_rec *out);
 
 /* ---- the scheduling cycle ---------------------------------------------------
  * Replaces minisched.go:40-85 for n_pods pods in queue order. Host arrays,
- * copied through pinned staging; out[i] is written before return. With
+ * copied to and from the device within the call (no pointer is kept after it
+ * returns); out[i] is written before return. With
  * MS_MODE_SEQUENTIAL every SUCCESS commits NodeInfo.AddPod on its node before
  * the next pod is decided (bit-exact to the one-at-a-time loop). */
 int ms_schedule_batch(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode,
