@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the e2e / class-indexed measurements")
-    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02t_pmc_C.json"),
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02v_pmc_C.json"),
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
     return ap.parse_args()
 
@@ -333,6 +333,9 @@ def main():
             "traffic": traffic,
             "kernel": PP_KERNEL if os.environ.get("MINISCHED_K1", "pp") == "pp" else os.environ["MINISCHED_K1"],
             "kernel_ms": kernel_ms,
+            # the same kernel's average under rocprofv3 --kernel-trace (the committed summary; the profiler's
+            # per-dispatch completion signals add a few %)
+            "kernel_ms_rocprof": (pj.get("kernel_avg_ns_rocprof") or 0) * 1e-6 if pj else None,
             "valu_insts_per_launch": valu,
             "lane_valu_per_pair": valu * 64 / kernel_evals if valu else None,
             "profile": os.path.relpath(args.profile_json, ROOT) if pj else None,
