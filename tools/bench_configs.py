@@ -45,7 +45,10 @@ def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(s)
-    sp = s.cuda_stream
+    # the device-resident configs run on the engine's own (context) stream, the
+    # API default (stream NULL): a caller stream adds a cross-queue event each
+    # way per call (~19 us at config B, tools/b_stream_ab.py)
+    sp = 0
     out = []
     for c in args.configs.split(","):
         cfg = synth.CONFIGS[c]
@@ -68,6 +71,7 @@ def main():
 
             def run():
                 eng.schedule_sequential_device(P, pods.data_ptr(), results.data_ptr(), sp)
+                torch.cuda.synchronize()
 
             reset()
             run()
@@ -85,7 +89,7 @@ def main():
             inf = eng.info()
             extra["seq_counters_all_reps"] = dict(pods=inf.seq_pods, resweep_tiles=inf.seq_resweep_tiles,
                                                   recomputes=inf.seq_recomputes, overflow=inf._pad)
-            mode = "exact sequential (device-resident)"
+            mode = "exact sequential (device-resident, context stream)"
         elif c == "C":
             eng.upsert(np.arange(N), nr)
             eng.flush()
@@ -97,9 +101,10 @@ def main():
 
             def run():
                 eng.select_batch_device(P, pods.data_ptr(), results.data_ptr(), sp)
+                torch.cuda.synchronize()
 
             med, mn = timed(run, args.reps, s.synchronize)
-            mode = "batched (device-resident fused cycle, one launch)"
+            mode = "batched (device-resident fused cycle, one launch, context stream)"
         line = dict(config=c, nodes=N, pods=P, plugins=cfg["plugins"], mode=mode, median_s=med, min_s=mn,
                     evals_per_s=N * P / med, pods_per_s=P / med, **extra)
         print(json.dumps(line), flush=True)
