@@ -460,19 +460,22 @@ hipError_t decode_for(const ms_ctx *c, const ms_pod_rec *pods, uint32_t n, const
 // fused launch for the whole batch (it needs key scratch only above
 // kPpMaxFusedRows rows); otherwise batch_cap chunks are swept into the
 // context's key/flag scratch, then decoded.
-int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s) {
+// The batched cycle into d_res; commit != 0 also commits every winner's bind
+// (NodeInfo.AddPod), inside the fused K1 pp launch where it runs.
+int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s,
+                  int commit = 0) {
     const uint32_t B = c->batch_cap;
     const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN && k1_pp();
     if (fused && c->rows_dev <= kPpMaxFusedRows) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), nullptr, d_res,
-                                  c->present_dev, c->num_cus, s));
+                                  c->present_dev, c->num_cus, s, commit));
         return MS_OK;
     }
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         if (fused) {
             MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods + s0, nb, seed32_of(c->cfg.seed), c->d_keys,
-                                      d_res + s0, c->present_dev, c->num_cus, s));
+                                      d_res + s0, c->present_dev, c->num_cus, s, commit));
             continue;
         }
         const bool want_flags = c->cfg.plugin_set != MS_PLUGINS_NU_NN;
@@ -480,6 +483,7 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
         if (rc) return rc;
         MS_HIP(c, decode_for(c, d_pods + s0, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev,
                              d_res + s0, s));
+        if (commit) MS_HIP(c, launch_apply_binds(c->t, d_pods + s0, nb, d_res + s0, s));
     }
     return MS_OK;
 }
@@ -736,9 +740,8 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
         } else {
             // NU+NN keys never read mutable node state, so the queue-order
             // loop equals the batched sweep; binds are committed after it.
-            rc = select_locked(c, nb, c->d_pods, c->d_res, s);
+            rc = select_locked(c, nb, c->d_pods, c->d_res, s, 1);
             if (rc) return rc;
-            MS_HIP(c, launch_apply_binds(c->t, c->d_pods, nb, c->d_res, s));
         }
         if (pageable) {
             MS_HIP(c, hipMemcpyAsync(out + s0, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
@@ -867,11 +870,7 @@ int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *
         rc = run_sequential(c, n_pods, pods_dev, results_dev, s);
     } else {
         // NU+NN: keys are independent of mutable state -> batched cycle + commit
-        rc = select_locked(c, n_pods, pods_dev, results_dev, s);
-        if (!rc) {
-            hipError_t e = launch_apply_binds(c->t, pods_dev, n_pods, results_dev, s);
-            if (e != hipSuccess) rc = fail(c, MS_E_HIP, std::string("apply binds: ") + hipGetErrorString(e));
-        }
+        rc = select_locked(c, n_pods, pods_dev, results_dev, s, 1);
     }
     if (rc) return rc;
     if (s == c->stream) {

@@ -100,4 +100,14 @@ __device__ __forceinline__ ms_result decode_key(u64 k, int8_t pod_digit, const u
     return r;
 }
 
+// NodeInfo.AddPod / RemovePod (sign -1) on local row `row` (upstream
+// types.go: Requested += req, NonZeroRequested += nz, len(Pods) += 1).
+__device__ __forceinline__ void add_pod(const NodeTable &t, uint32_t row, const ms_pod_rec &pr, int sign) {
+    atomicAdd(&t.pod_count[row], sign);
+    atomicAdd(reinterpret_cast<u64 *>(&t.req_cpu[row]), (u64)(sign * pr.req_milli_cpu));
+    atomicAdd(reinterpret_cast<u64 *>(&t.req_mem[row]), (u64)(sign * pr.req_memory));
+    atomicAdd(reinterpret_cast<u64 *>(&t.nz_cpu[row]), (u64)(sign * pr.nonzero_milli_cpu));
+    atomicAdd(reinterpret_cast<u64 *>(&t.nz_mem[row]), (u64)(sign * pr.nonzero_memory));
+}
+
 }  // namespace msgpu

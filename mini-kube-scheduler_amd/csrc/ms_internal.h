@@ -148,11 +148,12 @@ hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_r
                              uint32_t *work, int num_cus, hipStream_t s);
 // K1 "pp" (ms_sweep_pp.hip): every (pod, node) pair through NU + NN + selectHost.
 // results != nullptr: decoded ms_result per pod (single-shard cycle; keys is
-// scratch, needed only above 122,880 rows); else keys[i] = this shard's max
-// packed key (0 = none), overwritten. present: global present-node count (decode).
+// scratch, needed only above 122,880 rows), and with commit != 0 each winner's
+// NodeInfo.AddPod in the same launch; else keys[i] = this shard's max packed
+// key (0 = none), overwritten. present: global present-node count (decode).
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
-                           int num_cus, hipStream_t s);
+                           int num_cus, hipStream_t s, int commit = 0);
 // Rows one K1 pp workgroup holds (16 waves x 64 lanes x 4 groups of 30):
 // up to here the single-shard cycle is one launch with no key scratch.
 constexpr uint32_t kPpMaxFusedRows = 16u * 64u * 4u * kGroupRows;

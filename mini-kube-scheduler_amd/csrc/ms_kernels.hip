@@ -2484,14 +2484,6 @@ __global__ void k_decode_jobs(DecodeJobs jobs, uint32_t present) {
         decode_one(jb.pods, reinterpret_cast<const u64 *>(jb.keys), jb.flags, present, jb.results, i);
 }
 
-__device__ __forceinline__ void add_pod(const NodeTable &t, uint32_t row, const ms_pod_rec &pr, int sign) {
-    atomicAdd(&t.pod_count[row], sign);
-    atomicAdd(reinterpret_cast<u64 *>(&t.req_cpu[row]), (u64)(sign * pr.req_milli_cpu));
-    atomicAdd(reinterpret_cast<u64 *>(&t.req_mem[row]), (u64)(sign * pr.req_memory));
-    atomicAdd(reinterpret_cast<u64 *>(&t.nz_cpu[row]), (u64)(sign * pr.nonzero_milli_cpu));
-    atomicAdd(reinterpret_cast<u64 *>(&t.nz_mem[row]), (u64)(sign * pr.nonzero_memory));
-}
-
 __global__ void k_apply_binds(NodeTable t, const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
                               const ms_result *__restrict__ res) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

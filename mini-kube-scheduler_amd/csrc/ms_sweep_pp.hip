@@ -219,7 +219,7 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const uin
 __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
-    int atomic_keys, ms_result *__restrict__ results, uint32_t present) {
+    int atomic_keys, ms_result *__restrict__ results, uint32_t present, NodeTable tab, int commit) {
     // LDS: one combine slot per pod of the chunk, then the chunk's pod entries
     extern __shared__ u64 lds[];
     uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk);
@@ -290,7 +290,14 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
             if (!atomic_keys) keys[pbeg + i] = key;
             else if (key) atomicMax(&keys[pbeg + i], key);
         }
-        if (results) results[pbeg + i] = decode_key(key, (int8_t)(pe.y >> 8), nullptr, 0, present);
+        if (results) {
+            const ms_result r = decode_key(key, (int8_t)(pe.y >> 8), nullptr, 0, present);
+            results[pbeg + i] = r;
+            // assume-on-select in the same launch (ms_schedule_batch / the sequential
+            // NU+NN cycle): NodeInfo.AddPod on the winner, which this context owns
+            // (one workgroup holds all its rows)
+            if (commit && r.code == MS_CODE_SUCCESS) add_pod(tab, (uint32_t)r.node - tab.base, pods[pbeg + i], +1);
+        }
     }
 }
 
@@ -355,7 +362,7 @@ constexpr uint32_t kPpMaxChunk = 2048;
 
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
-                           int num_cus, hipStream_t s) {
+                           int num_cus, hipStream_t s, int commit) {
     if (n_pods == 0) return hipSuccess;
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
@@ -385,13 +392,17 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
         hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
-                           t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present);
+                           t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
+                           t, 0);
         e = hipGetLastError();
         if (e != hipSuccess || !results) return e;
-        return launch_decode(pods, n_pods, keys, nullptr, present, results, s);
+        e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
+        if (e != hipSuccess || !commit) return e;
+        return launch_apply_binds(t, pods, n_pods, results, s);
     }
     hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes, t.gcap,
-                       n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0, results, present);
+                       n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0, results, present, t,
+                       results ? commit : 0);
     return hipGetLastError();
 }
 
