@@ -360,6 +360,40 @@ def test_resource_sequential_capacity_forms(oracle, monkeypatch, fast, n_nodes, 
         assert e.info()._pad == 0
 
 
+def test_resource_sequential_with_deltas(oracle):
+    # the sequential engine across calls with node deltas in between: binds
+    # carried over, a fifth of the nodes deleted (tombstones), half of those
+    # re-added with fresh records; the derived rows of the binary64 sweep are
+    # rebuilt at every call from the table (tests the rebuild, not only the
+    # validator's write-back)
+    n, seed = 3000, 21
+    nr = synth.nodes(n, seed=seed, resources=True)
+    pr = synth.pods(4500, seed=seed, resources=True)
+    with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed) as e:
+        o1 = oracle.schedule(nr, pr[:1500], plugin_set=1, mode=1, seed=seed)
+        assert_same(e.schedule(pr[:1500], MODE_SEQUENTIAL), o1)
+        cols = o1["cols"]
+        dead = np.arange(7, n, 5)
+        e.delete(dead)
+        cols.flags[dead] |= 0x80
+        o2 = oracle.schedule(nr, pr[1500:3000], plugin_set=1, mode=1, seed=seed, cols=cols)
+        assert_same(e.schedule(pr[1500:3000], MODE_SEQUENTIAL), o2)
+        back = dead[::2]
+        e.upsert(back, nr[back])
+        cols.flags[back] = nr["unschedulable"][back] & 1
+        for c, f in (("pod_count", "pod_count"), ("req_cpu", "req_milli_cpu"), ("req_mem", "req_memory"),
+                     ("nz_cpu", "nonzero_milli_cpu"), ("nz_mem", "nonzero_memory")):
+            getattr(cols, c)[back] = nr[f][back]
+        o3 = oracle.schedule(nr, pr[3000:], plugin_set=1, mode=1, seed=seed, cols=cols)
+        assert_same(e.schedule(pr[3000:], MODE_SEQUENTIAL), o3)
+        t = e.read(0, n)
+        live = (cols.flags & 0x80) == 0
+        for k_dev, k_or in (("pod_count", "pod_count"), ("req_milli_cpu", "req_cpu"), ("req_memory", "req_mem"),
+                            ("nonzero_milli_cpu", "nz_cpu"), ("nonzero_memory", "nz_mem")):
+            assert np.array_equal(t[k_dev][live], getattr(cols, k_or)[live]), k_dev
+        assert e.info()._pad == 0
+
+
 def _pods_with_zero_hash(seed, n_nodes, want=4):
     # pods j for which some node ordinal r < n_nodes has tie-break hash exactly 0:
     # mix32(A + r * kG24) == 0 <=> A + r * kG24 == 0 (mix32 is a bijection fixing 0),
