@@ -68,6 +68,9 @@ struct ms_ctx {
     // while batch k validates (caller stream); every buffer above is double-
     // buffered by batch parity
     hipStream_t seq_stream = nullptr;
+    // ms_schedule_batch's chunked copies (schedule_chunked): H2D / D2H of host arrays beside the cycle
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_copy[4] = {nullptr, nullptr, nullptr, nullptr}, ev_cyc[4] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_valid[3] = {nullptr, nullptr, nullptr}, ev_swept[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
@@ -147,6 +150,14 @@ void free_all(ms_ctx *c) {
         if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
     }
     if (c->ev_seq) (void)hipEventDestroy(c->ev_seq);
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+        for (int i = 0; i < 4; ++i) {
+            if (c->ev_copy[i]) (void)hipEventDestroy(c->ev_copy[i]);
+            if (c->ev_cyc[i]) (void)hipEventDestroy(c->ev_cyc[i]);
+        }
+    }
     if (c->seq_stream) {
         (void)hipStreamSynchronize(c->seq_stream);
         (void)hipStreamDestroy(c->seq_stream);
@@ -488,6 +499,58 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
     return MS_OK;
 }
 
+// Chunks of ms_schedule_batch's host-array cycle (NU+NN / NA sets, pageable
+// copies): chunk i+1's H2D (copy stream; the runtime stages pageable memory on
+// the calling thread, which here overlaps chunk i's fused cycle) and chunk i-1's
+// D2H overlap chunk i on the context stream; one cross-stream wait per chunk.
+// MINISCHED_E2E_CHUNKS: 1 turns it off, at most 4.
+constexpr uint32_t kE2eMinChunk = 16384;
+
+uint32_t e2e_chunks(uint32_t n) {
+    static const uint32_t k = [] {
+        const char *e = getenv("MINISCHED_E2E_CHUNKS");
+        return e ? (uint32_t)std::min(4, std::max(1, atoi(e))) : 2u;
+    }();
+    return std::max(1u, std::min(k, n / kE2eMinChunk));
+}
+
+int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *out, uint32_t parts) {
+    const hipStream_t s = c->stream;
+    if (!c->copy_stream) {
+        MS_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        for (int i = 0; i < 4; ++i) {
+            MS_HIP(c, hipEventCreateWithFlags(&c->ev_copy[i], hipEventDisableTiming));
+            MS_HIP(c, hipEventCreateWithFlags(&c->ev_cyc[i], hipEventDisableTiming));
+        }
+    }
+    const hipStream_t cs = c->copy_stream;
+    const uint32_t per = cdiv(n, parts);
+    auto beg = [&](uint32_t i) { return std::min(n, i * per); };
+    auto cnt = [&](uint32_t i) { return beg(i + 1) - beg(i); };
+    MS_HIP(c, hipMemcpyAsync(c->d_pods, pods, sizeof(ms_pod_rec) * cnt(0), hipMemcpyHostToDevice, s));
+    for (uint32_t i = 0; i < parts; ++i) {
+        if (i > 0) MS_HIP(c, hipStreamWaitEvent(s, c->ev_copy[i], 0));
+        int rc = select_locked(c, cnt(i), c->d_pods + beg(i), c->d_res + beg(i), s, 1);
+        if (rc) return rc;
+        MS_HIP(c, hipEventRecord(c->ev_cyc[i], s));
+        if (i + 1 < parts) {
+            MS_HIP(c, hipMemcpyAsync(c->d_pods + beg(i + 1), pods + beg(i + 1), sizeof(ms_pod_rec) * cnt(i + 1),
+                                     hipMemcpyHostToDevice, cs));
+            MS_HIP(c, hipEventRecord(c->ev_copy[i + 1], cs));
+        }
+        if (i > 0) {
+            MS_HIP(c, hipStreamWaitEvent(cs, c->ev_cyc[i - 1], 0));
+            MS_HIP(c, hipMemcpyAsync(out + beg(i - 1), c->d_res + beg(i - 1), sizeof(ms_result) * cnt(i - 1),
+                                     hipMemcpyDeviceToHost, cs));
+        }
+    }
+    MS_HIP(c, hipMemcpyAsync(out + beg(parts - 1), c->d_res + beg(parts - 1), sizeof(ms_result) * cnt(parts - 1),
+                             hipMemcpyDeviceToHost, s));
+    MS_HIP(c, hipStreamSynchronize(cs));
+    MS_HIP(c, hipStreamSynchronize(s));
+    return MS_OK;
+}
+
 bool valid_ctx(const ms_ctx *c) { return c != nullptr; }
 
 }  // namespace
@@ -727,13 +790,19 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, hipStreamSynchronize(s));  // h_pods / h_res free to reuse
+        const bool seq_full = (mode == MS_MODE_SEQUENTIAL && c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA);
+        const uint32_t parts = (pageable && !seq_full) ? e2e_chunks(nb) : 1u;
+        if (parts > 1) {  // (NU+NN / NA: binds never change a later pod's keys, so chunks equal one batch)
+            rc = schedule_chunked(c, pods + s0, nb, out + s0, parts);
+            if (rc) return rc;
+            continue;
+        }
         if (pageable) {
             MS_HIP(c, hipMemcpyAsync(c->d_pods, pods + s0, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
         } else {
             std::memcpy(c->h_pods, pods + s0, sizeof(ms_pod_rec) * nb);
             MS_HIP(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
         }
-        const bool seq_full = (mode == MS_MODE_SEQUENTIAL && c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA);
         if (seq_full) {
             rc = run_sequential(c, nb, c->d_pods, c->d_res, s);
             if (rc) return rc;
