@@ -2048,6 +2048,11 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
             const uint32_t p = g + s;
             ++ctr.slow;
             const PodFull q = load_pod(S.pods[p], seed32);
+            // the pod's tile lists, issued before the top-4 re-evaluation below so
+            // their memory round trip overlaps it (every slow pod of config E scans
+            // them: all four entries touched, or a FitError needing the flags)
+            TileLists<J> B;
+            load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
             u64 b = 0;
             int wslot = -1;
             uint32_t fmask = 0;
@@ -2077,10 +2082,8 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
             } else {
                 scan = true;  // all four touched: rows below them are unknown
             }
-            TileLists<J> B;
             if (scan) {
                 ++ctr.scan;
-                load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
                 validate_scan<J>(S, t, n_rows, q, B, tiles, lane, ctr, b, wslot);
             }
             uint32_t info;
