@@ -467,12 +467,11 @@ hipError_t decode_for(const ms_ctx *c, const ms_pod_rec *pods, uint32_t n, const
 }
 
 // The stateless cycle of a batch on a single-shard context: filter + score +
-// selectHost + decode into results, no bind commit. NU+NN with K1 pp is one
-// fused launch for the whole batch (it needs key scratch only above
-// kPpMaxFusedRows rows); otherwise batch_cap chunks are swept into the
-// context's key/flag scratch, then decoded.
-// The batched cycle into d_res; commit != 0 also commits every winner's bind
-// (NodeInfo.AddPod), inside the fused K1 pp launch where it runs.
+// selectHost + decode into results; commit != 0 also commits every winner's
+// bind (NodeInfo.AddPod). NU+NN with K1 pp is one fused launch for the whole
+// batch, binds included (it needs key scratch only above kPpMaxFusedRows
+// rows); otherwise batch_cap chunks are swept into the context's key/flag
+// scratch, then decoded (and their binds applied).
 int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s,
                   int commit = 0) {
     const uint32_t B = c->batch_cap;
