@@ -356,8 +356,9 @@ hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, ui
 
 // Geometry: W waves (<= 16) of up to 256 groups each hold the rows (more
 // rows: grid.y workgroups per chunk); pods per workgroup sized for one
-// round of resident workgroups (32 waves per CU) in multiples of 8, at most
-// kPpMaxChunk (LDS). MINISCHED_PP_CHUNK overrides the chunk (tuning).
+// round of resident workgroups (16 waves per CU while chunks stay <= 1024
+// pods, else 32) in multiples of 8, at most kPpMaxChunk (LDS).
+// MINISCHED_PP_CHUNK overrides the chunk (tuning).
 constexpr uint32_t kPpMaxChunk = 2048;
 
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
@@ -378,11 +379,21 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     if (const char *w = getenv("MINISCHED_PP_WAVES")) W = (uint32_t)std::min(16, std::max(1, atoi(w)));
     if (!keys) W = std::max(W, std::min<uint32_t>(kPpMaxWaves, waves_needed));  // no scratch: one workgroup per chunk
     const uint32_t gy = std::max(1u, cdiv(n_groups, W * kPpWaveGroups));
-    const uint32_t per_cu = std::max(1u, 32u / W);
-    const uint32_t resident = per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256) / gy;
+    const uint32_t cus = (uint32_t)(num_cus > 0 ? num_cus : 256);
     // (multiples of 8: a wave takes pods 8 at a time, and a part-filled 8 costs
     // a full one -- exact chunks ran 11% slower at 25k rows, r02k_ab_chunk.txt)
-    uint32_t chunk = cdiv(cdiv(n_pods, std::max(1u, resident)), 8) * 8;
+    auto chunk_for = [&](uint32_t per_cu) {
+        const uint32_t resident = std::max(1u, per_cu * cus / gy);
+        return cdiv(cdiv(n_pods, resident), 8) * 8;
+    };
+    uint32_t chunk = chunk_for(std::max(1u, 32u / W));  // one round at 32 waves per CU
+    // Half as many workgroups (16 waves per CU, 4 per SIMD still saturate VALU
+    // issue) while chunks stay modest: each workgroup's fixed costs (plane
+    // loads, pod prologue, two barriers, epilogue) are paid half as often.
+    // Config C 334 -> 324 us and 350 -> 341 us on two boxes; at 1M pods (chunks
+    // near 2k) it was 1.3% slower, at 12.5k rows x 800k pods (784) 1.6% faster
+    // (profiles/r02zb_ab_chunk_half.jsonl).
+    if (32u / W > 1u && chunk_for(std::max(1u, 16u / W)) <= 1024u) chunk = chunk_for(std::max(1u, 16u / W));
     if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
     const dim3 grid(cdiv(n_pods, chunk), gy);
