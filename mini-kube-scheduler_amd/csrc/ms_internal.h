@@ -65,10 +65,16 @@ struct DRow {
     double a_cpu, a_mem;     // RN(RN((Allocatable - NonZeroRequested) * r) + 2^-43)
     int32_t room;            // AllowedPodNumber - len(Pods)
     uint32_t fd;             // flags | digit << 8
-    uint32_t ok;             // 1: the binary64 form is exact for this row
-    uint32_t pad;
+    uint32_t digit;          // name digit (0xFF: none)
+    uint32_t rbits;          // kRb* below: the row's static filter outcomes, precomputed
 };
 static_assert(sizeof(DRow) == 64, "DRow layout");
+// DRow::rbits. kRbUnsched and kRbNoRoom are set for present rows only.
+constexpr uint32_t kRbAbsent = 1u;   // not in Nodes().List
+constexpr uint32_t kRbUnsched = 2u;  // Spec.Unschedulable (NodeUnschedulable rejects unless tolerated)
+constexpr uint32_t kRbNoRoom = 4u;   // AllowedPodNumber - len(Pods) < 1 (NodeResourcesFit rejects every pod)
+constexpr uint32_t kRbSlow = 8u;     // the binary64 LeastAllocated form is not exact for this row
+constexpr uint32_t kRbBlocked = 16u; // absent or unschedulable: no pod that does not tolerate it may bind here
 
 constexpr uint32_t kGroupRows = 30;
 enum : uint32_t {

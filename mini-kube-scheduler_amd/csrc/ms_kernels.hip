@@ -785,8 +785,12 @@ __device__ __forceinline__ DRow make_drow(int64_t ac, int64_t am, int64_t rqc, i
     x.a_mem = la_a(am, zm, x.r_mem);
     x.room = room;
     x.fd = fd;
-    x.ok = (ac < kFastCap && am < kFastCap && zc >= 0 && zm >= 0) ? 1u : 0u;
-    x.pad = 0;
+    x.digit = fd >> 8;
+    const bool absent = (fd & kNodeAbsent) != 0;
+    const bool unsched = !absent && (fd & kNodeUnschedulable);
+    x.rbits = (absent ? kRbAbsent : 0u) | (unsched ? kRbUnsched : 0u) | (absent || unsched ? kRbBlocked : 0u) |
+              (!absent && room < 1 ? kRbNoRoom : 0u) |
+              ((ac < kFastCap && am < kFastCap && zc >= 0 && zm >= 0) ? 0u : kRbSlow);
     return x;
 }
 
@@ -796,8 +800,8 @@ __device__ __forceinline__ DRow absent_drow() {
     x.r_cpu = x.r_mem = x.a_cpu = x.a_mem = 0.0;
     x.room = 0;
     x.fd = kNodeAbsent | (0xFFu << 8);
-    x.ok = 1;
-    x.pad = 0;
+    x.digit = 0xFFu;
+    x.rbits = kRbAbsent | kRbBlocked;
     return x;
 }
 
@@ -817,6 +821,8 @@ struct PodFast {
     double nnc, nnm;   // -(double) non-zero requests (LeastAllocated)
     uint32_t A;
     uint32_t bits;     // digit (9 bits, sign-extended) | kPfTol | kPfZero | kPfOk
+    uint32_t rej;      // DRow::rbits that reject the pod statically: absent, no room, unschedulable unless tolerated
+    uint32_t cand;     // DRow::rbits that exclude a rejection from NodeResourcesFit: absent, NU-rejected
 };
 constexpr uint32_t kPfTol = 0x200u, kPfZero = 0x400u, kPfOk = 0x800u;
 
@@ -832,6 +838,8 @@ __device__ __forceinline__ PodFast load_pod_fast(const ms_pod_rec &pr, uint32_t 
     // the digit as 9 bits: a negative (non-digit) name never equals a node's digit byte
     q.bits = ((uint32_t)(int32_t)pr.name_digit & 0x1FFu) | (pr.tolerates_unschedulable ? kPfTol : 0u) |
              ((pr.req_milli_cpu == 0 && pr.req_memory == 0) ? kPfZero : 0u) | (ok ? kPfOk : 0u);
+    q.cand = kRbAbsent | (pr.tolerates_unschedulable ? 0u : kRbUnsched);
+    q.rej = q.cand | kRbNoRoom;
     return q;
 }
 
@@ -847,6 +855,8 @@ __device__ __forceinline__ PodFast pod_fast_of_lane(const PodFast &m, uint32_t i
     q.nnm = readlane_f64(m.nnm, i);
     q.A = (uint32_t)__builtin_amdgcn_readlane((int)m.A, (int)i);
     q.bits = (uint32_t)__builtin_amdgcn_readlane((int)m.bits, (int)i);
+    q.rej = (uint32_t)__builtin_amdgcn_readlane((int)m.rej, (int)i);
+    q.cand = (uint32_t)__builtin_amdgcn_readlane((int)m.cand, (int)i);
     return q;
 }
 
@@ -859,17 +869,17 @@ __device__ __forceinline__ uint32_t cvt_u32_sat(double x) {  // negatives -> 0
 // eval_full's key and first-failure flags through the binary64 LeastAllocated.
 __device__ __forceinline__ u64 eval_fast(const FastRow &x, uint32_t ord, const PodFast &q, uint32_t &nu,
                                          uint32_t &nrf) {
-    const uint32_t fl = x.fd & 0xFFu;
-    const bool absent = (fl & kNodeAbsent) != 0;
-    const bool f_nu = !absent && (fl & kNodeUnschedulable) != 0 && !(q.bits & kPfTol);
-    bool bad = x.room < 1;
+    const uint32_t rb = x.rbits;
+    const bool absent = (rb & kRbAbsent) != 0;
+    const bool f_nu = (rb & kRbUnsched) != 0 && !(q.bits & kPfTol);
+    bool bad = (rb & kRbNoRoom) != 0;
     if (!(q.bits & kPfZero)) bad = bad || (q.rc > x.fr_cpu) || (q.rm > x.fr_mem);
     const bool f_nrf = !absent && !f_nu && bad;
     nu = f_nu ? 1u : 0u;
     nrf = f_nrf ? 1u : 0u;
     const uint32_t s_cpu = cvt_u32_sat(__builtin_fma(q.nnc, x.r_cpu, x.a_cpu));
     const uint32_t s_mem = cvt_u32_sat(__builtin_fma(q.nnm, x.r_mem, x.a_mem));
-    const uint32_t nn = ((x.fd >> 8) == (q.bits & 0x1FFu)) ? 10u : 0u;
+    const uint32_t nn = (x.digit == (q.bits & 0x1FFu)) ? 10u : 0u;
     const u64 key = make_key(nn + ((s_cpu + s_mem) >> 1), tb_hash(q.A, ord), ord);
     return (absent || f_nu || bad) ? 0ull : key;
 }
@@ -1077,7 +1087,7 @@ __device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t til
 #pragma unroll
         for (int s = 0; s < kFullSlots; ++s) {
             x[s] = load_fast_row(a.t, row0 + s, a.n_rows);
-            ok = ok && x[s].ok;
+            ok = ok && !(x[s].rbits & kRbSlow);
         }
         ms_pod_rec z = {};
         const PodFast m = load_pod_fast(lane < cnt ? a.pods[pbeg + lane] : z, a.seed32);
@@ -1159,59 +1169,74 @@ __device__ __forceinline__ void quad_merge4(u64 (&k)[4], uint32_t &f) {
     f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, CTRL, 0xF, 0xF, false);
 }
 
-// eval_fast for the transposed form, where the pod differs per lane: branch-
-// free filters (bitwise, not short-circuit: no exec-mask branches), the flags
-// OR-ed straight into the lane's accumulators.
-__device__ __forceinline__ u64 eval_tp(const DRow &x, uint32_t ord, const PodFast &q, uint32_t &nu_any,
-                                       uint32_t &nrf_any) {
-    const uint32_t fl = x.fd;
-    const bool absent = (fl & kNodeAbsent) != 0;
-    const bool f_nu = (fl & kNodeUnschedulable) & !absent & !(q.bits & kPfTol);
+// eval_fast for the transposed form, where the pod differs per lane: the
+// static filters from the row's precomputed rbits (one AND + compare), Fit's
+// two compares; the filter flags come from the tile's rbits (TileBits).
+__device__ __forceinline__ u64 eval_tp(const DRow &x, uint32_t ord, const PodFast &q) {
     const bool fit_fail = (q.rc > x.fr_cpu) | (q.rm > x.fr_mem);
-    const bool bad = (x.room < 1) | (fit_fail & !(q.bits & kPfZero));
-    const bool reject = absent | f_nu | bad;
-    nu_any |= f_nu ? 1u : 0u;
-    nrf_any |= (bad & !absent & !f_nu) ? 1u : 0u;
+    const bool reject = ((x.rbits & q.rej) != 0) | (fit_fail & !(q.bits & kPfZero));
     const uint32_t s_cpu = cvt_u32_sat(__builtin_fma(q.nnc, x.r_cpu, x.a_cpu));
     const uint32_t s_mem = cvt_u32_sat(__builtin_fma(q.nnm, x.r_mem, x.a_mem));
-    const uint32_t nn = ((fl >> 8) == (q.bits & 0x1FFu)) ? 10u : 0u;
-    const u64 key = make_key(nn + ((s_cpu + s_mem) >> 1), tb_hash(q.A, ord), ord);
+    const uint32_t nn2 = x.digit == (q.bits & 0x1FFu) ? 20u : 0u;  // nn + floor(s / 2) = floor((s + 2 nn) / 2)
+    const u64 key = make_key((s_cpu + s_mem + nn2) >> 1, tb_hash(q.A, ord), ord);
     return reject ? 0ull : key;
+}
+
+// OR (any) and AND (all) of a staged tile's rbits, wave-uniform.
+struct TileBits {
+    uint32_t any, all;
+};
+
+__device__ __forceinline__ TileBits tile_bits(const DRow *rows, uint32_t lane) {
+    uint32_t o = 0, a = ~0u;
+#pragma unroll
+    for (int k = 0; k < (int)kFullWaveTile / 64; ++k) {
+        const uint32_t r = rows[lane + 64u * k].rbits;
+        o |= r;
+        a &= r;
+    }
+    TileBits b = {0u, 0u};
+#pragma unroll
+    for (uint32_t bit = 1; bit <= kRbBlocked; bit <<= 1) {
+        if (__ballot((o & bit) != 0)) b.any |= bit;
+        if (!__ballot((a & bit) == 0)) b.all |= bit;
+    }
+    return b;
 }
 
 // false: a row or pod of the task is outside the binary64 form's exact range
 // and nothing was written (the caller runs the lane = row form instead).
+// Tile flags: NodeUnschedulable if a present unschedulable row exists and the
+// pod does not tolerate it; NodeResourcesFit if a row is neither absent nor
+// NodeUnschedulable-rejected. For a tile with no feasible row that is exactly
+// "a row NodeResourcesFit rejected"; for a tile with a feasible row every
+// consumer (merge_pod_lists, the validator) sets NodeResourcesFit anyway.
 __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile, uint32_t grp, uint32_t lane,
-                                              const DRow *rows) {
+                                              const DRow *rows, TileBits tb) {
     const uint32_t pbeg = grp * kTpPods;
     if (pbeg >= a.n_pods) return true;  // wave-uniform
     const uint32_t cnt = min(kTpPods, a.n_pods - pbeg);
     const uint32_t pi = lane >> 2, part = lane & 3u;
     ms_pod_rec z = {};
     const PodFast q = load_pod_fast(pi < cnt ? a.pods[pbeg + pi] : z, a.seed32);
-    uint32_t ok = (pi >= cnt || (q.bits & kPfOk)) ? 1u : 0u;
+    if ((tb.any & kRbSlow) || __ballot(pi < cnt && !(q.bits & kPfOk))) return false;
     const uint32_t row0 = tile * kFullWaveTile + part;
     const uint32_t ord0 = a.t.base + row0;
     const DRow *d = rows + part;  // the tile's rows, staged in LDS
     u64 k[4] = {0ull, 0ull, 0ull, 0ull};
-    uint32_t nu_any = 0, nrf_any = 0;
     // rows 4 at a time (LDS reads issued together at the top of each block)
 #pragma unroll 2
     for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
         u64 x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const DRow &r = d[4 * (i + u)];
-            ok &= r.ok;
-            x[u] = eval_tp(r, ord0 + 4 * (i + u), q, nu_any, nrf_any);
-        }
+        for (int u = 0; u < 4; ++u) x[u] = eval_tp(d[4 * (i + u)], ord0 + 4 * (i + u), q);
         sort4_desc(x);
         merge4_desc(k, x);
     }
-    uint32_t f = (nu_any ? 1u : 0u) | (nrf_any ? 0x100u : 0u);
+    const bool tol = (q.bits & kPfTol) != 0;
+    uint32_t f = ((tb.any & kRbUnsched) && !tol ? 1u : 0u) | (tb.all & (tol ? kRbAbsent : kRbBlocked) ? 0u : 0x100u);
     quad_merge4<0xB1>(k, f);  // quad_perm [1,0,3,2]
     quad_merge4<0x4E>(k, f);  // quad_perm [2,3,0,1]
-    if (__ballot(ok == 0u) != 0) return false;
     if (pi < cnt) {
         const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
         tile_keys_store(a.tile_keys + cell * kTopK + part, part, k);
@@ -1239,11 +1264,12 @@ __device__ __forceinline__ void sweep_tp_tile(const SweepArgs &a, uint32_t tile,
     constexpr uint32_t kVec = kFullWaveTile * sizeof(DRow) / sizeof(uint4);
     for (uint32_t i = threadIdx.x; i < kVec; i += 64u * W) dst[i] = src[i];
     __syncthreads();
+    const TileBits tb = tile_bits(rows, lane);
     // groups outside the binary64 form's range (bit i: the wave's i-th group;
     // a batch holds at most kSeqBatch = 128 pods, i.e. 8 groups)
     uint32_t redo = 0;
     for (uint32_t grp = wave, i = 0; grp * kTpPods < a.n_pods; grp += W, ++i)
-        if (!sweep_tp_task(a, tile, grp, lane, rows)) redo |= 1u << i;
+        if (!sweep_tp_task(a, tile, grp, lane, rows, tb)) redo |= 1u << i;
     // (a separate loop: the lane = row form's registers do not add to the transposed form's)
     for (uint32_t grp = wave, i = 0; redo; grp += W, ++i)
         if (redo & (1u << i)) {
