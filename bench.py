@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the e2e / class-indexed measurements")
-    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02zc_pmc_C.json"),
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02zh_pmc_C.json"),
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
     return ap.parse_args()
 
