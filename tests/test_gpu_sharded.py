@@ -33,7 +33,17 @@ def _same(res, o, a, b, tag):
         assert np.array_equal(res[k_res], o[k_or][a:b]), f"{tag} {k_res}"
 
 
-def _worker(rank, world, port, split, depth, group, q):
+def _dead(kind):
+    """Global ordinals deleted before the cycle (the FitError mask must use the
+    cluster's present count; with every node gone the reference reports an empty plugin set)."""
+    if kind == "third":
+        return np.arange(0, N_NODES, 3)
+    if kind == "all":
+        return np.arange(N_NODES)
+    return np.arange(0)
+
+
+def _worker(rank, world, port, split, depth, group, q, dead=None):
     import torch
     import torch.distributed as dist
 
@@ -49,6 +59,11 @@ def _worker(rank, world, port, split, depth, group, q):
         eng = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NN, node_base=lo, seed=SEED)
         eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=SEED, start=lo))
         eng.flush()
+        gone = _dead(dead)
+        gone = gone[(gone >= lo) & (gone < hi)]
+        if len(gone):
+            eng.delete(gone.astype(np.uint32))
+            eng.flush()
         present = sharded.present_total(eng) if split == "nodes" else None
         pods = torch.from_numpy(synth.pods(N_PODS, seed=SEED).view(np.uint8).copy()).to(dev)
         stream = torch.cuda.Stream(device=dev)
@@ -67,13 +82,15 @@ def _worker(rank, world, port, split, depth, group, q):
         q.put((rank, 0, 0, None, None, repr(e)))
 
 
-@pytest.mark.parametrize("split,depth,group", [("nodes", 1, 1), ("nodes", 2, 2), ("nodes", 3, 1), ("pods", 1, 1)])
-def test_two_rank_cycle_on_gpu(oracle, split, depth, group):
+@pytest.mark.parametrize("split,depth,group,dead", [("nodes", 1, 1, None), ("nodes", 2, 2, None), ("nodes", 3, 1, None),
+                                                    ("pods", 1, 1, None), ("nodes", 1, 1, "third"),
+                                                    ("nodes", 1, 1, "all"), ("pods", 1, 1, "third")])
+def test_two_rank_cycle_on_gpu(oracle, split, depth, group, dead):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, split, depth, group, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, split, depth, group, q, dead)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=110) for _ in range(world)]
@@ -81,13 +98,17 @@ def test_two_rank_cycle_on_gpu(oracle, split, depth, group):
         p.join(timeout=60)
     errs = [e for *_, e in got if e]
     assert not errs, errs
-    o = oracle.schedule(synth.nodes(N_NODES, seed=SEED), synth.pods(N_PODS, seed=SEED), seed=SEED)
+    nr = synth.nodes(N_NODES, seed=SEED)
+    nr["allowed_pods"][_dead(dead)] = -1  # oracle: absent from the node list
+    o = oracle.schedule(nr, synth.pods(N_PODS, seed=SEED), seed=SEED)
     covered = 0
     for rank, a, b, res, present, _ in got:
         _same(res, o, a, b, f"rank {rank}")
         covered += b - a
         if split == "nodes":
-            assert present == N_NODES  # summed over the shards
+            assert present == N_NODES - len(_dead(dead))  # summed over the shards
+    if dead == "all":
+        assert (o["mask"] == 0).all() and (o["code"] != 0).all()
     assert covered == N_PODS
 
 
