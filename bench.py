@@ -9,28 +9,29 @@ at 100k nodes on 1/2/4/8 GPUs -> workload = config C: 100,000 nodes x
 One step = the whole pod batch through the hot path with inputs resident in HBM:
   N = 1: ms_select_batch_device — ONE fused launch: filter -> score ->
          selectHost argmax -> decode of every pod (minisched.go:40-85).
-  N > 1, --split nodes (default, the north star's node sharding): each rank
-         sweeps all P pods against its N/G-row shard (ms_sweep_device), one RCCL
-         reduce-scatter (MAX) of the packed keys leaves each rank the combined
-         keys of its P/G pods, and it decodes those; step k's collective overlaps
-         the next steps' sweeps (sharded.CrossStepPipeline), the last steps are
-         drained inside the timed region.
+  N > 1, --split nodes (default, the north star's node sharding): every rank's
+         context joins one in-library RCCL communicator (sharded.init_comm) and
+         a step is ms_sharded_submit: the sweep of all P pods against the
+         rank's N/G-row shard, ONE grouped reduce-scatter (uint64 MAX of the
+         packed keys) leaving each rank the combined keys of its P/G pods, and
+         their decode — the library pipelines step k's collective under the
+         next steps' sweeps; ms_sharded_drain ends the timed region. This is
+         the path a Go scheduleOne binds.
   N > 1, --split pods: every rank holds the whole (100 KB) node table and runs
          the fused cycle on its P/G pods; no collective.
 value = P * N / step time (max over ranks): whole-job evals/s.
 
-Scaling (--scaling, default weak): every GPU brings config C's 100k-pod batch,
-so at N GPUs one step schedules N x 100k pods against the same 100k nodes (each
-rank sweeps all N x 100k pods against its 100k/N rows and decodes its 100k;
-per-GPU evaluations stay 1e10). --scaling strong keeps the job at 100k pods
-split over the GPUs (at N = 8 a rank's step is ~60 us and fixed launch /
-collective latencies dominate).
+Scaling (--scaling, default strong): config C as BASELINE.json states it —
+100k nodes x 100k pods split over the N GPUs (each rank: 100k pods against its
+100k/N rows, decode of its 100k/N pods). --scaling weak: every GPU brings its
+own 100k-pod batch (N x 100k pods per step), a labelled extra.
 
-Extra fields (rank 0): the end-to-end pods/s of ms_schedule_batch with host
-arrays (H2D of the pods, the cycle, bind commit, D2H of the results; 1 warm-up, median of
-5), the class-indexed K1 v8 (round 1, a separately labelled
-shortcut, never `value`), the VALU-issue roofline of the timed kernel with its
-HBM figures, and the CPU baseline (oracle, OpenMP, on the box's host cores).
+Extra fields (rank 0): pods/s per SURVEY §8(d) — ms_schedule_batch on host
+arrays (H2D of the pods, the cycle, bind commit, D2H of the results; 1
+warm-up, median of 5; with N > 1 the collective host call over the
+communicator) — as the top-level `pods_per_s`, the device-resident rate as
+`device_pods_per_s`, the VALU-issue roofline of the timed kernel with its HBM
+figures, and the CPU baseline (oracle, OpenMP, on the box's host cores).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N > 1 the driver
 uses torch.distributed.run with one rank per GPU.
@@ -70,9 +71,9 @@ def parse():
     ap.add_argument("--config", default="C", choices=["B", "C", "D"])
     ap.add_argument("--split", default=None, choices=["nodes", "pods"],
                     help="N > 1 partition (default: nodes for B/C, pods for D)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak (default): every GPU brings the config's pod batch, so the job schedules "
-                         "N x P pods against the same N nodes; strong: the config's P pods split over the GPUs")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default): the config's P pods split over the GPUs (BASELINE config C); weak: "
+                         "every GPU brings the config's pod batch, so the job schedules N x P pods")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -174,23 +175,31 @@ def timed(fn, stream, reps):
     return a.elapsed_time(b) / reps
 
 
-def e2e_host(eng, pods_np, n_nodes):
-    """BASELINE.md §2 pods/s: ms_schedule_batch on host arrays (H2D of the pods,
-    the cycle, bind commit, D2H of the results), 1 warm-up then the median of 5."""
+def e2e_host(eng, pods_np, n_nodes, world=1):
+    """SURVEY §8(d) / BASELINE.md §2 pods/s: ms_schedule_batch on host arrays (H2D
+    of the pods, the cycle, bind commit, D2H of the results), 1 warm-up then the
+    median of 5. With N > 1 the call is collective over the in-library
+    communicator: every rank passes the same pods and receives every result."""
+    import torch.distributed as dist
+
     from minisched_amd import _lib
 
-    eng.schedule(pods_np, _lib.MODE_BATCHED)
+    out = np.zeros(len(pods_np), dtype=_lib.RESULT)
+    eng.schedule(pods_np, _lib.MODE_BATCHED, out=out)
     ts = []
     for _ in range(5):
+        if world > 1:
+            dist.barrier()
         t0 = time.perf_counter()
-        eng.schedule(pods_np, _lib.MODE_BATCHED)
+        eng.schedule(pods_np, _lib.MODE_BATCHED, out=out)
         ts.append(time.perf_counter() - t0)
     ms = float(np.median(ts)) * 1e3
     P = len(pods_np)
     return {"ms_median": ms, "pods_per_s": P / (ms * 1e-3), "evals_per_s": P * n_nodes / (ms * 1e-3),
             "runs": [t * 1e3 for t in ts],
-            "includes": "ms_schedule_batch: H2D pods (pageable host array), filter+score+selectHost+decode, "
-                        "bind commit, D2H results into the host array"}
+            "includes": "ms_schedule_batch: H2D pods (pageable host array), filter+score+selectHost+decode"
+                        + (", reduce-scatter + all-gather over the communicator" if world > 1 else "")
+                        + ", bind commit, D2H results into the host array"}
 
 
 def load_profile(path, n_local, n_pods):
@@ -199,8 +208,6 @@ def load_profile(path, n_local, n_pods):
     except Exception:
         return None
     if pj.get("kernel") != PP_KERNEL or pj.get("nodes") != n_local or pj.get("pods") != n_pods:
-        return None
-    if os.environ.get("MINISCHED_K1", "pp") != "pp":
         return None
     return pj
 
@@ -241,7 +248,12 @@ def main():
                       device=local_dev)
     eng.upsert(np.arange(lo, hi, dtype=np.uint32), synth.nodes(hi - lo, seed=args.seed, start=lo))
     eng.flush()
-    present = sharded.present_total(eng) if split == "nodes" else None
+    # N > 1 node split over RCCL: the in-library communicator (the Go-bindable path);
+    # gloo rehearsals keep the Python combine
+    use_lib = world > 1 and split == "nodes" and backend == "nccl"
+    if use_lib:
+        sharded.init_comm(eng)
+    present = sharded.present_total(eng) if split == "nodes" and not use_lib else None
 
     pods_np = synth.pods(P, seed=args.seed)
     pods = torch.from_numpy(pods_np.view(np.uint8).copy()).to(dev)
@@ -288,7 +300,12 @@ def main():
     # the dominant kernel alone, on the step stream: the fused cycle (N = 1 or
     # pod split) or this rank's sweep (node split)
     reps = max(3, min(args.steps, 10))
-    if cyc._collective:
+    if cyc.library:
+        kbuf = torch.empty(P, dtype=torch.int64, device=dev)
+        kernel_ms = timed(lambda: eng.sweep_device(P, pods.data_ptr(), kbuf.data_ptr(), 0, stream.cuda_stream),
+                          stream, reps)
+        kernel_evals = float(P) * float(hi - lo)
+    elif cyc._collective:
         kernel_ms = timed(lambda: cyc.sweep(0), stream, reps)
         kernel_evals = float(P) * float(hi - lo)
     else:
@@ -296,24 +313,12 @@ def main():
         kernel_evals = float(cyc.b - cyc.a) * float(hi - lo)
 
     extras = {}
-    if rank == 0 and world == 1 and not args.no_extras:
-        # class-indexed round-1 kernel (v8 class lists: NOT a per-pair evaluation)
-        keys = torch.empty(P, dtype=torch.int64, device=dev)
-        prev = os.environ.get("MINISCHED_K1")
-        os.environ["MINISCHED_K1"] = "v8"
+    if not args.no_extras:
+        # SURVEY §8(d) pods/s: ms_schedule_batch on host arrays (collective with N > 1)
         try:
-            ci_ms = timed(lambda: eng.sweep_device(P, pods.data_ptr(), keys.data_ptr(), 0, stream.cuda_stream),
-                          stream, reps)
-        finally:
-            if prev is None:
-                os.environ.pop("MINISCHED_K1", None)
-            else:
-                os.environ["MINISCHED_K1"] = prev
-        extras["class_indexed"] = {
-            "kernel": "k_sweep_nunn_v8 (+ k_pod_prep)", "ms": ci_ms, "evals_per_s": N * P / (ci_ms * 1e-3),
-            "note": "round-1 shortcut: per-tile, per-digit-class candidate lists; a pod hashes only its "
-                    "class's listed rows. Reported separately (SURVEY §7 no-shortcut rule), never the value"}
-        extras["e2e"] = e2e_host(eng, pods_np, N)
+            extras["e2e"] = e2e_host(eng, pods_np, N, world)
+        except Exception as ex:  # (reported, never fatal to the headline line)
+            extras["e2e"] = {"error": repr(ex)[:300]}
 
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
@@ -331,7 +336,7 @@ def main():
             "frac": (valu / kernel_s) / VALU_PEAK_NOMINAL if valu else None,
             "frac_of_measured_ceiling": (valu / kernel_s) / VALU_PEAK_MEASURED if valu else None,
             "traffic": traffic,
-            "kernel": PP_KERNEL if os.environ.get("MINISCHED_K1", "pp") == "pp" else os.environ["MINISCHED_K1"],
+            "kernel": PP_KERNEL,
             "kernel_ms": kernel_ms,
             # the same kernel's average under rocprofv3 --kernel-trace (the committed summary; the profiler's
             # per-dispatch completion signals add a few %)
@@ -365,16 +370,20 @@ def main():
             "dtype": "u32",
             "data": f"synthetic (splitmix64 seed {args.seed}, BASELINE.md §3)",
             "config": {
-                "workload": f"{args.config}: {N} nodes x {P} pods ({P // world} per GPU), {plugins}, batched, "
-                            "every pair evaluated, "
-                            + (f"node-sharded over {world} GPU" if split == "nodes" else f"pods split over {world} GPU"),
+                "workload": f"{args.config}: {N} nodes x {P} pods ({P // world} per GPU, {args.scaling} scaling), "
+                            f"{plugins}, batched, every pair evaluated, "
+                            + (f"node-sharded over {world} GPU" if split == "nodes" else f"pods split over {world} GPU")
+                            + (" (in-library RCCL communicator)" if cyc.library else ""),
                 "nodes": N,
                 "pods": P,
                 "pods_per_gpu": P // world,
                 "plugins": plugins,
                 "parallelism": f"{'node' if split == 'nodes' else 'pod'}-shard{world}",
             },
-            "pods_per_s": P * args.steps / elapsed,
+            # pods/s = ms_schedule_batch wall time on host arrays (e2e); the
+            # device-resident step rate separately
+            "pods_per_s": (extras.get("e2e") or {}).get("pods_per_s"),
+            "device_pods_per_s": P * args.steps / elapsed,
             "device_ms_per_step": step_dev_ms,
             "pods_scheduled": ok,
             "roofline": roofline,

@@ -41,13 +41,13 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 2
+#define MS_ABI_VERSION 3
 
 /* ---- return codes -------------------------------------------------------- */
 #define MS_OK 0
 #define MS_E_INVAL (-1)    /* bad argument / state                         */
 #define MS_E_HIP (-2)      /* a HIP runtime call failed                    */
-#define MS_E_RCCL (-3)     /* reserved: in-library collectives             */
+#define MS_E_RCCL (-3)     /* an RCCL call of the communicator failed      */
 #define MS_E_OOM (-4)      /* device or pinned allocation failed          */
 #define MS_E_CAPACITY (-5) /* ordinal outside this context's node range    */
 #define MS_E_NODEV (-6)    /* no usable gfx950 device                      */
@@ -138,6 +138,9 @@ typedef struct ms_info {
     /* exact sequential engine counters since ms_create (diagnostics):
      * pods validated, tiles re-swept, speculative entries re-evaluated */
     uint32_t seq_pods, seq_resweep_tiles, seq_recomputes, _pad;
+    /* communicator (ms_comm_init): this context's rank and the world size;
+     * both 0 when the context is not joined to one */
+    int32_t comm_rank, comm_world;
 } ms_info;
 
 typedef struct ms_ctx ms_ctx;
@@ -186,7 +189,8 @@ int ms_uncommit_bind(ms_ctx *ctx, uint32_t ordinal, const ms_pod_rec *pod);
  *   keys[i]  = max packed key over this shard's feasible nodes (0 = none)
  *   flags[i] = byte 0: some node here rejected by NodeUnschedulable (0/1),
  *              byte 1: some node here rejected by NodeResourcesFit  (0/1)
- *   Both arrays are overwritten. flags may be NULL for MS_PLUGINS_NU_NN.
+ *   Both arrays are overwritten. MS_PLUGINS_NU_NN takes no flags (NULL; the
+ *   mask follows from the key and the cluster's present-node count).
  *   Shards combine keys with an element-wise uint64 MAX and flags with a
  *   byte-wise uint8 MAX (= OR of 0/1 bytes): one reduction each.
  *   MS_PLUGINS_NU_NN_NA: keys use raw NodeAffinity scores and flags[i] is the
@@ -261,9 +265,58 @@ int ms_seq_candidates_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pod
 int ms_seq_validate_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
                            const ms_seq_cand *cands_all_dev, const uint32_t *flags_all_dev, ms_result *results_dev,
                            uint32_t *n_done_dev, void *stream);
-/* Whole exact sequential cycle on device-resident pods (single shard). */
+/* Whole exact sequential cycle on device-resident pods (single shard; on a
+ * context joined to a communicator, the node-sharded cycle below). */
 int ms_schedule_sequential_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,
                                   ms_result *results_dev, void *stream);
+
+/* ---- multi-GPU inside the library: one RCCL communicator per job ------------
+ * One process (or host thread) per GPU, one context per rank, each owning the
+ * contiguous node shard [node_base, node_base + max_nodes) of the cluster's
+ * ordinals (ranks in ordinal order; the shards need not be equal). Rank 0
+ * creates an id with ms_comm_id_create and hands its bytes to every rank out
+ * of band; every rank then calls ms_comm_init (collective: it returns once all
+ * ranks joined). The context then owns the communicator and its collective
+ * stream, and frees them in ms_destroy. Replaces selectHost over the union of
+ * the shards (minisched.go:304-325): keys embed the global ordinal, so the
+ * MAX reduction equals the single-GPU argmax whatever the tree.
+ *
+ * With a communicator, ms_schedule_batch and ms_schedule_sequential_device are
+ * collective: every rank calls them with the same pods (queue order) and gets
+ * every pod's result; each rank commits the binds that land on its own nodes.
+ *   batched (and NU+NN / NodeAffinity sequential, which equal it): this
+ *   shard's sweep, ONE grouped reduce-scatter (uint64 MAX of the packed keys,
+ *   the filter bytes / uint32 NodeAffinity anchors, the "a node is listed"
+ *   flag), the decode of this rank's pod slice, an all-gather of the results;
+ *   resource-aware sequential: per batch of pods, every shard's speculative
+ *   top-4 with records, one grouped all-gather, the replicated in-order
+ *   validation (ms_seq_* above); the queue cursor stays on the device, so
+ *   batches are issued without a host round trip (the host reads the cursor
+ *   once per round of ceil(remaining / batch) batches).
+ * ms_select_batch_device is single-shard and fails on such a context. */
+#define MS_COMM_ID_BYTES 128
+typedef struct ms_comm_id {
+    char internal[MS_COMM_ID_BYTES]; /* ncclUniqueId */
+} ms_comm_id;
+int ms_comm_id_create(ms_comm_id *out);
+int ms_comm_init(ms_ctx *ctx, const ms_comm_id *id, int32_t rank, int32_t world);
+
+/* Pipelined node-sharded batched cycle on device-resident pods (the bench's
+ * and a service loop's step). ms_sharded_submit enqueues this shard's sweep
+ * of the batch on `stream` and the grouped reduce-scatter on the context's
+ * collective stream, then, once more than the pipeline depth (4) batches are
+ * in flight, the decodes of the oldest ones on `stream`: batch k's collective
+ * overlaps the sweeps of the following batches. ms_sharded_drain enqueues
+ * every remaining decode. results_dev receives this rank's pod slice
+ * [first, first + count) of the batch (ms_sharded_slice), complete once the
+ * stream work of the submit or drain that decoded it is. pods_dev and
+ * results_dev must stay valid until then. Every rank submits the same batches
+ * in the same order. No binds are committed (stateless: NU+NN, NodeAffinity;
+ * for the resource-aware set each batch sees the state of its submit). */
+int ms_sharded_slice(const ms_ctx *ctx, uint32_t n_pods, uint32_t *first, uint32_t *count);
+int ms_sharded_submit(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
+                      void *stream);
+int ms_sharded_drain(ms_ctx *ctx, void *stream);
 
 #ifdef __cplusplus
 }

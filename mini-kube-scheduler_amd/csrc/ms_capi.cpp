@@ -16,100 +16,21 @@
 #include <unordered_map>
 #include <vector>
 
-#include "ms_internal.h"
+#include "ms_ctx.h"
 
 using namespace msgpu;
 
-struct ms_ctx {
-    ms_config cfg{};
-    hipStream_t stream = nullptr;
-    int num_cus = 0;
-    NodeTable t{};
 
-    // node deltas (informer goroutines) — guarded by delta_mu
-    std::mutex delta_mu;
-    std::vector<NodeDelta> pending;
-    std::vector<uint8_t> present;  // host mirror of presence, updated at enqueue
-    uint32_t present_count = 0;
-    uint32_t rows_used = 0;  // high-water mark of upserted rows (sweep extent)
-    // what the device table holds after the last flush: snapshots of the two
-    // counters above taken with the drained deltas (under delta_mu), read only
-    // by sched_mu holders
-    uint32_t rows_dev = 0, present_dev = 0;
-
-    // one scheduling caller at a time (minisched.go:28-30 runs one goroutine)
-    std::mutex sched_mu;
-
-    // staging
-    uint32_t batch_cap = 0;
-    ms_pod_rec *h_pods = nullptr;
-    ms_result *h_res = nullptr;
-    ms_pod_rec *d_pods = nullptr;
-    ms_result *d_res = nullptr;
-    unsigned long long *d_keys = nullptr;
-    uint32_t *d_flags = nullptr;  // per-pod filter flags (set 1) / NodeAffinity anchors (set 2)
-    uint32_t w_nn = 1, w_na = 1;  // score weights (MS_PLUGINS_NU_NN_NA)
-    NodeDelta *h_deltas = nullptr;
-    NodeDelta *d_deltas = nullptr;
-    uint32_t delta_cap = 0;
-    ms_pod_rec *d_one = nullptr;  // commit/uncommit staging
-
-    // sequential engine scratch
-    unsigned long long *d_tile_keys = nullptr;
-    uint32_t *d_tile_flags = nullptr;
-    unsigned long long *d_spec = nullptr;  // per-pod speculative winner key (atomicMax target)
-    uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
-    unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
-    int64_t *d_top4_rec = nullptr;         // their batch-start node records (validator layout)
-    uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
-    int64_t *d_prev_rec = nullptr;         // and their final records (x2)
-    DRow *d_drow = nullptr;                // derived rows of the binary64 sweep (tile_cap * kFullWaveTile)
-    // pipelined sequential engine: batch k+1's speculation (seq_stream) runs
-    // while batch k validates (caller stream); every buffer above is double-
-    // buffered by batch parity
-    hipStream_t seq_stream = nullptr;
-    // ms_schedule_batch's chunked copies (schedule_chunked): H2D / D2H of host arrays beside the cycle
-    hipStream_t copy_stream = nullptr;
-    hipEvent_t ev_copy[4] = {nullptr, nullptr, nullptr, nullptr}, ev_cyc[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t ev_valid[3] = {nullptr, nullptr, nullptr}, ev_swept[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t ev_seq = nullptr;
-    uint32_t tile_cap = 0;  // tiles allocated per pod
-    uint32_t *d_overflow = nullptr;
-    // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
-    ms_seq_cand *d_merged = nullptr;
-    uint32_t *d_merged_flags = nullptr;
-
-    // NU+NN pod stream of the class-indexed K1 forms (k_pod_prep output),
-    // reused call after call (ordered through the context stream like the table)
-    uint2 *d_pstream = nullptr;
-    uint32_t pstream_cap = 0;
-    uint32_t *d_work = nullptr;  // K1 v8 work-queue counters (kK1MaxColumns)
-
-    // Ordering. Every piece of work that reads or writes the node table or the
-    // context's scratch is totally ordered through the context stream: a call
-    // on a caller stream first waits for the context stream (order_after_ctx_
-    // stream), and its work is then chained back into the context stream
-    // (chain_back), so later deltas, binds, read-backs and calls on any other
-    // stream wait for it. ctx_seq counts enqueues on the context stream that a
-    // caller stream has not necessarily seen; a caller stream ordered after it
-    // at ctx_seq needs no new cross-stream wait (each costs ~6-10 us of idle
-    // device time even when already signalled, tools/ubench/xstream).
-    uint64_t ctx_seq = 0;
-    hipStream_t ordered_stream = nullptr;
-    uint64_t ordered_seq = 0;
-    hipEvent_t ev_order = nullptr;
-    hipEvent_t ev_back = nullptr;
-
-    std::string err;
-};
+namespace msgpu {
 
 namespace {
-
 thread_local std::string g_create_err;
 
 // validator counters: u32[6] (overflow, re-swept tiles, recomputes, pods, speculation misses,
 // list scans), then u64[4] phase cycles in the MS_VSTAMPS diagnostic build
 constexpr size_t kStatsBytes = 128;
+
+}  // namespace
 
 int fail(ms_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -117,27 +38,18 @@ int fail(ms_ctx *c, int code, const std::string &msg) {
     return code;
 }
 
-#define MS_HIP(c, call)                                                                          \
-    do {                                                                                         \
-        hipError_t e_ = (call);                                                                  \
-        if (e_ != hipSuccess)                                                                    \
-            return fail((c), MS_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_));       \
-    } while (0)
-
-uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
-
-constexpr uint32_t kTopKCands = 4;  // ms_seq_cand entries per pod and shard (the validator's top-K)
 constexpr int kSeqBufs = 3;         // sequential-engine batch buffer sets (pipeline depth <= 3)
 
 void free_all(ms_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
+    comm_free(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void *dev[] = {c->t.planes, c->t.zone, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
-                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow, c->d_pstream,
-                   c->d_work, c->d_merged, c->d_merged_flags, c->d_drow};
+                   c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
+                   c->d_merged, c->d_merged_flags, c->d_drow};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -403,32 +315,32 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     return MS_OK;
 }
 
-// The NU+NN pod stream scratch: grown on demand (hipFree synchronises the
-// device, so no in-flight sweep still reads the old buffer).
-int ensure_pstream(ms_ctx *c, uint32_t n_pods) {
-    const uint32_t need = n_pods + kPodStreamPad;
-    if (need <= c->pstream_cap) return MS_OK;
-    const uint32_t cap = std::max<uint32_t>(need, std::max<uint32_t>(4096, c->pstream_cap * 2));
-    if (c->d_pstream) (void)hipFree(c->d_pstream);
-    c->d_pstream = nullptr;
-    c->pstream_cap = 0;
-    if (!c->d_work && hipMalloc((void **)&c->d_work, sizeof(uint32_t) * kK1MaxColumns) != hipSuccess)
-        return fail(c, MS_E_OOM, "K1 work counters");
-    // cap stream entries, then the per-8-pod class masks (k_pod_prep writes them
-    // right after the call's n_pods + kPodStreamPad entries; launch_sweep_nunn)
-    if (hipMalloc((void **)&c->d_pstream, sizeof(uint2) * cap + sizeof(uint32_t) * (cap / 8 + 4)) != hipSuccess)
-        return fail(c, MS_E_OOM, "pod stream");
-    c->pstream_cap = cap;
-    return MS_OK;
-}
+// Plugin sets whose filters and scores read no mutable node state (NU, NN,
+// NodeAffinity): a bind never changes a later pod's outcome, so chunks of a
+// call, or the queue-order loop, equal one batched sweep.
+bool plugins_stateless(const ms_ctx *c) { return c->cfg.plugin_set != MS_PLUGINS_NU_NRF_NN_LA; }
 
-// K1 choice for NU+NN, read at each call so A/B runs can interleave forms in
-// one process: the per-pair "pp" kernel (default, MINISCHED_K1 unset or "pp"),
-// or the round-1 class-indexed forms "v7" / "v8" and the plain "v0"
-// (ms_kernels.hip), kept as labelled alternatives and cross-checks.
-bool k1_pp() {
-    const char *e = getenv("MINISCHED_K1");
-    return !e || !e[0] || (e[0] == 'p' && e[1] == 'p');
+// Pod / result staging for at least n pods (grown on demand; hipFree
+// synchronises the device, so no in-flight call still uses the old buffers).
+int ensure_stage(ms_ctx *c, uint32_t n) {
+    if (n <= c->stage_cap) return MS_OK;
+    void *dev[] = {c->d_pods, c->d_res};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    if (c->h_pods) (void)hipHostFree(c->h_pods);
+    if (c->h_res) (void)hipHostFree(c->h_res);
+    c->d_pods = nullptr;
+    c->d_res = nullptr;
+    c->h_pods = nullptr;
+    c->h_res = nullptr;
+    c->stage_cap = 0;
+    if (hipHostMalloc((void **)&c->h_pods, (size_t)n * sizeof(ms_pod_rec)) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_res, (size_t)n * sizeof(ms_result)) != hipSuccess ||
+        hipMalloc((void **)&c->d_pods, (size_t)n * sizeof(ms_pod_rec)) != hipSuccess ||
+        hipMalloc((void **)&c->d_res, (size_t)n * sizeof(ms_result)) != hipSuccess)
+        return fail(c, MS_E_OOM, "pod staging");
+    c->stage_cap = n;
+    return MS_OK;
 }
 
 // This shard's keys (and filter flags for the resource-aware set) for a batch.
@@ -436,15 +348,8 @@ int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned 
                  hipStream_t s) {
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NN) {
-        if (k1_pp()) {
-            MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
-                                      c->num_cus, s));
-            return MS_OK;
-        }
-        int rc = ensure_pstream(c, n_pods);
-        if (rc) return rc;
-        MS_HIP(c, launch_sweep_nunn(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->d_pstream, c->d_work,
-                                    c->num_cus, s));
+        MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
+                                  c->num_cus, s));
     } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
         MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
         MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
@@ -475,12 +380,16 @@ hipError_t decode_for(const ms_ctx *c, const ms_pod_rec *pods, uint32_t n, const
 int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s,
                   int commit = 0) {
     const uint32_t B = c->batch_cap;
-    const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN && k1_pp();
+    const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN;
     if (fused && c->rows_dev <= kPpMaxFusedRows) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), nullptr, d_res,
                                   c->present_dev, c->num_cus, s, commit));
         return MS_OK;
     }
+    // The resource-aware set reads Requested / pod_count: every chunk must be
+    // decided before any bind of the call lands (MS_MODE_BATCHED), so
+    // its binds are committed after the last chunk's decode.
+    const bool late_commit = commit && !plugins_stateless(c);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         if (fused) {
@@ -493,8 +402,9 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
         if (rc) return rc;
         MS_HIP(c, decode_for(c, d_pods + s0, nb, c->d_keys, want_flags ? c->d_flags : nullptr, c->present_dev,
                              d_res + s0, s));
-        if (commit) MS_HIP(c, launch_apply_binds(c->t, d_pods + s0, nb, d_res + s0, s));
+        if (commit && !late_commit) MS_HIP(c, launch_apply_binds(c->t, d_pods + s0, nb, d_res + s0, s));
     }
+    if (late_commit) MS_HIP(c, launch_apply_binds(c->t, d_pods, n_pods, d_res, s));
     return MS_OK;
 }
 
@@ -550,9 +460,34 @@ int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *o
     return MS_OK;
 }
 
+// This shard's speculative top-4 candidates with records, and its filter flags,
+// for a batch of at most MS_SEQ_SHARD_BATCH_MAX pods (ms_seq_candidates_device;
+// the in-library node-sharded sequential cycle).
+int seq_candidates_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_seq_cand *cands_dev,
+                          uint32_t *flags_dev, hipStream_t s) {
+    const uint32_t rows = c->rows_dev;
+    if (rows == 0) {  // no node listed: no candidates, no rejections
+        MS_HIP(c, hipMemsetAsync(cands_dev, 0, sizeof(ms_seq_cand) * kTopKCands * n_pods, s));
+        MS_HIP(c, hipMemsetAsync(flags_dev, 0, sizeof(uint32_t) * n_pods, s));
+        return MS_OK;
+    }
+    if (rows > seq_max_rows())
+        return fail(c, MS_E_CAPACITY, "ms_seq_candidates_device: at most " + std::to_string(seq_max_rows()) +
+                                          " rows per context");
+    const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
+    int rc = ensure_tiles(c, n_tiles);
+    if (rc) return rc;
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    MS_HIP(c, launch_sweep_full_tiles(c->t, rows, pods_dev, n_pods, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
+    MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, n_pods, n_tiles, c->d_top4, c->d_spec,
+                                c->d_spec_flags, c->t, nullptr, s));
+    MS_HIP(c, launch_seq_pack_cands(c->t, c->d_top4, c->d_tile_flags, n_tiles, n_pods, cands_dev, flags_dev, s));
+    return MS_OK;
+}
+
 bool valid_ctx(const ms_ctx *c) { return c != nullptr; }
 
-}  // namespace
+}  // namespace msgpu
 
 extern "C" {
 
@@ -628,10 +563,7 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     ok = ok && hipMalloc((void **)&t.planes, sizeof(uint32_t) * kPlanes * t.gcap) == hipSuccess;
     if (!ok) return bail(MS_E_OOM, "node table allocation");
     const size_t b = c->batch_cap;
-    ok = hipHostMalloc((void **)&c->h_pods, b * sizeof(ms_pod_rec)) == hipSuccess &&
-         hipHostMalloc((void **)&c->h_res, b * sizeof(ms_result)) == hipSuccess &&
-         hipMalloc((void **)&c->d_pods, b * sizeof(ms_pod_rec)) == hipSuccess &&
-         hipMalloc((void **)&c->d_res, b * sizeof(ms_result)) == hipSuccess &&
+    ok = ensure_stage(c, c->batch_cap) == MS_OK &&
          hipMalloc((void **)&c->d_keys, b * sizeof(unsigned long long)) == hipSuccess &&
          hipMalloc((void **)&c->d_flags, b * sizeof(uint32_t)) == hipSuccess &&
          hipMalloc((void **)&c->d_one, sizeof(ms_pod_rec)) == hipSuccess &&
@@ -693,6 +625,7 @@ int ms_get_info(const ms_ctx *c, ms_info *out) {
     out->seq_resweep_tiles = st[1];
     out->seq_recomputes = st[2];
     out->_pad = st[0];  // non-zero would mean a validator capacity violation
+    comm_rank_world(c, &out->comm_rank, &out->comm_world);
     return MS_OK;
 }
 
@@ -773,9 +706,17 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
+    if (c->comm) return comm_schedule_host(c, n_pods, pods, mode, out);  // node-sharded over the communicator
     const hipStream_t s = c->stream;
     ++c->ctx_seq;  // binds below write the table on the context stream
-    const uint32_t B = c->batch_cap;
+    uint32_t B = c->batch_cap;
+    if (mode == MS_MODE_BATCHED && !plugins_stateless(c)) {
+        // every pod of the call is decided on the same node state before any of
+        // its binds lands: one pass over the whole call (header contract)
+        rc = ensure_stage(c, n_pods);
+        if (rc) return rc;
+        B = n_pods;
+    }
     // Host arrays go straight to the device (the runtime's own pageable-copy
     // path, 0.56 ms for config C's 4 MB in + 2.4 MB out + cycle, against 0.72 ms
     // through a single-threaded memcpy into the pinned staging buffers;
@@ -790,7 +731,7 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, hipStreamSynchronize(s));  // h_pods / h_res free to reuse
         const bool seq_full = (mode == MS_MODE_SEQUENTIAL && c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA);
-        const uint32_t parts = (pageable && !seq_full) ? e2e_chunks(nb) : 1u;
+        const uint32_t parts = (pageable && plugins_stateless(c)) ? e2e_chunks(nb) : 1u;
         if (parts > 1) {  // (NU+NN / NA: binds never change a later pod's keys, so chunks equal one batch)
             rc = schedule_chunked(c, pods + s0, nb, out + s0, parts);
             if (rc) return rc;
@@ -863,6 +804,8 @@ int ms_sweep_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint
 int ms_select_batch_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
                            void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !results_dev))) return MS_E_INVAL;
+    if (c->comm)
+        return fail(c, MS_E_INVAL, "ms_select_batch_device: single-shard call on a sharded context (ms_sharded_submit)");
     if (n_pods == 0) return MS_OK;
     std::lock_guard<std::mutex> g(c->sched_mu);
     MS_HIP(c, hipSetDevice(c->cfg.device));
@@ -934,7 +877,9 @@ int ms_schedule_sequential_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
     if (rc) return rc;
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA) {
+    if (c->comm) {
+        rc = comm_schedule_device(c, n_pods, pods_dev, results_dev, s);  // node-sharded over the communicator
+    } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA) {
         rc = run_sequential(c, n_pods, pods_dev, results_dev, s);
     } else {
         // NU+NN: keys are independent of mutable state -> batched cycle + commit
@@ -962,23 +907,8 @@ int ms_seq_candidates_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);
     if (rc) return rc;
-    const uint32_t rows = c->rows_dev;
-    if (rows == 0) {  // no node listed: no candidates, no rejections
-        MS_HIP(c, hipMemsetAsync(cands_dev, 0, sizeof(ms_seq_cand) * kTopKCands * n_pods, s));
-        MS_HIP(c, hipMemsetAsync(flags_dev, 0, sizeof(uint32_t) * n_pods, s));
-        return chain_back(c, s);
-    }
-    if (rows > seq_max_rows())
-        return fail(c, MS_E_CAPACITY, "ms_seq_candidates_device: at most " + std::to_string(seq_max_rows()) +
-                                          " rows per context");
-    const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
-    rc = ensure_tiles(c, n_tiles);
+    rc = seq_candidates_locked(c, n_pods, pods_dev, cands_dev, flags_dev, s);
     if (rc) return rc;
-    const uint32_t seed32 = seed32_of(c->cfg.seed);
-    MS_HIP(c, launch_sweep_full_tiles(c->t, rows, pods_dev, n_pods, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
-    MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, n_pods, n_tiles, c->d_top4, c->d_spec,
-                                c->d_spec_flags, c->t, nullptr, s));
-    MS_HIP(c, launch_seq_pack_cands(c->t, c->d_top4, c->d_tile_flags, n_tiles, n_pods, cands_dev, flags_dev, s));
     return chain_back(c, s);
 }
 

@@ -1,0 +1,455 @@
+// ms_comm.cpp — multi-GPU inside the C ABI (include/minisched_gpu.h, "multi-GPU
+// inside the library"). A context joined to an RCCL communicator owns one node
+// shard per rank and runs the node-sharded cycles with their collectives in the
+// library, so the Go scheduleOne (/root/reference/minisched/minisched.go:32-85,
+// called from one goroutine, :28-30) drives G GPUs through the same cgo calls
+// it uses for one, with no RCCL binding of its own (SURVEY §8(b) Ownership).
+//
+// Batched cycle (config C; selectHost over the union of the shards,
+// minisched.go:304-325): this shard's sweep of the batch (K1 pp, the
+// NodeAffinity sweep or the resource sweep) -> ONE grouped ncclReduceScatter
+// on the collective stream:
+//   keys   uint64 MAX, G x per pods -> this rank's slice of per pods (the keys
+//          embed the global ordinal, so MAX is the global argmax);
+//   flags  NodeResourcesFit set: uint8 MAX of the filter bytes (byte-wise OR =
+//          FitError's UnschedulablePlugins over the cluster, :130-137);
+//          NodeAffinity set: uint32 MAX of the normalise anchors;
+//   pres   uint32 MAX of "this shard lists a node" (the NU+NN / NA FitError
+//          mask: F = 0 with a listed node means NodeUnschedulable rejected it);
+// -> the decode of the slice on the caller's stream. Pipelined: the decodes of
+// batch k are enqueued once `depth` later batches were submitted, so batch k's
+// collective overlaps their sweeps (RCCL runs one communicator's collectives in
+// issue order on the collective stream, so a drain waits for the newest only).
+//
+// Exact sequential cycle (config E): per window of W pods, every
+// shard's speculative top-4 with records (ms_seq_candidates_device) -> one
+// grouped ncclAllGather -> the replicated in-order validation on every rank,
+// which commits the binds on its own nodes. The queue cursor lives on the
+// device (k_seq_window_in / k_seq_window_out), so windows are issued without a
+// host round trip; the host reads the cursor once per round of
+// ceil(remaining / W) windows (every window decides at least one pod; one
+// round suffices unless a window stops early).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <new>
+
+#include "ms_ctx.h"
+
+namespace msgpu {
+
+namespace {
+
+constexpr uint32_t kPipeMax = 8;  // batch buffer sets: pipeline depth + 1 < kPipeMax
+static_assert(kPipeMax <= kMaxSliceJobs, "a full drain is one slice-decode launch");
+static_assert(sizeof(ncclUniqueId) == MS_COMM_ID_BYTES, "ms_comm_id holds an ncclUniqueId");
+
+// One in-flight batch's combine buffers.
+struct ShardSlot {
+    unsigned long long *keys = nullptr;       // G x cap: this shard's maxima, pod order
+    unsigned long long *keys_mine = nullptr;  // cap: the cluster's maxima of this rank's slice
+    uint32_t *flags = nullptr, *flags_mine = nullptr;
+    uint32_t *pres = nullptr, *pres_mine = nullptr;  // G words / 1 word
+    uint32_t cap = 0;                                // pods per slice the buffers hold
+};
+
+struct Pending {
+    uint32_t slot, n, first, count;
+    const ms_pod_rec *pods;  // the batch (decode reads pods + first)
+    ms_result *results;      // this rank's slice
+};
+
+}  // namespace
+
+struct CommState {
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+    hipStream_t cs = nullptr;  // collective stream
+    hipEvent_t ev_swept[kPipeMax] = {}, ev_comb[kPipeMax] = {};
+    ShardSlot slot[kPipeMax];
+    std::deque<Pending> pending;
+    uint64_t submitted = 0;
+    uint32_t depth = 4, group = 4;
+    hipStream_t pipe_stream = nullptr;  // the stream the pending batches were submitted on
+    // node-sharded exact sequential
+    uint32_t seq_w = 0;
+    ms_pod_rec *win_pods = nullptr;
+    ms_result *win_res = nullptr;
+    uint32_t *ctl = nullptr;    // {cursor, live, n_done, pad}
+    uint32_t *h_ctl = nullptr;  // pinned read-back of the cursor
+    ms_seq_cand *cands = nullptr, *cands_all = nullptr, *merged = nullptr;
+    uint32_t *sflags = nullptr, *sflags_all = nullptr, *merged_flags = nullptr;
+    uint64_t seq_windows = 0, seq_rounds = 0;
+};
+
+namespace {
+
+#define MS_NCCL(c, call)                                                                          \
+    do {                                                                                          \
+        ncclResult_t r_ = (call);                                                                 \
+        if (r_ != ncclSuccess)                                                                    \
+            return fail((c), MS_E_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_));      \
+    } while (0)
+
+void free_slot(ShardSlot &sl) {
+    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.pres, sl.pres_mine};
+    for (void *q : p)
+        if (q) (void)hipFree(q);
+    sl = ShardSlot{};
+}
+
+// Buffers of a slot for slices of `per` pods (grown; the slot's previous batch
+// has been drained, and hipFree waits for its decode).
+int slot_ensure(ms_ctx *c, ShardSlot &sl, uint32_t per) {
+    if (per <= sl.cap && sl.keys) return MS_OK;
+    const size_t G = (size_t)c->comm->world;
+    const uint32_t cap = std::max<uint32_t>(1024u, cdiv(per, 1024u) * 1024u);
+    free_slot(sl);
+    if (hipMalloc((void **)&sl.keys, G * cap * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&sl.keys_mine, cap * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&sl.flags, G * cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&sl.pres, G * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&sl.pres_mine, sizeof(uint32_t)) != hipSuccess) {
+        free_slot(sl);
+        return fail(c, MS_E_OOM, "sharded combine buffers");
+    }
+    sl.cap = cap;
+    return MS_OK;
+}
+
+void slice_of(const CommState &m, uint32_t n, uint32_t &first, uint32_t &count) {
+    const uint32_t per = cdiv(n, (uint32_t)m.world);
+    first = std::min<uint32_t>(n, (uint32_t)m.rank * per);
+    count = std::min<uint32_t>(n, first + per) - first;
+}
+
+// Decodes of the oldest k pending batches on s (after their combines).
+int drain_locked(ms_ctx *c, hipStream_t s, size_t k) {
+    CommState &m = *c->comm;
+    k = std::min(k, m.pending.size());
+    if (k == 0) return MS_OK;
+    MS_HIP(c, hipStreamWaitEvent(s, m.ev_comb[m.pending[k - 1].slot], 0));  // collectives run in issue order
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
+        for (size_t i = 0; i < k; ++i) {
+            const Pending &p = m.pending[i];
+            const ShardSlot &sl = m.slot[p.slot];
+            MS_HIP(c, launch_decode_na(p.pods + p.first, p.count, sl.keys_mine, sl.flags_mine, 0, seed32_of(c->cfg.seed),
+                                       c->w_nn, c->w_na, p.results, s, sl.pres_mine));
+        }
+    } else {
+        SliceJob jobs[kMaxSliceJobs];
+        const bool nrf = c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA;
+        for (size_t i = 0; i < k; ++i) {
+            const Pending &p = m.pending[i];
+            const ShardSlot &sl = m.slot[p.slot];
+            jobs[i] = SliceJob{p.pods + p.first, sl.keys_mine, nrf ? sl.flags_mine : nullptr, sl.pres_mine, p.results,
+                               p.count, 0};
+        }
+        MS_HIP(c, launch_decode_slices(jobs, (uint32_t)k, s));
+    }
+    m.pending.erase(m.pending.begin(), m.pending.begin() + (long)k);
+    return MS_OK;
+}
+
+// Everything pending, on the stream it was submitted on; the context stream
+// then waits for it (later submits on another stream reuse its buffers).
+int drain_all_locked(ms_ctx *c) {
+    CommState &m = *c->comm;
+    if (m.pending.empty()) return MS_OK;
+    int rc = drain_locked(c, m.pipe_stream, m.pending.size());
+    if (rc) return rc;
+    return chain_back(c, m.pipe_stream);
+}
+
+int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
+    CommState &m = *c->comm;
+    int rc = MS_OK;
+    if (!m.pending.empty() && m.pipe_stream != s) {
+        rc = drain_all_locked(c);
+        if (rc) return rc;
+    }
+    rc = order_after_ctx_stream(c, s);  // deltas, binds and the other stream's drains come first
+    if (rc) return rc;
+    m.pipe_stream = s;
+    const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
+    const uint32_t si = (uint32_t)(m.submitted % (m.depth + 1));
+    ShardSlot &sl = m.slot[si];
+    rc = slot_ensure(c, sl, per);
+    if (rc) return rc;
+    const int ps = c->cfg.plugin_set;
+    rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, s);
+    if (rc) return rc;
+    MS_HIP(c, hipMemsetD32Async(sl.pres, c->present_dev ? 1u : 0u, G, s));
+    MS_HIP(c, hipEventRecord(m.ev_swept[si], s));
+    MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_swept[si], 0));
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
+    if (r == ncclSuccess) r = ncclReduceScatter(sl.pres, sl.pres_mine, 1, ncclUint32, ncclMax, m.comm, m.cs);
+    if (r == ncclSuccess && ps == MS_PLUGINS_NU_NRF_NN_LA)  // 0/1 bytes: uint8 MAX = OR
+        r = ncclReduceScatter(sl.flags, sl.flags_mine, (size_t)per * 4, ncclUint8, ncclMax, m.comm, m.cs);
+    if (r == ncclSuccess && ps == MS_PLUGINS_NU_NN_NA)  // anchors < 2^21: uint32 MAX
+        r = ncclReduceScatter(sl.flags, sl.flags_mine, per, ncclUint32, ncclMax, m.comm, m.cs);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sharded reduce-scatter: ") + ncclGetErrorString(r));
+    MS_HIP(c, hipEventRecord(m.ev_comb[si], m.cs));
+    Pending p{si, n, 0, 0, pods, results};
+    slice_of(m, n, p.first, p.count);
+    m.pending.push_back(p);
+    ++m.submitted;
+    rc = chain_back(c, s);  // the context stream waits for the sweep (it read the table)
+    if (rc) return rc;
+    if (m.pending.size() > m.depth) return drain_locked(c, s, std::min<size_t>(m.group, m.pending.size()));
+    return MS_OK;
+}
+
+// Sequential-window buffers for windows of w pods.
+int seq_ensure(ms_ctx *c, uint32_t w) {
+    CommState &m = *c->comm;
+    if (w <= m.seq_w) return MS_OK;
+    MS_HIP(c, hipDeviceSynchronize());
+    void *old[] = {m.win_pods, m.win_res, m.ctl, m.cands, m.cands_all, m.merged, m.sflags, m.sflags_all, m.merged_flags};
+    for (void *q : old)
+        if (q) (void)hipFree(q);
+    if (m.h_ctl) (void)hipHostFree(m.h_ctl);
+    m.win_pods = nullptr;
+    m.win_res = nullptr;
+    m.ctl = m.h_ctl = m.sflags = m.sflags_all = m.merged_flags = nullptr;
+    m.cands = m.cands_all = m.merged = nullptr;
+    m.seq_w = 0;
+    const size_t G = (size_t)m.world, K = kTopKCands;
+    if (hipMalloc((void **)&m.win_pods, w * sizeof(ms_pod_rec)) != hipSuccess ||
+        hipMalloc((void **)&m.win_res, w * sizeof(ms_result)) != hipSuccess ||
+        hipMalloc((void **)&m.ctl, 4 * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc((void **)&m.h_ctl, 4 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&m.cands, w * K * sizeof(ms_seq_cand)) != hipSuccess ||
+        hipMalloc((void **)&m.cands_all, G * w * K * sizeof(ms_seq_cand)) != hipSuccess ||
+        hipMalloc((void **)&m.merged, w * K * sizeof(ms_seq_cand)) != hipSuccess ||
+        hipMalloc((void **)&m.sflags, w * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&m.sflags_all, G * w * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&m.merged_flags, w * sizeof(uint32_t)) != hipSuccess)
+        return fail(c, MS_E_OOM, "sharded sequential buffers");
+    m.seq_w = w;
+    return MS_OK;
+}
+
+// Pods per window of the node-sharded exact sequential cycle: each window costs
+// one all-gather of its candidates (W x 4 x 72 B per rank) and one validator
+// launch. MINISCHED_SHARD_SEQ_BATCH overrides (1..256).
+uint32_t seq_window() {
+    uint32_t w = 128;
+    if (const char *e = getenv("MINISCHED_SHARD_SEQ_BATCH")) w = (uint32_t)std::max(1, atoi(e));
+    return std::min<uint32_t>(w, MS_SEQ_SHARD_BATCH_MAX);
+}
+
+int seq_sharded_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
+    CommState &m = *c->comm;
+    const uint32_t W = seq_window();
+    int rc = seq_ensure(c, W);
+    if (rc) return rc;
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    MS_HIP(c, hipMemsetAsync(m.ctl, 0, 4 * sizeof(uint32_t), s));
+    const size_t cand_bytes = (size_t)W * kTopKCands * sizeof(ms_seq_cand);
+    uint32_t known = 0;
+    while (known < n) {
+        const uint32_t r = cdiv(n - known, W);  // windows that may finish the queue
+        for (uint32_t i = 0; i < r; ++i) {
+            MS_HIP(c, launch_seq_window_in(pods, n, m.ctl, m.win_pods, W, s));
+            rc = seq_candidates_locked(c, W, m.win_pods, m.cands, m.sflags, s);
+            if (rc) return rc;
+            ncclResult_t e = ncclGroupStart();
+            if (e == ncclSuccess) e = ncclAllGather(m.cands, m.cands_all, cand_bytes, ncclUint8, m.comm, s);
+            if (e == ncclSuccess) e = ncclAllGather(m.sflags, m.sflags_all, W, ncclUint32, m.comm, s);
+            const ncclResult_t e2 = ncclGroupEnd();
+            if (e == ncclSuccess) e = e2;
+            if (e != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sequential all-gather: ") + ncclGetErrorString(e));
+            MS_HIP(c, launch_seq_validate_rep(c->t, W, m.win_pods, seed32, (uint32_t)m.world, m.cands_all, m.sflags_all,
+                                              m.merged, m.merged_flags, m.win_res, m.ctl + 2, s, m.ctl + 1));
+            MS_HIP(c, launch_seq_window_out(m.win_res, m.ctl, results, n, s));
+            ++m.seq_windows;
+        }
+        MS_HIP(c, hipMemcpyAsync(m.h_ctl, m.ctl, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        MS_HIP(c, hipStreamSynchronize(s));
+        ++m.seq_rounds;
+        const uint32_t now = m.h_ctl[0];
+        if (now <= known || now > n) return fail(c, MS_E_HIP, "sharded sequential cycle made no progress");
+        known = now;
+    }
+    return MS_OK;
+}
+
+// The batched cycle of all n pods with every result on every rank: submit +
+// drain (this rank's slice into stage + first), one all-gather of the slices
+// (in place: slices are contiguous in pod order), then this shard's binds.
+int batched_all_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *stage, hipStream_t s, bool commit) {
+    CommState &m = *c->comm;
+    uint32_t first = 0, count = 0;
+    slice_of(m, n, first, count);
+    const uint32_t per = cdiv(n, (uint32_t)m.world);
+    int rc = submit_locked(c, n, pods, stage + first, s);
+    if (rc) return rc;
+    rc = drain_locked(c, s, m.pending.size());
+    if (rc) return rc;
+    // (a rank whose slice is short or empty sends entries past n: never read)
+    const size_t bytes = (size_t)per * sizeof(ms_result);
+    MS_NCCL(c, ncclAllGather(reinterpret_cast<char *>(stage) + (size_t)m.rank * bytes, stage, bytes, ncclUint8, m.comm, s));
+    if (commit) MS_HIP(c, launch_apply_binds(c->t, pods, n, stage, s));  // NodeInfo.AddPod on this shard's winners
+    return MS_OK;
+}
+
+}  // namespace
+
+void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world) {
+    *rank = c->comm ? c->comm->rank : 0;
+    *world = c->comm ? c->comm->world : 0;
+}
+
+void comm_free(ms_ctx *c) {
+    CommState *m = c->comm;
+    if (!m) return;
+    if (m->cs) (void)hipStreamSynchronize(m->cs);
+    if (m->pipe_stream) (void)hipStreamSynchronize(m->pipe_stream);
+    (void)hipDeviceSynchronize();
+    if (m->comm) (void)ncclCommDestroy(m->comm);
+    for (uint32_t i = 0; i < kPipeMax; ++i) {
+        free_slot(m->slot[i]);
+        if (m->ev_swept[i]) (void)hipEventDestroy(m->ev_swept[i]);
+        if (m->ev_comb[i]) (void)hipEventDestroy(m->ev_comb[i]);
+    }
+    void *dev[] = {m->win_pods, m->win_res, m->ctl, m->cands, m->cands_all, m->merged, m->sflags, m->sflags_all,
+                   m->merged_flags};
+    for (void *q : dev)
+        if (q) (void)hipFree(q);
+    if (m->h_ctl) (void)hipHostFree(m->h_ctl);
+    if (m->cs) (void)hipStreamDestroy(m->cs);
+    delete m;
+    c->comm = nullptr;
+}
+
+int comm_schedule_host(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, int32_t mode, ms_result *out) {
+    CommState &m = *c->comm;
+    const hipStream_t s = c->stream;
+    int rc = drain_all_locked(c);  // device-resident batches in flight use the combine buffers
+    if (rc) return rc;
+    const uint32_t per = cdiv(n, (uint32_t)m.world);
+    rc = ensure_stage(c, std::max<uint32_t>(n, per * (uint32_t)m.world));
+    if (rc) return rc;
+    ++c->ctx_seq;  // binds below write the table on the context stream
+    MS_HIP(c, hipMemcpyAsync(c->d_pods, pods, sizeof(ms_pod_rec) * n, hipMemcpyHostToDevice, s));
+    if (mode == MS_MODE_SEQUENTIAL && !plugins_stateless(c)) rc = seq_sharded_locked(c, n, c->d_pods, c->d_res, s);
+    else rc = batched_all_locked(c, n, c->d_pods, c->d_res, s, true);
+    if (rc) return rc;
+    MS_HIP(c, hipMemcpyAsync(out, c->d_res, sizeof(ms_result) * n, hipMemcpyDeviceToHost, s));
+    MS_HIP(c, hipStreamSynchronize(s));
+    return MS_OK;
+}
+
+int comm_schedule_device(ms_ctx *c, uint32_t n, const ms_pod_rec *pods_dev, ms_result *results_dev, hipStream_t s) {
+    CommState &m = *c->comm;
+    if (!plugins_stateless(c)) return seq_sharded_locked(c, n, pods_dev, results_dev, s);
+    // NU+NN / NodeAffinity: the batched cycle with its binds (equal to the queue-order loop)
+    const uint32_t per = cdiv(n, (uint32_t)m.world);
+    int rc = drain_all_locked(c);
+    if (rc) return rc;
+    rc = ensure_stage(c, per * (uint32_t)m.world);
+    if (rc) return rc;
+    rc = batched_all_locked(c, n, pods_dev, c->d_res, s, true);
+    if (rc) return rc;
+    MS_HIP(c, hipMemcpyAsync(results_dev, c->d_res, sizeof(ms_result) * n, hipMemcpyDeviceToDevice, s));
+    return MS_OK;
+}
+
+}  // namespace msgpu
+
+using namespace msgpu;
+
+extern "C" {
+
+int ms_comm_id_create(ms_comm_id *out) {
+    if (!out) return MS_E_INVAL;
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(nullptr, MS_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(out->internal, &id, sizeof(id));
+    return MS_OK;
+}
+
+int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
+    if (!c || !id || world < 1 || rank < 0 || rank >= world) return MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    if (c->comm) return fail(c, MS_E_INVAL, "ms_comm_init: the context already has a communicator");
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    CommState *m = new (std::nothrow) CommState();
+    if (!m) return fail(c, MS_E_OOM, "ms_comm_init: host allocation");
+    m->rank = rank;
+    m->world = world;
+    if (const char *e = getenv("MINISCHED_PIPE_DEPTH")) m->depth = (uint32_t)std::max(1, atoi(e));
+    m->depth = std::min<uint32_t>(m->depth, kPipeMax - 2);  // slot kPipeMax-1 stays free (ms_sharded_drain's event)
+    m->group = m->depth;
+    if (const char *e = getenv("MINISCHED_PIPE_GROUP")) m->group = (uint32_t)std::max(1, atoi(e));
+    m->group = std::min(m->group, m->depth);
+    c->comm = m;  // (comm_free releases a partial state)
+    MS_HIP(c, hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking));
+    for (uint32_t i = 0; i < kPipeMax; ++i) {
+        MS_HIP(c, hipEventCreateWithFlags(&m->ev_swept[i], hipEventDisableTiming));
+        MS_HIP(c, hipEventCreateWithFlags(&m->ev_comb[i], hipEventDisableTiming));
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id->internal, sizeof(uid));
+    const ncclResult_t r = ncclCommInitRank(&m->comm, world, uid, rank);
+    if (r != ncclSuccess) {
+        m->comm = nullptr;
+        comm_free(c);
+        return fail(c, MS_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    return MS_OK;
+}
+
+int ms_sharded_slice(const ms_ctx *c, uint32_t n, uint32_t *first, uint32_t *count) {
+    if (!c || !first || !count) return MS_E_INVAL;
+    if (!c->comm) {
+        *first = 0;
+        *count = n;
+        return MS_OK;
+    }
+    slice_of(*c->comm, n, *first, *count);
+    return MS_OK;
+}
+
+int ms_sharded_submit(ms_ctx *c, uint32_t n, const ms_pod_rec *pods_dev, ms_result *results_dev, void *stream) {
+    if (!c || (n && !pods_dev)) return MS_E_INVAL;
+    if (!c->comm) return fail(c, MS_E_INVAL, "ms_sharded_submit: the context has no communicator (ms_comm_init)");
+    if (n == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    uint32_t first = 0, count = 0;
+    slice_of(*c->comm, n, first, count);
+    if (count && !results_dev) return fail(c, MS_E_INVAL, "ms_sharded_submit: results_dev is required");
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    return submit_locked(c, n, pods_dev, results_dev, pick_stream(c, stream));
+}
+
+int ms_sharded_drain(ms_ctx *c, void *stream) {
+    if (!c) return MS_E_INVAL;
+    if (!c->comm) return fail(c, MS_E_INVAL, "ms_sharded_drain: the context has no communicator (ms_comm_init)");
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    CommState &m = *c->comm;
+    if (m.pending.empty()) return MS_OK;
+    const hipStream_t ps = m.pipe_stream, s = pick_stream(c, stream);
+    int rc = drain_locked(c, ps, m.pending.size());
+    if (rc) return rc;
+    if (s != ps) {  // the caller's stream sees the decodes
+        hipEvent_t ev = m.ev_swept[kPipeMax - 1];  // (slot kPipeMax-1 is unused: depth + 1 < kPipeMax)
+        MS_HIP(c, hipEventRecord(ev, ps));
+        MS_HIP(c, hipStreamWaitEvent(s, ev, 0));
+    }
+    return chain_back(c, ps);
+}
+
+}  // extern "C"

@@ -13,7 +13,7 @@ namespace msgpu {
 constexpr uint8_t kNodeUnschedulable = 0x01;  // node.Spec.Unschedulable
 constexpr uint8_t kNodeAbsent = 0x80;         // tombstone / never added: not in Nodes().List
 
-// K1 (NU+NN sweep) geometry: one node per lane-slot, 16 slots per lane.
+// NodeAffinity sweep geometry: one node per lane-slot, 16 slots per lane.
 constexpr int kNunnThreads = 256;
 constexpr int kNunnSlots = 16;
 constexpr int kNunnTile = kNunnThreads * kNunnSlots;  // nodes per block
@@ -26,11 +26,8 @@ constexpr int kFullTile = kFullThreads * kFullSlots;      // nodes per block
 
 constexpr uint32_t kGolden32 = 0x9E3779B1u;  // LDS map hashing in the validator
 
-// K1 v7 reads the pod stream in 8-pod groups, one group ahead; the stream is
-// padded so those reads stay in bounds.
-constexpr uint32_t kPodStreamPad = 16;
-// Bytes of padding after the flags/digit columns: K1 v7 reads a lane's rows
-// as an aligned dword window that may run up to 7 bytes past the last row.
+// Bytes of padding after the flags/digit/zone columns (vector loads of a
+// lane's rows may run past the last row).
 constexpr uint32_t kColumnPad = 64;
 
 // Device-resident node table, structure of arrays, indexed by LOCAL ordinal.
@@ -145,13 +142,6 @@ __host__ __device__ inline uint32_t tb_unhash(uint32_t A, uint32_t h) { return (
 // All return hipError_t of the launch; none synchronises.
 hipError_t launch_apply_deltas(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
 hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
-// NU+NN sweep: k_pod_prep (pod stream, zeroes keys/flags) then the K1 sweep.
-// pstream holds >= n_pods + kPodStreamPad entries.
-// work: K1 work counters, >= kK1MaxColumns u32 (zeroed by the pod prep as needed).
-constexpr uint32_t kK1MaxColumns = (MS_MAX_ORDINAL + 1) / 64 + 1;
-hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
-                             uint32_t *work, int num_cus, hipStream_t s);
 // K1 "pp" (ms_sweep_pp.hip): every (pod, node) pair through NU + NN + selectHost.
 // results != nullptr: decoded ms_result per pod (single-shard cycle; keys is
 // scratch, needed only above 122,880 rows), and with commit != 0 each winner's
@@ -176,7 +166,7 @@ hipError_t launch_sweep_na(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
 // decode of the NU+NN+NA set: the anchor's score becomes w_na * 100
 hipError_t launch_decode_na(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
                             const uint32_t *fkeys, uint32_t present_nodes, uint32_t seed32, uint32_t w_nn,
-                            uint32_t w_na, ms_result *out, hipStream_t s);
+                            uint32_t w_na, ms_result *out, hipStream_t s, const uint32_t *present_dev = nullptr);
 hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, unsigned long long *keys, uint32_t *flags, int num_cus,
                              hipStream_t s);
@@ -229,17 +219,38 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
 // (merged / merged_flags: n_pods * 4 / n_pods scratch).
 hipError_t launch_seq_pack_cands(const NodeTable &t, const unsigned long long *top4, const uint32_t *tile_flags,
                                  uint32_t n_tiles, uint32_t n_pods, ms_seq_cand *cands, uint32_t *flags, hipStream_t s);
+// live (optional): validate only the first min(n_pods, *live) pods (a cursor window)
 hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms_pod_rec *pods, uint32_t seed32,
                                    uint32_t n_shards, const ms_seq_cand *cands_all, const uint32_t *flags_all,
                                    ms_seq_cand *merged, uint32_t *merged_flags, ms_result *results, uint32_t *n_done,
-                                   hipStream_t s);
+                                   hipStream_t s, const uint32_t *live = nullptr);
+// Device cursor of the in-library node-sharded sequential cycle: ctl = {cursor,
+// live, n_done}; window_in stages pods [cursor, cursor + live) of n into win (w
+// entries), window_out copies ctl[2] decided results to res[cursor ..] and
+// advances the cursor (ms_kernels.hip).
+hipError_t launch_seq_window_in(const ms_pod_rec *pods, uint32_t n, uint32_t *ctl, ms_pod_rec *win, uint32_t w,
+                                hipStream_t s);
+hipError_t launch_seq_window_out(const ms_result *win_res, uint32_t *ctl, ms_result *res, uint32_t n, hipStream_t s);
 // Derived rows [0, n_total) of the sequential engine's table copy (t.drow): rows
 // at or past n_rows are absent.
 hipError_t launch_build_drows(const NodeTable &t, uint32_t n_rows, uint32_t n_total, hipStream_t s);
 // Rows the sequential engine's validator supports (tile lists held in registers).
 uint32_t seq_max_rows();
+// present_dev (optional): read the present count from the device (node-sharded combine)
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
-                         const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s);
+                         const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s,
+                         const uint32_t *present_dev = nullptr);
+// One launch decoding several batches' pod slices, each with a device-side present flag.
+constexpr uint32_t kMaxSliceJobs = 8;
+struct SliceJob {
+    const ms_pod_rec *pods;
+    const unsigned long long *keys;
+    const uint32_t *flags;    // NodeResourcesFit set: combined filter bytes; else nullptr
+    const uint32_t *present;  // device: non-zero iff some shard lists a node
+    ms_result *results;
+    uint32_t n_pods, _pad;
+};
+hipError_t launch_decode_slices(const SliceJob *jobs, uint32_t n_jobs, hipStream_t s);
 // n_jobs in [1, MS_DECODE_MAX_JOBS] (checked by the caller)
 hipError_t launch_decode_jobs(const ms_decode_job *jobs, uint32_t n_jobs, uint32_t present_nodes, hipStream_t s);
 hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32_t n_pods,

@@ -33,557 +33,6 @@ __device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
 }
 
 // ----------------------------------------------------------------------------
-// K1 v0: NodeUnschedulable + NodeNumber, batched (stateless) sweep, the plain
-// form: every (pod, node) pair is filtered, scored and hashed, one 64-bit key
-// max per pair. Kept as an independent GPU cross-check of the production
-// kernel (MINISCHED_K1=v0).
-//   grid.x = node tiles of kNunnTile rows, grid.y = pod chunks (multiple of 64)
-// ----------------------------------------------------------------------------
-template <bool WANT_FLAGS>
-__global__ __launch_bounds__(kNunnThreads) void k_sweep_nunn(
-    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk,
-    uint32_t seed32, u64 *__restrict__ keys, uint32_t *__restrict__ pflags) {
-    const uint32_t lane = lane_id();
-    const uint32_t row0 = blockIdx.x * kNunnTile + threadIdx.x * kNunnSlots;
-
-    uint32_t dw[4];  // 16 digits, 4 per dword
-    uint32_t unsched = 0, absent = 0;
-    if (row0 + kNunnSlots <= n_rows) {
-        const uint4 f4 = *reinterpret_cast<const uint4 *>(nflags + row0);
-        const uint4 d4 = *reinterpret_cast<const uint4 *>(ndigit + row0);
-        const uint32_t fw[4] = {f4.x, f4.y, f4.z, f4.w};
-        dw[0] = d4.x; dw[1] = d4.y; dw[2] = d4.z; dw[3] = d4.w;
-#pragma unroll
-        for (int i = 0; i < kNunnSlots; ++i) {
-            const uint32_t f = (fw[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-            unsched |= (f & kNodeUnschedulable) ? (1u << i) : 0u;
-            absent |= (f & kNodeAbsent) ? (1u << i) : 0u;
-        }
-    } else {
-        dw[0] = dw[1] = dw[2] = dw[3] = 0xFFFFFFFFu;
-#pragma unroll
-        for (int i = 0; i < kNunnSlots; ++i) {
-            const uint32_t r = row0 + i;
-            const uint32_t f = r < n_rows ? nflags[r] : kNodeAbsent;
-            const uint32_t d = r < n_rows ? ndigit[r] : 0xFFu;
-            dw[i >> 2] = (dw[i >> 2] & ~(0xFFu << ((i & 3) * 8))) | (d << ((i & 3) * 8));
-            unsched |= (f & kNodeUnschedulable) ? (1u << i) : 0u;
-            absent |= (f & kNodeAbsent) ? (1u << i) : 0u;
-        }
-    }
-    const uint32_t ord0 = node_base + row0;
-    const uint32_t unsched_present = unsched & ~absent;
-
-    const uint32_t pbeg = blockIdx.y * chunk;
-    const uint32_t pend = min(n_pods, pbeg + chunk);
-    u64 mine = 0;
-    uint32_t myflag = 0;
-    for (uint32_t p = pbeg; p < pend; ++p) {
-        const ms_pod_rec pr = pods[p];  // wave-uniform
-        const uint32_t A = tb_pod(seed32, pr.ordinal);
-        const int dig = pr.name_digit;
-        const uint32_t infeas = pr.tolerates_unschedulable ? absent : (absent | unsched);
-        u64 best = 0;
-#pragma unroll
-        for (int i = 0; i < kNunnSlots; ++i) {
-            const int nd = (int)((dw[i >> 2] >> ((i & 3) * 8)) & 0xFFu);
-            const uint32_t score = (nd == dig) ? 10u : 0u;
-            const u64 key = make_key(score, tb_hash(A, ord0 + i), ord0 + i);
-            best = ((infeas >> i) & 1u) ? best : umax64(best, key);
-        }
-        best = wave_max_u64(best);
-        const uint32_t slot = (p - pbeg) & 63u;
-        if (lane == slot) mine = best;
-        if (WANT_FLAGS) {
-            const bool nu = !pr.tolerates_unschedulable && unsched_present != 0;
-            const bool any_nu = __ballot(nu) != 0;
-            if (lane == slot) myflag = any_nu ? 1u : 0u;
-        }
-        if (slot == 63u || p + 1 == pend) {
-            const uint32_t pp = p - slot + lane;
-            if (lane <= slot && mine) atomicMax(&keys[pp], mine);
-            if (WANT_FLAGS && lane <= slot && myflag) atomicOr(&pflags[pp], myflag);
-            mine = 0;
-            myflag = 0;
-        }
-    }
-}
-
-// ----------------------------------------------------------------------------
-// Pod stream: one 8-byte entry per pod, built once per batch by k_pod_prep
-// (which also zeroes the batch's keys/flags, replacing two memsets):
-//   .x = A = tb_pod(seed32, ordinal)   (the pod half of the tie-break hash)
-//   .y = class = digit (0..9, 10 = name does not end in a digit) | tolerates << 4
-// Every node wave reads it through the scalar cache, two pods per 16-byte load.
-// The buffer carries kPodStreamPad padding entries so the sweep's reads of
-// whole 8-pod groups, one group ahead, never need a bounds check.
-// ----------------------------------------------------------------------------
-// gmask[q] = OR over pods 8q .. 8q+7 of (1 << class): the sweep's group test is
-// then one scalar AND-NOT against the wave's list-path classes. Groups past the
-// stream read as class 10 (never on the list path).
-__global__ void k_pod_prep(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t seed32,
-                           uint2 *__restrict__ ps, u64 *__restrict__ keys, uint32_t *__restrict__ flags,
-                           uint32_t *__restrict__ work, uint32_t n_work, uint32_t *__restrict__ gmask) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n_work) work[i] = 0;  // K1 v8's per-column work counters
-    uint32_t cls = 10u;
-    if (i < n) {
-        const ms_pod_rec pr = pods[i];
-        const uint32_t d = (uint32_t)pr.name_digit <= 9u ? (uint32_t)pr.name_digit : 10u;
-        cls = d | (pr.tolerates_unschedulable ? 16u : 0u);
-        ps[i] = make_uint2(tb_pod(seed32, pr.ordinal), cls);
-        keys[i] = 0;
-        if (flags) flags[i] = 0;
-    } else if (i < n + kPodStreamPad) {
-        ps[i] = make_uint2(0u, 10u);
-    }
-    uint32_t m = 1u << cls;  // blockDim is a multiple of 64: groups of 8 never straddle a wave
-    m |= __shfl_xor(m, 1);
-    m |= __shfl_xor(m, 2);
-    m |= __shfl_xor(m, 4);
-    if ((i & 7u) == 0u && i < n + kPodStreamPad + 16u) gmask[i >> 3] = m;
-}
-
-// ----------------------------------------------------------------------------
-// K1 v7, the production NU+NN sweep: per-wave candidate lists by pod class.
-//
-// Layout: a wave owns 64 lanes x rpl (<= 32) consecutive rows for its whole
-// lifetime and streams a chunk of pods through them. At load each lane turns
-// its digit bytes into four bit planes and then ten one-hot row masks (bit s
-// <=> row row0+s has name digit d), and its flag bytes into unschedulable /
-// absent masks. For a non-tolerating pod of digit d the lane's candidates
-// (rows passing NodeUnschedulable that score NodeNumber's 10) are the set bits
-// of onehot[d] & feasible; there are at most K of them per lane when rpl <=
-// 10K (digits of consecutive names cycle). Each lane keeps, per class d, the
-// hash inputs (node_ordinal * kG24) of those rows in K registers, padded with
-// a duplicate of one of the wave's own class-d candidates, so a pod costs K
-// hashes per lane with no bit scanning and no lane-divergent loop: the
-// filter+score of all the lane's rows is the class-list lookup, and the
-// tie-break hash (rule r3) of each candidate is v_add + mix32. A class with
-// more than K candidates in some lane of the wave, a tolerating pod, and a
-// pod whose digit has no feasible row in the wave (every feasible row scores
-// 0) take the general path: the lane's mask from LDS / registers and a
-// branch-free v_ffbl loop over it.
-//
-// Argmax: rule r3 makes the hash a bijection of the node ordinal for a pod,
-// so the wave only needs the maximum hash; tb_unhash returns its row. Lane
-// maxima of 8 pods are reduced together by a transposed butterfly
-// (v_permlane32_swap, v_permlane16_swap, one DPP row_ror:8 exchange, then
-// three DPP steps): 2.25 VALU per pod instead of a 6-step DPP chain per pod.
-// The 8 results go to LDS and every 64 pods the lanes unhash and leave as one
-// coalesced atomicMax wave-instruction.
-//
-// Grid: one block = one wave; grid.x = node waves, grid.y = pod chunks
-// (launch_v7).
-// ----------------------------------------------------------------------------
-struct Bits32Cols {
-    uint32_t onehot[10];
-    uint32_t unsched, absent;
-};
-
-// bit `bit` of each byte of x -> 4 bits (byte 0 lowest)
-__device__ __forceinline__ uint32_t gather4(uint32_t x, int bit) {
-    return ((((x >> bit) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
-}
-
-// Bit planes of the lane's digit bytes (bit i of every byte in one register,
-// four rows per multiply), then onehot[v] = AND of the four planes or their
-// complements; 0xFF ("no digit") is 15 in the low nibble and matches nothing.
-// Rows row0 .. row0+rpl-1 (rpl <= 32, wave-uniform); slots >= rpl are absent.
-// The columns carry 64 bytes of padding, so the aligned dword window of a
-// full lane may read up to 7 bytes past row0 + rpl.
-__device__ __forceinline__ void load_bits32_planes(const uint8_t *__restrict__ nflags,
-                                                   const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-                                                   uint32_t row0, uint32_t rpl, Bits32Cols &c) {
-    uint32_t dv[8], fv[8];
-    if (row0 + rpl <= n_rows) {  // lane-varying only in a shard's last wave
-        const uint32_t *dp = reinterpret_cast<const uint32_t *>(ndigit + (row0 & ~3u));
-        const uint32_t *fp = reinterpret_cast<const uint32_t *>(nflags + (row0 & ~3u));
-        const uint32_t sh = (row0 & 3u) * 8u;
-        uint32_t dw[9], fw[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const bool in = 4u * k < rpl + 3u;  // wave-uniform: skip dwords past the lane's rows
-            dw[k] = in ? dp[k] : 0xFFFFFFFFu;
-            fw[k] = in ? fp[k] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            // bytes 4k .. 4k+3 of the lane's window; slots >= rpl become absent
-            const uint32_t nv = rpl > 4u * k ? min(4u, rpl - 4u * k) : 0u;
-            const uint32_t keep = nv >= 4u ? 0xFFFFFFFFu : (1u << (8u * nv)) - 1u;
-            dv[k] = (__builtin_amdgcn_alignbit(dw[k + 1], dw[k], sh) & keep) | ~keep;
-            fv[k] = (__builtin_amdgcn_alignbit(fw[k + 1], fw[k], sh) & keep) | (kNodeAbsent * 0x01010101u & ~keep);
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            dv[k] = 0;
-            fv[k] = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t r = row0 + 4 * k + j;
-                const bool in = (uint32_t)(4 * k + j) < rpl && r < n_rows;
-                dv[k] |= (in ? (uint32_t)ndigit[r] : 0xFFu) << (8 * j);
-                fv[k] |= (in ? (uint32_t)nflags[r] : (uint32_t)kNodeAbsent) << (8 * j);
-            }
-        }
-    }
-    uint32_t pl[4] = {0, 0, 0, 0};
-    c.unsched = c.absent = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pl[i] |= gather4(dv[k], i) << (4 * k);
-        c.unsched |= gather4(fv[k], 0) << (4 * k);  // kNodeUnschedulable = bit 0
-        c.absent |= gather4(fv[k], 7) << (4 * k);   // kNodeAbsent = bit 7
-    }
-#pragma unroll
-    for (int v = 0; v < 10; ++v)
-        c.onehot[v] = ((v & 1) ? pl[0] : ~pl[0]) & ((v & 2) ? pl[1] : ~pl[1]) & ((v & 4) ? pl[2] : ~pl[2]) &
-                      ((v & 8) ? pl[3] : ~pl[3]);
-}
-
-typedef uint32_t u32x10 __attribute__((ext_vector_type(10)));
-
-template <int K>
-struct ClassLists {
-    u32x10 h[K];  // h[i][d]: node_ordinal * kG24 of the lane's i-th class-d candidate (padded)
-};
-
-// Wave state a pod is evaluated against.
-template <int K>
-struct WaveRows {
-    ClassLists<K> L;
-    uint32_t feasN, feasT;  // rows passing NodeUnschedulable for a non-tolerating / tolerating pod
-    uint32_t hterm0;        // (ordinal of the lane's first row) * kG24
-    uint32_t fast;          // wave-uniform: bit d = class d takes the list path
-    uint32_t fast_tol;      // wave-uniform: bit 16+d = tolerating class d takes the list path (LDS)
-};
-
-// List path of one pod: the lane's maximum hash over its K class-d entries.
-template <int K>
-__device__ __forceinline__ uint32_t list_max(const ClassLists<K> &L, uint32_t A, uint32_t d) {
-    uint32_t h[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) h[i] = mix32(A + L.h[i][d]);
-    uint32_t kb = h[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i) kb = max(kb, h[i]);
-    return kb;
-}
-
-// list_max<3> with the class index applied to the adds themselves: under
-// s_set_gpr_idx_on (SRC0 mode) a VALU's first source register is offset by
-// the class, so v_add reads h[i][d] directly and the K indexed v_mov copies
-// disappear. The lists are pinned to v[34:63] for this (the register
-// allocator keeps them there for the kernel's lifetime: `make asm` shows no
-// copies into that range in the pod loop).
-__device__ __forceinline__ uint32_t list_max3_idx(const ClassLists<3> &L, uint32_t A, uint32_t d) {
-    uint32_t x0, x1, x2;
-    asm volatile(
-        "s_set_gpr_idx_on %[d], gpr_idx(SRC0)\n\t"
-        "v_add_u32_e64 %[x0], v34, %[A]\n\t"
-        "v_add_u32_e64 %[x1], v44, %[A]\n\t"
-        "v_add_u32_e64 %[x2], v54, %[A]\n\t"
-        "s_set_gpr_idx_off"
-        : [x0] "=&v"(x0), [x1] "=&v"(x1), [x2] "=&v"(x2)
-        : [d] "s"(d), [A] "s"(A), "{v[34:43]}"(L.h[0]), "{v[44:53]}"(L.h[1]), "{v[54:63]}"(L.h[2]));
-    return max(max(mix32(x0), mix32(x1)), mix32(x2));
-}
-
-// General path of one pod (pod stream entry: A, cls): tolerating pods, classes
-// whose lists overflowed, pods with no digit match in the wave. Returns the
-// lane's maximum candidate hash; fs (wave-uniform) bit 0 = the wave has a
-// feasible row for the pod, bit 1 = the best score is NodeNumber's 10.
-__device__ __forceinline__ uint32_t eval_general(uint32_t feasN, uint32_t feasT, uint32_t hterm0,
-                                                 const uint32_t (*raw)[64], uint32_t lane, uint32_t A, uint32_t cls,
-                                                 uint32_t &fs) {
-    const uint32_t d = cls & 15u;
-    const bool tol = cls >= 16u;
-    uint32_t m = d < 10u ? (raw[d][lane] & (tol ? feasT : feasN)) : 0u;
-    const bool s10 = __ballot(m != 0) != 0;
-    if (!s10) m = tol ? feasT : feasN;  // no digit match in this wave: every feasible row scores 0
-    const bool found = s10 || __ballot(m != 0) != 0;
-    fs = (uint32_t)__builtin_amdgcn_readfirstlane((found ? 1 : 0) | (s10 ? 2 : 0));
-    const uint32_t AH = A + hterm0;
-    uint32_t kb = 0;
-    while (__ballot(m != 0)) {  // lane-divergent trip count, branch-free body
-        const uint32_t s = first_slot(m);
-        const bool live = m != 0;
-        m &= m - 1u;
-        kb = max(kb, mix32(live ? AH + __umul24(s, kG24) : 0u));  // mix32(0) = 0
-    }
-    return kb;
-}
-
-// LDS state of a workgroup's node tile: the one-hot masks (general path), wave
-// 0's class lists (W > 1), then feasN, feasT, hterm0 (the general path reads
-// those three from here, so they hold no VGPRs through the pod loop), and the
-// wave-uniform fast-class mask and "some row is unschedulable" bit.
-template <int K, int W>
-struct TileLds {
-    static constexpr int kMisc = W > 1 ? 10 * K : 0;
-    uint32_t raw[10][64];
-    uint32_t tile[kMisc + 3][64];
-    uint32_t tol[K][10][64];  // class lists of tolerating pods (every present row of the digit)
-    uint32_t bits[3];       // wave 0's fast, wave_unsched, fast_tol
-    uint32_t slots[W][64];  // each wave's maxima of its current 64 pods
-};
-
-// Class lists of the wave's rows in m_all (per class d: m_all[d]), padded as in
-// tile_build; returns the wave-uniform mask of classes whose lists fit.
-template <int K, typename Store>
-__device__ __forceinline__ uint32_t build_lists(const uint32_t (&m_all)[10], uint32_t hterm0, Store store) {
-    uint32_t fit = 0;
-#pragma unroll
-    for (int d = 0; d < 10; ++d) {
-        uint32_t m = m_all[d];
-        const uint32_t cnt = __popc(m);
-        const u64 any = __ballot(m != 0);
-        const bool ovf = __ballot(cnt > (uint32_t)K) != 0;
-        const uint32_t first = hterm0 + __umul24(first_slot(m), kG24);
-        const uint32_t donor = (uint32_t)__builtin_amdgcn_readlane((int)first, any ? (int)__builtin_ctzll(any) : 0);
-        const uint32_t pad = cnt ? first : donor;  // a class-d candidate of this wave
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const uint32_t v = hterm0 + __umul24(first_slot(m), kG24);
-            m &= m - 1u;
-            store(i, d, (uint32_t)i < cnt ? v : pad);
-        }
-        if (any && !ovf) fit |= 1u << d;
-    }
-    return fit;
-}
-
-// Tolerating pod of digit d on the list path: the lists live in LDS.
-template <int K, int W>
-__device__ __forceinline__ uint32_t list_max_tol(const TileLds<K, W> &S, uint32_t lane, uint32_t A, uint32_t d) {
-    uint32_t kb = 0;
-#pragma unroll
-    for (int i = 0; i < K; ++i) kb = max(kb, mix32(A + S.tol[i][d][lane]));
-    return kb;
-}
-
-// Wave 0: builds the tile of rows wave_row0 + lane*rpl .. (+rpl) into w and LDS.
-template <int K, int W>
-__device__ __forceinline__ void tile_build(TileLds<K, W> &S, const uint8_t *__restrict__ nflags,
-                                           const uint8_t *__restrict__ ndigit, uint32_t n_rows, uint32_t node_base,
-                                           uint32_t row0, uint32_t rpl, uint32_t lane, uint32_t fast_mask,
-                                           WaveRows<K> &w, bool &wave_unsched) {
-    constexpr int kMisc = TileLds<K, W>::kMisc;
-    Bits32Cols c;
-    load_bits32_planes(nflags, ndigit, n_rows, row0, rpl, c);
-    w.feasN = ~(c.absent | c.unsched);
-    w.feasT = ~c.absent;
-    w.hterm0 = (node_base + row0) * kG24;
-    w.fast = 0;
-    wave_unsched = __ballot((c.unsched & ~c.absent) != 0) != 0;
-    uint32_t mN[10], mT[10];
-#pragma unroll
-    for (int d = 0; d < 10; ++d) {
-        S.raw[d][lane] = c.onehot[d];
-        mN[d] = c.onehot[d] & w.feasN;
-        mT[d] = c.onehot[d] & w.feasT;
-    }
-    // non-tolerating classes (fast bits 0..9, lists in registers); tolerating
-    // classes (cls = d | 16: fast bits 16..25, lists in LDS)
-    w.fast = build_lists<K>(mN, w.hterm0, [&](int i, int d, uint32_t v) { w.L.h[i][d] = v; }) & fast_mask;
-    w.fast_tol = (build_lists<K>(mT, w.hterm0, [&](int i, int d, uint32_t v) { S.tol[i][d][lane] = v; }) << 16) &
-                 fast_mask;  // (tests and A/B: fast_mask 0x3FF sends tolerating pods down the general path)
-    S.tile[kMisc][lane] = w.feasN;
-    S.tile[kMisc + 1][lane] = w.feasT;
-    S.tile[kMisc + 2][lane] = w.hterm0;
-    if (W > 1) {
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-#pragma unroll
-            for (int d = 0; d < 10; ++d) S.tile[i * 10 + d][lane] = w.L.h[i][d];
-        if (lane == 0) {
-            S.bits[0] = w.fast;
-            S.bits[1] = wave_unsched ? 1u : 0u;
-            S.bits[2] = w.fast_tol;
-        }
-    }
-}
-
-// Waves 1..W-1: the tile wave 0 built (after a workgroup barrier).
-template <int K, int W>
-__device__ __forceinline__ void tile_load(const TileLds<K, W> &S, uint32_t lane, WaveRows<K> &w, bool &wave_unsched) {
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-#pragma unroll
-        for (int d = 0; d < 10; ++d) w.L.h[i][d] = S.tile[i * 10 + d][lane];
-    w.fast = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.bits[0]);
-    wave_unsched = __builtin_amdgcn_readfirstlane((int)S.bits[1]) != 0;
-    w.fast_tol = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.bits[2]);
-}
-
-// One wave sweeps pods [pbeg, pend) of the pod stream against its tile.
-template <int K, bool WANT_FLAGS, int W>
-__device__ __forceinline__ void sweep_pods(const TileLds<K, W> &S, uint32_t *slot, const WaveRows<K> &w,
-                                           bool wave_unsched, uint32_t lane, const uint2 *__restrict__ ps,
-                                           uint32_t pbeg, uint32_t pend, u64 *__restrict__ keys,
-                                           uint32_t *__restrict__ pflags, uint32_t group_test,
-                                           const uint32_t *__restrict__ gmask) {
-    constexpr int kMisc = TileLds<K, W>::kMisc;
-    const uint4 *__restrict__ q4 = reinterpret_cast<const uint4 *>(ps) + (pbeg >> 1);
-    uint4 nx0 = q4[0], nx1 = q4[1], nx2 = q4[2], nx3 = q4[3];
-    const uint32_t *__restrict__ gq = gmask + (pbeg >> 3);  // ranges start on 8-pod groups
-    uint32_t gnext = gq[0];
-    for (uint32_t g = pbeg; g < pend; g += 64) {  // 64-pod blocks: one flush each
-        const uint32_t gn = min(64u, pend - g);
-        u64 found = 0, s10m = 0, num = 0;
-        // the flush's pod halves A (for tb_unhash), loaded now so the load's latency
-        // hides under the block's sweep instead of stalling the flush
-        const uint32_t a_flush = lane < gn ? ps[g + lane].x : 0u;
-        for (uint32_t sub = 0; sub < gn; sub += 8) {
-            const uint32_t e[16] = {nx0.x, nx0.y, nx0.z, nx0.w, nx1.x, nx1.y, nx1.z, nx1.w,
-                                    nx2.x, nx2.y, nx2.z, nx2.w, nx3.x, nx3.y, nx3.z, nx3.w};
-            const uint32_t gcur = gnext;
-            gnext = *++gq;  // the next group's class mask (written two groups past the stream)
-            q4 += 4;
-            nx0 = q4[0];  // prefetch the next 8 pods; the stream is padded past n_pods
-            nx1 = q4[1];
-            nx2 = q4[2];
-            nx3 = q4[3];
-            // Pods past the range's end in its last group are evaluated too (the
-            // stream is padded; a range is a multiple of 8 pods except at the
-            // batch's end) and masked out of the outcome bits.
-            uint32_t r[8];
-            u64 gfound = 0, gs10 = 0, gnum = 0;
-            // Group test: when all 8 pods are non-tolerating with fitting class lists
-            // (the common case; k_pod_prep's OR of the group's class bits against the
-            // wave's list-path classes), one scalar branch per group instead of one
-            // per pod, and the 8 list lookups run straight through (MINISCHED_K1_GROUP=0: off).
-            if (group_test && (gcur & ~w.fast) == 0u) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    if constexpr (K == 3)
-                        r[j] = list_max3_idx(w.L, e[2 * j], e[2 * j + 1]);
-                    else
-                        r[j] = list_max<K>(w.L, e[2 * j], e[2 * j + 1]);
-                }
-                gfound = gs10 = 0xFFull;
-                if (WANT_FLAGS && wave_unsched) gnum = 0xFFull;  // all 8 are non-tolerating
-            } else
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t A = e[2 * j], cls = e[2 * j + 1];
-                uint32_t fs = 3u;            // found, score 10
-                // one SALU bit test on the common path: w.fast holds the non-tolerating
-                // classes only (cls >= 16 shifts them out); w.fast_tol the tolerating ones
-                if ((w.fast >> cls) & 1u) {  // non-tolerating, class lists fit
-                    if constexpr (K == 3)
-                        r[j] = list_max3_idx(w.L, A, cls);  // the production geometry (30 rows per lane)
-                    else
-                        r[j] = list_max<K>(w.L, A, cls);
-                } else if ((w.fast_tol >> cls) & 1u)  // tolerating pod, class lists fit (LDS)
-                    r[j] = list_max_tol<K, W>(S, lane, A, cls - 16u);
-                else
-                    r[j] = eval_general(S.tile[kMisc][lane], S.tile[kMisc + 1][lane], S.tile[kMisc + 2][lane],
-                                        S.raw, lane, A, cls, fs);
-                gfound |= (u64)(fs & 1u) << j;
-                gs10 |= (u64)(fs >> 1) << j;
-                if (WANT_FLAGS) gnum |= (u64)(cls < 16u && wave_unsched) << j;
-            }
-            const u64 gmask = gn - sub >= 8u ? 0xFFull : (1ull << (gn - sub)) - 1ull;
-            found |= (gfound & gmask) << sub;
-            s10m |= (gs10 & gmask) << sub;
-            if (WANT_FLAGS) num |= (gnum & gmask) << sub;
-            const uint32_t u = reduce8(r, lane);
-            if ((lane & 7u) == 0u) slot[sub + rev3(lane >> 3)] = u;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane < gn && ((found >> lane) & 1u)) {
-            const uint32_t h = slot[lane];
-            const uint32_t ord = tb_unhash(a_flush, h);
-            atomicMax(&keys[g + lane], make_key(((s10m >> lane) & 1u) ? 10u : 0u, h, ord));
-        }
-        if (WANT_FLAGS && lane < gn && ((num >> lane) & 1u)) atomicOr(&pflags[g + lane], 1u);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// K1 v7 grid: grid.x = node waves, grid.y = pod chunk groups. W waves per
-// workgroup share one node tile: wave 0 builds it and hands the class lists and
-// masks to the others through LDS, so the tile build (about 550 VALU per wave)
-// is paid once per W pod chunks.
-template <int K, bool WANT_FLAGS, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v7(
-    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
-    u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t fast_mask) {
-    __shared__ TileLds<K, W> S;
-    const uint32_t lane = lane_id();
-    const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
-    const uint32_t wave_row0 = blockIdx.x * 64u * rpl;
-    const uint32_t pbeg = (blockIdx.y * W + wv) * chunk;
-    const uint32_t pend = min(n_pods, pbeg + chunk);
-    if (wave_row0 >= n_rows) return;     // block-uniform
-    if (W == 1 && pbeg >= pend) return;  // wave-uniform (W > 1: after the hand-off)
-    WaveRows<K> w;
-    bool wave_unsched;
-    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane,
-                                  fast_mask, w, wave_unsched);
-    if (W > 1) {
-        __syncthreads();
-        if (wv != 0) tile_load<K, W>(S, lane, w, wave_unsched);
-        if (pbeg >= pend) return;  // wave-uniform
-    }
-    // W == 1: each lane reads only its own LDS entries, no barrier needed
-    sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags,
-                                 fast_mask >> 31, reinterpret_cast<const uint32_t *>(ps + n_pods + kPodStreamPad));
-}
-
-// K1 v8: the same sweep as a persistent grid with a work queue. One workgroup
-// per resident slot; workgroup b serves node column b % n_cols and takes the
-// column's items (W consecutive pod chunks, one per wave) from the column's
-// counter until it is spent. The tile is built once per workgroup, the next
-// item is claimed while the current one is swept, and the queue evens out the
-// workgroups of a column without rounds of fresh waves. (Moving to another
-// column when the own one is spent needs a tile rebuild inside the loop, and
-// the register pressure of that spills.) col_next[n_cols] must be zero on
-// entry (k_pod_prep zeroes it).
-template <int K, bool WANT_FLAGS, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_nunn_v8(
-    const uint8_t *__restrict__ nflags, const uint8_t *__restrict__ ndigit, uint32_t n_rows,
-    uint32_t node_base, uint32_t rpl, const uint2 *__restrict__ ps, uint32_t n_pods, uint32_t chunk,
-    u64 *__restrict__ keys, uint32_t *__restrict__ pflags, uint32_t *__restrict__ col_next, uint32_t n_cols,
-    uint32_t fast_mask) {
-    __shared__ TileLds<K, W> S;
-    __shared__ uint32_t s_item;
-    const uint32_t lane = lane_id();
-    const uint32_t wv = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
-    const uint32_t per_col = (n_pods + chunk * W - 1) / (chunk * W);  // items per column
-    const uint32_t col = blockIdx.x % n_cols;
-    if (threadIdx.x == 0) s_item = atomicAdd(&col_next[col], 1u);
-    WaveRows<K> w;
-    bool wave_unsched;
-    const uint32_t wave_row0 = col * 64u * rpl;
-    if (wv == 0) tile_build<K, W>(S, nflags, ndigit, n_rows, node_base, wave_row0 + lane * rpl, rpl, lane,
-                                  fast_mask, w, wave_unsched);
-    __syncthreads();
-    if (W > 1 && wv != 0) tile_load<K, W>(S, lane, w, wave_unsched);
-    uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-    while (it < per_col) {  // workgroup-uniform
-        uint32_t nxt = 0;
-        if (threadIdx.x == 0) nxt = atomicAdd(&col_next[col], 1u);  // claimed now, read after the sweep
-        const uint32_t pbeg = (it * W + wv) * chunk;
-        const uint32_t pend = min(n_pods, pbeg + chunk);
-        if (pbeg < pend) sweep_pods<K, WANT_FLAGS, W>(S, S.slots[wv], w, wave_unsched, lane, ps, pbeg, pend, keys, pflags,
-                                 fast_mask >> 31, reinterpret_cast<const uint32_t *>(ps + n_pods + kPodStreamPad));
-        __syncthreads();  // every wave has read s_item
-        if (threadIdx.x == 0) s_item = nxt;
-        __syncthreads();
-        it = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_item);
-    }
-}
-
-// ----------------------------------------------------------------------------
 // K3: NodeUnschedulable + NodeResourcesFit filters, NodeNumber + LeastAllocated
 // scores (upstream v1.22 semantics restated in oracle/ms_oracle.c).
 // ----------------------------------------------------------------------------
@@ -2397,9 +1846,11 @@ __global__ __launch_bounds__(64) void k_seq_validate_rep(NodeTable t, uint32_t n
                                                          const ms_seq_cand *__restrict__ merged,
                                                          const uint32_t *__restrict__ merged_flags,
                                                          ms_result *__restrict__ results,
-                                                         uint32_t *__restrict__ n_done) {
+                                                         uint32_t *__restrict__ n_done,
+                                                         const uint32_t *__restrict__ live) {
     __shared__ RepShared S;
     const uint32_t lane = threadIdx.x;
+    if (live) n_pods = min(n_pods, *live);  // a cursor window: only its live pods are validated
     for (uint32_t i = lane; i < n_pods * kTopK; i += 64) S.c[i] = merged[i];
     for (uint32_t i = lane; i < (uint32_t)kRepMapCap; i += 64) S.map[i] = 0;
     if (lane == 0) S.n_bound = 0;
@@ -2494,10 +1945,13 @@ __device__ __forceinline__ void decode_one(const ms_pod_rec *__restrict__ pods, 
     out[i] = decode_key(keys[i], pods[i].name_digit, flags, i, present);
 }
 
+// present_dev (optional): the present count as the node-sharded combine left
+// it on the device (non-zero iff some shard lists a node), instead of present.
 __global__ void k_decode(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const u64 *__restrict__ keys,
-                         const uint32_t *__restrict__ flags, uint32_t present, ms_result *__restrict__ out) {
+                         const uint32_t *__restrict__ flags, uint32_t present, const uint32_t *__restrict__ present_dev,
+                         ms_result *__restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n_pods) decode_one(pods, keys, flags, present, out, i);
+    if (i < n_pods) decode_one(pods, keys, flags, present_dev ? *present_dev : present, out, i);
 }
 
 // Several batches' decodes in one launch (grid.y = job): the grouped drain of
@@ -2511,6 +1965,45 @@ __global__ void k_decode_jobs(DecodeJobs jobs, uint32_t present) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < jb.n_pods)
         decode_one(jb.pods, reinterpret_cast<const u64 *>(jb.keys), jb.flags, present, jb.results, i);
+}
+
+// The in-library node-sharded drain: several batches' pod slices, each with
+// its own device-side present flag (ms_comm.cpp).
+struct SliceJobs {
+    SliceJob j[kMaxSliceJobs];
+};
+
+__global__ void k_decode_slices(SliceJobs jobs) {
+    const SliceJob &jb = jobs.j[blockIdx.y];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < jb.n_pods) decode_one(jb.pods, jb.keys, jb.flags, *jb.present, jb.results, i);
+}
+
+// Node-sharded exact sequential with a device-side queue cursor (ms_comm.cpp):
+// ctl[0] = next pod of the queue, ctl[1] = live pods of the current window,
+// ctl[2] = pods the window's validation decided (k_seq_validate_rep n_done).
+// window_in copies pods [cursor, cursor + live) into the fixed window (zeroes
+// the rest: those entries are swept but never validated); window_out copies
+// the decided results back to the queue order and advances the cursor, so the
+// host issues batches without reading n_done.
+__global__ void k_seq_window_in(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t *__restrict__ ctl,
+                                ms_pod_rec *__restrict__ win, uint32_t w) {
+    const uint32_t cur = min(ctl[0], n);
+    const uint32_t live = min(w, n - cur);
+    for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) {
+        ms_pod_rec z = {};
+        win[i] = i < live ? pods[cur + i] : z;
+    }
+    if (threadIdx.x == 0) ctl[1] = live;
+}
+
+__global__ void k_seq_window_out(const ms_result *__restrict__ win_res, uint32_t *__restrict__ ctl,
+                                 ms_result *__restrict__ res, uint32_t n) {
+    const uint32_t cur = min(ctl[0], n);
+    const uint32_t done = min(ctl[2], n - cur);
+    for (uint32_t i = threadIdx.x; i < done; i += blockDim.x) res[cur + i] = win_res[i];
+    __syncthreads();  // every thread read ctl[0] before it moves
+    if (threadIdx.x == 0) ctl[0] = cur + done;
 }
 
 __global__ void k_apply_binds(NodeTable t, const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
@@ -2649,8 +2142,8 @@ __global__ __launch_bounds__(kNunnThreads) void k_sweep_na(
 }
 
 __global__ void k_decode_na(const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const u64 *__restrict__ keys,
-                            const uint32_t *__restrict__ fkeys, uint32_t present, uint32_t seed32, uint32_t w_nn,
-                            uint32_t w_na, ms_result *__restrict__ out) {
+                            const uint32_t *__restrict__ fkeys, uint32_t present, const uint32_t *__restrict__ present_dev,
+                            uint32_t seed32, uint32_t w_nn, uint32_t w_na, ms_result *__restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_pods) return;
     u64 k = keys[i];
@@ -2659,7 +2152,7 @@ __global__ void k_decode_na(const ms_pod_rec *__restrict__ pods, uint32_t n_pods
         const uint32_t ord = 0xFFFFFu - ((a - 1u) >> 1), nn = (a - 1u) & 1u;
         k = umax64(k, make_key(w_nn * 10u * nn + w_na * 100u, tb_hash(tb_pod(seed32, pods[i].ordinal), ord), ord));
     }
-    out[i] = decode_key(k, pods[i].name_digit, nullptr, 0, present);
+    out[i] = decode_key(k, pods[i].name_digit, nullptr, 0, present_dev ? *present_dev : present);
 }
 
 inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -2677,187 +2170,6 @@ inline uint32_t pod_chunk(uint32_t n_pods, uint32_t node_blocks, int num_cus) {
 
 }  // namespace
 
-// K1 variant, read from MINISCHED_K1 at each launch so A/B runs can
-// interleave variants inside one process: "v0" (hash every pair, the plain
-// cross-check) or the default v7.
-// Default: the persistent v8 for shards of >= kK1V8MinColumns node columns (its
-// per-column counters are contended by too many workgroups on small shards),
-// v7 below (profiles/r01j_k1_v8_ab.jsonl: 100k rows 0.232 vs 0.241 ms, 12.5k
-// rows 0.088 vs 0.049 ms).
-enum K1Variant { K1_V0 = 0, K1_V7 = 7, K1_V8 = 8, K1_AUTO = -1 };
-static int k1_variant() {
-    const char *e = getenv("MINISCHED_K1");
-    if (e && e[0] == 'v' && e[1] == '0') return K1_V0;
-    if (e && e[0] == 'v' && e[1] == '8') return K1_V8;
-    if (e && e[0] == 'v' && e[1] == '7') return K1_V7;
-    return K1_AUTO;
-}
-
-// Geometry. Rows: at most kK1MaxRpl = 30 rows per lane, spread evenly over
-// the shard's waves (no near-empty last wave, whose pods would cost a full
-// wave's). A lane of rpl consecutive names holds at most ceil(rpl/10) rows of
-// one digit, so K = ceil(rpl/10) list entries per class keep the synthetic
-// clusters on the list path; 30 rows is the most that K = 3 covers.
-// Pods: each wave sweeps a chunk of pods (a multiple of 8: pods are read and
-// reduced in groups of 8) sized for about four rounds of resident waves,
-// within [kK1WavePods, 2 kK1WavePods], and never more than one round: short
-// waves in several rounds let the dispatcher even out the SIMDs, long ones
-// amortise the tile build (profiles/r01g_geom.jsonl: 192 pods per wave at
-// 100k rows, 96 at 25k and 12.5k).
-// MINISCHED_K1_ROUNDS=r instead splits the one-round chunk r ways,
-// MINISCHED_K1_CHUNK fixes the chunk and MINISCHED_K1_RPL the rows per lane
-// (<= 32), for experiments.
-typedef void (*K1Kernel)(const uint8_t *, const uint8_t *, uint32_t, uint32_t, uint32_t, const uint2 *, uint32_t,
-                         uint32_t, unsigned long long *, uint32_t *, uint32_t);
-
-// Classes on K1's list path: bits 0..9 non-tolerating, 16..25 tolerating pods; bit 31
-// enables the per-8-pod group test in sweep_pods.
-// MINISCHED_K1_TOL=0 sends tolerating pods down the general path (tests, A/B).
-static uint32_t k1_fast_mask() {
-    const char *e = getenv("MINISCHED_K1_TOL");
-    uint32_t m = (e && atoi(e) == 0) ? 0x3FFu : 0x3FF03FFu;
-    // bit 31: K1's per-8-pod group test (MINISCHED_K1_GROUP=0 turns it off for A/B)
-    const char *g = getenv("MINISCHED_K1_GROUP");
-    if (!(g && atoi(g) == 0)) m |= 0x80000000u;
-    return m;
-}
-
-constexpr uint32_t kK1MaxRpl = 30;
-constexpr int kK1Waves = 4;  // waves per workgroup sharing one tile build (MINISCHED_K1_WAVES; profiles/r01i_k1_waves.jsonl)
-constexpr uint32_t kK1WavePods = 96;
-
-static uint32_t k1_rows_per_lane(uint32_t n_rows) {
-    if (const char *e = getenv("MINISCHED_K1_RPL")) return (uint32_t)std::min(32, std::max(1, atoi(e)));
-    const uint32_t waves = std::max(1u, cdiv(n_rows, 64u * kK1MaxRpl));
-    return std::max(1u, cdiv(n_rows, 64u * waves));
-}
-
-template <int K, bool WANT_FLAGS, int W>
-static hipError_t launch_v7(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps, uint32_t n_pods,
-                            unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
-    const K1Kernel kern = k_sweep_nunn_v7<K, WANT_FLAGS, W>;
-    static int bpc = 0;  // resident blocks per CU (one per template instance)
-    if (!bpc) {
-        int nb = 0;
-        hipError_t e =
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64 * W, 0);
-        if (e != hipSuccess) return e;
-        bpc = nb > 0 ? nb : 1;
-    }
-    const uint32_t gx = cdiv(n_rows, 64u * rpl);
-    const uint32_t resident = (uint32_t)bpc * W * (uint32_t)(num_cus > 0 ? num_cus : 256);  // waves
-    const uint32_t one_round = cdiv(cdiv(n_pods, std::max<uint32_t>(1, resident / gx)), 8) * 8;
-    // about four rounds of waves, between kK1WavePods and 2 kK1WavePods pods each
-    uint32_t chunk = std::min(one_round, std::min(2 * kK1WavePods, std::max(kK1WavePods, cdiv(one_round, 32) * 8)));
-    if (const char *r = getenv("MINISCHED_K1_ROUNDS"))
-        chunk = cdiv(cdiv(one_round, (uint32_t)std::max(1, atoi(r))), 8) * 8;
-    if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
-    hipLaunchKernelGGL(kern, dim3(gx, cdiv(n_pods, chunk * W)), dim3(64 * W), 0, s, t.flags, t.digit, n_rows,
-                       t.base, rpl, ps, n_pods, chunk, keys, flags, k1_fast_mask());
-    return hipGetLastError();
-}
-
-template <int K, bool WANT_FLAGS>
-static hipError_t launch_v7_waves(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps,
-                                  uint32_t n_pods, unsigned long long *keys, uint32_t *flags, int num_cus,
-                                  hipStream_t s) {
-    int w = kK1Waves;
-    if (const char *e = getenv("MINISCHED_K1_WAVES")) w = atoi(e);
-    if (w >= 4) return launch_v7<K, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-    if (w == 2) return launch_v7<K, WANT_FLAGS, 2>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-    return launch_v7<K, WANT_FLAGS, 1>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-}
-
-template <bool WANT_FLAGS>
-static hipError_t launch_v7_rows(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
-                                 unsigned long long *keys, uint32_t *flags, int num_cus, hipStream_t s) {
-    const uint32_t rpl = k1_rows_per_lane(n_rows);
-    if (rpl <= 20) return launch_v7_waves<2, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-    if (rpl <= 30) return launch_v7_waves<3, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-    return launch_v7_waves<4, WANT_FLAGS>(t, n_rows, rpl, ps, n_pods, keys, flags, num_cus, s);
-}
-
-// K1 v8 geometry: the v7 rows per lane; items of W chunks of kK1V8Pods pods
-// (MINISCHED_K1_CHUNK), one persistent workgroup per resident slot.
-constexpr uint32_t kK1V8Pods = 64;
-constexpr uint32_t kK1V8MinColumns = 40;
-
-static uint32_t k1_columns(uint32_t n_rows) { return cdiv(n_rows, 64u * k1_rows_per_lane(n_rows)); }
-
-template <int K, bool WANT_FLAGS, int W>
-static hipError_t launch_v8(const NodeTable &t, uint32_t n_rows, uint32_t rpl, const uint2 *ps, uint32_t n_pods,
-                            unsigned long long *keys, uint32_t *flags, uint32_t *work, int num_cus, hipStream_t s) {
-    const auto kern = k_sweep_nunn_v8<K, WANT_FLAGS, W>;
-    static int bpc = 0;  // resident blocks per CU (one per template instance)
-    if (!bpc) {
-        int nb = 0;
-        hipError_t e =
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(kern), 64 * W, 0);
-        if (e != hipSuccess) return e;
-        bpc = nb > 0 ? nb : 1;
-    }
-    uint32_t chunk = kK1V8Pods;
-    if (const char *c = getenv("MINISCHED_K1_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
-    const uint32_t n_cols = cdiv(n_rows, 64u * rpl);
-    const uint32_t items = n_cols * cdiv(n_pods, chunk * W);
-    // resident workgroups: 8 waves per SIMD, 4 SIMDs per CU (the occupancy API
-    // under-reports kernels with scratch; MINISCHED_K1_DEBUG prints both)
-    const uint32_t per_cu = std::max<uint32_t>((uint32_t)bpc, 32u / W);
-    // at least one workgroup per column: workgroup b serves column b % n_cols only, so
-    // fewer blocks than columns would leave columns unswept (small CU counts, many rows)
-    uint32_t blocks = std::min(items, per_cu * (uint32_t)(num_cus > 0 ? num_cus : 256));
-    if (const char *c = getenv("MINISCHED_K1_V8_BLOCKS")) blocks = (uint32_t)std::max(1, atoi(c));  // tests
-    blocks = std::max(blocks, std::min(items, n_cols));
-    if (getenv("MINISCHED_K1_DEBUG"))
-        fprintf(stderr, "k1 v8: api blocks/CU %d, used %u, cols %u, items %u, blocks %u, chunk %u\n", bpc, per_cu,
-                n_cols, items, blocks, chunk);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * W), 0, s, t.flags, t.digit, n_rows, t.base, rpl, ps, n_pods,
-                       chunk, keys, flags, work, n_cols, k1_fast_mask());
-    return hipGetLastError();
-}
-
-template <bool WANT_FLAGS>
-static hipError_t launch_v8_rows(const NodeTable &t, uint32_t n_rows, const uint2 *ps, uint32_t n_pods,
-                                 unsigned long long *keys, uint32_t *flags, uint32_t *work, int num_cus,
-                                 hipStream_t s) {
-    const uint32_t rpl = k1_rows_per_lane(n_rows);
-    if (rpl <= 20) return launch_v8<2, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, work, num_cus, s);
-    if (rpl <= 30) return launch_v8<3, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, work, num_cus, s);
-    return launch_v8<4, WANT_FLAGS, 4>(t, n_rows, rpl, ps, n_pods, keys, flags, work, num_cus, s);
-}
-
-hipError_t launch_sweep_nunn(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                             uint32_t seed32, unsigned long long *keys, uint32_t *flags, uint2 *pstream,
-                             uint32_t *work, int num_cus, hipStream_t s) {
-    if (n_pods == 0) return hipSuccess;
-    // pod stream + zeroed keys/flags (the sweep's atomicMax/atomicOr targets)
-    const uint32_t n_prep = n_pods + kPodStreamPad + 16u;  // + two groups of class masks past the stream
-    const int var = k1_variant();
-    const bool v8 = var == K1_V8 || (var == K1_AUTO && k1_columns(n_rows) >= kK1V8MinColumns);
-    const uint32_t n_work = v8 ? k1_columns(n_rows) : 0u;
-    uint32_t *gmask = reinterpret_cast<uint32_t *>(pstream + n_pods + kPodStreamPad);
-    hipLaunchKernelGGL(k_pod_prep, dim3(cdiv(std::max(n_prep, n_work), 256)), dim3(256), 0, s, pods, n_pods, seed32,
-                       pstream, keys, flags, work, n_work, gmask);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || n_rows == 0) return e;
-    if (k1_variant() == K1_V0) {
-        const uint32_t gx = cdiv(n_rows, kNunnTile);
-        const uint32_t chunk = pod_chunk(n_pods, gx, num_cus);
-        const dim3 grid(gx, cdiv(n_pods, chunk));
-        if (flags)
-            hipLaunchKernelGGL(k_sweep_nunn<true>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows, t.base,
-                               pods, n_pods, chunk, seed32, keys, flags);
-        else
-            hipLaunchKernelGGL(k_sweep_nunn<false>, grid, dim3(kNunnThreads), 0, s, t.flags, t.digit, n_rows,
-                               t.base, pods, n_pods, chunk, seed32, keys, flags);
-        return hipGetLastError();
-    }
-    if (v8)
-        return flags ? launch_v8_rows<true>(t, n_rows, pstream, n_pods, keys, flags, work, num_cus, s)
-                     : launch_v8_rows<false>(t, n_rows, pstream, n_pods, keys, flags, work, num_cus, s);
-    return flags ? launch_v7_rows<true>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s)
-                 : launch_v7_rows<false>(t, n_rows, pstream, n_pods, keys, flags, num_cus, s);
-}
 
 hipError_t launch_sweep_na(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, uint32_t w_nn, uint32_t w_na, unsigned long long *keys, uint32_t *fkeys,
@@ -2872,10 +2184,10 @@ hipError_t launch_sweep_na(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
 
 hipError_t launch_decode_na(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
                             const uint32_t *fkeys, uint32_t present_nodes, uint32_t seed32, uint32_t w_nn,
-                            uint32_t w_na, ms_result *out, hipStream_t s) {
+                            uint32_t w_na, ms_result *out, hipStream_t s, const uint32_t *present_dev) {
     if (n_pods == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode_na, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, pods, n_pods, keys, fkeys,
-                       present_nodes, seed32, w_nn, w_na, out);
+                       present_nodes, present_dev, seed32, w_nn, w_na, out);
     return hipGetLastError();
 }
 
@@ -3004,10 +2316,35 @@ hipError_t launch_build_drows(const NodeTable &t, uint32_t n_rows, uint32_t n_to
 uint32_t seq_max_rows() { return 64u * kSeqMaxJ * kFullWaveTile; }
 
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
-                         const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s) {
+                         const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s,
+                         const uint32_t *present_dev) {
     if (n_pods == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, pods, n_pods, keys, flags,
-                       present_nodes, out);
+                       present_nodes, present_dev, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_slices(const SliceJob *jobs, uint32_t n_jobs, hipStream_t s) {
+    if (n_jobs == 0 || n_jobs > kMaxSliceJobs) return n_jobs ? hipErrorInvalidValue : hipSuccess;
+    SliceJobs sj = {};
+    uint32_t most = 0;
+    for (uint32_t i = 0; i < n_jobs; ++i) {
+        sj.j[i] = jobs[i];
+        most = std::max(most, jobs[i].n_pods);
+    }
+    if (most == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_slices, dim3(cdiv(most, 256), n_jobs), dim3(256), 0, s, sj);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_window_in(const ms_pod_rec *pods, uint32_t n, uint32_t *ctl, ms_pod_rec *win, uint32_t w,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_seq_window_in, dim3(1), dim3(256), 0, s, pods, n, ctl, win, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_seq_window_out(const ms_result *win_res, uint32_t *ctl, ms_result *res, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_seq_window_out, dim3(1), dim3(256), 0, s, win_res, ctl, res, n);
     return hipGetLastError();
 }
 
@@ -3065,7 +2402,7 @@ hipError_t launch_seq_pack_cands(const NodeTable &t, const unsigned long long *t
 hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms_pod_rec *pods, uint32_t seed32,
                                    uint32_t n_shards, const ms_seq_cand *cands_all, const uint32_t *flags_all,
                                    ms_seq_cand *merged, uint32_t *merged_flags, ms_result *results, uint32_t *n_done,
-                                   hipStream_t s) {
+                                   hipStream_t s, const uint32_t *live) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > MS_SEQ_SHARD_BATCH_MAX || n_shards == 0 || n_shards > MS_SEQ_MAX_SHARDS) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_seq_merge_shards, dim3(n_pods), dim3(64), 0, s, n_pods, n_shards, cands_all, flags_all, merged,
@@ -3073,7 +2410,7 @@ hipError_t launch_seq_validate_rep(const NodeTable &t, uint32_t n_pods, const ms
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_seq_validate_rep, dim3(1), dim3(64), 0, s, t, n_pods, pods, seed32, merged, merged_flags,
-                       results, n_done);
+                       results, n_done, live);
     return hipGetLastError();
 }
 

@@ -121,7 +121,16 @@ class ms_info(ctypes.Structure):
         ("seq_resweep_tiles", ctypes.c_uint32),
         ("seq_recomputes", ctypes.c_uint32),
         ("_pad", ctypes.c_uint32),
+        ("comm_rank", ctypes.c_int32),
+        ("comm_world", ctypes.c_int32),
     ]
+
+
+COMM_ID_BYTES = 128  # MS_COMM_ID_BYTES (an ncclUniqueId)
+
+
+class ms_comm_id(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * COMM_ID_BYTES)]
 
 
 # Every function the header declares, with its ctypes signature.
@@ -148,6 +157,11 @@ SIGNATURES = {
     "ms_select_batch_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_seq_candidates_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "ms_seq_validate_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "ms_comm_id_create": (ctypes.c_int, [ctypes.POINTER(ms_comm_id)]),
+    "ms_comm_init": (ctypes.c_int, [_vp, ctypes.POINTER(ms_comm_id), _i32, _i32]),
+    "ms_sharded_slice": (ctypes.c_int, [_vp, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    "ms_sharded_submit": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_sharded_drain": (ctypes.c_int, [_vp, _vp]),
 }
 
 DECODE_MAX_JOBS = 8  # MS_DECODE_MAX_JOBS
@@ -200,6 +214,16 @@ class MSError(RuntimeError):
 
 def _ptr(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def comm_id_create() -> bytes:
+    """A new communicator id (rank 0 creates it and ships the bytes to every rank)."""
+    out = ms_comm_id()
+    lib = load()
+    rc = lib.ms_comm_id_create(ctypes.byref(out))
+    if rc != MS_OK:
+        raise MSError("ms_comm_id_create", rc, lib.ms_last_error(None).decode())
+    return bytes(out.internal)
 
 
 def device_count() -> int:
@@ -274,9 +298,14 @@ class Engine:
         self._check("ms_nodes_read", self.lib.ms_nodes_read(self.h, first, n, _ptr(out)))
         return out
 
-    def schedule(self, pods: np.ndarray, mode: int = MODE_BATCHED) -> np.ndarray:
+    def schedule(self, pods: np.ndarray, mode: int = MODE_BATCHED, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """ms_schedule_batch. out: a reusable RESULT array of len(pods) (the
+        caller's buffer, as a cgo caller would pass it)."""
         p = np.ascontiguousarray(pods, dtype=POD_REC)
-        out = np.zeros(len(p), dtype=RESULT)
+        if out is None:
+            out = np.zeros(len(p), dtype=RESULT)
+        elif out.dtype != RESULT or len(out) != len(p) or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous RESULT array of len(pods)")
         self._check("ms_schedule_batch", self.lib.ms_schedule_batch(self.h, len(p), _ptr(p), mode, _ptr(out)))
         return out
 
@@ -336,6 +365,29 @@ class Engine:
         self._check("ms_seq_validate_device",
                     self.lib.ms_seq_validate_device(self.h, n_pods, pods_dev, n_shards, cands_all_dev, flags_all_dev,
                                                     results_dev, n_done_dev, stream or None))
+
+    # ---- in-library multi-GPU (a communicator per job) -------------------------
+    def comm_init(self, comm_id: bytes, rank: int, world: int):
+        """Joins this context (one node shard) to the job's RCCL communicator
+        (collective over the ranks)."""
+        if len(comm_id) != COMM_ID_BYTES:
+            raise ValueError("comm_id must be MS_COMM_ID_BYTES bytes")
+        cid = ms_comm_id()
+        ctypes.memmove(ctypes.addressof(cid), comm_id, COMM_ID_BYTES)
+        self._check("ms_comm_init", self.lib.ms_comm_init(self.h, ctypes.byref(cid), rank, world))
+
+    def sharded_slice(self, n_pods: int):
+        """(first, count): the pod slice of an n_pods batch this rank decodes."""
+        a, b = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check("ms_sharded_slice", self.lib.ms_sharded_slice(self.h, n_pods, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def sharded_submit(self, n_pods, pods_dev, results_dev, stream=0):
+        self._check("ms_sharded_submit",
+                    self.lib.ms_sharded_submit(self.h, n_pods, pods_dev, results_dev or None, stream or None))
+
+    def sharded_drain(self, stream=0):
+        self._check("ms_sharded_drain", self.lib.ms_sharded_drain(self.h, stream or None))
 
     def schedule_sequential_device(self, n_pods, pods_dev, results_dev, stream=0):
         self._check(

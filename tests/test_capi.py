@@ -51,11 +51,19 @@ def test_struct_sizes_match_header():
     assert _lib.POD_REC.itemsize == 40
     assert _lib.RESULT.itemsize == 24
     assert ctypes.sizeof(_lib.ms_config) == 32
+    assert ctypes.sizeof(_lib.ms_info) == 56
+    assert ctypes.sizeof(_lib.ms_comm_id) == _lib.COMM_ID_BYTES == 128
+
+
+def test_library_links_rccl():
+    # the node-sharded cycles run their collectives in-library (ms_comm.cpp)
+    out = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "librccl.so" in out
 
 
 def test_abi_version_and_no_device_error_path():
     lib = _lib.load()
-    assert lib.ms_abi_version() == 2
+    assert lib.ms_abi_version() == 3
     if _lib.device_count() > 0:
         pytest.skip("a device is visible; the no-device path is exercised on CPU hosts")
     cfg = _lib.ms_config(0, 0, 16, 0, 64, (ctypes.c_uint16 * 2)(), 1)

@@ -68,22 +68,9 @@ def test_readme_scenario_gpu(oracle):
         assert e.read(9, 1)["pod_count"][0] == 1  # assume-on-select
 
 
-@pytest.fixture(params=["pp", "v7", "v7w2", "v7w4", "v7w4-gen", "v8", "v0"])
-def k1_variant(request, monkeypatch):
-    # every NU+NN sweep form stays bit-exact: pp (the per-pair bit-sliced production kernel),
-    # the class-indexed v7 with 1, 2 or 4 waves per workgroup sharing one tile build (and with
-    # tolerating pods on the general path: -gen), the persistent v8, and v0 (hash every pair),
-    # the plain cross-check
-    v = request.param
-    monkeypatch.setenv("MINISCHED_K1", v[:2])
-    monkeypatch.setenv("MINISCHED_K1_WAVES", v[3] if "w" in v else "1")
-    monkeypatch.setenv("MINISCHED_K1_TOL", "0" if v.endswith("-gen") else "1")
-    return v
-
-
 @pytest.mark.parametrize("n_nodes", [1, 15, 16, 17, 1000, 2047, 2048, 2049, 4096, 8193, 12345])
 @pytest.mark.parametrize("n_pods", [1, 63, 64, 65, 700])
-def test_nunn_random_sizes(oracle, k1_variant, n_nodes, n_pods):
+def test_nunn_random_sizes(oracle, n_nodes, n_pods):
     seed = 1000 + n_nodes * 7 + n_pods
     nr = synth.nodes(n_nodes, seed=seed)
     pr = synth.pods(n_pods, seed=seed)
@@ -95,13 +82,14 @@ def test_nunn_random_sizes(oracle, k1_variant, n_nodes, n_pods):
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 
-@pytest.mark.parametrize("rpl", [None, "1", "7", "20", "21", "28", "29", "30", "31", "32"])
+@pytest.mark.parametrize("waves", [None, "1", "2", "4", "16"])
 @pytest.mark.parametrize("n_nodes,node_base", [(12_500, 37_500), (25_000, 0), (3001, 99_000)])
-def test_nunn_rows_per_lane(oracle, monkeypatch, k1_variant, rpl, n_nodes, node_base):
-    # K1's row geometry (rows per lane, balanced waves over a shard, byte/dword/vector
-    # tile loads) and the global-ordinal arithmetic of a shard that starts at node_base
-    if rpl is not None:
-        monkeypatch.setenv("MINISCHED_K1_RPL", rpl)
+def test_nunn_shard_geometry(oracle, monkeypatch, waves, n_nodes, node_base):
+    # K1 pp's workgroup geometry (waves per workgroup holding a shard's groups, the
+    # round-robin deal of groups over waves) and the global-ordinal arithmetic of a
+    # shard that starts at node_base
+    if waves is not None:
+        monkeypatch.setenv("MINISCHED_PP_WAVES", waves)
     seed = 77 + n_nodes
     nr = synth.nodes(n_nodes, seed=seed, start=node_base)
     pr = synth.pods(1000, seed=seed)
@@ -114,9 +102,8 @@ def test_nunn_rows_per_lane(oracle, monkeypatch, k1_variant, rpl, n_nodes, node_
 
 @pytest.mark.parametrize("n_nodes,node_base", [(100_000, 0), (76_800, 12_345), (50_000, 50_000)])
 def test_nunn_default_kernel_large_shards(oracle, monkeypatch, n_nodes, node_base):
-    # the default K1 choice (persistent v8 from 40 node columns up, v7 below) at shard sizes
-    # on both sides of the switch
-    monkeypatch.delenv("MINISCHED_K1", raising=False)
+    # K1 pp at shard sizes around one 16-wave workgroup's 122,880 rows and a shard
+    # that starts at a non-zero ordinal
     seed = 5 + n_nodes
     nr = synth.nodes(n_nodes, seed=seed, start=node_base)
     pr = synth.pods(2000, seed=seed)
@@ -129,9 +116,9 @@ def test_nunn_default_kernel_large_shards(oracle, monkeypatch, n_nodes, node_bas
 
 @pytest.mark.parametrize("layout", ["runs", "skewed", "single"])
 def test_nunn_uneven_digits(oracle, layout):
-    # K1 v7 keeps at most K rows per (lane, digit) in its class lists; clusters whose
-    # name digits do not cycle overflow them and take the general path for that class
-    # (runs of equal digits, a skewed digit mix, every name ending in the same digit)
+    # K1 pp's three fast slots cover at most 3 rows of one digit per 30-row group; clusters
+    # whose name digits do not cycle set the group's "over" plane and take the bit-scan
+    # path (runs of equal digits, a skewed digit mix, every name ending in the same digit)
     n_nodes = 9000
     seed = {"runs": 11, "skewed": 12, "single": 13}[layout]
     rng = np.random.default_rng(seed)
@@ -149,7 +136,7 @@ def test_nunn_uneven_digits(oracle, layout):
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 
-def test_nunn_edge_cases(oracle, k1_variant):
+def test_nunn_edge_cases(oracle):
     pr = synth.pods(130, seed=4)
     # empty table: FitError with an empty mask
     with Engine(max_nodes=64) as e:
@@ -178,7 +165,7 @@ def test_nunn_edge_cases(oracle, k1_variant):
         assert e.info().present_nodes == 5000
 
 
-def test_config_b_exact_sequential(oracle, k1_variant):
+def test_config_b_exact_sequential(oracle):
     # BASELINE config B: 5k nodes x 10k pods, NU+NN, exact sequential
     nr = synth.nodes(5000, seed=1)
     pr = synth.pods(10000, seed=1)
@@ -189,7 +176,7 @@ def test_config_b_exact_sequential(oracle, k1_variant):
         assert_table_equal(e, o["cols"], 5000)
 
 
-def test_config_c_shape_prefix(oracle, k1_variant):
+def test_config_c_shape_prefix(oracle):
     # config C nodes (100k) against a 1k-pod prefix, plus a 20k-pod run
     # checked on a strided sample
     nr = synth.nodes(100_000, seed=1)
@@ -249,6 +236,21 @@ def test_resource_batched(oracle, n_nodes, n_pods):
     with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed) as e:
         assert_same(e.schedule(pr, MODE_BATCHED), o)
         assert_table_equal(e, o["cols"], n_nodes)
+
+
+@pytest.mark.parametrize("max_batch", [1 << 16, 8192])
+def test_resource_batched_large_call(oracle, max_batch):
+    # a MODE_BATCHED call of the resource-aware set decides every pod on
+    # the same node state, whatever the call size: 40k pods used to be split into chunks
+    # whose binds landed before the next chunk was swept (and max_batch chunks likewise)
+    nr = synth.nodes(3000, seed=91, resources=True)
+    pr = synth.pods(40_000, seed=91, resources=True)
+    nr["req_milli_cpu"] = nr["alloc_milli_cpu"] // 3
+    nr["nonzero_milli_cpu"] = nr["req_milli_cpu"]
+    o = oracle.schedule_batched_commit(nr, pr, 1, seed=91)
+    with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=91, max_batch=max_batch) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+        assert_table_equal(e, o["cols"], 3000)
 
 
 @pytest.mark.parametrize("n_nodes,n_pods", [(1, 5), (50, 400), (700, 5000), (3000, 12000)])
@@ -493,21 +495,6 @@ def test_stream_ordering_deltas_binds_reads(oracle):
     keep = ~touched
     assert np.array_equal(t["pod_count"][keep], placed[keep])
 
-
-def test_v8_covers_every_column_with_few_blocks(oracle, monkeypatch):
-    # K1 v8 serves column b % n_cols from workgroup b; a launch capped below
-    # the column count (few CUs, many rows) must still sweep every column
-    monkeypatch.setenv("MINISCHED_K1", "v8")
-    monkeypatch.setenv("MINISCHED_K1_V8_BLOCKS", "7")
-    n = 60_000  # 32 columns of 1920 rows
-    nr = synth.nodes(n, seed=14)
-    pr = synth.pods(900, seed=14)
-    o = oracle.schedule(nr, pr, seed=14)
-    with engine_with(nr, seed=14) as e:
-        assert_same(e.schedule(pr, MODE_BATCHED), o)
-
-
-# ---- MS_PLUGINS_NU_NN_NA: weights + the in-loop NormalizeScore hook ----
 
 @pytest.mark.parametrize("weights", [(1, 1), (2, 3), (10, 10)])
 @pytest.mark.parametrize("n_nodes,n_pods", [(1, 5), (17, 64), (300, 200), (5000, 700), (40_000, 300)])

@@ -299,3 +299,244 @@ def test_sharded_sequential_class_rccl(oracle):
                         plugin_set=1, mode=1, seed=5)
     _same(res, o, 0, 9000, "rccl seq")
     assert np.array_equal(cnt, o["cols"].pod_count)
+
+
+# ---- multi-GPU inside the library (ms_comm_*): a 1-rank RCCL communicator -----
+# RCCL refuses two ranks of one communicator on the same GPU ("Duplicate GPU
+# detected", tools/probe_rccl_dup.py), so on a 1-GPU box the in-library path
+# runs as a 1-rank communicator: the same submit / grouped reduce-scatter /
+# slice decode / all-gather code with G = 1. The G > 1 slicing and combine
+# arithmetic is checked at full size by the multi-context tests below.
+
+def _comm_engine(nr, plugin_set, seed, node_base=0, **kw):
+    from minisched_amd import _lib, sharded
+
+    e = _lib.Engine(max_nodes=len(nr), plugin_set=plugin_set, node_base=node_base, seed=seed, **kw)
+    e.upsert(np.arange(node_base, node_base + len(nr)), nr)
+    e.flush()
+    sharded.init_comm(e)  # no process group: a 1-rank communicator
+    info = e.info()
+    assert (info.comm_rank, info.comm_world) == (0, 1)
+    return e
+
+
+@pytest.mark.parametrize("plugin_set", [0, 1, 2])
+def test_library_sharded_cycle_1rank(oracle, plugin_set):
+    # ShardedCycle on a communicator: ms_sharded_submit / ms_sharded_drain, pipelined
+    # (more steps than the depth), every plugin set's combine (keys, filter bytes,
+    # NodeAffinity anchors, the listed-node flag)
+    import torch
+
+    from minisched_amd import _lib, sharded
+
+    seed = 60 + plugin_set
+    res_set, zones = plugin_set == 1, plugin_set == 2
+    nr = synth.nodes(9000, seed=seed, resources=res_set, zones=zones)
+    pr = synth.pods(3001, seed=seed, resources=res_set, zones=zones)
+    pr["name_digit"][::17] = -1
+    if plugin_set == 2:
+        o = oracle.schedule_na(nr, pr, seed=seed, literal=False)
+    else:
+        o = oracle.schedule(nr, pr, plugin_set=plugin_set, seed=seed)
+    dev = torch.device("cuda:0")
+    e = _comm_engine(nr, plugin_set, seed)
+    try:
+        stream = torch.cuda.Stream(device=dev)
+        pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+        cyc = sharded.ShardedCycle(e, len(nr), len(pr), pods, stream)
+        assert cyc.library and (cyc.a, cyc.b) == (0, len(pr))
+        for _ in range(7):
+            cyc.step()
+        cyc.finish()
+        stream.synchronize()
+        res = cyc.results.cpu().numpy().view(_lib.RESULT)
+        with pytest.raises(_lib.MSError):  # single-shard call on a sharded context
+            e.select_batch_device(len(pr), pods.data_ptr(), cyc.results.data_ptr(), stream.cuda_stream)
+    finally:
+        e.close()
+    _same(res, o, 0, len(pr), "library cycle")
+
+
+def test_library_schedule_batch_1rank(oracle):
+    # ms_schedule_batch on a communicator: every pod's result on every rank (all-gather of
+    # the slices), binds committed on the rank's own shard; NU+NN batched and sequential,
+    # the resource-aware set batched (one state for the whole call) and exact sequential
+    # (the device-cursor windows), the node tables after the binds
+    from minisched_amd import _lib
+
+    nr = synth.nodes(4000, seed=71)
+    pr = synth.pods(5000, seed=71)
+    e = _comm_engine(nr, 0, 71)
+    try:
+        _same(e.schedule(pr, _lib.MODE_BATCHED), oracle.schedule(nr, pr, seed=71), 0, len(pr), "NU+NN batched")
+        _same(e.schedule(pr, _lib.MODE_SEQUENTIAL), oracle.schedule(nr, pr, seed=71), 0, len(pr), "NU+NN seq")
+        assert e.read(0, 4000)["pod_count"].sum() == 2 * (oracle.schedule(nr, pr, seed=71)["code"] == 0).sum()
+    finally:
+        e.close()
+    nr = synth.nodes(3000, seed=72, resources=True)
+    pr = synth.pods(9000, seed=72, resources=True)
+    pr["name_digit"][::23] = -1
+    ob = oracle.schedule_batched_commit(nr, pr, 1, seed=72)
+    e = _comm_engine(nr, 1, 72)
+    try:
+        _same(e.schedule(pr, _lib.MODE_BATCHED), ob, 0, len(pr), "NRF batched")
+        t = e.read(0, 3000)
+        assert np.array_equal(t["pod_count"], ob["cols"].pod_count)
+    finally:
+        e.close()
+    os_ = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=72)
+    assert (os_["code"] == 2).sum() > 0  # saturation reached
+    e = _comm_engine(nr, 1, 72)
+    try:
+        _same(e.schedule(pr, _lib.MODE_SEQUENTIAL), os_, 0, len(pr), "NRF sequential")
+        t = e.read(0, 3000)
+        for k_dev, k_or in (("pod_count", "pod_count"), ("req_milli_cpu", "req_cpu"), ("nonzero_memory", "nz_mem")):
+            assert np.array_equal(t[k_dev], getattr(os_["cols"], k_or)), k_dev
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("window", ["1", "7", "128", "256"])
+def test_library_sequential_device_cursor(oracle, monkeypatch, window):
+    # ms_schedule_sequential_device on a communicator: windows of W pods issued back to
+    # back with the queue cursor on the device (window 1: every pod its own window;
+    # windows that stop early at an undecidable pod make the host loop run more rounds)
+    import torch
+
+    from minisched_amd import _lib, sharded
+
+    monkeypatch.setenv("MINISCHED_SHARD_SEQ_BATCH", window)
+    seed = 80 + int(window)
+    nr = synth.nodes(700, seed=seed, resources=True)
+    pr = synth.pods(2600, seed=seed, resources=True)
+    pr["name_digit"][::31] = -1
+    o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed)
+    dev = torch.device("cuda:0")
+    e = _comm_engine(nr, 1, seed)
+    try:
+        stream = torch.cuda.Stream(device=dev)
+        pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+        seq = sharded.ShardedSequential(e, len(pr), pods, stream)
+        assert seq.library
+        res = seq.run()
+        stream.synchronize()
+        res = res.cpu().numpy().view(_lib.RESULT)
+        t = e.read(0, len(nr))
+    finally:
+        e.close()
+    _same(res, o, 0, len(pr), f"window {window}")
+    assert np.array_equal(t["pod_count"], o["cols"].pod_count)
+
+
+# ---- full-size node-sharded parity: the bench's N > 1 shard shapes ----------
+# One context per rank on one GPU: each sweeps ALL pods against its node shard
+# (ms_sweep_device, K1 pp) into a key buffer padded to G * ceil(P/G); the
+# reduce-scatter (uint64 MAX) is emulated with torch; each rank decodes its own
+# pod slice (ms_decode_device, the cluster's present count). Every pod must equal
+# the OpenMP oracle over the whole cluster (config C's shard shapes).
+
+def _sharded_c(oracle, n_nodes, n_pods, G, seed=1):
+    import torch
+
+    from minisched_amd import _lib, sharded
+
+    nr = synth.nodes(n_nodes, seed=seed)
+    pr = synth.pods(n_pods, seed=seed)
+    o = oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=16)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    sp = s.cuda_stream
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    pp = sharded.padded_pods(n_pods, G)
+    per = pp // G
+    keys = []
+    for r in range(G):
+        lo, hi = sharded.shard_bounds(n_nodes, r, G)
+        with _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=seed) as e:
+            e.upsert(np.arange(lo, hi), nr[lo:hi])
+            e.flush()
+            k = torch.zeros(pp, dtype=torch.int64, device=dev)
+            e.sweep_device(n_pods, pods.data_ptr(), k.data_ptr(), 0, sp)
+            s.synchronize()
+            keys.append(k)
+    with torch.cuda.stream(s):
+        comb = torch.stack(keys).max(0).values  # the reduce-scatter's MAX, all slices at once
+    for r in range(G):
+        a, b = sharded.pod_slice(n_pods, r, G)
+        lo, hi = sharded.shard_bounds(n_nodes, r, G)
+        with _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=seed) as e:
+            res = torch.empty(max(1, b - a) * 24, dtype=torch.uint8, device=dev)
+            if b > a:
+                e.decode_device(b - a, pods.data_ptr() + 40 * a, comb.data_ptr() + 8 * r * per, 0, n_nodes,
+                                res.data_ptr(), sp)
+            s.synchronize()
+            _same(res.cpu().numpy().view(_lib.RESULT)[: b - a], o, a, b, f"G={G} rank {r}")
+    assert np.array_equal(comb[:n_pods].cpu().numpy().view(np.uint64), o["key"])
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_config_c_node_sharded_full(oracle, G):
+    # strong scaling: 100k nodes x 100k pods split over G node shards
+    _sharded_c(oracle, 100_000, 100_000, G)
+
+
+def test_config_c_weak_shard_full(oracle):
+    # weak scaling at G = 8: every rank sweeps 800k pods against its 12.5k-row shard
+    _sharded_c(oracle, 100_000, 800_000, 8)
+
+
+def test_config_e_four_contexts_full():
+    # config E (50k nodes x 200k pods, exact sequential) over 4 node shards through
+    # ms_seq_candidates_device / ms_seq_validate_device, against the committed fixture
+    import hashlib
+
+    import torch
+
+    from minisched_amd import _lib, sharded
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    fx = np.load(os.path.join(here, "golden", "config_e_full_seed1.npz"))
+    N, P, G, B = 50_000, 200_000, 4, 128
+    nr = synth.nodes(N, seed=1, resources=True)
+    pr = synth.pods(P, seed=1, resources=True)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    sp = s.cuda_stream
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    engines, cuts = [], [sharded.shard_bounds(N, r, G) for r in range(G)]
+    for lo, hi in cuts:
+        e = _lib.Engine(max_nodes=hi - lo, plugin_set=_lib.PLUGINS_NU_NRF_NN_LA, node_base=lo, seed=1)
+        e.upsert(np.arange(lo, hi), nr[lo:hi])
+        engines.append(e)
+    cb = _lib.SEQ_CAND.itemsize * _lib.SEQ_TOPK
+    cands = [torch.zeros(B * cb, dtype=torch.uint8, device=dev) for _ in range(G)]
+    flags = [torch.zeros(B, dtype=torch.int32, device=dev) for _ in range(G)]
+    res = [torch.zeros(P * 24, dtype=torch.uint8, device=dev) for _ in range(G)]
+    done = torch.zeros(G, dtype=torch.int32, device=dev)
+    a = 0
+    try:
+        while a < P:
+            nb = min(B, P - a)
+            for g, e in enumerate(engines):
+                e.seq_candidates_device(nb, pods.data_ptr() + 40 * a, cands[g].data_ptr(), flags[g].data_ptr(), sp)
+            with torch.cuda.stream(s):
+                call = torch.cat([c[: nb * cb] for c in cands])
+                fall = torch.cat([f[:nb] for f in flags])
+            for g, e in enumerate(engines):
+                e.seq_validate_device(nb, pods.data_ptr() + 40 * a, G, call.data_ptr(), fall.data_ptr(),
+                                      res[g].data_ptr() + 24 * a, done.data_ptr() + 4 * g, sp)
+            s.synchronize()
+            nd = done.cpu().numpy()
+            assert (nd == nd[0]).all() and nd[0] >= 1, nd
+            a += int(nd[0])
+        tables = np.concatenate([e.read(lo, hi - lo) for e, (lo, hi) in zip(engines, cuts)])
+    finally:
+        for e in engines:
+            e.close()
+    o = {k: fx[k] for k in ("node", "code", "score", "mask")}
+    for g in range(G):
+        _same(res[g].cpu().numpy().view(_lib.RESULT), o, 0, P, f"E shard {g}")
+    h = hashlib.sha256()
+    for k in ("pod_count", "req_milli_cpu", "req_memory", "nonzero_milli_cpu", "nonzero_memory"):
+        h.update(np.ascontiguousarray(tables[k], dtype=np.int64).tobytes())
+    assert h.hexdigest() == str(fx["table_sha256"])

@@ -310,3 +310,74 @@ def test_node_sharded_sequential_protocol_gloo(oracle, world, n_nodes, n_pods, b
     req = np.concatenate([g[4] for g in got])
     nzm = np.concatenate([g[5] for g in got])
     assert np.array_equal(cnt, cols.pod_count) and np.array_equal(req, cols.req_cpu) and np.array_equal(nzm, cols.nz_mem)
+
+
+def _na_anchors(nr, pr, lo, hi):
+    """NodeAffinity normalise anchors of the shard [lo, hi) (minisched_gpu.h
+    ms_sweep_device, MS_PLUGINS_NU_NN_NA): per pod, over the shard's feasible nodes
+    with a non-zero raw NodeAffinity score, max of ((0xFFFFF - ordinal) << 1 | NN
+    match) + 1 — the first such node in LIST order; 0 = none."""
+    out = np.zeros(len(pr), dtype=np.uint32)
+    ords = np.arange(lo, hi)
+    for j in range(len(pr)):
+        p = pr[j]
+        feas = (nr["unschedulable"][lo:hi] == 0) | (p["tolerates_unschedulable"] != 0)
+        hit = feas & (p["pref_zone"] != 0) & (nr["zone"][lo:hi] == p["pref_zone"])
+        if hit.any():
+            i = int(np.argmax(hit))
+            nn = int(nr["name_digit"][lo + i] == p["name_digit"])
+            out[j] = (((0xFFFFF - int(ords[i])) << 1) | nn) + 1
+    return out
+
+
+def _na_worker(rank, world, port, n_nodes, n_pods, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nr = synth.nodes(n_nodes, seed=21, zones=True)
+    pr = synth.pods(n_pods, seed=21, zones=True)
+    lo, hi = sharded.shard_bounds(n_nodes, rank, world)
+    pp = sharded.padded_pods(n_pods, world)
+    flags = torch.zeros(pp, dtype=torch.int32)
+    flags[:n_pods] = torch.from_numpy(_na_anchors(nr, pr, lo, hi).astype(np.int32))
+    keys = torch.zeros(pp, dtype=torch.int64)
+    kout = torch.zeros(pp // world, dtype=torch.int64)
+    fout = torch.zeros(pp // world, dtype=torch.int32)
+    sharded.combine_scatter_(keys, kout, flags, fout, flags_op=sharded.FLAGS_U32)
+    a, b = sharded.pod_slice(n_pods, rank, world)
+    q.put((rank, a, b, fout.numpy().astype(np.uint32)[: b - a].copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_na_anchor_combine_gloo(world):
+    # ADVICE r2 (medium): NodeAffinity anchors combine with an element-wise 32-bit MAX;
+    # a byte-wise MAX mixes bytes of different shards' anchors
+    n_nodes, n_pods = 600, 200
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_na_worker, args=(r, world, port, n_nodes, n_pods, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nr = synth.nodes(n_nodes, seed=21, zones=True)
+    pr = synth.pods(n_pods, seed=21, zones=True)
+    full = _na_anchors(nr, pr, 0, n_nodes)
+    for rank, a, b, fl in got:
+        assert np.array_equal(fl, full[a:b]), f"rank {rank}"
+    # the byte-wise form really differs on these inputs
+    per_shard = [_na_anchors(nr, pr, *sharded.shard_bounds(n_nodes, r, world)) for r in range(world)]
+    bytewise = np.max(np.stack([s.view(np.uint8).reshape(-1, 4) for s in per_shard]), 0).copy().view(np.uint32)[:, 0]
+    assert (bytewise != full).any()
+
+
+def test_flags_op_per_plugin_set():
+    from minisched_amd import _lib
+
+    assert sharded.flags_op_for(_lib.PLUGINS_NU_NN) is None
+    assert sharded.flags_op_for(_lib.PLUGINS_NU_NRF_NN_LA) == sharded.FLAGS_BYTES
+    assert sharded.flags_op_for(_lib.PLUGINS_NU_NN_NA) == sharded.FLAGS_U32

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""K1 pp at config C on three node-naming layouts.
+
+  cycling : node{i} at ordinal i (digit = i % 10, the synthetic default)
+  iid     : digits i.i.d. uniform 0..9 (names unrelated to ordinals)
+  perm    : ordinal i holds node{perm[i]} (informer Add order != name order)
+
+Each: mean device time of the fused single-launch cycle (ms_select_batch_device)
+over K launches, the fraction of 30-row groups whose "over" plane is set (the
+bit-scan path), and parity of every pod against the OpenMP oracle.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def layouts(n, seed):
+    from minisched_amd import synth
+
+    base = synth.nodes(n, seed=seed)
+    rng = np.random.default_rng(12345)
+    iid = base.copy()
+    iid["name_digit"] = rng.integers(0, 10, n).astype(np.uint8)
+    perm = base.copy()
+    perm["name_digit"] = (rng.permutation(n) % 10).astype(np.uint8)
+    return {"cycling": base, "iid": iid, "perm": perm}
+
+
+def over_frac(nr):
+    d = nr["name_digit"].astype(np.int64)
+    g = len(d) // 30
+    d = d[: g * 30].reshape(g, 30)
+    cnt = np.stack([(d == v).sum(1) for v in range(10)], 1)
+    return float((cnt.max(1) > 3).mean())
+
+
+def main():
+    import torch
+
+    import _oracle  # checker only
+    from minisched_amd import _lib, synth
+
+    N, P, K = 100_000, 100_000, int(os.environ.get("PROBE_REPS", 20))
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pr = synth.pods(P, seed=1)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    out = {}
+    for name, nr in layouts(N, 1).items():
+        with _lib.Engine(max_nodes=N, seed=1) as e:
+            e.upsert(np.arange(N), nr)
+            e.flush()
+            run = lambda: e.select_batch_device(P, pods.data_ptr(), res.data_ptr(), s.cuda_stream)
+            run()
+            s.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(K):
+                run()
+            e1.record(s)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / K
+            got = res.cpu().numpy().view(_lib.RESULT)
+        t0 = time.perf_counter()
+        o = _oracle.schedule_nunn_omp(nr, pr, seed=1, threads=16)
+        ok = all(np.array_equal(got[a].astype(np.int64), o[b].astype(np.int64))
+                 for a, b in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")))
+        out[name] = {"ms": ms, "evals_per_s": N * P / (ms * 1e-3), "over_group_frac": over_frac(nr),
+                     "parity": ok, "oracle_s": time.perf_counter() - t0}
+        print(name, json.dumps(out[name]), flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
