@@ -175,31 +175,40 @@ def timed(fn, stream, reps):
     return a.elapsed_time(b) / reps
 
 
-def e2e_host(eng, pods_np, n_nodes, world=1):
+def e2e_host(eng, pods_np, n_nodes, world=1, compact=False):
     """SURVEY §8(d) / BASELINE.md §2 pods/s: ms_schedule_batch on host arrays (H2D
     of the pods, the cycle, bind commit, D2H of the results), 1 warm-up then the
-    median of 5. With N > 1 the call is collective over the in-library
-    communicator: every rank passes the same pods and receives every result."""
+    median of 5; compact=True: ms_schedule_batch_compact (8 B per pod each way).
+    With N > 1 the call is collective over the in-library communicator: every
+    rank passes the same pods and receives every result."""
     import torch.distributed as dist
 
     from minisched_amd import _lib
 
-    out = np.zeros(len(pods_np), dtype=_lib.RESULT)
-    eng.schedule(pods_np, _lib.MODE_BATCHED, out=out)
+    if compact:
+        pods_np = _lib.compact_pods(pods_np)
+        out = np.zeros(len(pods_np), dtype=_lib.RESULT_COMPACT)
+        call = lambda: eng.schedule_compact(pods_np, _lib.MODE_BATCHED, out=out)  # noqa: E731
+    else:
+        out = np.zeros(len(pods_np), dtype=_lib.RESULT)
+        call = lambda: eng.schedule(pods_np, _lib.MODE_BATCHED, out=out)  # noqa: E731
+    call()
     ts = []
     for _ in range(5):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        eng.schedule(pods_np, _lib.MODE_BATCHED, out=out)
+        call()
         ts.append(time.perf_counter() - t0)
     ms = float(np.median(ts)) * 1e3
     P = len(pods_np)
     return {"ms_median": ms, "pods_per_s": P / (ms * 1e-3), "evals_per_s": P * n_nodes / (ms * 1e-3),
             "runs": [t * 1e3 for t in ts],
-            "includes": "ms_schedule_batch: H2D pods (pageable host array), filter+score+selectHost+decode"
+            "includes": ("ms_schedule_batch_compact: H2D of 8 B pods" if compact else
+                         "ms_schedule_batch: H2D of 40 B pods")
+                        + " (pageable host array), filter+score+selectHost+decode"
                         + (", reduce-scatter + all-gather over the communicator" if world > 1 else "")
-                        + ", bind commit, D2H results into the host array"}
+                        + ", bind commit, D2H of " + ("8" if compact else "24") + " B results into the host array"}
 
 
 def load_profile(path, n_local, n_pods):
@@ -315,10 +324,11 @@ def main():
     extras = {}
     if not args.no_extras:
         # SURVEY §8(d) pods/s: ms_schedule_batch on host arrays (collective with N > 1)
-        try:
-            extras["e2e"] = e2e_host(eng, pods_np, N, world)
-        except Exception as ex:  # (reported, never fatal to the headline line)
-            extras["e2e"] = {"error": repr(ex)[:300]}
+        for key, compact in (("e2e_compact", True), ("e2e", False)):
+            try:
+                extras[key] = e2e_host(eng, pods_np, N, world, compact=compact)
+            except Exception as ex:  # (reported, never fatal to the headline line)
+                extras[key] = {"error": repr(ex)[:300]}
 
     if rank == 0:
         ms_step = elapsed * 1e3 / args.steps
@@ -382,7 +392,7 @@ def main():
             },
             # pods/s = ms_schedule_batch wall time on host arrays (e2e); the
             # device-resident step rate separately
-            "pods_per_s": (extras.get("e2e") or {}).get("pods_per_s"),
+            "pods_per_s": (extras.get("e2e_compact") or {}).get("pods_per_s"),
             "device_pods_per_s": P * args.steps / elapsed,
             "device_ms_per_step": step_dev_ms,
             "pods_scheduled": ok,

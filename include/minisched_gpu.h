@@ -116,6 +116,25 @@ typedef struct ms_result {
     uint32_t _pad;
 } ms_result;
 
+/* Compact records for the plugin sets that read no resources (MS_PLUGINS_NU_NN,
+ * MS_PLUGINS_NU_NN_NA): 8 bytes each way instead of 40 + 24, for
+ * ms_schedule_batch_compact. ms_pod_compact is the first 8 bytes of ms_pod_rec;
+ * its resource requests are zero (a bind adds one pod to len(NodeInfo.Pods)). */
+typedef struct ms_pod_compact {
+    uint32_t ordinal;
+    int8_t name_digit;
+    uint8_t tolerates_unschedulable;
+    uint8_t pref_zone;
+    uint8_t pref_weight;
+} ms_pod_compact;
+
+typedef struct ms_result_compact {
+    int32_t node;        /* global ordinal; -1 if none                              */
+    uint16_t score;      /* summed score (< 2048)                                   */
+    uint8_t code;        /* MS_CODE_*                                               */
+    uint8_t plugin_mask; /* MS_MASK_* when code == MS_CODE_UNSCHEDULABLE, else 0     */
+} ms_result_compact;
+
 typedef struct ms_config {
     int32_t device;      /* HIP device ordinal (within HIP_VISIBLE_DEVICES)     */
     int32_t plugin_set;  /* MS_PLUGINS_*                                        */
@@ -174,6 +193,11 @@ int ms_nodes_read(ms_ctx *ctx, uint32_t first, uint32_t n, ms_node_rec *out);
  * the next pod is decided (bit-exact to the one-at-a-time loop). */
 int ms_schedule_batch(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode,
                       ms_result *out);
+
+/* ms_schedule_batch with compact records (MS_PLUGINS_NU_NN / _NU_NN_NA only):
+ * the same cycle, binds and results, with 8 B per pod over PCIe each way. */
+int ms_schedule_batch_compact(ms_ctx *ctx, uint32_t n_pods, const ms_pod_compact *pods, int32_t mode,
+                              ms_result_compact *out);
 
 /* Assume / forget for the live scheduler (upstream cache.AssumePod/ForgetPod):
  * add / remove one pod's requests on a node. */

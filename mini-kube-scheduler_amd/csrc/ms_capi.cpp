@@ -49,6 +49,7 @@ void free_all(ms_ctx *c) {
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
+                   c->d_podc, c->d_resc,
                    c->d_merged, c->d_merged_flags, c->d_drow};
     for (void *p : dev)
         if (p) (void)hipFree(p);
@@ -761,6 +762,46 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
             std::memcpy(out + s0, c->h_res, sizeof(ms_result) * nb);
         }
     }
+    return MS_OK;
+}
+
+int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods, int32_t mode, ms_result_compact *out) {
+    if (!valid_ctx(c) || (n && (!pods || !out))) return MS_E_INVAL;
+    if (mode != MS_MODE_BATCHED && mode != MS_MODE_SEQUENTIAL) return fail(c, MS_E_INVAL, "unknown mode");
+    if (!plugins_stateless(c))
+        return fail(c, MS_E_INVAL, "ms_schedule_batch_compact: the resource-aware set needs ms_schedule_batch");
+    if (n == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    rc = c->comm ? comm_stage(c, n) : ensure_stage(c, n);
+    if (rc) return rc;
+    if (n > c->compact_cap) {
+        if (c->d_podc) (void)hipFree(c->d_podc);
+        if (c->d_resc) (void)hipFree(c->d_resc);
+        c->d_podc = nullptr;
+        c->d_resc = nullptr;
+        c->compact_cap = 0;
+        if (hipMalloc((void **)&c->d_podc, sizeof(ms_pod_compact) * n) != hipSuccess ||
+            hipMalloc((void **)&c->d_resc, sizeof(ms_result_compact) * n) != hipSuccess)
+            return fail(c, MS_E_OOM, "compact staging");
+        c->compact_cap = n;
+    }
+    const hipStream_t s = c->stream;
+    // 8 B per pod in and out over PCIe; widened / narrowed on the device
+    MS_HIP(c, hipMemcpyAsync(c->d_podc, pods, sizeof(ms_pod_compact) * n, hipMemcpyHostToDevice, s));
+    MS_HIP(c, launch_pods_widen(c->d_podc, n, c->d_pods, s));
+    if (c->comm) {
+        rc = comm_cycle_staged(c, n, mode);
+    } else {
+        ++c->ctx_seq;  // binds write the table on the context stream
+        rc = select_locked(c, n, c->d_pods, c->d_res, s, 1);  // (stateless sets: sequential == batched)
+    }
+    if (rc) return rc;
+    MS_HIP(c, launch_results_narrow(c->d_res, n, c->d_resc, s));
+    MS_HIP(c, hipMemcpyAsync(out, c->d_resc, sizeof(ms_result_compact) * n, hipMemcpyDeviceToHost, s));
+    MS_HIP(c, hipStreamSynchronize(s));
     return MS_OK;
 }
 

@@ -330,18 +330,29 @@ void comm_free(ms_ctx *c) {
     c->comm = nullptr;
 }
 
-int comm_schedule_host(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, int32_t mode, ms_result *out) {
+int comm_cycle_staged(ms_ctx *c, uint32_t n, int32_t mode) {
     CommState &m = *c->comm;
     const hipStream_t s = c->stream;
+    ++c->ctx_seq;  // binds below write the table on the context stream
+    if (mode == MS_MODE_SEQUENTIAL && !plugins_stateless(c)) return seq_sharded_locked(c, n, c->d_pods, c->d_res, s);
+    (void)m;
+    return batched_all_locked(c, n, c->d_pods, c->d_res, s, true);
+}
+
+int comm_stage(ms_ctx *c, uint32_t n) {
+    CommState &m = *c->comm;
     int rc = drain_all_locked(c);  // device-resident batches in flight use the combine buffers
     if (rc) return rc;
     const uint32_t per = cdiv(n, (uint32_t)m.world);
-    rc = ensure_stage(c, std::max<uint32_t>(n, per * (uint32_t)m.world));
+    return ensure_stage(c, std::max<uint32_t>(n, per * (uint32_t)m.world));
+}
+
+int comm_schedule_host(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, int32_t mode, ms_result *out) {
+    const hipStream_t s = c->stream;
+    int rc = comm_stage(c, n);
     if (rc) return rc;
-    ++c->ctx_seq;  // binds below write the table on the context stream
     MS_HIP(c, hipMemcpyAsync(c->d_pods, pods, sizeof(ms_pod_rec) * n, hipMemcpyHostToDevice, s));
-    if (mode == MS_MODE_SEQUENTIAL && !plugins_stateless(c)) rc = seq_sharded_locked(c, n, c->d_pods, c->d_res, s);
-    else rc = batched_all_locked(c, n, c->d_pods, c->d_res, s, true);
+    rc = comm_cycle_staged(c, n, mode);
     if (rc) return rc;
     MS_HIP(c, hipMemcpyAsync(out, c->d_res, sizeof(ms_result) * n, hipMemcpyDeviceToHost, s));
     MS_HIP(c, hipStreamSynchronize(s));

@@ -41,8 +41,10 @@ struct ms_ctx {
     std::mutex sched_mu;
 
     // staging (d_pods / d_res / h_pods / h_res hold stage_cap pods; the key and
-    // flag scratch batch_cap)
-    uint32_t batch_cap = 0, stage_cap = 0;
+    // flag scratch batch_cap; the compact records compact_cap)
+    uint32_t batch_cap = 0, stage_cap = 0, compact_cap = 0;
+    ms_pod_compact *d_podc = nullptr;
+    ms_result_compact *d_resc = nullptr;
     ms_pod_rec *h_pods = nullptr;
     ms_result *h_res = nullptr;
     ms_pod_rec *d_pods = nullptr;
@@ -137,6 +139,9 @@ void comm_free(ms_ctx *c);
 // ms_schedule_batch / ms_schedule_sequential_device on a context joined to a
 // communicator (callers hold sched_mu; deltas flushed)
 int comm_schedule_host(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode, ms_result *out);
+// the same on pods already staged in c->d_pods (comm_stage(n) first), results in c->d_res
+int comm_stage(ms_ctx *c, uint32_t n_pods);
+int comm_cycle_staged(ms_ctx *c, uint32_t n_pods, int32_t mode);
 int comm_schedule_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
                          hipStream_t s);
 void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world);

@@ -94,6 +94,8 @@ struct NodeDelta {
 static_assert(sizeof(ms_node_rec) == 64, "ms_node_rec layout");
 static_assert(sizeof(ms_pod_rec) == 40, "ms_pod_rec layout");
 static_assert(sizeof(ms_result) == 24, "ms_result layout");
+static_assert(sizeof(ms_pod_compact) == 8, "ms_pod_compact layout");
+static_assert(sizeof(ms_result_compact) == 8, "ms_result_compact layout");
 
 __host__ __device__ inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
@@ -258,6 +260,10 @@ hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32
 hipError_t launch_bind_one(const NodeTable &t, uint32_t local, const ms_pod_rec *pod_dev, int sign,
                            hipStream_t s);
 hipError_t launch_read_rows(const NodeTable &t, uint32_t first, uint32_t n, ms_node_rec *out, hipStream_t s);
+// Compact records (ms_schedule_batch_compact): pods widened to ms_pod_rec (zero
+// requests), results narrowed to ms_result_compact, on the device.
+hipError_t launch_pods_widen(const ms_pod_compact *in, uint32_t n, ms_pod_rec *out, hipStream_t s);
+hipError_t launch_results_narrow(const ms_result *in, uint32_t n, ms_result_compact *out, hipStream_t s);
 // Largest speculative batch the sequential validator accepts.
 uint32_t seq_batch_limit();
 // i64 fields per validator node record; stale nodes per prev list.

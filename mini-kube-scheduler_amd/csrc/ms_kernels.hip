@@ -2006,6 +2006,27 @@ __global__ void k_seq_window_out(const ms_result *__restrict__ win_res, uint32_t
     if (threadIdx.x == 0) ctl[0] = cur + done;
 }
 
+__global__ void k_pods_widen(const ms_pod_compact *__restrict__ in, uint32_t n, ms_pod_rec *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint2 v = *reinterpret_cast<const uint2 *>(in + i);  // = the first 8 bytes of ms_pod_rec
+    uint2 *o = reinterpret_cast<uint2 *>(out + i);
+    o[0] = v;
+    o[1] = o[2] = o[3] = o[4] = make_uint2(0u, 0u);
+}
+
+__global__ void k_results_narrow(const ms_result *__restrict__ in, uint32_t n, ms_result_compact *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ms_result r = in[i];
+    ms_result_compact c;
+    c.node = r.node;
+    c.score = (uint16_t)r.score;
+    c.code = (uint8_t)r.code;
+    c.plugin_mask = (uint8_t)r.plugin_mask;
+    out[i] = c;
+}
+
 __global__ void k_apply_binds(NodeTable t, const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
                               const ms_result *__restrict__ res) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2364,6 +2385,18 @@ hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32
                               hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     hipLaunchKernelGGL(k_apply_binds, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, t, pods, n_pods, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_pods_widen(const ms_pod_compact *in, uint32_t n, ms_pod_rec *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pods_widen, dim3(cdiv(n, 256)), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_results_narrow(const ms_result *in, uint32_t n, ms_result_compact *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_results_narrow, dim3(cdiv(n, 256)), dim3(256), 0, s, in, n, out);
     return hipGetLastError();
 }
 

@@ -74,6 +74,10 @@ POD_REC = np.dtype(
 RESULT = np.dtype(
     [("node", "<i4"), ("code", "<i4"), ("score", "<i8"), ("plugin_mask", "<u4"), ("_pad", "<u4")]
 )
+# compact records (ms_schedule_batch_compact; NU+NN / NodeAffinity sets): 8 B each way
+POD_COMPACT = np.dtype([("ordinal", "<u4"), ("name_digit", "i1"), ("tolerates_unschedulable", "u1"),
+                        ("pref_zone", "u1"), ("pref_weight", "u1")])
+RESULT_COMPACT = np.dtype([("node", "<i4"), ("score", "<u2"), ("code", "u1"), ("plugin_mask", "u1")])
 # ms_seq_cand: a shard's speculative candidate with the node's record (node-sharded sequential mode)
 SEQ_CAND = np.dtype(
     [
@@ -94,6 +98,16 @@ SEQ_TOPK = 4
 SEQ_SHARD_BATCH_MAX = 256
 SEQ_MAX_SHARDS = 16
 assert NODE_REC.itemsize == 64 and POD_REC.itemsize == 40 and RESULT.itemsize == 24 and SEQ_CAND.itemsize == 72
+assert POD_COMPACT.itemsize == 8 and RESULT_COMPACT.itemsize == 8
+
+
+def compact_pods(pods: np.ndarray) -> np.ndarray:
+    """ms_pod_compact of pod records (their first 8 bytes)."""
+    p = np.ascontiguousarray(pods, dtype=POD_REC)
+    out = np.empty(len(p), dtype=POD_COMPACT)
+    for f in POD_COMPACT.names:
+        out[f] = p[f]
+    return out
 
 
 class ms_config(ctypes.Structure):
@@ -147,6 +161,7 @@ SIGNATURES = {
     "ms_nodes_flush": (ctypes.c_int, [_vp]),
     "ms_nodes_read": (ctypes.c_int, [_vp, _u32, _u32, _vp]),
     "ms_schedule_batch": (ctypes.c_int, [_vp, _u32, _vp, _i32, _vp]),
+    "ms_schedule_batch_compact": (ctypes.c_int, [_vp, _u32, _vp, _i32, _vp]),
     "ms_commit_bind": (ctypes.c_int, [_vp, _u32, _vp]),
     "ms_uncommit_bind": (ctypes.c_int, [_vp, _u32, _vp]),
     "ms_sweep_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp]),
@@ -307,6 +322,18 @@ class Engine:
         elif out.dtype != RESULT or len(out) != len(p) or not out.flags.c_contiguous:
             raise ValueError("out must be a contiguous RESULT array of len(pods)")
         self._check("ms_schedule_batch", self.lib.ms_schedule_batch(self.h, len(p), _ptr(p), mode, _ptr(out)))
+        return out
+
+    def schedule_compact(self, pods: np.ndarray, mode: int = MODE_BATCHED,
+                         out: Optional[np.ndarray] = None) -> np.ndarray:
+        """ms_schedule_batch_compact: POD_COMPACT in, RESULT_COMPACT out (8 B each way)."""
+        p = np.ascontiguousarray(pods, dtype=POD_COMPACT)
+        if out is None:
+            out = np.zeros(len(p), dtype=RESULT_COMPACT)
+        elif out.dtype != RESULT_COMPACT or len(out) != len(p) or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous RESULT_COMPACT array of len(pods)")
+        self._check("ms_schedule_batch_compact",
+                    self.lib.ms_schedule_batch_compact(self.h, len(p), _ptr(p), mode, _ptr(out)))
         return out
 
     def commit_bind(self, ordinal: int, pod: np.ndarray):

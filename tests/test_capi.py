@@ -53,6 +53,12 @@ def test_struct_sizes_match_header():
     assert ctypes.sizeof(_lib.ms_config) == 32
     assert ctypes.sizeof(_lib.ms_info) == 56
     assert ctypes.sizeof(_lib.ms_comm_id) == _lib.COMM_ID_BYTES == 128
+    assert _lib.POD_COMPACT.itemsize == _lib.RESULT_COMPACT.itemsize == 8
+    # ms_pod_compact is the first 8 bytes of ms_pod_rec
+    from minisched_amd import synth
+
+    pr = synth.pods(50, seed=3, zones=True)
+    assert _lib.compact_pods(pr).tobytes() == b"".join(r.tobytes()[:8] for r in pr)
 
 
 def test_library_links_rccl():

@@ -279,6 +279,29 @@ def test_config_e_prefix(oracle):
         assert e.info()._pad == 0
 
 
+@pytest.mark.parametrize("plugin_set", [PLUGINS_NU_NN, _lib.PLUGINS_NU_NN_NA])
+@pytest.mark.parametrize("n_pods", [1, 777, 40_000])
+def test_compact_records(oracle, plugin_set, n_pods):
+    # ms_schedule_batch_compact: 8 B pods in, 8 B results out, the same outcomes and binds
+    # (pod_count) as the full records
+    seed = 300 + n_pods + plugin_set
+    zones = plugin_set == _lib.PLUGINS_NU_NN_NA
+    nr = synth.nodes(6000, seed=seed, zones=zones)
+    pr = synth.pods(n_pods, seed=seed, zones=zones)
+    pr["name_digit"][::13] = -1
+    pr["tolerates_unschedulable"][::7] = 1
+    o = oracle.schedule_na(nr, pr, seed=seed, literal=False) if zones else oracle.schedule(nr, pr, seed=seed)
+    with engine_with(nr, plugin_set=plugin_set, seed=seed) as e:
+        r = e.schedule_compact(_lib.compact_pods(pr))
+        for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
+            assert np.array_equal(r[k_res].astype(np.int64), o[k_or].astype(np.int64)), k_res
+        placed = np.bincount(o["node"][o["code"] == 0], minlength=6000)
+        assert np.array_equal(e.read(0, 6000)["pod_count"], placed)
+    with engine_with(synth.nodes(10, seed=1, resources=True), plugin_set=PLUGINS_NU_NRF_NN_LA) as e:
+        with pytest.raises(_lib.MSError):  # the resource-aware set needs the full records
+            e.schedule_compact(_lib.compact_pods(pr[:3]))
+
+
 def test_commit_uncommit(oracle):
     nr = synth.nodes(10, seed=2, resources=True)
     pr = synth.pods(1, seed=2, resources=True)
