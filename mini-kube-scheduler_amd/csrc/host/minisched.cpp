@@ -183,7 +183,7 @@ void register_events(const std::string &name, std::map<ClusterEvent, std::set<st
 }
 }  // namespace
 
-Scheduler::Scheduler(const Options &opt) : opt_(opt) {
+Scheduler::Scheduler(const Options &opt) : opt_(opt), ordinals_(opt.max_nodes) {
     // createFilterPlugins / createScorePlugins (initialize.go:80-121); the
     // resource-aware set adds NodeResourcesFit to both extension points.
     filter_.push_back(std::make_unique<NodeUnschedulable>());
@@ -231,18 +231,49 @@ const NodeUsage *Scheduler::Usage(const std::string &node) const {
     return it == usage_.end() ? nullptr : &it->second;
 }
 
+OrdinalAllocator::OrdinalAllocator(uint32_t capacity) : cap_(capacity) {
+    for (uint32_t d = 0; d < 10; ++d) next_[d] = d;
+}
+
+uint32_t OrdinalAllocator::LowestAny() {
+    uint32_t best = UINT32_MAX, bd = 10;
+    for (uint32_t d = 0; d < 10; ++d) {
+        const uint32_t o = free_[d].empty() ? next_[d] : *free_[d].begin();
+        if (o < cap_ && o < best) {
+            best = o;
+            bd = d;
+        }
+    }
+    if (bd == 10) throw std::length_error("node table full");
+    if (!free_[bd].empty() && *free_[bd].begin() == best) free_[bd].erase(free_[bd].begin());
+    else next_[bd] += 10;
+    return best;
+}
+
+uint32_t OrdinalAllocator::Allocate(int digit) {
+    uint32_t o;
+    if (digit >= 0 && digit <= 9 && !free_[digit].empty()) {
+        o = *free_[digit].begin();
+        free_[digit].erase(free_[digit].begin());
+    } else if (digit >= 0 && digit <= 9 && next_[digit] < cap_) {
+        o = next_[digit];
+        next_[digit] += 10;
+    } else {
+        o = LowestAny();  // no digit, or the digit's residue is full
+    }
+    high_ = std::max(high_, o + 1);
+    return o;
+}
+
+void OrdinalAllocator::Release(uint32_t o) { free_[o % 10].insert(o); }
+
+uint32_t OrdinalAllocator::HighWater() const { return high_; }
+
 uint32_t Scheduler::NodeOrdinal(const std::string &name, bool create) {
     auto it = ordinal_.find(name);
     if (it != ordinal_.end()) return it->second;
     if (!create) throw std::out_of_range("unknown node " + name);
-    uint32_t o;
-    if (!free_.empty()) {
-        o = free_.back();
-        free_.pop_back();
-    } else {
-        o = (uint32_t)ordinal_.size();
-        if (o >= opt_.max_nodes) throw std::length_error("node table full");
-    }
+    const uint32_t o = ordinals_.Allocate(NameDigit(name));
     ordinal_[name] = o;
     names_[o] = name;
     return o;
@@ -278,7 +309,7 @@ void Scheduler::OnNodeDelete(const v1::Node &node) {  // eventhandler.go:51-56
     if (ms_nodes_delete(ctx_, 1, &o) != MS_OK) throw std::runtime_error(ms_last_error(ctx_));
     ordinal_.erase(it);
     names_[o].clear();
-    free_.push_back(o);
+    ordinals_.Release(o);
     nodes_.erase(node.name);
     usage_.erase(node.name);
     if (Gvk(framework::kNode) & framework::Delete)

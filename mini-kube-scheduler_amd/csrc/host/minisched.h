@@ -195,6 +195,31 @@ struct ScheduleResult {
 // Record encoders (what the cgo shim computes per object).
 int NameDigit(const std::string &name);  // strconv.Atoi(name[len-1:]) : 0..9 or -1
 ms_pod_rec EncodePod(const v1::Pod &pod, uint32_t ordinal);
+
+// Node ordinals aligned to the name digit: a node whose name ends in digit d
+// gets an ordinal with ordinal % 10 == d (the lowest free one), so every 30
+// consecutive ordinals hold at most 3 nodes of one digit whatever the informer
+// Add order — the layout K1 pp's three fast hash slots cover.
+// The ordinal is an internal handle: the tie-break is a pure function of
+// (seed, pod, ordinal), uniform over tied nodes whichever ordinals they hold.
+// Names without a digit never score NodeNumber's 10 and fill the lowest free
+// ordinal of any residue. When a digit's residue is full up to the capacity,
+// its nodes take the lowest free ordinal of any residue (correct, on the
+// kernel's bit-scan path).
+class OrdinalAllocator {
+   public:
+    explicit OrdinalAllocator(uint32_t capacity);
+    uint32_t Allocate(int digit);  // digit 0..9, or -1; throws std::length_error when full
+    void Release(uint32_t ordinal);
+    uint32_t HighWater() const;    // 1 + the highest ordinal ever handed out (0 if none)
+
+   private:
+    uint32_t LowestAny();
+    uint32_t cap_;
+    uint32_t next_[10];            // lowest never-used ordinal of residue d
+    std::set<uint32_t> free_[10];  // released ordinals per residue
+    uint32_t high_ = 0;
+};
 struct NodeUsage {  // NodeInfo.Requested / NonZeroRequested / len(Pods)
     int64_t req_cpu = 0, req_mem = 0, nz_cpu = 0, nz_mem = 0;
     int32_t pods = 0;
@@ -258,7 +283,7 @@ class Scheduler {
     std::unique_ptr<SchedulingQueue> queue_;
     std::map<std::string, uint32_t> ordinal_;  // node name -> global ordinal
     std::vector<std::string> names_;           // ordinal -> node name ("" when free)
-    std::vector<uint32_t> free_;               // recycled ordinals
+    OrdinalAllocator ordinals_;                // digit-aligned node ordinals
     std::map<std::string, v1::Node> nodes_;
     std::map<std::string, NodeUsage> usage_;
     std::map<std::string, uint32_t> pod_ordinal_;

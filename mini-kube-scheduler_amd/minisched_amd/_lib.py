@@ -238,7 +238,7 @@ def comm_id_create() -> bytes:
     rc = lib.ms_comm_id_create(ctypes.byref(out))
     if rc != MS_OK:
         raise MSError("ms_comm_id_create", rc, lib.ms_last_error(None).decode())
-    return bytes(out.internal)
+    return ctypes.string_at(ctypes.addressof(out), COMM_ID_BYTES)  # (.internal stops at a NUL)
 
 
 def device_count() -> int:

@@ -161,3 +161,55 @@ def node_records(nodes: List[Node], zone_ids: Optional[ZoneIds] = None) -> np.nd
         rec[i]["alloc_milli_cpu"] = n.allocatable.get("cpu", 0)
         rec[i]["alloc_memory"] = n.allocatable.get("memory", 0)
     return rec
+
+
+class DigitOrdinals:
+    """Digit-aligned node ordinals (the host mirror's OrdinalAllocator,
+    csrc/host/minisched.h): a node whose name ends in digit d
+    gets the lowest free ordinal with ordinal % 10 == d, so every 30 consecutive
+    ordinals hold at most 3 nodes of one digit whatever the informer Add order
+    (the layout K1 pp's fast hash slots cover). Names without a digit, and
+    digits whose residue is full up to the capacity, take the lowest free
+    ordinal of any residue."""
+
+    def __init__(self, capacity: int):
+        import heapq  # noqa: F401  (free lists are min-heaps)
+
+        self.cap = capacity
+        self.next = list(range(10))
+        self.free: List[List[int]] = [[] for _ in range(10)]
+        self.high = 0
+
+    def _lowest_any(self) -> int:
+        import heapq
+
+        best, bd = None, None
+        for d in range(10):
+            o = self.free[d][0] if self.free[d] else self.next[d]
+            if o < self.cap and (best is None or o < best):
+                best, bd = o, d
+        if best is None:
+            raise OverflowError("node table full")
+        if self.free[bd] and self.free[bd][0] == best:
+            heapq.heappop(self.free[bd])
+        else:
+            self.next[bd] += 10
+        return best
+
+    def allocate(self, digit: int) -> int:
+        import heapq
+
+        if 0 <= digit <= 9 and self.free[digit]:
+            o = heapq.heappop(self.free[digit])
+        elif 0 <= digit <= 9 and self.next[digit] < self.cap:
+            o = self.next[digit]
+            self.next[digit] += 10
+        else:
+            o = self._lowest_any()
+        self.high = max(self.high, o + 1)
+        return o
+
+    def release(self, ordinal: int) -> None:
+        import heapq
+
+        heapq.heappush(self.free[ordinal % 10], ordinal)

@@ -5,6 +5,7 @@
 //
 // The GPU cases replay the reference's only end-to-end scenario (sched.go:70-140)
 // through the same objects and events the Go scheduler would see.
+#include <stdexcept>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -96,6 +97,46 @@ static void cpu_tests() {
         ms_node_rec n = EncodeNode(node("nodeQ", true, 1000, 2000), NodeUsage{5, 6, 7, 8, 9});
         CHECK(n.unschedulable == 1 && n.name_digit == 0xFF && n.allowed_pods == 110);
         CHECK(n.req_milli_cpu == 5 && n.nonzero_memory == 8 && n.pod_count == 9);
+    });
+    run("ordinal allocator: ordinal % 10 == name digit, holes reused", [] {
+        OrdinalAllocator a(100);
+        // informer Add order with arbitrary name digits
+        const int digits[] = {7, 7, 7, 3, -1, 0, 7, -1, 9, 3};
+        std::vector<uint32_t> got;
+        for (int d : digits) got.push_back(a.Allocate(d));
+        CHECK(got[0] == 7 && got[1] == 17 && got[2] == 27 && got[3] == 3 && got[6] == 37 && got[9] == 13);
+        CHECK(got[4] == 0 && got[7] == 1);  // no digit: the lowest free ordinal of any residue
+        CHECK(got[5] == 10 && got[8] == 9);
+        for (size_t i = 0; i < got.size(); ++i)
+            if (digits[i] >= 0) CHECK((int)(got[i] % 10) == digits[i]);
+        a.Release(17);
+        CHECK(a.Allocate(7) == 17);  // its residue's hole first
+        a.Release(27);
+        CHECK(a.Allocate(-1) == 2);  // (2 < 27)
+        // every 30 consecutive ordinals hold at most 3 of one digit
+        OrdinalAllocator b(3000);
+        uint64_t x = 12345;
+        std::vector<int> dig(3000, -2);
+        for (int i = 0; i < 2500; ++i) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            const int d = (int)((x >> 33) % 10);
+            dig[b.Allocate(d)] = d;
+        }
+        for (uint32_t g = 0; g + 30 <= 3000; g += 30)
+            for (int d = 0; d < 10; ++d) {
+                int c = 0;
+                for (uint32_t i = g; i < g + 30; ++i) c += dig[i] == d;
+                CHECK(c <= 3);
+            }
+        OrdinalAllocator full(12);
+        for (int i = 0; i < 12; ++i) (void)full.Allocate(5);  // residue 5 has 5 only: the rest spill
+        bool threw = false;
+        try {
+            (void)full.Allocate(5);
+        } catch (const std::length_error &) {
+            threw = true;
+        }
+        CHECK(threw && full.HighWater() == 12);
     });
     run("queue: FIFO, backoff 1 s, event matching (queue.go)", [] {
         FakeClock clk;

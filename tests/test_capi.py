@@ -109,3 +109,10 @@ def test_single_hip_runtime_per_process():
 
     _lib.load()
     assert len(hip_runtimes_mapped()) == 1, hip_runtimes_mapped()
+
+
+def test_comm_id_create_on_host():
+    # ms_comm_id_create (ncclGetUniqueId) needs no device: rank 0 makes the id, every
+    # rank receives its 128 bytes out of band (sharded.init_comm broadcasts them)
+    a, b = _lib.comm_id_create(), _lib.comm_id_create()
+    assert len(a) == len(b) == _lib.COMM_ID_BYTES and a != b

@@ -53,15 +53,19 @@ def test_host_mirror_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("plugin_set,n_nodes,n_pods", [(1, 300, 1500), (0, 2000, 800)])
-def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes, n_pods):
+@pytest.mark.parametrize("plugin_set,n_nodes,n_pods,shuffle", [(1, 300, 1500, False), (0, 2000, 800, False),
+                                                               (1, 300, 1500, True), (0, 2000, 800, True)])
+def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes, n_pods, shuffle):
     # the host mirror checked against the oracle, not against itself.
     # v1 objects go through the informer handlers, the queue (FIFO), the encoders, ScheduleOne,
     # the binder and ErrorFunc; every cycle's outcome must equal the sequential oracle's
-    # for the same cluster, with pod ordinals in queue order and node ordinals in Add order.
+    # for the same cluster, with pod ordinals in queue order and node ordinals from the
+    # digit-aligned allocator (encode.DigitOrdinals, the host mirror's OrdinalAllocator):
+    # in Add order node{i} gets ordinal i; shuffled, the Add order and the names differ and
+    # some names end in a letter
     import numpy as np
 
-    from minisched_amd import synth
+    from minisched_amd import encode, synth
 
     seed = 17 + plugin_set
     nr = synth.nodes(n_nodes, seed=seed, resources=True)
@@ -69,9 +73,15 @@ def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes
     pr["tolerates_unschedulable"][::9] = 1
     names = [f"pod{j}" if j % 37 else f"pod{j}x" for j in range(n_pods)]  # some names end in a letter
     pr["name_digit"] = [int(n[-1]) if n[-1].isdigit() else -1 for n in names]
+    order = np.random.default_rng(seed).permutation(n_nodes) if shuffle else np.arange(n_nodes)
+    node_names = [f"node{i}" if not shuffle or i % 23 else f"node{i}z" for i in range(n_nodes)]
+    alloc = encode.DigitOrdinals(n_nodes)
+    ords = np.zeros(n_nodes, dtype=np.int64)
+    for i in order:
+        ords[i] = alloc.allocate(encode.name_digit(node_names[i]))
     lines = []
-    for i in range(n_nodes):
-        lines.append(f"N node{i} {int(nr['unschedulable'][i])} {int(nr['alloc_milli_cpu'][i])} "
+    for i in order:
+        lines.append(f"N {node_names[i]} {int(nr['unschedulable'][i])} {int(nr['alloc_milli_cpu'][i])} "
                      f"{int(nr['alloc_memory'][i])} {int(nr['allowed_pods'][i])}")
     for j in range(n_pods):
         none = pr["req_milli_cpu"][j] == 0 and pr["req_memory"][j] == 0
@@ -85,12 +95,16 @@ def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes
     rows = [l.split() for l in out.read_text().splitlines()]
     assert [r[0] for r in rows] == names  # one cycle per pod, in queue order
     code = np.array([{1: 0, 2: 2, 3: 1}[int(r[1])] for r in rows])
-    node = np.array([-1 if r[2] == "-" else int(r[2][4:]) for r in rows])
+    by_name = {n: i for i, n in enumerate(node_names)}
+    node = np.array([-1 if r[2] == "-" else int(ords[by_name[r[2]]]) for r in rows])
     score = np.array([int(r[3]) for r in rows])
     mask = np.array([int(r[4]) for r in rows])
     if plugin_set == 0:  # NU+NN reads no resources: the oracle's records need none
         nr["alloc_milli_cpu"] = nr["alloc_memory"] = 0
-    o = oracle.schedule(nr, pr, plugin_set=plugin_set, mode=1, seed=seed)
+    nr["name_digit"] = [max(encode.name_digit(n), -1) & 0xFF for n in node_names]
+    table = np.zeros(n_nodes, dtype=nr.dtype)  # the oracle's records at the allocated ordinals
+    table[ords] = nr
+    o = oracle.schedule(table, pr, plugin_set=plugin_set, mode=1, seed=seed)
     assert np.array_equal(code, o["code"])
     assert np.array_equal(node, o["node"])
     assert np.array_equal(score, o["score"])

@@ -267,3 +267,31 @@ def test_tiebreak_hash_is_invertible():
         assert unhash(a, _pyref.h32(seed, pod, node)) == node
     hs = {_pyref.h32(9, 4242, n) for n in range(20000)}
     assert len(hs) == 20000
+
+
+def test_digit_ordinals_allocator():
+    # encode.DigitOrdinals == the host mirror's OrdinalAllocator (tests/cpp/test_host.cpp
+    # checks the same sequence): ordinal % 10 == name digit, holes reused, no-digit names
+    # fill the lowest free ordinal, at most 3 of one digit per 30 consecutive ordinals
+    from minisched_amd import encode
+
+    a = encode.DigitOrdinals(100)
+    got = [a.allocate(d) for d in (7, 7, 7, 3, -1, 0, 7, -1, 9, 3)]
+    assert got == [7, 17, 27, 3, 0, 10, 37, 1, 9, 13]
+    a.release(17)
+    assert a.allocate(7) == 17
+    a.release(27)
+    assert a.allocate(-1) == 2
+    rng = np.random.default_rng(5)
+    b = encode.DigitOrdinals(12_000)
+    dig = np.full(12_000, -2)
+    for d in rng.integers(0, 10, 10_000):
+        dig[b.allocate(int(d))] = d
+    for g in range(0, 12_000, 30):
+        w = dig[g:g + 30]
+        assert max((w == d).sum() for d in range(10)) <= 3
+    assert b.high <= 12_000
+    full = encode.DigitOrdinals(12)
+    assert sorted(full.allocate(5) for _ in range(12)) == list(range(12))
+    with pytest.raises(OverflowError):
+        full.allocate(5)

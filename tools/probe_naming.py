@@ -4,6 +4,9 @@
   cycling : node{i} at ordinal i (digit = i % 10, the synthetic default)
   iid     : digits i.i.d. uniform 0..9 (names unrelated to ordinals)
   perm    : ordinal i holds node{perm[i]} (informer Add order != name order)
+  iid_allocated : the iid names, ordinals from the digit-aligned allocator
+            (encode.DigitOrdinals, the host mirror's OrdinalAllocator) in Add
+            order; the table spans the allocator's high-water mark (holes absent)
 
 Each: mean device time of the fused single-launch cycle (ms_select_batch_device)
 over K launches, the fraction of 30-row groups whose "over" plane is set (the
@@ -30,11 +33,18 @@ def layouts(n, seed):
     iid["name_digit"] = rng.integers(0, 10, n).astype(np.uint8)
     perm = base.copy()
     perm["name_digit"] = (rng.permutation(n) % 10).astype(np.uint8)
-    return {"cycling": base, "iid": iid, "perm": perm}
+    from minisched_amd import encode
+
+    alloc = encode.DigitOrdinals(n + n // 10)
+    ords = np.array([alloc.allocate(int(d)) for d in iid["name_digit"]])
+    allocated = np.zeros(alloc.high, dtype=base.dtype)
+    allocated["allowed_pods"] = -1  # never added: absent from the LIST
+    allocated[ords] = iid
+    return {"cycling": base, "iid": iid, "perm": perm, "iid_allocated": allocated}
 
 
 def over_frac(nr):
-    d = nr["name_digit"].astype(np.int64)
+    d = np.where(nr["allowed_pods"] >= 0, nr["name_digit"].astype(np.int64), 99)
     g = len(d) // 30
     d = d[: g * 30].reshape(g, 30)
     cnt = np.stack([(d == v).sum(1) for v in range(10)], 1)
@@ -55,8 +65,10 @@ def main():
     res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
     out = {}
     for name, nr in layouts(N, 1).items():
-        with _lib.Engine(max_nodes=N, seed=1) as e:
-            e.upsert(np.arange(N), nr)
+        rows = len(nr)
+        listed = np.nonzero(nr["allowed_pods"] >= 0)[0]
+        with _lib.Engine(max_nodes=rows, seed=1) as e:
+            e.upsert(listed, nr[listed])
             e.flush()
             run = lambda: e.select_batch_device(P, pods.data_ptr(), res.data_ptr(), s.cuda_stream)
             run()
@@ -73,7 +85,7 @@ def main():
         o = _oracle.schedule_nunn_omp(nr, pr, seed=1, threads=16)
         ok = all(np.array_equal(got[a].astype(np.int64), o[b].astype(np.int64))
                  for a, b in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")))
-        out[name] = {"ms": ms, "evals_per_s": N * P / (ms * 1e-3), "over_group_frac": over_frac(nr),
+        out[name] = {"ms": ms, "rows": rows, "evals_per_s": N * P / (ms * 1e-3), "over_group_frac": over_frac(nr),
                      "parity": ok, "oracle_s": time.perf_counter() - t0}
         print(name, json.dumps(out[name]), flush=True)
     print(json.dumps(out))
