@@ -77,9 +77,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the e2e / class-indexed measurements")
+    ap.add_argument("--no-extras", action="store_true", help="skip the e2e measurements and configs B, D, E")
+    ap.add_argument("--no-configs", action="store_true", help="skip configs B, D, E (device + CPU baselines)")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r02zh_pmc_C.json"),
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
+    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r03_pmc_E.json"),
+                    help="rocprofv3 counter summary of config E's step kernel (tools/profile_e.sh)")
     return ap.parse_args()
 
 
@@ -209,6 +212,170 @@ def e2e_host(eng, pods_np, n_nodes, world=1, compact=False):
                         + " (pageable host array), filter+score+selectHost+decode"
                         + (", reduce-scatter + all-gather over the communicator" if world > 1 else "")
                         + ", bind commit, D2H of " + ("8" if compact else "24") + " B results into the host array"}
+
+
+def _cpu_info(threads):
+    return {"cores": threads, "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+
+
+def _median_time(fn, reps=5, before=None, sync=None):
+    """1 warm-up, then the median wall time of `reps` runs (before() untimed)."""
+    if before:
+        before()
+    fn()
+    if sync:
+        sync()
+    ts = []
+    for _ in range(reps):
+        if before:
+            before()
+        t0 = time.perf_counter()
+        fn()
+        if sync:
+            sync()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def other_configs(args, dev, stream):
+    """BASELINE.json's other configs on this GPU, each with a same-run CPU
+    baseline: B 5k x 10k NU+NN exact sequential (CPU in full),
+    D 50k x 1M NU+NN batched (CPU on a pod prefix), E 50k x 200k resource-aware
+    exact sequential (CPU on an exact 2,000-pod prefix of the queue). Device
+    figures: inputs resident in HBM, the engine's context stream, 1 warm-up then
+    the median of 5 (B and E reset the node table before each run, untimed)."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle  # checker / CPU baseline only; never on the measured GPU path
+
+    from minisched_amd import _lib, synth
+
+    threads = min(16, os.cpu_count() or 1)
+    out = {}
+    sync = torch.cuda.synchronize
+
+    # ---- B: 5k nodes x 10k pods, NU+NN, exact sequential (assume-on-select binds)
+    N, P = 5_000, 10_000
+    nr, pr = synth.nodes(N, seed=args.seed), synth.pods(P, seed=args.seed)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    with _lib.Engine(max_nodes=N, seed=args.seed, device=dev.index) as e:
+        def reset():
+            e.upsert(np.arange(N), nr)
+            e.flush()
+        med, ts = _median_time(lambda: e.schedule_sequential_device(P, pods.data_ptr(), res.data_ptr()),
+                               before=reset, sync=sync)
+        got = res.cpu().numpy().view(_lib.RESULT)
+    t0 = time.perf_counter()
+    o = _oracle.schedule(nr, pr, plugin_set=0, mode=1, seed=args.seed)
+    cpu_seq = time.perf_counter() - t0
+    names = [f"node{i}" for i in range(N)]
+    t0 = time.perf_counter()
+    _oracle.schedule_nunn_names(names, np.ascontiguousarray(nr["unschedulable"]), [f"pod{j}" for j in range(P)],
+                                pr["tolerates_unschedulable"], pr["ordinal"], seed=args.seed)
+    cpu_faithful = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    _oracle.schedule_nunn_omp(nr, pr, seed=args.seed, threads=threads)
+    cpu_omp = time.perf_counter() - t0
+    out["B"] = {
+        "workload": "B: 5000 nodes x 10000 pods, NU+NN, exact sequential (binds committed in queue order)",
+        "ms": med * 1e3, "runs_ms": [t * 1e3 for t in ts], "evals_per_s": N * P / med, "pods_per_s": P / med,
+        "parity_vs_oracle": bool(np.array_equal(got["node"], o["node"]) and np.array_equal(got["code"], o["code"])),
+        "cpu_baseline": dict(value=N * P / cpu_faithful, unit="pod×node evals/s", kind="port",
+                             sample=f"oracle msor_schedule_nunn_names (1 thread, per-pair name parse as "
+                                    f"nodenumber.go:81-87), all {P} pods ({cpu_faithful:.2f} s)",
+                             soa_1t=N * P / cpu_seq, omp=N * P / cpu_omp, omp_threads=threads,
+                             **_cpu_info(1)),
+    }
+
+    # ---- D: 50k nodes x 1M pods, NU+NN, batched (stateless), one fused launch
+    N, P = 50_000, 1_000_000
+    nr, pr = synth.nodes(N, seed=args.seed), synth.pods(P, seed=args.seed)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    with _lib.Engine(max_nodes=N, seed=args.seed, device=dev.index) as e:
+        e.upsert(np.arange(N), nr)
+        e.flush()
+        med, ts = _median_time(lambda: e.select_batch_device(P, pods.data_ptr(), res.data_ptr()), sync=sync)
+        got = res.cpu().numpy().view(_lib.RESULT)[:4096]
+    n_omp = 20_000  # pod prefix for the CPU legs (BASELINE.md §4: prefix-extrapolated)
+    t0 = time.perf_counter()
+    o = _oracle.schedule_nunn_omp(nr, pr[:n_omp], seed=args.seed, threads=threads)
+    cpu_omp = time.perf_counter() - t0
+    n_f = 2_000
+    names = [f"node{i}" for i in range(N)]
+    t0 = time.perf_counter()
+    _oracle.schedule_nunn_names(names, np.ascontiguousarray(nr["unschedulable"]), [f"pod{j}" for j in range(n_f)],
+                                pr["tolerates_unschedulable"][:n_f], pr["ordinal"][:n_f], seed=args.seed)
+    cpu_faithful = time.perf_counter() - t0
+    out["D"] = {
+        "workload": "D: 50000 nodes x 1000000 pods, NU+NN, batched (stateless), one fused launch",
+        "ms": med * 1e3, "runs_ms": [t * 1e3 for t in ts], "evals_per_s": N * P / med, "pods_per_s": P / med,
+        "parity_vs_oracle_prefix": bool(np.array_equal(got["node"], o["node"][:4096])),
+        "cpu_baseline": dict(value=N * n_omp / cpu_omp, unit="pod×node evals/s", kind="port",
+                             sample=f"oracle msor_schedule_nunn_omp ({threads} threads), first {n_omp} pods, "
+                                    f"prefix-extrapolated ({cpu_omp:.2f} s)",
+                             faithful_1t=N * n_f / cpu_faithful, faithful_sample=f"first {n_f} pods",
+                             **_cpu_info(threads)),
+    }
+    del pods, res
+
+    # ---- E: 50k nodes x 200k pods, NU+NRF+NN+LA, exact sequential (assume-on-select)
+    N, P = 50_000, 200_000
+    nr, pr = synth.nodes(N, seed=args.seed, resources=True), synth.pods(P, seed=args.seed, resources=True)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    with _lib.Engine(max_nodes=N, plugin_set=_lib.PLUGINS_NU_NRF_NN_LA, seed=args.seed, device=dev.index) as e:
+        def reset():
+            e.upsert(np.arange(N), nr)
+            e.flush()
+        med, ts = _median_time(lambda: e.schedule_sequential_device(P, pods.data_ptr(), res.data_ptr()),
+                               before=reset, sync=sync)
+        got = res.cpu().numpy().view(_lib.RESULT)
+        inf = e.info()
+    n_pre = 2_000
+    t0 = time.perf_counter()
+    o = _oracle.schedule(nr, pr[:n_pre], plugin_set=1, mode=1, seed=args.seed)
+    cpu_e = time.perf_counter() - t0
+    n_batches = (P + 127) // 128
+    line = {
+        "workload": "E: 50000 nodes x 200000 pods, NU+NRF+NN+LA, exact sequential (assume-on-select), "
+                    "speculative sweep + in-order validator, 128-pod batches",
+        "ms": med * 1e3, "runs_ms": [t * 1e3 for t in ts], "evals_per_s": N * P / med, "pods_per_s": P / med,
+        "us_per_batch": med * 1e6 / n_batches, "ns_per_pod": med * 1e9 / P,
+        "parity_vs_oracle_prefix": bool(np.array_equal(got["node"][:n_pre], o["node"])
+                                        and np.array_equal(got["code"][:n_pre], o["code"])),
+        "fit_errors": int((got["code"] == _lib.CODE_UNSCHEDULABLE).sum()),
+        "seq_counters_all_runs": dict(pods=inf.seq_pods, resweep_tiles=inf.seq_resweep_tiles,
+                                      recomputes=inf.seq_recomputes, overflow=inf._pad),
+        "cpu_baseline": dict(value=N * n_pre / cpu_e, unit="pod×node evals/s", kind="port",
+                             sample=f"oracle msor_schedule (1 thread, exact sequential with binds), first "
+                                    f"{n_pre} pods of the queue ({cpu_e:.2f} s)",
+                             pods_per_s=n_pre / cpu_e, **_cpu_info(1)),
+    }
+    pj = None
+    try:
+        pj = json.load(open(args.profile_json_e))
+    except Exception:
+        pass
+    if pj and pj.get("nodes") == N and pj.get("pods") == P:
+        step_s = pj["step_avg_ns_rocprof"] * 1e-9
+        valu = pj["step_SQ_INSTS_VALU"]
+        line["roofline"] = {
+            "bound": "valu", "kernel": "k_seq_step",
+            "achieved": valu / step_s, "peak": VALU_PEAK_NOMINAL, "unit": "wave-instr/s",
+            "frac": valu / step_s / VALU_PEAK_NOMINAL,
+            "valu_insts_per_launch": valu, "kernel_ms_rocprof": step_s * 1e3,
+            "validator_ns_per_pod": pj.get("validator_ns_per_pod"),
+            "validator_frac_of_step": pj.get("validator_frac_of_step"),
+            "traffic": pj.get("step_hbm_bytes"),
+            "hbm": {"algorithmic_bytes_per_eval": BYTES_PER_EVAL["NU+NRF+NN+LA"],
+                    "algorithmic_GBps": N * P * BYTES_PER_EVAL["NU+NRF+NN+LA"] / med / 1e9},
+            "profile": os.path.relpath(args.profile_json_e, ROOT),
+        }
+    out["E"] = line
+    return out
 
 
 def load_profile(path, n_local, n_pods):
@@ -402,6 +569,11 @@ def main():
         line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(N, args.seed, args.cpu_seconds)
+        if world == 1 and not args.no_extras and not args.no_configs:
+            try:
+                line["configs"] = other_configs(args, dev, stream)
+            except Exception as ex:  # (reported, never fatal to the headline line)
+                line["configs"] = {"error": repr(ex)[:300]}
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_e.sh run into profiles/<tag>_pmc_E.json and
+profiles/<tag>_e_kernel_stats.csv: config E's per-launch counters of the fused
+step kernel (k_seq_step: validation of batch k beside the speculative sweep of
+batch k+1) and of the top-4 merge, plus the validator wave's share.
+
+traffic: (2 x FETCH_SIZE + WRITE_SIZE) KB per launch (MI355X_MICROARCH.md §HBM,
+gfx950 wide-read correction). Validator: MS_VSTAMPS wave durations
+(s_memrealtime, 100 MHz) summed over the run, over the pods it validated.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+
+src, tag = sys.argv[1], sys.argv[2]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+dst = os.path.join(root, "profiles")
+KERNELS = ("k_seq_step", "k_topk_merge")
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def counters(sub):
+    agg = {}
+    for f in glob.glob(os.path.join(src, sub, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k:
+                agg.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+
+
+stats = glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)[0]
+shutil.copy(stats, os.path.join(dst, f"{tag}_e_kernel_stats.csv"))
+avg = {}
+for r in csv.DictReader(open(stats)):
+    k = short(r["Name"])
+    if k:
+        avg[k] = (float(r["AverageNs"]), int(r["Calls"]), float(r["TotalDurationNs"]))
+sq, fe, wr = counters("sq"), counters("fetch"), counters("write")
+bench = [json.loads(l) for l in open(os.path.join(src, "bench_stats.jsonl")) if l.startswith("{")][-1]
+vst = open(os.path.join(src, "vst.err")).read()
+m = re.search(r"MS_VSTAMPS pods=(\d+).*validator=(\d+) sweep_sum=(\d+) sweep_waves=(\d+)", vst)
+step = sq.get("k_seq_step", {})
+out = {
+    "config": "E", "nodes": bench["nodes"], "pods": bench["pods"],
+    "step_avg_ns_rocprof": avg["k_seq_step"][0], "step_calls": avg["k_seq_step"][1],
+    "merge_avg_ns_rocprof": avg.get("k_topk_merge", (None,))[0],
+    "step_SQ_INSTS_VALU": step.get("SQ_INSTS_VALU"),
+    "step_sq_counters": step, "merge_sq_counters": sq.get("k_topk_merge"),
+    "step_FETCH_SIZE_KB": fe.get("k_seq_step", {}).get("FETCH_SIZE"),
+    "step_WRITE_SIZE_KB": wr.get("k_seq_step", {}).get("WRITE_SIZE"),
+}
+if out["step_FETCH_SIZE_KB"] is not None and out["step_WRITE_SIZE_KB"] is not None:
+    out["step_hbm_bytes"] = (2 * out["step_FETCH_SIZE_KB"] + out["step_WRITE_SIZE_KB"]) * 1024
+if m:
+    pods, val = int(m.group(1)), int(m.group(2)) * 10  # ns
+    out["vstamps"] = {"pods": pods, "validator_ns_total": val, "sweep_wave_ns_sum": int(m.group(3)) * 10,
+                      "sweep_waves": int(m.group(4))}
+    out["validator_ns_per_pod"] = val / pods
+    out["validator_frac_of_step"] = (val / (pods / 128.0)) / avg["k_seq_step"][0]
+if step and avg.get("k_seq_step"):
+    out["valu_wave_instr_per_s"] = step["SQ_INSTS_VALU"] / (avg["k_seq_step"][0] * 1e-9)
+json.dump(out, open(os.path.join(dst, f"{tag}_pmc_E.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
