@@ -373,14 +373,14 @@ def test_library_schedule_batch_1rank(oracle):
         assert e.read(0, 4000)["pod_count"].sum() == 2 * (oracle.schedule(nr, pr, seed=71)["code"] == 0).sum()
     finally:
         e.close()
-    nr = synth.nodes(3000, seed=72, resources=True)
+    nr = synth.nodes(1000, seed=72, resources=True)
     pr = synth.pods(9000, seed=72, resources=True)
     pr["name_digit"][::23] = -1
     ob = oracle.schedule_batched_commit(nr, pr, 1, seed=72)
     e = _comm_engine(nr, 1, 72)
     try:
         _same(e.schedule(pr, _lib.MODE_BATCHED), ob, 0, len(pr), "NRF batched")
-        t = e.read(0, 3000)
+        t = e.read(0, 1000)
         assert np.array_equal(t["pod_count"], ob["cols"].pod_count)
     finally:
         e.close()
@@ -389,7 +389,7 @@ def test_library_schedule_batch_1rank(oracle):
     e = _comm_engine(nr, 1, 72)
     try:
         _same(e.schedule(pr, _lib.MODE_SEQUENTIAL), os_, 0, len(pr), "NRF sequential")
-        t = e.read(0, 3000)
+        t = e.read(0, 1000)
         for k_dev, k_or in (("pod_count", "pod_count"), ("req_milli_cpu", "req_cpu"), ("nonzero_memory", "nz_mem")):
             assert np.array_equal(t[k_dev], getattr(os_["cols"], k_or)), k_dev
     finally:

@@ -4,7 +4,8 @@
 # tracing domains), and the validator's wave durations from the MS_VSTAMPS
 # diagnostic build (`make -C mini-kube-scheduler_amd vstamps`, built in-tree
 # beforehand). Summary -> profiles/<tag>_pmc_E.json (read by bench.py's config
-# E roofline) and profiles/<tag>_e_kernel_stats.csv.
+# E roofline) and profiles/<tag>_e_kernel_stats.csv (the box keeps only
+# gpurun_out/: rerun the summary here on the merged gpurun_out/prof_e_<tag>).
 set -o pipefail
 TAG=${1:-r03}
 OUT=gpurun_out/prof_e_${TAG}
