@@ -54,9 +54,10 @@ constexpr uint32_t truth3(F f) {  // v_bitop3 table, S0 the most significant ind
 constexpr uint32_t kXnorAnd = truth3([](int a, int b, int c) { return c && a == b; });  // c & ~(a ^ b)
 constexpr uint32_t kSelect = truth3([](int a, int b, int c) { return c ? a : b; });     // c ? a : b
 
-constexpr int kPpWords = 4;      // 30-row groups per lane
+constexpr int kPpWords = 4;      // 30-row groups per lane (KW, shards above kPpSmallGroups)
+constexpr int kPpWordsSmall = 8; // KW for small shards: one wave holds every row
 constexpr int kPpMaxWaves = 16;  // 1024-thread workgroups
-constexpr uint32_t kPpWaveGroups = 64u * kPpWords;
+constexpr uint32_t kPpSmallGroups = 64u * kPpWordsSmall;  // 15,360 rows
 
 struct Word {
     uint32_t d0, d1, d2, d3;  // digit bit planes
@@ -137,8 +138,8 @@ __device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
 // flags: level 11 (score 10 + 1) over the score-10 rows, else level 1 over
 // every feasible row (all score 0). Returns level<<32 | max hash (wave-uniform),
 // 0 when no row of the wave is feasible.
-template <int NW>
-__device__ __forceinline__ u64 pod_slow(const Word (&W)[kPpWords], const Pod &q) {
+template <int KW, int NW>
+__device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Pod &q) {
     uint32_t h = 0;
     bool found = false;
 #pragma unroll
@@ -169,8 +170,8 @@ __device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, 
 }
 
 // One wave sweeps the chunk's pods [0, np) through its NW groups into lds[p].
-template <int NW, bool GEN>
-__device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const uint2 *pinfo, uint32_t np,
+template <int KW, int NW, bool GEN>
+__device__ __forceinline__ void sweep_range(const Word (&W)[KW], const uint2 *pinfo, uint32_t np,
                                             uint32_t lane, u64 *lds) {
     for (uint32_t pb = 0; pb < np; pb += 64) {
         const uint32_t nblk = min(64u, np - pb);
@@ -209,13 +210,20 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[kPpWords], const uin
                 const uint32_t t = rev3(l >> 3);
                 const Pod qs = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
                                         (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
-                const u64 v = pod_slow<NW>(W, qs);
+                const u64 v = pod_slow<KW, NW>(W, qs);
                 if (lane == 0 && v) atomicMax(&lds[pb + j + t], v);
             }
         }
     }
 }
 
+// KW words per lane: 4 (workgroups of up to 16 waves split the rows) or 8 for
+// shards of at most kPpSmallGroups groups, where ONE wave holds every row: then
+// every wave does the same work whatever SIMD it lands on (with 4 words a
+// 12.5k-row shard dealt over 4 waves gave them 2, 2, 2 and 1 words, and the
+// SIMD that hosts the short waves idled), and the per-pod reduction is paid
+// once per 7 words instead of once per 2.
+template <int KW>
 __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
@@ -237,12 +245,12 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     // word counts differ by at most one: word k of lane l is group
     // g0 + (k * waves + wv) * 64 + l
     const uint32_t waves = blockDim.x >> 6;
-    const uint32_t g0 = blockIdx.y * waves * kPpWaveGroups;
-    Word W[kPpWords];
+    const uint32_t g0 = blockIdx.y * waves * 64u * KW;
+    Word W[KW];
     int nw = 0;
     bool over = false;
 #pragma unroll
-    for (int k = 0; k < kPpWords; ++k) {
+    for (int k = 0; k < KW; ++k) {
         const uint32_t gw = g0 + (k * waves + wv) * 64u;
         const uint32_t g = gw + lane;
         const bool in = g < n_groups;
@@ -263,15 +271,19 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
         switch (nw * 2 + (gen ? 1 : 0)) {  // wave-uniform
 #define MS_PP_CASE(N)                                                                     \
     case 2 * N:                                                                           \
-        sweep_range<N, false>(W, pinfo, np, lane, lds);                                   \
+        if constexpr (N <= KW) sweep_range<KW, (N <= KW ? N : KW), false>(W, pinfo, np, lane, lds); \
         break;                                                                            \
     case 2 * N + 1:                                                                       \
-        sweep_range<N, true>(W, pinfo, np, lane, lds);                                    \
+        if constexpr (N <= KW) sweep_range<KW, (N <= KW ? N : KW), true>(W, pinfo, np, lane, lds);  \
         break;
             MS_PP_CASE(1)
             MS_PP_CASE(2)
             MS_PP_CASE(3)
             MS_PP_CASE(4)
+            MS_PP_CASE(5)
+            MS_PP_CASE(6)
+            MS_PP_CASE(7)
+            MS_PP_CASE(8)
 #undef MS_PP_CASE
             default:
                 break;  // no groups in this wave
@@ -367,7 +379,17 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     if (n_pods == 0) return hipSuccess;
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
-    const uint32_t waves_needed = std::max(1u, cdiv(n_groups, kPpWaveGroups));
+    // small shards with many pods: KW = 8, one single-wave workgroup per pod
+    // chunk holds every row. It needs enough pods per wave to balance whole
+    // waves over the SIMDs: 12.5k rows x 800k pods 347 vs 412 us, but x 100k
+    // pods 58.8 vs 52.7 us (profiles/r03_pp_words_ab.txt). MINISCHED_PP_WORDS
+    // = 4 / 8 forces a form (A/B).
+    const char *wenv = getenv("MINISCHED_PP_WORDS");
+    const uint32_t cus_ = (uint32_t)(num_cus > 0 ? num_cus : 256);
+    bool small = n_groups <= kPpSmallGroups && n_pods >= 512u * cus_ && !getenv("MINISCHED_PP_WAVES");
+    if (wenv) small = n_groups <= kPpSmallGroups && atoi(wenv) == 8;
+    const uint32_t KW = small ? (uint32_t)kPpWordsSmall : (uint32_t)kPpWords;
+    const uint32_t waves_needed = std::max(1u, cdiv(n_groups, 64u * KW));
     // W a power of two (32 / W workgroups per CU fill all 8 wave slots per
     // SIMD; W = 7 leaves one idle and was 9% slower at 50k rows): large shards
     // 16-wave workgroups (the groups are dealt round-robin, so every wave holds
@@ -378,7 +400,7 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
         while (W < std::max(4u, waves_needed) && W < (uint32_t)kPpMaxWaves) W *= 2;
     if (const char *w = getenv("MINISCHED_PP_WAVES")) W = (uint32_t)std::min(16, std::max(1, atoi(w)));
     if (!keys) W = std::max(W, std::min<uint32_t>(kPpMaxWaves, waves_needed));  // no scratch: one workgroup per chunk
-    const uint32_t gy = std::max(1u, cdiv(n_groups, W * kPpWaveGroups));
+    const uint32_t gy = std::max(1u, cdiv(n_groups, W * 64u * KW));
     const uint32_t cus = (uint32_t)(num_cus > 0 ? num_cus : 256);
     // (multiples of 8: a wave takes pods 8 at a time, and a part-filled 8 costs
     // a full one -- exact chunks ran 11% slower at 25k rows, r02k_ab_chunk.txt)
@@ -402,7 +424,7 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
         if (!keys) return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
+        hipLaunchKernelGGL(k_sweep_nunn_pp<kPpWords>, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
                            t, 0);
         e = hipGetLastError();
@@ -411,9 +433,14 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
         if (e != hipSuccess || !commit) return e;
         return launch_apply_binds(t, pods, n_pods, results, s);
     }
-    hipLaunchKernelGGL(k_sweep_nunn_pp, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes, t.gcap,
-                       n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0, results, present, t,
-                       results ? commit : 0);
+    if (KW == (uint32_t)kPpWordsSmall)
+        hipLaunchKernelGGL(k_sweep_nunn_pp<kPpWordsSmall>, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s,
+                           t.planes, t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0,
+                           results, present, t, results ? commit : 0);
+    else
+        hipLaunchKernelGGL(k_sweep_nunn_pp<kPpWords>, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s,
+                           t.planes, t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0,
+                           results, present, t, results ? commit : 0);
     return hipGetLastError();
 }
 
