@@ -96,6 +96,11 @@ int ensure_delta_cap(ms_ctx *c, uint32_t n) {
 
 // Drains the delta queue onto the stream (caller holds sched_mu).
 int flush_locked(ms_ctx *c) {
+    // deltas and binds land on the context stream: after the sweeps still
+    // reading the table on the communicator's streams
+    const int fenced = comm_fence_reads(c, c->stream);
+    if (fenced < 0) return fenced;
+    if (fenced) ++c->fence_seq;
     std::vector<NodeDelta> batch;
     {
         std::lock_guard<std::mutex> g(c->delta_mu);
@@ -129,14 +134,19 @@ hipStream_t pick_stream(ms_ctx *c, void *s) { return s ? (hipStream_t)s : c->str
 
 // Makes work later enqueued on s wait for everything already on the context stream.
 int order_after_ctx_stream(ms_ctx *c, hipStream_t s) {
+    const int fenced = comm_fence_reads(c, c->stream);
+    if (fenced < 0) return fenced;
+    if (fenced) ++c->fence_seq;
     if (s == c->stream) return MS_OK;
-    if (s == c->ordered_stream && c->ordered_seq == c->ctx_seq) return MS_OK;  // nothing new on the ctx stream
+    if (s == c->ordered_stream && c->ordered_seq == c->ctx_seq && c->ordered_fence == c->fence_seq)
+        return MS_OK;  // nothing new on the ctx stream
     if (!c->ev_order) MS_HIP(c, hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming));
     hipError_t e = hipEventRecord(c->ev_order, c->stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->ev_order, 0);
     if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("stream ordering: ") + hipGetErrorString(e));
     c->ordered_stream = s;
     c->ordered_seq = c->ctx_seq;
+    c->ordered_fence = c->fence_seq;
     return MS_OK;
 }
 
@@ -155,6 +165,7 @@ int chain_back(ms_ctx *c, hipStream_t s) {
         ++c->ctx_seq;
         c->ordered_stream = s;
         c->ordered_seq = c->ctx_seq;
+        c->ordered_fence = c->fence_seq;
     }
     return MS_OK;
 }

@@ -20,6 +20,13 @@
 // batch k are enqueued once `depth` later batches were submitted, so batch k's
 // collective overlaps their sweeps (RCCL runs one communicator's collectives in
 // issue order on the collective stream, so a drain waits for the newest only).
+// Consecutive sweeps alternate between two internal streams: on one stream each
+// launch waits for the previous one to drain, and at the strong-scaling shard
+// (12.5k rows x 100k pods) that ramp and tail were a quarter of the sweep
+// (55.4 vs 42.9 us per sweep, tools/probe_streams.py, profiles/r03_two_streams.json).
+// The sweeps only read the node table; writers (deltas, binds) are fenced
+// behind the in-flight ones (comm_fence_reads) instead of every sweep being
+// chained into the context stream, which would serialize them again.
 //
 // Exact sequential cycle (config E): per window of W pods, every
 // shard's speculative top-4 with records (ms_seq_candidates_device) -> one
@@ -43,7 +50,7 @@ namespace msgpu {
 
 namespace {
 
-constexpr uint32_t kPipeMax = 8;  // batch buffer sets: pipeline depth + 1 < kPipeMax
+constexpr uint32_t kPipeMax = 8;  // batch buffer sets: pipeline depth + 1 <= kPipeMax
 static_assert(kPipeMax <= kMaxSliceJobs, "a full drain is one slice-decode launch");
 static_assert(sizeof(ncclUniqueId) == MS_COMM_ID_BYTES, "ms_comm_id holds an ncclUniqueId");
 
@@ -54,6 +61,7 @@ struct ShardSlot {
     uint32_t *flags = nullptr, *flags_mine = nullptr;
     uint32_t *pres = nullptr, *pres_mine = nullptr;  // G words / 1 word
     uint32_t cap = 0;                                // pods per slice the buffers hold
+    bool used = false;                               // a batch went through this slot
 };
 
 struct Pending {
@@ -68,12 +76,19 @@ struct CommState {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     hipStream_t cs = nullptr;  // collective stream
-    hipEvent_t ev_swept[kPipeMax] = {}, ev_comb[kPipeMax] = {};
+    hipStream_t ss[2] = {nullptr, nullptr};  // sweep streams, alternating batch by batch
+    hipEvent_t ev_swept[kPipeMax] = {}, ev_comb[kPipeMax] = {}, ev_decoded[kPipeMax] = {};
+    hipEvent_t ev_in = nullptr, ev_ctx = nullptr;  // caller stream -> sweep stream, context stream -> sweep stream
+    hipEvent_t ev_last[2] = {nullptr, nullptr};    // after the newest sweep on each sweep stream
+    bool swept[2] = {false, false};
+    bool reads_outstanding = false;                // sweeps since the last fence
+    uint64_t ctx_seen = ~0ull;                     // ctx_seq the sweep streams were last ordered after
     ShardSlot slot[kPipeMax];
     std::deque<Pending> pending;
     uint64_t submitted = 0;
     uint32_t depth = 4, group = 4;
-    hipStream_t pipe_stream = nullptr;  // the stream the pending batches were submitted on
+    hipStream_t ds = nullptr;           // decode stream (the drains; callers wait on it in ms_sharded_drain)
+    hipEvent_t ev_ds = nullptr;
     // node-sharded exact sequential
     uint32_t seq_w = 0;
     ms_pod_rec *win_pods = nullptr;
@@ -127,9 +142,12 @@ void slice_of(const CommState &m, uint32_t n, uint32_t &first, uint32_t &count) 
     count = std::min<uint32_t>(n, first + per) - first;
 }
 
-// Decodes of the oldest k pending batches on s (after their combines).
-int drain_locked(ms_ctx *c, hipStream_t s, size_t k) {
+// Decodes of the oldest k pending batches on the decode stream (after their
+// combines). The caller's stream is not involved: a sweep stream that orders
+// after the caller's stream would otherwise wait for these combines too.
+int drain_locked(ms_ctx *c, size_t k) {
     CommState &m = *c->comm;
+    const hipStream_t s = m.ds;
     k = std::min(k, m.pending.size());
     if (k == 0) return MS_OK;
     MS_HIP(c, hipStreamWaitEvent(s, m.ev_comb[m.pending[k - 1].slot], 0));  // collectives run in issue order
@@ -151,41 +169,55 @@ int drain_locked(ms_ctx *c, hipStream_t s, size_t k) {
         }
         MS_HIP(c, launch_decode_slices(jobs, (uint32_t)k, s));
     }
+    for (size_t i = 0; i < k; ++i) MS_HIP(c, hipEventRecord(m.ev_decoded[m.pending[i].slot], s));
     m.pending.erase(m.pending.begin(), m.pending.begin() + (long)k);
     return MS_OK;
 }
 
-// Everything pending, on the stream it was submitted on; the context stream
-// then waits for it (later submits on another stream reuse its buffers).
-int drain_all_locked(ms_ctx *c) {
+// Everything pending decoded; then `s` waits for the decode stream.
+int drain_to(ms_ctx *c, hipStream_t s) {
     CommState &m = *c->comm;
-    if (m.pending.empty()) return MS_OK;
-    int rc = drain_locked(c, m.pipe_stream, m.pending.size());
+    int rc = drain_locked(c, m.pending.size());
     if (rc) return rc;
-    return chain_back(c, m.pipe_stream);
+    MS_HIP(c, hipEventRecord(m.ev_ds, m.ds));
+    MS_HIP(c, hipStreamWaitEvent(s, m.ev_ds, 0));
+    return MS_OK;
 }
 
 int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
     CommState &m = *c->comm;
     int rc = MS_OK;
-    if (!m.pending.empty() && m.pipe_stream != s) {
-        rc = drain_all_locked(c);
-        if (rc) return rc;
-    }
-    rc = order_after_ctx_stream(c, s);  // deltas, binds and the other stream's drains come first
-    if (rc) return rc;
-    m.pipe_stream = s;
     const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
     const uint32_t si = (uint32_t)(m.submitted % (m.depth + 1));
+    const int xi = (int)(m.submitted & 1u);
+    const hipStream_t X = m.ss[xi];
     ShardSlot &sl = m.slot[si];
     rc = slot_ensure(c, sl, per);
     if (rc) return rc;
+    // the sweep stream after: the caller's stream (its pods), the context stream
+    // when it wrote the table since (deltas, binds), the slot's previous
+    // collective (it read the keys this sweep overwrites)
+    MS_HIP(c, hipEventRecord(m.ev_in, s));
+    MS_HIP(c, hipStreamWaitEvent(X, m.ev_in, 0));
+    if (m.ctx_seen != c->ctx_seq) {
+        MS_HIP(c, hipEventRecord(m.ev_ctx, c->stream));
+        MS_HIP(c, hipStreamWaitEvent(X, m.ev_ctx, 0));
+        MS_HIP(c, hipStreamWaitEvent(m.ss[xi ^ 1], m.ev_ctx, 0));
+        m.ctx_seen = c->ctx_seq;
+    }
+    if (sl.used) MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
     const int ps = c->cfg.plugin_set;
-    rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, s);
+    rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X);
     if (rc) return rc;
-    MS_HIP(c, hipMemsetD32Async(sl.pres, c->present_dev ? 1u : 0u, G, s));
-    MS_HIP(c, hipEventRecord(m.ev_swept[si], s));
+    MS_HIP(c, hipMemsetD32Async(sl.pres, c->present_dev ? 1u : 0u, G, X));
+    MS_HIP(c, hipEventRecord(m.ev_swept[si], X));
+    MS_HIP(c, hipEventRecord(m.ev_last[xi], X));
+    m.swept[xi] = true;
+    m.reads_outstanding = true;
+    // the collective after the sweep and after the slot's previous decode (it read keys_mine)
     MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_swept[si], 0));
+    if (sl.used) MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_decoded[si], 0));
+    sl.used = true;
     ncclResult_t r = ncclGroupStart();
     if (r == ncclSuccess) r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
     if (r == ncclSuccess) r = ncclReduceScatter(sl.pres, sl.pres_mine, 1, ncclUint32, ncclMax, m.comm, m.cs);
@@ -201,9 +233,7 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     slice_of(m, n, p.first, p.count);
     m.pending.push_back(p);
     ++m.submitted;
-    rc = chain_back(c, s);  // the context stream waits for the sweep (it read the table)
-    if (rc) return rc;
-    if (m.pending.size() > m.depth) return drain_locked(c, s, std::min<size_t>(m.group, m.pending.size()));
+    if (m.pending.size() > m.depth) return drain_locked(c, std::min<size_t>(m.group, m.pending.size()));
     return MS_OK;
 }
 
@@ -292,7 +322,7 @@ int batched_all_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result 
     const uint32_t per = cdiv(n, (uint32_t)m.world);
     int rc = submit_locked(c, n, pods, stage + first, s);
     if (rc) return rc;
-    rc = drain_locked(c, s, m.pending.size());
+    rc = drain_to(c, s);
     if (rc) return rc;
     // (a rank whose slice is short or empty sends entries past n: never read)
     const size_t bytes = (size_t)per * sizeof(ms_result);
@@ -308,18 +338,38 @@ void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world) {
     *world = c->comm ? c->comm->world : 0;
 }
 
+int comm_fence_reads(ms_ctx *c, hipStream_t writer) {
+    CommState *m = c->comm;
+    if (!m || !m->reads_outstanding) return 0;
+    for (int i = 0; i < 2; ++i)
+        if (m->swept[i]) MS_HIP(c, hipStreamWaitEvent(writer, m->ev_last[i], 0));
+    m->reads_outstanding = false;
+    return 1;
+}
+
 void comm_free(ms_ctx *c) {
     CommState *m = c->comm;
     if (!m) return;
+    for (hipStream_t q : m->ss)
+        if (q) (void)hipStreamSynchronize(q);
     if (m->cs) (void)hipStreamSynchronize(m->cs);
-    if (m->pipe_stream) (void)hipStreamSynchronize(m->pipe_stream);
+    if (m->ds) (void)hipStreamSynchronize(m->ds);
     (void)hipDeviceSynchronize();
     if (m->comm) (void)ncclCommDestroy(m->comm);
     for (uint32_t i = 0; i < kPipeMax; ++i) {
         free_slot(m->slot[i]);
         if (m->ev_swept[i]) (void)hipEventDestroy(m->ev_swept[i]);
         if (m->ev_comb[i]) (void)hipEventDestroy(m->ev_comb[i]);
+        if (m->ev_decoded[i]) (void)hipEventDestroy(m->ev_decoded[i]);
     }
+    for (hipEvent_t e : m->ev_last)
+        if (e) (void)hipEventDestroy(e);
+    if (m->ev_in) (void)hipEventDestroy(m->ev_in);
+    if (m->ev_ds) (void)hipEventDestroy(m->ev_ds);
+    if (m->ds) (void)hipStreamDestroy(m->ds);
+    if (m->ev_ctx) (void)hipEventDestroy(m->ev_ctx);
+    for (hipStream_t q : m->ss)
+        if (q) (void)hipStreamDestroy(q);
     void *dev[] = {m->win_pods, m->win_res, m->ctl, m->cands, m->cands_all, m->merged, m->sflags, m->sflags_all,
                    m->merged_flags};
     for (void *q : dev)
@@ -341,7 +391,7 @@ int comm_cycle_staged(ms_ctx *c, uint32_t n, int32_t mode) {
 
 int comm_stage(ms_ctx *c, uint32_t n) {
     CommState &m = *c->comm;
-    int rc = drain_all_locked(c);  // device-resident batches in flight use the combine buffers
+    int rc = drain_to(c, c->stream);  // device-resident batches in flight finish first
     if (rc) return rc;
     const uint32_t per = cdiv(n, (uint32_t)m.world);
     return ensure_stage(c, std::max<uint32_t>(n, per * (uint32_t)m.world));
@@ -364,7 +414,7 @@ int comm_schedule_device(ms_ctx *c, uint32_t n, const ms_pod_rec *pods_dev, ms_r
     if (!plugins_stateless(c)) return seq_sharded_locked(c, n, pods_dev, results_dev, s);
     // NU+NN / NodeAffinity: the batched cycle with its binds (equal to the queue-order loop)
     const uint32_t per = cdiv(n, (uint32_t)m.world);
-    int rc = drain_all_locked(c);
+    int rc = drain_to(c, s);
     if (rc) return rc;
     rc = ensure_stage(c, per * (uint32_t)m.world);
     if (rc) return rc;
@@ -399,16 +449,23 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     m->rank = rank;
     m->world = world;
     if (const char *e = getenv("MINISCHED_PIPE_DEPTH")) m->depth = (uint32_t)std::max(1, atoi(e));
-    m->depth = std::min<uint32_t>(m->depth, kPipeMax - 2);  // slot kPipeMax-1 stays free (ms_sharded_drain's event)
+    m->depth = std::min<uint32_t>(m->depth, kPipeMax - 1);
     m->group = m->depth;
     if (const char *e = getenv("MINISCHED_PIPE_GROUP")) m->group = (uint32_t)std::max(1, atoi(e));
     m->group = std::min(m->group, m->depth);
     c->comm = m;  // (comm_free releases a partial state)
     MS_HIP(c, hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking));
+    for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+    MS_HIP(c, hipStreamCreateWithFlags(&m->ds, hipStreamNonBlocking));
+    MS_HIP(c, hipEventCreateWithFlags(&m->ev_ds, hipEventDisableTiming));
     for (uint32_t i = 0; i < kPipeMax; ++i) {
         MS_HIP(c, hipEventCreateWithFlags(&m->ev_swept[i], hipEventDisableTiming));
         MS_HIP(c, hipEventCreateWithFlags(&m->ev_comb[i], hipEventDisableTiming));
+        MS_HIP(c, hipEventCreateWithFlags(&m->ev_decoded[i], hipEventDisableTiming));
     }
+    for (hipEvent_t &e : m->ev_last) MS_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MS_HIP(c, hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
+    MS_HIP(c, hipEventCreateWithFlags(&m->ev_ctx, hipEventDisableTiming));
     ncclUniqueId uid;
     std::memcpy(&uid, id->internal, sizeof(uid));
     const ncclResult_t r = ncclCommInitRank(&m->comm, world, uid, rank);
@@ -450,17 +507,7 @@ int ms_sharded_drain(ms_ctx *c, void *stream) {
     if (!c->comm) return fail(c, MS_E_INVAL, "ms_sharded_drain: the context has no communicator (ms_comm_init)");
     std::lock_guard<std::mutex> g(c->sched_mu);
     MS_HIP(c, hipSetDevice(c->cfg.device));
-    CommState &m = *c->comm;
-    if (m.pending.empty()) return MS_OK;
-    const hipStream_t ps = m.pipe_stream, s = pick_stream(c, stream);
-    int rc = drain_locked(c, ps, m.pending.size());
-    if (rc) return rc;
-    if (s != ps) {  // the caller's stream sees the decodes
-        hipEvent_t ev = m.ev_swept[kPipeMax - 1];  // (slot kPipeMax-1 is unused: depth + 1 < kPipeMax)
-        MS_HIP(c, hipEventRecord(ev, ps));
-        MS_HIP(c, hipStreamWaitEvent(s, ev, 0));
-    }
-    return chain_back(c, ps);
+    return drain_to(c, pick_stream(c, stream));
 }
 
 }  // extern "C"

@@ -93,6 +93,10 @@ struct ms_ctx {
     // at ctx_seq needs no new cross-stream wait (each costs ~6-10 us of idle
     // device time even when already signalled, tools/ubench/xstream).
     uint64_t ctx_seq = 0;
+    // fence_seq counts the times the context stream was made to wait for the
+    // communicator's in-flight sweeps (table readers on its internal streams,
+    // comm_fence_reads); a stream ordered before the last fence must wait again
+    uint64_t fence_seq = 0, ordered_fence = 0;
     hipStream_t ordered_stream = nullptr;
     uint64_t ordered_seq = 0;
     hipEvent_t ev_order = nullptr;
@@ -145,5 +149,9 @@ int comm_cycle_staged(ms_ctx *c, uint32_t n_pods, int32_t mode);
 int comm_schedule_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
                          hipStream_t s);
 void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world);
+// Makes `writer` wait for the node-sharded sweeps still reading the table on the
+// communicator's internal streams; returns 1 if it inserted waits, 0 if none
+// were outstanding (or no communicator), < 0 on failure.
+int comm_fence_reads(ms_ctx *c, hipStream_t writer);
 
 }  // namespace msgpu
