@@ -81,6 +81,7 @@ struct CommState {
     hipEvent_t ev_in = nullptr, ev_ctx = nullptr;  // caller stream -> sweep stream, context stream -> sweep stream
     hipEvent_t ev_last[2] = {nullptr, nullptr};    // after the newest sweep on each sweep stream
     bool swept[2] = {false, false};
+    bool one_stream = false;  // MINISCHED_SHARD_STREAMS=1: every sweep on one stream (A/B)
     bool reads_outstanding = false;                // sweeps since the last fence
     uint64_t ctx_seen = ~0ull;                     // ctx_seq the sweep streams were last ordered after
     ShardSlot slot[kPipeMax];
@@ -189,7 +190,7 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     int rc = MS_OK;
     const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
     const uint32_t si = (uint32_t)(m.submitted % (m.depth + 1));
-    const int xi = (int)(m.submitted & 1u);
+    const int xi = m.one_stream ? 0 : (int)(m.submitted & 1u);
     const hipStream_t X = m.ss[xi];
     ShardSlot &sl = m.slot[si];
     rc = slot_ensure(c, sl, per);
@@ -453,6 +454,7 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     m->group = m->depth;
     if (const char *e = getenv("MINISCHED_PIPE_GROUP")) m->group = (uint32_t)std::max(1, atoi(e));
     m->group = std::min(m->group, m->depth);
+    if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->one_stream = atoi(e) == 1;
     c->comm = m;  // (comm_free releases a partial state)
     MS_HIP(c, hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking));
     for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithFlags(&q, hipStreamNonBlocking));

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-rank step of bench.py's N > 1 path through the in-library communicator,
+on one GPU: a 1-rank communicator whose context holds the shard rank G-1 of
+config C would own (100k/G rows), stepping all 100k pods through
+ms_sharded_submit (sweep on the alternating sweep streams, reduce-scatter,
+slice decode on the decode stream) exactly as ShardedCycle does, K steps
+between HIP events, then ms_sharded_drain. With one rank the reduce-scatter is
+a copy and the slice is all 100k pods (a G-rank slice is 100k/G), so this
+slightly over-counts the decode. MINISCHED_SHARD_STREAMS=1 (set per variant)
+puts every sweep on one stream.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mini-kube-scheduler_amd"))
+
+
+def main():
+    import torch
+
+    from minisched_amd import _lib, sharded, synth
+
+    N, P, K = 100_000, 100_000, int(os.environ.get("PROBE_STEPS", 100))
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pods = torch.from_numpy(synth.pods(P, seed=1).view(np.uint8).copy()).to(dev)
+    out = {}
+    for streams in ("2", "1"):
+        os.environ["MINISCHED_SHARD_STREAMS"] = streams
+        for G in (1, 2, 4, 8, 16):
+            lo, hi = sharded.shard_bounds(N, G - 1, G)
+            eng = _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=1)
+            eng.upsert(np.arange(lo, hi), synth.nodes(hi - lo, seed=1, start=lo))
+            eng.flush()
+            sharded.init_comm(eng)
+            cyc = sharded.ShardedCycle(eng, N, P, pods, s)
+            for _ in range(10):
+                cyc.step()
+            cyc.finish()
+            s.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(K):
+                cyc.step()
+            cyc.finish()
+            e1.record(s)
+            e1.synchronize()
+            out[f"G{G}_streams{streams}_us"] = round(e0.elapsed_time(e1) * 1e3 / K, 2)
+            eng.close()
+            print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
