@@ -17,7 +17,7 @@
  * function returns 0 (MS_OK) or a negative MS_E_* code and never aborts the
  * process; per-pod outcomes are data in ms_result, not errors.
  *
- * Node ordinals are global (0 .. 2^20-2). A context owns the contiguous
+ * Node ordinals are global (0 .. MS_MAX_ORDINAL = 2^20-3). A context owns the contiguous
  * ordinal range [node_base, node_base + max_nodes) — one shard when nodes are
  * split across GPUs. The tie-break that replaces rand.Intn
  * (minisched.go:316-321) is the packed key
@@ -76,7 +76,7 @@ extern "C" {
 #define MS_MASK_NODE_UNSCHEDULABLE (1u << 0) /* "NodeUnschedulable" */
 #define MS_MASK_NODE_RESOURCES_FIT (1u << 1) /* "NodeResourcesFit"  */
 
-#define MS_MAX_ORDINAL 0xFFFFEu
+#define MS_MAX_ORDINAL 0xFFFFDu /* (keys 0 and 1 are reserved: no feasible node) */
 
 /* Flat node record (v1.Node + framework.NodeInfo columns the plugins read).
  * 64 bytes. Resource columns are ignored by MS_PLUGINS_NU_NN. */
@@ -210,7 +210,10 @@ int ms_uncommit_bind(ms_ctx *ctx, uint32_t ordinal, const ms_pod_rec *pod);
  * the stream.
  *
  * ms_sweep_device: this shard's part of filter+score+selectHost for a batch.
- *   keys[i]  = max packed key over this shard's feasible nodes (0 = none)
+ *   keys[i]  = max packed key over this shard's feasible nodes; with none, 1
+ *              when this shard lists at least one node, else 0 (real keys
+ *              are >= 2), so the MAX over the shards also tells the decode
+ *              whether the cluster lists any node
  *   flags[i] = byte 0: some node here rejected by NodeUnschedulable (0/1),
  *              byte 1: some node here rejected by NodeResourcesFit  (0/1)
  *   Both arrays are overwritten. MS_PLUGINS_NU_NN takes no flags (NULL; the
@@ -221,8 +224,9 @@ int ms_uncommit_bind(ms_ctx *ctx, uint32_t ordinal, const ms_pod_rec *pod);
  *   normalise anchor, ((0xFFFFF - ordinal) << 1 | NodeNumber match) + 1 of this
  *   shard's first feasible node with a non-zero NodeAffinity score (0 = none);
  *   shards combine it with an element-wise uint32 MAX.
- * ms_decode_device: combined keys/flags -> ms_result. present_nodes is the
- *   global count of present nodes (used when flags is NULL).
+ * ms_decode_device: combined keys/flags -> ms_result. present_nodes: the
+ *   global count of present nodes, or 0 to take it from the combined key (1 =
+ *   some node listed); used when flags is NULL.
  * ms_apply_binds_device: NodeInfo.AddPod on this shard for every SUCCESS
  *   in results (the batched-mode bind commit). */
 int ms_sweep_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint64_t *keys_dev,

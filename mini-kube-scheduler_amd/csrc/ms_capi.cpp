@@ -363,12 +363,12 @@ int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned 
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
                                   c->num_cus, s));
     } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
-        MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
+        MS_HIP(c, launch_fill_keys(keys, n_pods, c->present_dev ? kKeyListed : 0ull, s));
         MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
         MS_HIP(c, launch_sweep_na(c->t, c->rows_dev, d_pods, n_pods, seed32, c->w_nn, c->w_na, keys, flags,
                                   c->num_cus, s));
     } else {
-        MS_HIP(c, hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s));
+        MS_HIP(c, launch_fill_keys(keys, n_pods, c->present_dev ? kKeyListed : 0ull, s));
         if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
         MS_HIP(c, launch_sweep_full(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
     }

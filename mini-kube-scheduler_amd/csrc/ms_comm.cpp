@@ -11,11 +11,13 @@
 // on the collective stream:
 //   keys   uint64 MAX, G x per pods -> this rank's slice of per pods (the keys
 //          embed the global ordinal, so MAX is the global argmax);
+//          A pod with no feasible node on a shard has key 1 there when the
+//          shard lists a node (kKeyListed), so the MAX also carries the NU+NN /
+//          NodeAffinity FitError mask: F = 0 with a listed node means
+//          NodeUnschedulable rejected every node;
 //   flags  NodeResourcesFit set: uint8 MAX of the filter bytes (byte-wise OR =
 //          FitError's UnschedulablePlugins over the cluster, :130-137);
 //          NodeAffinity set: uint32 MAX of the normalise anchors;
-//   pres   uint32 MAX of "this shard lists a node" (the NU+NN / NA FitError
-//          mask: F = 0 with a listed node means NodeUnschedulable rejected it);
 // -> the decode of the slice on the caller's stream. Pipelined: the decodes of
 // batch k are enqueued once `depth` later batches were submitted, so batch k's
 // collective overlaps their sweeps (RCCL runs one communicator's collectives in
@@ -39,6 +41,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -59,9 +63,9 @@ struct ShardSlot {
     unsigned long long *keys = nullptr;       // G x cap: this shard's maxima, pod order
     unsigned long long *keys_mine = nullptr;  // cap: the cluster's maxima of this rank's slice
     uint32_t *flags = nullptr, *flags_mine = nullptr;
-    uint32_t *pres = nullptr, *pres_mine = nullptr;  // G words / 1 word
-    uint32_t cap = 0;                                // pods per slice the buffers hold
-    bool used = false;                               // a batch went through this slot
+    uint32_t cap = 0;       // pods per slice the buffers hold
+    bool used = false;      // a batch went through this slot
+    uint64_t dec_gen = 0;   // the drain that decoded its last batch
 };
 
 struct Pending {
@@ -77,10 +81,10 @@ struct CommState {
     int rank = 0, world = 1;
     hipStream_t cs = nullptr;  // collective stream
     hipStream_t ss[2] = {nullptr, nullptr};  // sweep streams, alternating batch by batch
-    hipEvent_t ev_swept[kPipeMax] = {}, ev_comb[kPipeMax] = {}, ev_decoded[kPipeMax] = {};
+    hipEvent_t ev_swept[kPipeMax] = {}, ev_comb[kPipeMax] = {};
     hipEvent_t ev_in = nullptr, ev_ctx = nullptr;  // caller stream -> sweep stream, context stream -> sweep stream
-    hipEvent_t ev_last[2] = {nullptr, nullptr};    // after the newest sweep on each sweep stream
-    bool swept[2] = {false, false};
+    hipEvent_t ev_drained = nullptr;               // after the newest drain's decodes (decode stream)
+    uint64_t drains = 0, cs_drain_seen = 0;        // drains enqueued / the newest the collective stream waited for
     bool one_stream = false;  // MINISCHED_SHARD_STREAMS=1: every sweep on one stream (A/B)
     bool reads_outstanding = false;                // sweeps since the last fence
     uint64_t ctx_seen = ~0ull;                     // ctx_seq the sweep streams were last ordered after
@@ -99,6 +103,9 @@ struct CommState {
     ms_seq_cand *cands = nullptr, *cands_all = nullptr, *merged = nullptr;
     uint32_t *sflags = nullptr, *sflags_all = nullptr, *merged_flags = nullptr;
     uint64_t seq_windows = 0, seq_rounds = 0;
+    // MINISCHED_HOST_PROF=1: host time of ms_sharded_submit's phases (ns), printed at ms_destroy
+    bool host_prof = false;
+    uint64_t hp[6] = {0, 0, 0, 0, 0, 0}, hp_calls = 0;
 };
 
 namespace {
@@ -111,7 +118,7 @@ namespace {
     } while (0)
 
 void free_slot(ShardSlot &sl) {
-    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.pres, sl.pres_mine};
+    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine};
     for (void *q : p)
         if (q) (void)hipFree(q);
     sl = ShardSlot{};
@@ -127,9 +134,7 @@ int slot_ensure(ms_ctx *c, ShardSlot &sl, uint32_t per) {
     if (hipMalloc((void **)&sl.keys, G * cap * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&sl.keys_mine, cap * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&sl.flags, G * cap * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&sl.pres, G * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&sl.pres_mine, sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess) {
         free_slot(sl);
         return fail(c, MS_E_OOM, "sharded combine buffers");
     }
@@ -157,7 +162,7 @@ int drain_locked(ms_ctx *c, size_t k) {
             const Pending &p = m.pending[i];
             const ShardSlot &sl = m.slot[p.slot];
             MS_HIP(c, launch_decode_na(p.pods + p.first, p.count, sl.keys_mine, sl.flags_mine, 0, seed32_of(c->cfg.seed),
-                                       c->w_nn, c->w_na, p.results, s, sl.pres_mine));
+                                       c->w_nn, c->w_na, p.results, s));
         }
     } else {
         SliceJob jobs[kMaxSliceJobs];
@@ -165,12 +170,14 @@ int drain_locked(ms_ctx *c, size_t k) {
         for (size_t i = 0; i < k; ++i) {
             const Pending &p = m.pending[i];
             const ShardSlot &sl = m.slot[p.slot];
-            jobs[i] = SliceJob{p.pods + p.first, sl.keys_mine, nrf ? sl.flags_mine : nullptr, sl.pres_mine, p.results,
+            jobs[i] = SliceJob{p.pods + p.first, sl.keys_mine, nrf ? sl.flags_mine : nullptr, nullptr, p.results,
                                p.count, 0};
         }
         MS_HIP(c, launch_decode_slices(jobs, (uint32_t)k, s));
     }
-    for (size_t i = 0; i < k; ++i) MS_HIP(c, hipEventRecord(m.ev_decoded[m.pending[i].slot], s));
+    ++m.drains;
+    for (size_t i = 0; i < k; ++i) m.slot[m.pending[i].slot].dec_gen = m.drains;
+    MS_HIP(c, hipEventRecord(m.ev_drained, s));
     m.pending.erase(m.pending.begin(), m.pending.begin() + (long)k);
     return MS_OK;
 }
@@ -185,9 +192,19 @@ int drain_to(ms_ctx *c, hipStream_t s) {
     return MS_OK;
 }
 
+using HostClock = std::chrono::steady_clock;
+inline void host_tick(CommState &m, int i, HostClock::time_point &t) {
+    if (!m.host_prof) return;
+    const auto now = HostClock::now();
+    m.hp[i] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+    t = now;
+}
+
 int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
     CommState &m = *c->comm;
     int rc = MS_OK;
+    HostClock::time_point tp = m.host_prof ? HostClock::now() : HostClock::time_point();
+    if (m.host_prof) ++m.hp_calls;
     const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
     const uint32_t si = (uint32_t)(m.submitted % (m.depth + 1));
     const int xi = m.one_stream ? 0 : (int)(m.submitted & 1u);
@@ -207,35 +224,45 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
         m.ctx_seen = c->ctx_seq;
     }
     if (sl.used) MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
+    host_tick(m, 0, tp);  // ordering of the sweep stream
     const int ps = c->cfg.plugin_set;
     rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X);
     if (rc) return rc;
-    MS_HIP(c, hipMemsetD32Async(sl.pres, c->present_dev ? 1u : 0u, G, X));
+    host_tick(m, 1, tp);  // the sweep launch
     MS_HIP(c, hipEventRecord(m.ev_swept[si], X));
-    MS_HIP(c, hipEventRecord(m.ev_last[xi], X));
-    m.swept[xi] = true;
     m.reads_outstanding = true;
-    // the collective after the sweep and after the slot's previous decode (it read keys_mine)
+    // the collective after the sweep, and after the drain that decoded the
+    // slot's previous batch (it read keys_mine); one wait covers a whole drain
     MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_swept[si], 0));
-    if (sl.used) MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_decoded[si], 0));
+    if (sl.used && sl.dec_gen > m.cs_drain_seen) {
+        MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_drained, 0));
+        m.cs_drain_seen = m.drains;
+    }
     sl.used = true;
-    ncclResult_t r = ncclGroupStart();
-    if (r == ncclSuccess) r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
-    if (r == ncclSuccess) r = ncclReduceScatter(sl.pres, sl.pres_mine, 1, ncclUint32, ncclMax, m.comm, m.cs);
-    if (r == ncclSuccess && ps == MS_PLUGINS_NU_NRF_NN_LA)  // 0/1 bytes: uint8 MAX = OR
-        r = ncclReduceScatter(sl.flags, sl.flags_mine, (size_t)per * 4, ncclUint8, ncclMax, m.comm, m.cs);
-    if (r == ncclSuccess && ps == MS_PLUGINS_NU_NN_NA)  // anchors < 2^21: uint32 MAX
-        r = ncclReduceScatter(sl.flags, sl.flags_mine, per, ncclUint32, ncclMax, m.comm, m.cs);
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r == ncclSuccess) r = r2;
+    host_tick(m, 2, tp);  // events to the collective stream
+    ncclResult_t r = ncclSuccess;
+    if (ps == MS_PLUGINS_NU_NN) {  // the keys alone: one call, no group
+        r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
+    } else {
+        r = ncclGroupStart();
+        if (r == ncclSuccess) r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
+        if (r == ncclSuccess && ps == MS_PLUGINS_NU_NRF_NN_LA)  // 0/1 bytes: uint8 MAX = OR
+            r = ncclReduceScatter(sl.flags, sl.flags_mine, (size_t)per * 4, ncclUint8, ncclMax, m.comm, m.cs);
+        if (r == ncclSuccess && ps == MS_PLUGINS_NU_NN_NA)  // anchors < 2^21: uint32 MAX
+            r = ncclReduceScatter(sl.flags, sl.flags_mine, per, ncclUint32, ncclMax, m.comm, m.cs);
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
+    }
     if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sharded reduce-scatter: ") + ncclGetErrorString(r));
+    host_tick(m, 3, tp);  // the grouped reduce-scatter
     MS_HIP(c, hipEventRecord(m.ev_comb[si], m.cs));
     Pending p{si, n, 0, 0, pods, results};
     slice_of(m, n, p.first, p.count);
     m.pending.push_back(p);
     ++m.submitted;
-    if (m.pending.size() > m.depth) return drain_locked(c, std::min<size_t>(m.group, m.pending.size()));
-    return MS_OK;
+    if (m.pending.size() > m.depth) rc = drain_locked(c, std::min<size_t>(m.group, m.pending.size()));
+    host_tick(m, 4, tp);  // bookkeeping + drains
+    return rc;
 }
 
 // Sequential-window buffers for windows of w pods.
@@ -342,8 +369,10 @@ void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world) {
 int comm_fence_reads(ms_ctx *c, hipStream_t writer) {
     CommState *m = c->comm;
     if (!m || !m->reads_outstanding) return 0;
-    for (int i = 0; i < 2; ++i)
-        if (m->swept[i]) MS_HIP(c, hipStreamWaitEvent(writer, m->ev_last[i], 0));
+    // every sweep in flight is the newest of its slot (a slot is swept again only
+    // after the collective that read its previous sweep): wait for each slot's
+    for (uint32_t i = 0; i < kPipeMax; ++i)
+        if (m->slot[i].used) MS_HIP(c, hipStreamWaitEvent(writer, m->ev_swept[i], 0));
     m->reads_outstanding = false;
     return 1;
 }
@@ -351,6 +380,10 @@ int comm_fence_reads(ms_ctx *c, hipStream_t writer) {
 void comm_free(ms_ctx *c) {
     CommState *m = c->comm;
     if (!m) return;
+    if (m->host_prof && m->hp_calls)
+        std::fprintf(stderr, "MS_HOST_PROF submits=%llu us/submit: order=%.2f sweep=%.2f events=%.2f rccl=%.2f tail=%.2f\n",
+                     (unsigned long long)m->hp_calls, m->hp[0] * 1e-3 / m->hp_calls, m->hp[1] * 1e-3 / m->hp_calls,
+                     m->hp[2] * 1e-3 / m->hp_calls, m->hp[3] * 1e-3 / m->hp_calls, m->hp[4] * 1e-3 / m->hp_calls);
     for (hipStream_t q : m->ss)
         if (q) (void)hipStreamSynchronize(q);
     if (m->cs) (void)hipStreamSynchronize(m->cs);
@@ -361,10 +394,8 @@ void comm_free(ms_ctx *c) {
         free_slot(m->slot[i]);
         if (m->ev_swept[i]) (void)hipEventDestroy(m->ev_swept[i]);
         if (m->ev_comb[i]) (void)hipEventDestroy(m->ev_comb[i]);
-        if (m->ev_decoded[i]) (void)hipEventDestroy(m->ev_decoded[i]);
     }
-    for (hipEvent_t e : m->ev_last)
-        if (e) (void)hipEventDestroy(e);
+    if (m->ev_drained) (void)hipEventDestroy(m->ev_drained);
     if (m->ev_in) (void)hipEventDestroy(m->ev_in);
     if (m->ev_ds) (void)hipEventDestroy(m->ev_ds);
     if (m->ds) (void)hipStreamDestroy(m->ds);
@@ -455,17 +486,25 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     if (const char *e = getenv("MINISCHED_PIPE_GROUP")) m->group = (uint32_t)std::max(1, atoi(e));
     m->group = std::min(m->group, m->depth);
     if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->one_stream = atoi(e) == 1;
+    if (const char *e = getenv("MINISCHED_HOST_PROF")) m->host_prof = atoi(e) == 1;
     c->comm = m;  // (comm_free releases a partial state)
     MS_HIP(c, hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking));
-    for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+    // the sweep streams must land on different hardware queues to overlap:
+    // normal-priority streams share the process's GPU_MAX_HW_QUEUES queues with
+    // torch's and ours, and both sweep streams were seen on one queue; created
+    // with the highest priority they get queues of their own (tools/
+    // gpu_queues_r03.sh). MINISCHED_SWEEP_PRIO=0: normal priority (A/B)
+    const char *pe = getenv("MINISCHED_SWEEP_PRIO");
+    int lo = 0, hi = 0;
+    if (!(pe && atoi(pe) == 0)) MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi));
     MS_HIP(c, hipStreamCreateWithFlags(&m->ds, hipStreamNonBlocking));
     MS_HIP(c, hipEventCreateWithFlags(&m->ev_ds, hipEventDisableTiming));
     for (uint32_t i = 0; i < kPipeMax; ++i) {
         MS_HIP(c, hipEventCreateWithFlags(&m->ev_swept[i], hipEventDisableTiming));
         MS_HIP(c, hipEventCreateWithFlags(&m->ev_comb[i], hipEventDisableTiming));
-        MS_HIP(c, hipEventCreateWithFlags(&m->ev_decoded[i], hipEventDisableTiming));
     }
-    for (hipEvent_t &e : m->ev_last) MS_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MS_HIP(c, hipEventCreateWithFlags(&m->ev_drained, hipEventDisableTiming));
     MS_HIP(c, hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
     MS_HIP(c, hipEventCreateWithFlags(&m->ev_ctx, hipEventDisableTiming));
     ncclUniqueId uid;

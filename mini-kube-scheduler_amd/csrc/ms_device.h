@@ -66,14 +66,17 @@ __device__ __forceinline__ uint32_t first_slot(uint32_t m) {
 }
 
 // Combined key -> per-pod outcome (minisched.go:143-148 FitError, :70-75 the
-// score-error path, :80 selectHost's node). flags: per-pod filter bytes of the
-// resource-aware set (byte 0 NU, byte 1 NRF) or nullptr for NU+NN, where the
-// mask follows from the key and the global present-node count.
+// score-error path, :80 selectHost's node). Keys 0 and 1 carry no node: 1 =
+// some shard lists a node but none is feasible (kKeyListed), 0 = no shard
+// lists any. flags: per-pod filter bytes of the resource-aware set (byte 0 NU,
+// byte 1 NRF) or nullptr for NU+NN / NodeAffinity, where NodeUnschedulable is
+// the only filter: F = 0 with a node listed (key 1, or a non-zero present
+// count) means it rejected every node.
 __device__ __forceinline__ ms_result decode_key(u64 k, int8_t pod_digit, const uint32_t *flags, uint32_t i,
                                                 uint32_t present) {
     ms_result r;
     r._pad = 0;
-    if (k == 0) {  // FitError: no feasible node anywhere
+    if (k <= kKeyListed) {  // FitError: no feasible node anywhere
         r.node = -1;
         r.code = MS_CODE_UNSCHEDULABLE;
         r.score = 0;
@@ -84,7 +87,7 @@ __device__ __forceinline__ ms_result decode_key(u64 k, int8_t pod_digit, const u
         } else {
             // NU+NN: NodeUnschedulable is the only filter, so F == 0 with at
             // least one node listed means every node was rejected by it.
-            r.plugin_mask = present ? MS_MASK_NODE_UNSCHEDULABLE : 0u;
+            r.plugin_mask = (k == kKeyListed || present) ? MS_MASK_NODE_UNSCHEDULABLE : 0u;
         }
     } else if (pod_digit < 0) {  // NodeNumber.Score error, F > 0
         r.node = -1;

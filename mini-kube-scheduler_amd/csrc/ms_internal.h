@@ -97,6 +97,12 @@ static_assert(sizeof(ms_result) == 24, "ms_result layout");
 static_assert(sizeof(ms_pod_compact) == 8, "ms_pod_compact layout");
 static_assert(sizeof(ms_result_compact) == 8, "ms_result_compact layout");
 
+// A shard's key for a pod with no feasible node on it: 1 when the shard lists at
+// least one node, else 0 (real keys are >= 2: ordinals stop at MS_MAX_ORDINAL =
+// 0xFFFFD, so the ordinal field 0xFFFFF - ordinal is >= 2). The element-wise MAX
+// over shards then also tells the decode whether the cluster lists any node.
+constexpr unsigned long long kKeyListed = 1ull;
+
 __host__ __device__ inline uint32_t fmix32(uint32_t h) {
     h ^= h >> 16;
     h *= 0x85ebca6bu;
@@ -157,6 +163,9 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
 constexpr uint32_t kPpMaxFusedRows = 16u * 64u * 4u * kGroupRows;
 // Rebuilds the bit planes of the groups touched by deltas (or all groups when d_deltas is null).
 hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, uint32_t n, hipStream_t s);
+// keys[0, n) = v (the atomicMax targets of the NodeAffinity / resource sweeps
+// start at kKeyListed when the shard lists a node, else 0)
+hipError_t launch_fill_keys(unsigned long long *keys, uint32_t n, unsigned long long v, hipStream_t s);
 // MS_PLUGINS_NU_NN_NA sweep (one pair per lane-slot): keys[i] = max packed key
 // with raw NodeAffinity scores, fkeys[i] = max over this shard's feasible nodes
 // with a non-zero raw NodeAffinity score of ((0xFFFFF - ordinal) << 1 | NN
@@ -248,7 +257,7 @@ struct SliceJob {
     const ms_pod_rec *pods;
     const unsigned long long *keys;
     const uint32_t *flags;    // NodeResourcesFit set: combined filter bytes; else nullptr
-    const uint32_t *present;  // device: non-zero iff some shard lists a node
+    const uint32_t *present;  // device present count, or nullptr: from the key (kKeyListed)
     ms_result *results;
     uint32_t n_pods, _pad;
 };

@@ -1976,7 +1976,7 @@ struct SliceJobs {
 __global__ void k_decode_slices(SliceJobs jobs) {
     const SliceJob &jb = jobs.j[blockIdx.y];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < jb.n_pods) decode_one(jb.pods, jb.keys, jb.flags, *jb.present, jb.results, i);
+    if (i < jb.n_pods) decode_one(jb.pods, jb.keys, jb.flags, jb.present ? *jb.present : 0u, jb.results, i);
 }
 
 // Node-sharded exact sequential with a device-side queue cursor (ms_comm.cpp):
@@ -2004,6 +2004,11 @@ __global__ void k_seq_window_out(const ms_result *__restrict__ win_res, uint32_t
     for (uint32_t i = threadIdx.x; i < done; i += blockDim.x) res[cur + i] = win_res[i];
     __syncthreads();  // every thread read ctl[0] before it moves
     if (threadIdx.x == 0) ctl[0] = cur + done;
+}
+
+__global__ void k_fill_keys(u64 *__restrict__ keys, uint32_t n, u64 v) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = v;
 }
 
 __global__ void k_pods_widen(const ms_pod_compact *__restrict__ in, uint32_t n, ms_pod_rec *__restrict__ out) {
@@ -2385,6 +2390,12 @@ hipError_t launch_apply_binds(const NodeTable &t, const ms_pod_rec *pods, uint32
                               hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     hipLaunchKernelGGL(k_apply_binds, dim3(cdiv(n_pods, 256)), dim3(256), 0, s, t, pods, n_pods, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_keys(unsigned long long *keys, uint32_t n, unsigned long long v, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_keys, dim3(cdiv(n, 256)), dim3(256), 0, s, reinterpret_cast<u64 *>(keys), n, (u64)v);
     return hipGetLastError();
 }
 

@@ -293,7 +293,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
         const u64 v = lds[i];
         const uint2 pe = pinfo[i];
-        u64 key = 0;
+        u64 key = present ? kKeyListed : 0ull;  // no feasible row: listed or not (decode_key)
         if (v) {
             const uint32_t h = (uint32_t)v;
             key = make_key((uint32_t)(v >> 32) - 1u, h, tb_unhash(pe.x, h));

@@ -29,7 +29,7 @@ MODE_SEQUENTIAL = 1
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE = 0, 1, 2
 MASK_NODE_UNSCHEDULABLE = 1
 MASK_NODE_RESOURCES_FIT = 2
-MAX_ORDINAL = 0xFFFFE
+MAX_ORDINAL = 0xFFFFD  # keys 0 / 1 are reserved (no feasible node)
 
 ERRNAMES = {
     MS_E_INVAL: "MS_E_INVAL",

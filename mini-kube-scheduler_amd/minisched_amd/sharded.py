@@ -271,6 +271,11 @@ class ShardedCycle:
             self._collective = True
             self._results = [torch.empty(max(1, n_mine) * self.RESULT_BYTES, dtype=torch.uint8, device=dev)]
             self._last = 0
+            # the step is one C call with fixed arguments: no torch stream context, no
+            # per-step pointer lookups (host enqueue time bounds the pipelined step at
+            # small shards)
+            self._submit_args = (engine.h, n_pods, pods_dev.data_ptr(), self._results[0].data_ptr(),
+                                 stream.cuda_stream)
             return
         self.a, self.b = pod_slice(n_pods, rank, world)
         # collective=True forces the Python node-split pipeline at world 1 (a 1-rank
@@ -356,11 +361,12 @@ class ShardedCycle:
     def step(self):
         import torch
 
+        if self._library:
+            rc = self.eng.lib.ms_sharded_submit(*self._submit_args)
+            if rc:
+                self.eng._check("ms_sharded_submit", rc)
+            return
         with torch.cuda.stream(self.stream):
-            if self._library:
-                self.eng.sharded_submit(self.P, self.pods.data_ptr(), self._results[0].data_ptr(),
-                                        self.stream.cuda_stream)
-                return
             if self._pipe is not None:
                 self._pipe.step()
                 return

@@ -12,6 +12,7 @@ puts every sweep on one stream.
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -29,9 +30,9 @@ def main():
     s = torch.cuda.Stream(device=dev)
     pods = torch.from_numpy(synth.pods(P, seed=1).view(np.uint8).copy()).to(dev)
     out = {}
-    for streams in ("2", "1"):
+    for streams in os.environ.get("PROBE_STREAMS", "2,1").split(","):
         os.environ["MINISCHED_SHARD_STREAMS"] = streams
-        for G in (1, 2, 4, 8, 16):
+        for G in [int(g) for g in os.environ.get("PROBE_G", "1,2,4,8,16").split(",")]:
             lo, hi = sharded.shard_bounds(N, G - 1, G)
             eng = _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=1)
             eng.upsert(np.arange(lo, hi), synth.nodes(hi - lo, seed=1, start=lo))
@@ -44,12 +45,23 @@ def main():
             s.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
+            t0 = time.perf_counter()
             for _ in range(K):
                 cyc.step()
+            host = time.perf_counter() - t0
             cyc.finish()
             e1.record(s)
             e1.synchronize()
             out[f"G{G}_streams{streams}_us"] = round(e0.elapsed_time(e1) * 1e3 / K, 2)
+            out[f"G{G}_streams{streams}_host_enqueue_us"] = round(host * 1e6 / K, 2)
+            # the sweep alone, back to back on one stream (the per-rank compute floor)
+            kb = torch.empty(P, dtype=torch.int64, device=dev)
+            e0.record(s)
+            for _ in range(K):
+                eng.sweep_device(P, pods.data_ptr(), kb.data_ptr(), 0, s.cuda_stream)
+            e1.record(s)
+            e1.synchronize()
+            out[f"G{G}_sweep_only_us"] = round(e0.elapsed_time(e1) * 1e3 / K, 2)
             eng.close()
             print(json.dumps(out), flush=True)
 
