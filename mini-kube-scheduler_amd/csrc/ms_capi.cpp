@@ -96,11 +96,6 @@ int ensure_delta_cap(ms_ctx *c, uint32_t n) {
 
 // Drains the delta queue onto the stream (caller holds sched_mu).
 int flush_locked(ms_ctx *c) {
-    // deltas and binds land on the context stream: after the sweeps still
-    // reading the table on the communicator's streams
-    const int fenced = comm_fence_reads(c, c->stream);
-    if (fenced < 0) return fenced;
-    if (fenced) ++c->fence_seq;
     std::vector<NodeDelta> batch;
     {
         std::lock_guard<std::mutex> g(c->delta_mu);
@@ -109,6 +104,11 @@ int flush_locked(ms_ctx *c) {
         c->present_dev = c->present_count;
     }
     if (batch.empty()) return MS_OK;
+    // the deltas land on the context stream: after the sweeps still reading the
+    // table on the communicator's streams
+    const int fenced = comm_fence_reads(c, c->stream);
+    if (fenced < 0) return fenced;
+    if (fenced) ++c->fence_seq;
     // later deltas to one row win: keep the last occurrence only
     std::unordered_map<uint32_t, uint32_t> last;
     last.reserve(batch.size() * 2);
@@ -824,6 +824,9 @@ static int bind_common(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod, int s
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
+    rc = comm_fence_reads(c, c->stream);  // (the bind writes the table: after in-flight sharded sweeps)
+    if (rc < 0) return rc;
+    if (rc) ++c->fence_seq;
     // the context stream already waits for earlier caller-stream work (chain_back)
     MS_HIP(c, hipMemcpyAsync(c->d_one, pod, sizeof(ms_pod_rec), hipMemcpyHostToDevice, c->stream));
     MS_HIP(c, launch_bind_one(c->t, ordinal - c->cfg.node_base, c->d_one, sign, c->stream));

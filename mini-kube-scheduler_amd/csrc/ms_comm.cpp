@@ -22,13 +22,17 @@
 // batch k are enqueued once `depth` later batches were submitted, so batch k's
 // collective overlaps their sweeps (RCCL runs one communicator's collectives in
 // issue order on the collective stream, so a drain waits for the newest only).
-// Consecutive sweeps alternate between two internal streams: on one stream each
-// launch waits for the previous one to drain, and at the strong-scaling shard
-// (12.5k rows x 100k pods) that ramp and tail were a quarter of the sweep
-// (55.4 vs 42.9 us per sweep, tools/probe_streams.py, profiles/r03_two_streams.json).
-// The sweeps only read the node table; writers (deltas, binds) are fenced
-// behind the in-flight ones (comm_fence_reads) instead of every sweep being
-// chained into the context stream, which would serialize them again.
+// The sweeps run on the caller's stream, the collectives on the collective
+// stream and the decodes on a decode stream, so no sweep waits for a
+// collective or a decode (one cross-queue wait per step: the collective on
+// its sweep). The sweeps only read the node table; writers (deltas, binds) are
+// fenced behind the in-flight ones (comm_fence_reads) instead of every sweep
+// being chained into the context stream. MINISCHED_SHARD_STREAMS=2 alternates
+// the sweeps over two internal streams instead (two independent streams on
+// separate hardware queues overlap one sweep's ramp and tail with the next:
+// 55.4 vs 42.9 us per 12.5k-row sweep, tools/probe_streams.py; but the
+// library's streams share the process's hardware queues and the extra waits
+// made the pipelined step slower: profiles/r03_step_streams_ab.json).
 //
 // Exact sequential cycle (config E): per window of W pods, every
 // shard's speculative top-4 with records (ms_seq_candidates_device) -> one
@@ -85,9 +89,10 @@ struct CommState {
     hipEvent_t ev_in = nullptr, ev_ctx = nullptr;  // caller stream -> sweep stream, context stream -> sweep stream
     hipEvent_t ev_drained = nullptr;               // after the newest drain's decodes (decode stream)
     uint64_t drains = 0, cs_drain_seen = 0;        // drains enqueued / the newest the collective stream waited for
-    bool one_stream = false;  // MINISCHED_SHARD_STREAMS=1: every sweep on one stream (A/B)
+    bool two_streams = false;  // MINISCHED_SHARD_STREAMS=2: sweeps alternate over ss[0], ss[1] (A/B)
     bool reads_outstanding = false;                // sweeps since the last fence
     uint64_t ctx_seen = ~0ull;                     // ctx_seq the sweep streams were last ordered after
+    hipStream_t ctx_seen_stream = nullptr;         // (and the caller's stream then)
     ShardSlot slot[kPipeMax];
     std::deque<Pending> pending;
     uint64_t submitted = 0;
@@ -207,21 +212,24 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     if (m.host_prof) ++m.hp_calls;
     const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
     const uint32_t si = (uint32_t)(m.submitted % (m.depth + 1));
-    const int xi = m.one_stream ? 0 : (int)(m.submitted & 1u);
-    const hipStream_t X = m.ss[xi];
+    const int xi = (int)(m.submitted & 1u);
+    const hipStream_t X = m.two_streams ? m.ss[xi] : s;
     ShardSlot &sl = m.slot[si];
     rc = slot_ensure(c, sl, per);
     if (rc) return rc;
     // the sweep stream after: the caller's stream (its pods), the context stream
     // when it wrote the table since (deltas, binds), the slot's previous
     // collective (it read the keys this sweep overwrites)
-    MS_HIP(c, hipEventRecord(m.ev_in, s));
-    MS_HIP(c, hipStreamWaitEvent(X, m.ev_in, 0));
-    if (m.ctx_seen != c->ctx_seq) {
+    if (X != s) {
+        MS_HIP(c, hipEventRecord(m.ev_in, s));
+        MS_HIP(c, hipStreamWaitEvent(X, m.ev_in, 0));
+    }
+    if (m.ctx_seen != c->ctx_seq || m.ctx_seen_stream != s) {
         MS_HIP(c, hipEventRecord(m.ev_ctx, c->stream));
         MS_HIP(c, hipStreamWaitEvent(X, m.ev_ctx, 0));
-        MS_HIP(c, hipStreamWaitEvent(m.ss[xi ^ 1], m.ev_ctx, 0));
+        if (m.two_streams) MS_HIP(c, hipStreamWaitEvent(m.ss[xi ^ 1], m.ev_ctx, 0));
         m.ctx_seen = c->ctx_seq;
+        m.ctx_seen_stream = s;
     }
     if (sl.used) MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
     host_tick(m, 0, tp);  // ordering of the sweep stream
@@ -485,18 +493,16 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     m->group = m->depth;
     if (const char *e = getenv("MINISCHED_PIPE_GROUP")) m->group = (uint32_t)std::max(1, atoi(e));
     m->group = std::min(m->group, m->depth);
-    if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->one_stream = atoi(e) == 1;
+    if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->two_streams = atoi(e) == 2;
     if (const char *e = getenv("MINISCHED_HOST_PROF")) m->host_prof = atoi(e) == 1;
     c->comm = m;  // (comm_free releases a partial state)
     MS_HIP(c, hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking));
-    // the sweep streams must land on different hardware queues to overlap:
-    // normal-priority streams share the process's GPU_MAX_HW_QUEUES queues with
-    // torch's and ours, and both sweep streams were seen on one queue; created
-    // with the highest priority they get queues of their own (tools/
-    // gpu_queues_r03.sh). MINISCHED_SWEEP_PRIO=0: normal priority (A/B)
+    // (MINISCHED_SHARD_STREAMS=2) MINISCHED_SWEEP_PRIO=1 creates the two sweep
+    // streams with the highest priority: they then land on queues of their own,
+    // but the collectives on the normal-priority stream fell behind (A/B)
     const char *pe = getenv("MINISCHED_SWEEP_PRIO");
     int lo = 0, hi = 0;
-    if (!(pe && atoi(pe) == 0)) MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    if (pe && atoi(pe) == 1) MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
     for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi));
     MS_HIP(c, hipStreamCreateWithFlags(&m->ds, hipStreamNonBlocking));
     MS_HIP(c, hipEventCreateWithFlags(&m->ev_ds, hipEventDisableTiming));

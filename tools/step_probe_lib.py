@@ -30,8 +30,14 @@ def main():
     s = torch.cuda.Stream(device=dev)
     pods = torch.from_numpy(synth.pods(P, seed=1).view(np.uint8).copy()).to(dev)
     out = {}
-    for streams in os.environ.get("PROBE_STREAMS", "2,1").split(","):
+    # PROBE_VARIANTS "prio:streams,...": MINISCHED_SWEEP_PRIO x MINISCHED_SHARD_STREAMS
+    variants = os.environ.get("PROBE_VARIANTS", "")
+    variants = [v.split(":") for v in variants.split(",")] if variants else \
+        [("1", st) for st in os.environ.get("PROBE_STREAMS", "2,1").split(",")]
+    for prio, streams in variants * int(os.environ.get("PROBE_REPEAT", "1")):
         os.environ["MINISCHED_SHARD_STREAMS"] = streams
+        os.environ["MINISCHED_SWEEP_PRIO"] = prio
+        streams = f"{streams}p{prio}"
         for G in [int(g) for g in os.environ.get("PROBE_G", "1,2,4,8,16").split(",")]:
             lo, hi = sharded.shard_bounds(N, G - 1, G)
             eng = _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=1)
@@ -52,8 +58,8 @@ def main():
             cyc.finish()
             e1.record(s)
             e1.synchronize()
-            out[f"G{G}_streams{streams}_us"] = round(e0.elapsed_time(e1) * 1e3 / K, 2)
-            out[f"G{G}_streams{streams}_host_enqueue_us"] = round(host * 1e6 / K, 2)
+            out.setdefault(f"G{G}_streams{streams}_us", []).append(round(e0.elapsed_time(e1) * 1e3 / K, 2))
+            out.setdefault(f"G{G}_streams{streams}_host_enqueue_us", []).append(round(host * 1e6 / K, 2))
             # the sweep alone, back to back on one stream (the per-rank compute floor)
             kb = torch.empty(P, dtype=torch.int64, device=dev)
             e0.record(s)
