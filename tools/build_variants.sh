@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B builds of libminisched_gpu.so with extra -D flags on ms_kernels.hip, for
+# MINISCHED_LIB=... runs (tools/gpu_*.sh). Usage: tools/build_variants.sh NAME "-DFOO=1 ..." [vst]
+# -> mini-kube-scheduler_amd/minisched_amd/libminisched_gpu_NAME.so (vst: with the MS_VSTAMPS stamps)
+set -e
+cd "$(dirname "$0")/../mini-kube-scheduler_amd"
+NAME=$1; DEFS=$2; VST=$3
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I../include -Icsrc"
+mkdir -p build
+if [ "$VST" = vst ]; then
+  $H -DMS_VSTAMPS $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
+  [ -f build/ms_capi_vst.o ] || $H -DMS_VSTAMPS -c csrc/ms_capi.cpp -o build/ms_capi_vst.o
+  CAPI=build/ms_capi_vst.o
+else
+  $H $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
+  CAPI=build/ms_capi.o
+fi
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o minisched_amd/libminisched_gpu_$NAME.so build/ms_kernels_$NAME.o build/ms_sweep_pp.o $CAPI build/ms_comm.o -L/opt/rocm/lib -lrccl
+echo built minisched_amd/libminisched_gpu_$NAME.so
