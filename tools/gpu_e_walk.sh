@@ -2,7 +2,7 @@
 # config E A/B: the default build against variant builds (tools/build_variants.sh), with phase stamps
 # usage: tools/gpu_e_walk.sh TAG "v1 v2 ..." "vst1 vst2 ..."
 set -o pipefail
-TAG=${1:-r03k}; VARS=${2:-"default w65"}; VSTS=${3:-"vw17 vw65"}
+TAG=${1:-r03k}; VARS=${2:-"default w65"}; VSTS=${3-"vw17 vw65"}
 mkdir -p gpurun_out/$TAG
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 T="timeout -k 10"
