@@ -219,7 +219,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
 // lists valid; more pods amortise the two launches. MINISCHED_SEQ_BATCH
 // overrides (tuning), clamped to the validator's LDS capacity.
 uint32_t seq_batch(const ms_ctx *) {
-    uint32_t b = 128;  // measured best for config E (profiles/r01_e_batch_sweep.jsonl)
+    uint32_t b = seq_batch_limit();  // the build's batch (128: profiles/r01_e_batch_sweep.jsonl, r03o)
     if (const char *e = getenv("MINISCHED_SEQ_BATCH")) b = (uint32_t)std::max(1, atoi(e));
     return std::min(b, seq_batch_limit());
 }

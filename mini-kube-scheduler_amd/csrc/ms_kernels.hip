@@ -715,7 +715,7 @@ __device__ __forceinline__ void sweep_tp_tile(const SweepArgs &a, uint32_t tile,
     __syncthreads();
     const TileBits tb = tile_bits(rows, lane);
     // groups outside the binary64 form's range (bit i: the wave's i-th group;
-    // a batch holds at most kSeqBatch = 128 pods, i.e. 8 groups)
+    // a batch holds at most kSeqBatch <= 256 pods, i.e. 16 groups)
     uint32_t redo = 0;
     for (uint32_t grp = wave, i = 0; grp * kTpPods < a.n_pods; grp += W, ++i)
         if (!sweep_tp_task(a, tile, grp, lane, rows, tb)) redo |= 1u << i;
@@ -887,7 +887,10 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
 //  - the bind (NodeInfo.AddPod) updates that LDS record, one field per lane.
 // Results and records stay in LDS until the batch ends.
 // ----------------------------------------------------------------------------
-constexpr int kSeqBatch = 128;  // pods per speculative batch (host clamps)
+#ifndef MS_SEQ_BATCH
+#define MS_SEQ_BATCH 128
+#endif
+constexpr int kSeqBatch = MS_SEQ_BATCH;  // pods per speculative batch (host clamps); a multiple of 64
 constexpr int kMapBits = 11;
 constexpr int kMapCap = 1 << kMapBits;  // >= 4 x the nodes a batch and its predecessor bind
 constexpr int kSeqMaxJ = 16;            // tile lists per lane in registers: n_tiles <= 1024 (262k rows)
@@ -896,9 +899,11 @@ constexpr int kClaimCap = 1 << kClaimBits;
 constexpr uint32_t kForceSlow = 0xFFFFu;  // spec_slot: speculation could not be re-resolved
 constexpr int kPrevCap = 2 * kSeqBatch;              // stale nodes: the two previous batches' binds
 constexpr int kPrevSlot0 = kTopK * kSeqBatch;         // first slot of the stale nodes
-constexpr int kSeqSlots = kPrevSlot0 + kPrevCap;      // < 1024 (the map's slot field)
+constexpr int kSeqSlots = kPrevSlot0 + kPrevCap;      // <= 2048 (the map's slot field)
 constexpr int kPrevWords = 2 + kPrevCap;              // prev lists: {n_own, n_carried, rows...}
-static_assert(kSeqSlots <= 1024, "map entries hold a 10-bit slot");
+constexpr uint32_t kSlotBits = 11;  // map entry = (row + 1) << kSlotBits | slot (rows < 2^21)
+static_assert(kSeqSlots <= (1 << kSlotBits), "map entries hold an 11-bit slot");
+static_assert(kSeqBatch % 64 == 0, "the validator takes pods 64 at a time");
 
 // Record slots: rec[4p + r] is the batch-start record of pod p's top-4 entry
 // r (k_topk_merge wrote it; it becomes that node's live record when pod p
@@ -913,7 +918,7 @@ struct WalkResult {
 };
 
 struct SeqShared {
-    alignas(16) uint32_t map[kMapCap];  // ((row + 1) << 10) | slot; 0 = empty
+    alignas(16) uint32_t map[kMapCap];  // ((row + 1) << kSlotBits) | slot; 0 = empty
     int64_t rec[kSeqSlots][kRecF];
     alignas(16) uint8_t bound[kSeqSlots];  // binds on the slot in this batch (<= 128: no wrap)
     uint32_t n_out;
@@ -940,7 +945,7 @@ __device__ __forceinline__ int map_resolve(const SeqShared &S, uint32_t row, uin
     const uint32_t key = row + 1;
     for (;;) {
         if (v == 0) return -1;
-        if ((v >> 10) == key) return (int)(v & 1023u);
+        if ((v >> kSlotBits) == key) return (int)(v & ((1u << kSlotBits) - 1u));
         h = (h + 1) & (kMapCap - 1);
         v = S.map[h];
     }
@@ -1193,7 +1198,7 @@ __device__ __forceinline__ void flush_pending(SeqShared &S, uint32_t &prow, uint
                                               const ms_pod_rec &mypod) {
     if (prow != 0xFFFFFFFFu) {
         uint32_t h = map_hash(prow);
-        const uint32_t v = ((prow + 1) << 10) | pslot;
+        const uint32_t v = ((prow + 1) << kSlotBits) | pslot;
         while (atomicCAS(&S.map[h], 0u, v) != 0u) h = (h + 1) & (kMapCap - 1);
         prow = 0xFFFFFFFFu;
     }
@@ -1375,7 +1380,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         if (a >= 2 && a < n_prev + 2) {
             const uint32_t r = vprow[k];
             uint32_t h = map_hash(r);
-            while (atomicCAS(&S.map[h], 0u, ((r + 1) << 10) | (uint32_t)(kPrevSlot0 + a - 2)) != 0u)
+            while (atomicCAS(&S.map[h], 0u, ((r + 1) << kSlotBits) | (uint32_t)(kPrevSlot0 + a - 2)) != 0u)
                 h = (h + 1) & (kMapCap - 1);
         }
     }
