@@ -50,7 +50,7 @@ void free_all(ms_ctx *c) {
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
                    c->d_podc, c->d_resc,
-                   c->d_merged, c->d_merged_flags, c->d_drow};
+                   c->d_merged, c->d_merged_flags, c->d_drow, c->d_top_ext};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
@@ -183,7 +183,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (n_tiles <= c->tile_cap) return MS_OK;
     MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
     void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev,
-                   c->d_prev_rec, c->d_drow};
+                   c->d_prev_rec, c->d_drow, c->d_top_ext};
     for (void *q : old)
         if (q) (void)hipFree(q);
     c->d_tile_keys = nullptr;
@@ -195,6 +195,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     c->d_prev = nullptr;
     c->d_prev_rec = nullptr;
     c->d_drow = nullptr;
+    c->d_top_ext = nullptr;
     c->tile_cap = 0;
     // (ms_seq_candidates_device uses the same buffers for up to kSeqBufs * B pods)
     const size_t B = seq_batch_limit(), NB = kSeqBufs * B, n = NB * n_tiles;
@@ -206,7 +207,8 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
         hipMalloc((void **)&c->d_top4_rec, NB * seq_topk() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess ||
         hipMalloc((void **)&c->d_prev, 2 * (2 + seq_prev_cap()) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&c->d_prev_rec, 2 * seq_prev_cap() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess ||
-        hipMalloc((void **)&c->d_drow, (size_t)n_tiles * kFullWaveTile * sizeof(DRow)) != hipSuccess)
+        hipMalloc((void **)&c->d_drow, (size_t)n_tiles * kFullWaveTile * sizeof(DRow)) != hipSuccess ||
+        hipMalloc((void **)&c->d_top_ext, NB * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential-engine scratch");
     MS_HIP(c, hipMemsetAsync(c->d_spec, 0, NB * sizeof(unsigned long long), c->stream));
     MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, NB * sizeof(uint32_t), c->stream));
@@ -262,6 +264,12 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     // critical path: each chain then runs back to back instead of paying a
     // cross-stream event per batch (profiles/r02j_e_timeline*.json).
     const uint32_t B = seq_batch(c), SB = seq_batch_limit();
+    // ranks 4..7 of the merge for the validator's slow pods (MINISCHED_SEQ_EXT=0: top-4 only, A/B)
+    static const bool use_ext = [] {
+        const char *e = getenv("MINISCHED_SEQ_EXT");
+        return !(e && e[0] == '0');
+    }();
+    unsigned long long *const top_ext = use_ext ? c->d_top_ext : nullptr;
     const size_t prev_words = 2 + seq_prev_cap(), prev_fields = (size_t)seq_prev_cap() * seq_rec_fields();
     const size_t cells_per_set = (size_t)SB * n_tiles, recs_per_set = (size_t)SB * seq_topk() * seq_rec_fields();
     const char *pipe_env = getenv("MINISCHED_SEQ_PIPE");
@@ -274,7 +282,7 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         const uint32_t nb0 = std::min(B, n_pods);
         MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
         MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, nb0, n_tiles, c->d_top4, c->d_spec,
-                                    c->d_spec_flags, tq, c->d_top4_rec, s));
+                                    c->d_spec_flags, tq, c->d_top4_rec, s, top_ext));
         uint32_t k = 0;
         for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
             const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
@@ -288,11 +296,13 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
                                       k ? c->d_prev + prev_words * nxt : nullptr,
                                       k ? c->d_prev_rec + prev_fields * nxt : nullptr, c->d_prev + prev_words * cur,
                                       c->d_prev_rec + prev_fields * cur, d_res + s0, c->d_overflow,
-                                      nn ? d_pods + s1 : nullptr, nn, tk1, tf1, c->num_cus, s));
+                                      nn ? d_pods + s1 : nullptr, nn, tk1, tf1, c->num_cus, s,
+                                      top_ext ? top_ext + (size_t)SB * seq_topk() * cur : nullptr));
             if (nn)
                 MS_HIP(c, launch_topk_merge(tk1, tf1, nn, n_tiles, c->d_top4 + (size_t)SB * seq_topk() * nxt,
                                             c->d_spec + SB * nxt, c->d_spec_flags + SB * nxt, c->t,
-                                            c->d_top4_rec + recs_per_set * nxt, s));
+                                            c->d_top4_rec + recs_per_set * nxt, s,
+                                            top_ext ? top_ext + (size_t)SB * seq_topk() * nxt : nullptr));
         }
         return MS_OK;
     }
@@ -313,7 +323,8 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         int64_t *trec = c->d_top4_rec + recs_per_set * slot;
         if (k >= D) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[(k - D) % kSeqBufs], 0));
         MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods + s0, nb, seed32, tk, tf, n_tiles, c->seq_stream));
-        MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->t, trec, c->seq_stream));
+        unsigned long long *ext = top_ext ? top_ext + (size_t)SB * seq_topk() * slot : nullptr;
+        MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->t, trec, c->seq_stream, ext));
         MS_HIP(c, hipEventRecord(c->ev_swept[slot], c->seq_stream));
         MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[slot], 0));
         const bool has_prev = D > 1 && k;
@@ -321,7 +332,7 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
                                       has_prev ? c->d_prev + prev_words * (par ^ 1u) : nullptr,
                                       has_prev ? c->d_prev_rec + prev_fields * (par ^ 1u) : nullptr,
                                       c->d_prev + prev_words * par, c->d_prev_rec + prev_fields * par, D > 2 ? 1 : 0,
-                                      d_res + s0, c->d_overflow, s));
+                                      d_res + s0, c->d_overflow, s, ext));
         MS_HIP(c, hipEventRecord(c->ev_valid[slot], s));
     }
     return MS_OK;

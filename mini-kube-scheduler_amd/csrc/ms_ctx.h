@@ -64,6 +64,7 @@ struct ms_ctx {
     uint32_t *d_spec_flags = nullptr;      // per-pod flags of tiles with no feasible row (atomicOr target)
     unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
     int64_t *d_top4_rec = nullptr;         // their batch-start node records (validator layout)
+    unsigned long long *d_top_ext = nullptr;  // ranks 4..7 per pod (the validator's slow pods)
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
     int64_t *d_prev_rec = nullptr;         // and their final records (x2)
     DRow *d_drow = nullptr;                // derived rows of the binary64 sweep (tile_cap * kFullWaveTile)

@@ -193,10 +193,12 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 // Per pod: global speculative top-4 from the tile lists (top[p*4 + r]), the
 // speculative winner (rank 0) and the filters of tiles with no feasible row;
 // recs (optional, n_pods * 4 * seq_rec_fields() i64) gets the four entries'
-// batch-start node records for the in-order validator.
+// batch-start node records for the in-order validator; ext (optional, n_pods * 4)
+// ranks 4..7 for its slow pods, with the certified rank count in spec_flags
+// bits 28-31 (the validators pass it as top_ext).
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
                              uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
-                             const NodeTable &t, int64_t *recs, hipStream_t s);
+                             const NodeTable &t, int64_t *recs, hipStream_t s, unsigned long long *ext = nullptr);
 // In-order validation of a speculative batch (single workgroup); writes
 // results and commits binds to the table. prev_in / prev_recs_in: the stale
 // nodes (bound by the previous one or two batches) with their final records
@@ -212,7 +214,8 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
                                const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
                                const int64_t *top4_recs, uint32_t n_tiles, const uint32_t *prev_in,
                                const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
-                               ms_result *results, uint32_t *stats, hipStream_t s);
+                               ms_result *results, uint32_t *stats, hipStream_t s,
+                               const unsigned long long *top_ext = nullptr);
 // One single-stream step: validate batch k (n_pods, carry 0: batch k's sweep
 // ran beside batch k-1's validation) while sweeping batch k+1 (n_next pods,
 // tile lists only; launch_topk_merge follows). Either count may be 0.
@@ -223,7 +226,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s);
+                           hipStream_t s, const unsigned long long *top_ext = nullptr);
 // Node-sharded sequential mode (minisched_gpu.h ms_seq_*): this shard's top-4
 // candidates with records + all-tile filter flags per pod, from the top-4 merge
 // output; and the replicated validation over the shards' gathered lists

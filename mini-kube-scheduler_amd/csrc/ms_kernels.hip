@@ -428,6 +428,7 @@ __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
 // than K feasible rows) and the tile's filter flags.
 // ----------------------------------------------------------------------------
 constexpr int kTopK = 4;
+constexpr int kTopExt = 8;  // ranks the merge lists for the validator's slow pods (4 beyond the top-4)
 static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
 
 #ifndef MS_SWEEP_WMAX
@@ -791,15 +792,18 @@ __device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int6
     for (int f = 0; f < kRecF; f += 2) d[f / 2] = make_longlong2(v[f], v[f + 1]);
 }
 
-// One wave merges pod p's tile lists: lane r < 4 gets the global rank-r key
+// One wave merges pod p's tile lists: lane r < R gets the global rank-r key
 // (out, 0 past the feasible rows), f the filters of the tiles with no feasible
 // row (bit0 NodeUnschedulable, bit8 NodeResourcesFit; wave-uniform) and, in
 // bits 16 / 24, those of all tiles with NodeResourcesFit for a tile that had a
 // feasible row: the FitError mask once binds have filled every feasible row.
-template <int J>
+// cert: how many ranks are exact. A rank past 3 may miss a row when a tile's
+// full list of four was used up before it (its fifth row is not listed), so
+// the ranks after the one that exhausts a full list are not certified.
+template <int J, int R = kTopK>
 __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_keys,
                                                 const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
-                                                uint32_t lane, u64 &out, uint32_t &f) {
+                                                uint32_t lane, u64 &out, uint32_t &f, uint32_t *cert_out = nullptr) {
     u64 e[J][kTopK];
     uint32_t pos[J];
     uint32_t fl = 0;  // filters of this lane's tiles that have no feasible row
@@ -820,8 +824,9 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
         if (tt < n_tiles) fa |= tf | (e[j][0] != 0 ? 0x100u : 0u);
     }
     out = 0;
+    uint32_t cert = R;
 #pragma unroll
-    for (int r = 0; r < kTopK; ++r) {
+    for (int r = 0; r < R; ++r) {
         u64 head = 0;  // this lane's best list head
         int hj = -1;
 #pragma unroll
@@ -836,8 +841,18 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
         }
         const u64 m = wave_max_u64_dpp(head);
         if (lane == (uint32_t)r) out = m;
-        if (m != 0 && head == m) pos[hj] += 1;  // keys are unique: exactly one lane pops
+        bool used_up = false;
+        if (m != 0 && head == m) {  // keys are unique: exactly one lane pops
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+                if (j == hj) {
+                    pos[j] += 1;
+                    used_up = pos[j] == (uint32_t)kTopK;
+                }
+        }
+        if (R > kTopK && cert == (uint32_t)R && __ballot(used_up)) cert = (uint32_t)r + 1u;
     }
+    if (cert_out) *cert_out = cert;
     f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u) |
         (__ballot((fa & 0xFFu) != 0) ? 0x10000u : 0u) | (__ballot((fa & 0xFF00u) != 0) ? 0x1000000u : 0u);
 }
@@ -845,23 +860,30 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
 // Per pod (one wave): merge the tiles' top-4 lists into the global top-4, the
 // speculative winner and the no-feasible-row filter flags; recs (optional)
 // gets the batch-start records of the four entries for the in-order validator.
+// ext (optional): ranks 4..7 at ext[p * 4 + r - 4] and the number of certified
+// ranks (4..8) in bits 28-31 of spec_flags (merge_pod_lists).
 template <int J>
 __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
                                                    const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
                                                    uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
                                                    uint32_t *__restrict__ spec_flags, NodeTable t,
-                                                   int64_t *__restrict__ recs) {
+                                                   int64_t *__restrict__ recs, u64 *__restrict__ ext) {
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_pods) return;
     u64 out;
-    uint32_t f;
-    merge_pod_lists<J>(tile_keys, tile_flags, p, n_tiles, lane, out, f);
+    uint32_t f, cert = 0;
+    if (ext) {
+        merge_pod_lists<J, kTopExt>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert);
+        if (lane >= (uint32_t)kTopK && lane < (uint32_t)kTopExt) ext[(size_t)p * kTopK + lane - kTopK] = out;
+    } else {
+        merge_pod_lists<J>(tile_keys, tile_flags, p, n_tiles, lane, out, f);
+    }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
     if (recs && lane < (uint32_t)kTopK) store_merged_rec(t, out, recs + ((size_t)p * kTopK + lane) * kRecF);
     // the speculative winner (rank 0) and, when no row is feasible, the filters
     if (lane == 0) {
         spec[p] = out;
-        spec_flags[p] = f;
+        spec_flags[p] = f | (cert << 28);
     }
 }
 
@@ -926,6 +948,8 @@ struct SeqShared {
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
     uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
     u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
+    u64 top_ext[kSeqBatch][kTopK];   // ranks 4..7 (keys only), exact up to cert[]
+    uint8_t cert[kSeqBatch];         // certified ranks, 4..8 (4 without the extension)
     alignas(16) uint32_t claim[kClaimCap];  // per round: lowest lane whose speculative winner hashes here
     uint16_t spec_slot[kSeqBatch];   // slot of the speculative winner's record (kForceSlow: unresolved)
     uint32_t walk[16];               // a round's re-resolution pass: lanes whose pod walks its top-4
@@ -1273,6 +1297,7 @@ struct SeqArgs {
     const uint32_t *spec_flags;
     const u64 *top4;
     const int64_t *top4_recs;
+    const u64 *top_ext;  // optional: k_topk_merge's ranks 4..7 (certified count in spec_flags bits 28-31)
     uint32_t n_tiles;
     const uint32_t *prev_in;
     const int64_t *prev_recs_in;
@@ -1321,6 +1346,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                       kSpecU * 64 == kSeqBatch,
                   "prologue copies tile the LDS arrays exactly");
     lds_dma16<kRecU>(&S.rec[0][0], top4_recs, n_pods * kTopK * kRecF / 2, lane);
+    if (va.top_ext) lds_dma16<kTopU>(&S.top_ext[0][0], va.top_ext, n_pods * kTopK / 2, lane);
     if (prev_in) {  // (a writer without carry left at most kSeqBatch entries)
         if (carry) lds_dma16<kPrevU>(&S.rec[kPrevSlot0][0], prev_recs_in, kPrevCap * kRecF / 2, lane);
         else lds_dma16<kPrevU / 2>(&S.rec[kPrevSlot0][0], prev_recs_in, kSeqBatch * kRecF / 2, lane);
@@ -1359,9 +1385,10 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 #pragma unroll
         for (int k = 0; k < kTopU; ++k) dt[lane + 64u * k] = vtop[k];
 #pragma unroll
-        for (int k = 0; k < kSpecU; ++k) {
+        for (int k = 0; k < kSpecU; ++k) {  // (bits 28-31: the merge's certified ranks, 0 without ranks 4..7)
             S.spec_key[lane + 64u * k] = vspec[k];
-            S.spec_flags[lane + 64u * k] = vflag[k];
+            S.spec_flags[lane + 64u * k] = vflag[k] & 0x0FFFFFFFu;
+            S.cert[lane + 64u * k] = (uint8_t)max(vflag[k] >> 28, (uint32_t)kTopK);
         }
     }
     __builtin_amdgcn_s_waitcnt(0);  // the LDS DMA above has landed
@@ -1528,51 +1555,55 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
             const uint32_t p = g + s;
             ++ctr.slow;
             const PodFull q = load_pod(S.pods[p], seed32);
-            // the pod's tile lists, issued before the top-4 re-evaluation below so
-            // their memory round trip overlaps it (every slow pod of config E scans
-            // them: all four entries touched, or a FitError needing the flags)
-            TileLists<J> B;
-            load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
             u64 b = 0;
             int wslot = -1;
             uint32_t fmask = 0;
-            // global top-4 (lanes 0-3): touched entries are re-evaluated, the first
-            // untouched one is exact and bounds every row below it
-            const u64 e = lane < (uint32_t)kTopK ? S.top4[p][lane] : 0ull;
-            const int esl = e ? map_find(S, row_of_key(e, t.base)) : -1;
-            const u64 untouched = __ballot(e != 0 && esl < 0);
-            const u64 present = __ballot(e != 0);
+            // the global list (lanes 0-3: the top-4, 4..7: the merge's further
+            // ranks, exact below cert): touched entries are re-evaluated from
+            // their records, the first untouched one is exact and bounds every row
+            // below it; an entry 0 within the certified ranks ends the list (every
+            // feasible row was listed). No untouched or ending entry among them:
+            // the rows below are unknown and the tile lists decide.
+            const uint32_t C = S.cert[p];
+            const bool known = lane < C;
+            const u64 e = lane < (uint32_t)kTopK ? S.top4[p][lane] : known ? S.top_ext[p][lane - kTopK] : 0ull;
+            const int esl = (known && e) ? map_find(S, row_of_key(e, t.base)) : -1;
+            const u64 untouched = __ballot(known && e != 0 && esl < 0);
+            const u64 stop = untouched | __ballot(known && e == 0);
             bool scan = false;
-            if (untouched || __builtin_popcountll(present) < kTopK) {
-                const uint32_t f = untouched ? (uint32_t)__builtin_ctzll(untouched) : (uint32_t)kTopK;
+            TileLists<J> B;
+            if (stop) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(stop);
                 u64 v = 0;
                 int vs = -1;
-                if (lane < f && e != 0) {
+                if (lane < f) {  // (touched, non-zero)
                     uint32_t nu, nrf;
                     v = eval_full(slot_row(S, esl), row_of_key(e, t.base) + t.base, q, nu, nrf);
                     vs = esl;
                     ++ctr.recompute;
                 } else if (lane == f) {
-                    v = e;
+                    v = e;  // untouched: exact; or 0, the end of the list
                 }
                 b = wave_max_u64_dpp(v);
                 const u64 own = __ballot(b != 0 && v == b);
                 wslot = own ? __builtin_amdgcn_readlane(vs, (int)__builtin_ctzll(own)) : -1;
-                scan = b == 0;  // FitError: its plugin mask needs the tiles' flags
             } else {
-                scan = true;  // all four touched: rows below them are unknown
-            }
-            if (scan) {
+                scan = true;  // every known entry touched: rows below them are unknown
+                load_lists(B, tile_keys, tile_flags, p, n_pods, n_tiles, lane);
                 ++ctr.scan;
                 validate_scan<J>(S, t, n_rows, q, B, tiles, lane, ctr, b, wslot);
             }
             uint32_t info;
             if (b == 0) {  // per tile: speculative flags, + NRF if its feasible rows were all bound away
-                uint32_t fl = 0;
+                if (scan) {
+                    uint32_t fl = 0;
 #pragma unroll
-                for (int j = 0; j < J; ++j)
-                    if ((tiles >> j) & 1u) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
-                fmask = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+                    for (int j = 0; j < J; ++j)
+                        if ((tiles >> j) & 1u) fl |= B.f[j] | (B.e[j][0] != 0 ? 0x100u : 0u);
+                    fmask = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
+                } else {
+                    fmask = S.spec_flags[p] >> 16;  // the same OR over tiles, kept by the merge (bits 16 / 24)
+                }
                 info = MS_CODE_UNSCHEDULABLE | ((((fmask & 0xFFu) ? MS_MASK_NODE_UNSCHEDULABLE : 0u) |
                                                  ((fmask & 0xFF00u) ? MS_MASK_NODE_RESOURCES_FIT : 0u))
                                                 << 8);
@@ -2265,13 +2296,13 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
                                const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
                                const int64_t *top4_recs, uint32_t n_tiles, const uint32_t *prev_in,
                                const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
-                               ms_result *results, uint32_t *stats, hipStream_t s) {
+                               ms_result *results, uint32_t *stats, hipStream_t s, const unsigned long long *top_ext) {
     if (n_pods == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || !top4_recs || (prev_in && !prev_recs_in) ||
         (prev_out && !prev_recs_out))
         return hipErrorInvalidValue;
     const SeqArgs va = {t,        n_rows,       pods,     n_pods,        seed32, tile_keys, tile_flags,
-                        spec,     spec_flags,   top4,     top4_recs,     n_tiles, prev_in,  prev_recs_in,
+                        spec,     spec_flags,   top4,     top4_recs,     top_ext, n_tiles, prev_in,  prev_recs_in,
                         prev_out, prev_recs_out, carry,   results,       stats};
 #define MS_VAL(J) hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, va)
     if (n_tiles <= 64) MS_VAL(1);
@@ -2290,13 +2321,13 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s) {
+                           hipStream_t s, const unsigned long long *top_ext) {
     if (n_pods == 0 && n_next == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
         (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
         return hipErrorInvalidValue;
     const SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
-                        spec,     spec_flags,   top4,    top4_recs,  n_tiles, prev_in, prev_recs_in,
+                        spec,     spec_flags,   top4,    top4_recs,  top_ext, n_tiles, prev_in, prev_recs_in,
                         prev_out, prev_recs_out, 0,      results,    stats};
     // tasks: (tile, chunk of next pods) pairs, sized to fit one pass of the
     // sweep workgroups (one per CU beside the validator's)
@@ -2323,12 +2354,12 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
 
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
                              uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
-                             const NodeTable &t, int64_t *recs, hipStream_t s) {
+                             const NodeTable &t, int64_t *recs, hipStream_t s, unsigned long long *ext) {
     if (n_pods == 0 || n_tiles == 0) return hipSuccess;
     if (n_tiles > 64u * kSeqMaxJ) return hipErrorInvalidValue;
 #define MS_MERGE(J)                                                                                           \
     hipLaunchKernelGGL(k_topk_merge<J>, dim3(n_pods), dim3(64), 0, s, tile_keys, tile_flags, n_pods, n_tiles, top, \
-                       spec, spec_flags, t, recs)
+                       spec, spec_flags, t, recs, ext)
     if (n_tiles <= 64) MS_MERGE(1);
     else if (n_tiles <= 128) MS_MERGE(2);
     else if (n_tiles <= 256) MS_MERGE(4);
