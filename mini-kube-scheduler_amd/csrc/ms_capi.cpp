@@ -155,10 +155,12 @@ int order_after_ctx_stream(ms_ctx *c, hipStream_t s) {
 // order after the context stream) come after this call's table and scratch
 // accesses. s itself needs no new wait (ordered_seq is kept), another stream
 // does (ordered_stream differs).
-int chain_back(ms_ctx *c, hipStream_t s) {
+// recorded: ev_back was already recorded on s after the call's last launch
+// (by that launch's own dispatch).
+int chain_back(ms_ctx *c, hipStream_t s, bool recorded) {
     if (s == c->stream) return MS_OK;
     if (!c->ev_back) MS_HIP(c, hipEventCreateWithFlags(&c->ev_back, hipEventDisableTiming));
-    hipError_t e = hipEventRecord(c->ev_back, s);
+    hipError_t e = recorded ? hipSuccess : hipEventRecord(c->ev_back, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_back, 0);
     if (e != hipSuccess) return fail(c, MS_E_HIP, std::string("stream ordering: ") + hipGetErrorString(e));
     if (c->ordered_stream != s) {  // the ctx stream now holds s's work: other streams must wait for it
@@ -368,11 +370,12 @@ int ensure_stage(ms_ctx *c, uint32_t n) {
 
 // This shard's keys (and filter flags for the resource-aware set) for a batch.
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
-                 hipStream_t s) {
+                 hipStream_t s, hipEvent_t done) {
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NN) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
-                                  c->num_cus, s));
+                                  c->num_cus, s, 0, done));
+        return MS_OK;
     } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
         MS_HIP(c, launch_fill_keys(keys, n_pods, c->present_dev ? kKeyListed : 0ull, s));
         MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
@@ -383,6 +386,7 @@ int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned 
         if (flags) MS_HIP(c, hipMemsetAsync(flags, 0, sizeof(uint32_t) * n_pods, s));
         MS_HIP(c, launch_sweep_full(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, flags, c->num_cus, s));
     }
+    if (done) MS_HIP(c, hipEventRecord(done, s));
     return MS_OK;
 }
 
@@ -862,9 +866,15 @@ int ms_sweep_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);  // deltas were applied on the context stream
     if (rc) return rc;
-    rc = sweep_locked(c, n_pods, pods_dev, reinterpret_cast<unsigned long long *>(keys_dev), flags_dev, s);
+    // on a caller stream the chain-back event is recorded by the sweep's own dispatch
+    hipEvent_t back = nullptr;
+    if (s != c->stream) {
+        if (!c->ev_back) MS_HIP(c, hipEventCreateWithFlags(&c->ev_back, hipEventDisableTiming));
+        back = c->ev_back;
+    }
+    rc = sweep_locked(c, n_pods, pods_dev, reinterpret_cast<unsigned long long *>(keys_dev), flags_dev, s, back);
     if (rc) return rc;
-    return chain_back(c, s);
+    return chain_back(c, s, back != nullptr);
 }
 
 int ms_select_batch_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,

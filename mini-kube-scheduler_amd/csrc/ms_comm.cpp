@@ -234,10 +234,11 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     if (sl.used) MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
     host_tick(m, 0, tp);  // ordering of the sweep stream
     const int ps = c->cfg.plugin_set;
-    rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X);
+    // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
+    // packet between consecutive sweeps on X)
+    rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X, m.ev_swept[si]);
     if (rc) return rc;
     host_tick(m, 1, tp);  // the sweep launch
-    MS_HIP(c, hipEventRecord(m.ev_swept[si], X));
     m.reads_outstanding = true;
     // the collective after the sweep, and after the drain that decoded the
     // slot's previous batch (it read keys_mine); one wait covers a whole drain

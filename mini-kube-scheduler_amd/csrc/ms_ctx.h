@@ -130,12 +130,13 @@ constexpr uint32_t kTopKCands = 4;  // ms_seq_cand entries per pod and shard (th
 int flush_locked(ms_ctx *c);
 hipStream_t pick_stream(ms_ctx *c, void *s);
 int order_after_ctx_stream(ms_ctx *c, hipStream_t s);
-int chain_back(ms_ctx *c, hipStream_t s);
+int chain_back(ms_ctx *c, hipStream_t s, bool recorded = false);
 int ensure_tiles(ms_ctx *c, uint32_t n_tiles);
 int ensure_stage(ms_ctx *c, uint32_t n);
 bool plugins_stateless(const ms_ctx *c);
+// done (optional): recorded on s after the sweep (by the K1 dispatch itself when it is one launch)
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
-                 hipStream_t s);
+                 hipStream_t s, hipEvent_t done = nullptr);
 int seq_candidates_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_seq_cand *cands_dev,
                           uint32_t *flags_dev, hipStream_t s);
 

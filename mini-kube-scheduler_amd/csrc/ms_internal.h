@@ -157,7 +157,9 @@ hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
 // key (0 = none), overwritten. present: global present-node count (decode).
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
-                           int num_cus, hipStream_t s, int commit = 0);
+                           int num_cus, hipStream_t s, int commit = 0, hipEvent_t done = nullptr);
+// (done, optional: recorded after the sweep, by its own dispatch when it is
+// one launch: no separate event packet on s)
 // Rows one K1 pp workgroup holds (16 waves x 64 lanes x 4 groups of 30):
 // up to here the single-shard cycle is one launch with no key scratch.
 constexpr uint32_t kPpMaxFusedRows = 16u * 64u * 4u * kGroupRows;

@@ -35,6 +35,8 @@
 // the workgroup unhashes each pod's winner (tb_unhash) and writes either the
 // packed key (ms_sweep_device: one plain store per pod, no zeroing, no
 // atomics) or the decoded ms_result directly (the fused single-shard cycle).
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -375,8 +377,8 @@ constexpr uint32_t kPpMaxChunk = 2048;
 
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
-                           int num_cus, hipStream_t s, int commit) {
-    if (n_pods == 0) return hipSuccess;
+                           int num_cus, hipStream_t s, int commit, hipEvent_t done) {
+    if (n_pods == 0) return done ? hipEventRecord(done, s) : hipSuccess;
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
     // small shards with many pods: KW = 8, one single-wave workgroup per pod
@@ -421,6 +423,7 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     const dim3 grid(cdiv(n_pods, chunk), gy);
     if (gy > 1) {
         // several workgroups per chunk: combine keys with atomicMax, then decode
+        // (done: an event record after the last of these launches)
         if (!keys) return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
         if (e != hipSuccess) return e;
@@ -428,19 +431,22 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
                            t, 0);
         e = hipGetLastError();
-        if (e != hipSuccess || !results) return e;
-        e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
-        if (e != hipSuccess || !commit) return e;
-        return launch_apply_binds(t, pods, n_pods, results, s);
+        if (e == hipSuccess && results) e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
+        if (e == hipSuccess && results && commit) e = launch_apply_binds(t, pods, n_pods, results, s);
+        if (e == hipSuccess && done) e = hipEventRecord(done, s);
+        return e;
     }
+    // done: recorded by the dispatch itself (hipExtLaunchKernel's stop event: no
+    // separate event packet between this sweep and the next launch on s)
+    const uint32_t lds = chunk * (sizeof(u64) + sizeof(uint2));
+    unsigned long long *kk = results ? nullptr : keys;
+    const int cm = results ? commit : 0;
     if (KW == (uint32_t)kPpWordsSmall)
-        hipLaunchKernelGGL(k_sweep_nunn_pp<kPpWordsSmall>, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s,
-                           t.planes, t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0,
-                           results, present, t, results ? commit : 0);
+        hipExtLaunchKernelGGL(k_sweep_nunn_pp<kPpWordsSmall>, grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes,
+                              t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm);
     else
-        hipLaunchKernelGGL(k_sweep_nunn_pp<kPpWords>, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s,
-                           t.planes, t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, results ? nullptr : keys, 0,
-                           results, present, t, results ? commit : 0);
+        hipExtLaunchKernelGGL(k_sweep_nunn_pp<kPpWords>, grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes,
+                              t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm);
     return hipGetLastError();
 }
 
