@@ -96,6 +96,8 @@ struct CommState {
     ShardSlot slot[kPipeMax];
     std::deque<Pending> pending;
     uint64_t submitted = 0;
+    uint64_t x_comb_seen = 0;       // x_stream waited for the collectives of submissions < this
+    hipStream_t x_stream = nullptr;
     uint32_t depth = 4, group = 4;
     hipStream_t ds = nullptr;           // decode stream (the drains; callers wait on it in ms_sharded_drain)
     hipEvent_t ev_ds = nullptr;
@@ -231,7 +233,21 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
         m.ctx_seen = c->ctx_seq;
         m.ctx_seen_stream = s;
     }
-    if (sl.used) MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
+    // the slot's previous collective (submission k - depth - 1) read the keys
+    // this sweep overwrites. Collectives complete in issue order, so one wait
+    // covers all older ones: wait for submission k - 2's (two steps old,
+    // normally done, and never the one the previous sweep feeds) and skip the
+    // next waits it covers.
+    if (sl.used) {
+        const uint64_t k = m.submitted, prev = k - (m.depth + 1);
+        if (m.two_streams || m.depth + 1 < 3) {
+            MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
+        } else if (m.x_stream != X || m.x_comb_seen <= prev) {
+            m.x_stream = X;
+            MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[(k - 2) % (m.depth + 1)], 0));
+            m.x_comb_seen = k - 1;
+        }
+    }
     host_tick(m, 0, tp);  // ordering of the sweep stream
     const int ps = c->cfg.plugin_set;
     // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
