@@ -404,13 +404,15 @@ hipError_t decode_for(const ms_ctx *c, const ms_pod_rec *pods, uint32_t n, const
 // batch, binds included (it needs key scratch only above kPpMaxFusedRows
 // rows); otherwise batch_cap chunks are swept into the context's key/flag
 // scratch, then decoded (and their binds applied).
+// done (optional): recorded on s after the call's last launch (by the fused
+// K1 dispatch itself when the cycle is that one launch).
 int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, hipStream_t s,
-                  int commit = 0) {
+                  int commit = 0, hipEvent_t done = nullptr) {
     const uint32_t B = c->batch_cap;
     const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN;
     if (fused && c->rows_dev <= kPpMaxFusedRows) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), nullptr, d_res,
-                                  c->present_dev, c->num_cus, s, commit));
+                                  c->present_dev, c->num_cus, s, commit, done));
         return MS_OK;
     }
     // The resource-aware set reads Requested / pod_count: every chunk must be
@@ -432,6 +434,7 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
         if (commit && !late_commit) MS_HIP(c, launch_apply_binds(c->t, d_pods + s0, nb, d_res + s0, s));
     }
     if (late_commit) MS_HIP(c, launch_apply_binds(c->t, d_pods, n_pods, d_res, s));
+    if (done) MS_HIP(c, hipEventRecord(done, s));
     return MS_OK;
 }
 
@@ -890,9 +893,15 @@ int ms_select_batch_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_de
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);
     if (rc) return rc;
-    rc = select_locked(c, n_pods, pods_dev, results_dev, s);
+    // on a caller stream the chain-back event is recorded by the cycle's own dispatch
+    hipEvent_t back = nullptr;
+    if (s != c->stream) {
+        if (!c->ev_back) MS_HIP(c, hipEventCreateWithFlags(&c->ev_back, hipEventDisableTiming));
+        back = c->ev_back;
+    }
+    rc = select_locked(c, n_pods, pods_dev, results_dev, s, 0, back);
     if (rc) return rc;
-    return chain_back(c, s);
+    return chain_back(c, s, back != nullptr);
 }
 
 int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, const uint64_t *keys_dev,
