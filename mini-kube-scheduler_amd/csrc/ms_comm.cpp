@@ -513,15 +513,25 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->two_streams = atoi(e) == 2;
     if (const char *e = getenv("MINISCHED_HOST_PROF")) m->host_prof = atoi(e) == 1;
     c->comm = m;  // (comm_free releases a partial state)
-    MS_HIP(c, hipStreamCreateWithFlags(&m->cs, hipStreamNonBlocking));
-    // (MINISCHED_SHARD_STREAMS=2) MINISCHED_SWEEP_PRIO=1 creates the two sweep
-    // streams with the highest priority: they then land on queues of their own,
-    // but the collectives on the normal-priority stream fell behind (A/B)
-    const char *pe = getenv("MINISCHED_SWEEP_PRIO");
+    // The collective and decode streams get the highest priority: high-priority
+    // streams are served by hardware queues of their own, so the caller's
+    // (sweep) stream can never share a queue with them and serialise a
+    // reduce-scatter or a decode behind the next sweep; their short kernels are
+    // dispatched ahead of the sweep's pending workgroups. MINISCHED_COMM_PRIO=0:
+    // normal priority (A/B).
     int lo = 0, hi = 0;
-    if (pe && atoi(pe) == 1) MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi));
-    MS_HIP(c, hipStreamCreateWithFlags(&m->ds, hipStreamNonBlocking));
+    MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const char *cp = getenv("MINISCHED_COMM_PRIO");
+    const int cprio = (cp && cp[0] == '0') ? 0 : hi;
+    MS_HIP(c, hipStreamCreateWithPriority(&m->cs, hipStreamNonBlocking, cprio));
+    // (MINISCHED_SHARD_STREAMS=2 only) two sweep streams; MINISCHED_SWEEP_PRIO=1
+    // creates them with the highest priority (A/B: the collectives then fell behind)
+    if (m->two_streams) {
+        const char *pe = getenv("MINISCHED_SWEEP_PRIO");
+        const int sprio = (pe && atoi(pe) == 1) ? hi : 0;
+        for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, sprio));
+    }
+    MS_HIP(c, hipStreamCreateWithPriority(&m->ds, hipStreamNonBlocking, cprio));
     MS_HIP(c, hipEventCreateWithFlags(&m->ev_ds, hipEventDisableTiming));
     for (uint32_t i = 0; i < kPipeMax; ++i) {
         MS_HIP(c, hipEventCreateWithFlags(&m->ev_swept[i], hipEventDisableTiming));
