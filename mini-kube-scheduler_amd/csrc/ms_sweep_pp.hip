@@ -56,6 +56,13 @@ constexpr uint32_t truth3(F f) {  // v_bitop3 table, S0 the most significant ind
 constexpr uint32_t kXnorAnd = truth3([](int a, int b, int c) { return c && a == b; });  // c & ~(a ^ b)
 constexpr uint32_t kSelect = truth3([](int a, int b, int c) { return c ? a : b; });     // c ? a : b
 
+#ifndef MS_TAIL_PACK
+#define MS_TAIL_PACK 1  // (0: the last partial word as a full one, A/B)
+#endif
+#ifndef MS_TAIL_SHARE
+#define MS_TAIL_SHARE 4  // waves sharing the packed last word (A/B)
+#endif
+
 constexpr int kPpWords = 4;      // 30-row groups per lane (KW, shards above kPpSmallGroups)
 constexpr int kPpWordsSmall = 8; // KW for small shards: one wave holds every row
 constexpr int kPpMaxWaves = 16;  // 1024-thread workgroups
@@ -140,8 +147,10 @@ __device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
 // flags: level 11 (score 10 + 1) over the score-10 rows, else level 1 over
 // every feasible row (all score 0). Returns level<<32 | max hash (wave-uniform),
 // 0 when no row of the wave is feasible.
+// tail: the wave's packed last word (below) is evaluated here like a full one:
+// its groups repeat in every lane segment, and repeats leave the max unchanged.
 template <int KW, int NW>
-__device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Pod &q) {
+__device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Word &Wt, bool tail, const Pod &q) {
     uint32_t h = 0;
     bool found = false;
 #pragma unroll
@@ -150,12 +159,22 @@ __device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Pod &q) {
         found = found || m != 0;
         h = max(h, word_scan(m, W[k].hb + q.A));
     }
+    if (tail) {
+        const uint32_t m = match10(Wt, q);
+        found = found || m != 0;
+        h = max(h, word_scan(m, Wt.hb + q.A));
+    }
     if (__ballot(found) != 0) return (11ull << 32) | wave_max_u32_dpp(h);
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
         const uint32_t m = feasible(W[k], q);
         found = found || m != 0;
         h = max(h, word_scan(m, W[k].hb + q.A));
+    }
+    if (tail) {
+        const uint32_t m = feasible(Wt, q);
+        found = found || m != 0;
+        h = max(h, word_scan(m, Wt.hb + q.A));
     }
     if (__ballot(found) != 0) return (1ull << 32) | wave_max_u32_dpp(h);
     return 0;
@@ -171,10 +190,19 @@ __device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, 
     return make_uint2(tb_pod(seed32, pr.x), info | ((pr.y & 0xFFu) << 8));
 }
 
-// One wave sweeps the chunk's pods [0, np) through its NW groups into lds[p].
-template <int KW, int NW, bool GEN>
-__device__ __forceinline__ void sweep_range(const Word (&W)[KW], const uint2 *pinfo, uint32_t np,
-                                            uint32_t lane, u64 *lds) {
+// One wave sweeps the chunk's pods [0, np) through its NW words into lds[p].
+// tpt != 0: the wave also holds the workgroup's packed last word Wt, whose
+// T <= 64 / tpt groups repeat in tpt lane segments of 64 / tpt lanes: segment
+// i evaluates pod i of a group of tpt pods (its bits from the lanes' block
+// entries by ds_bpermute), so a partial word costs 8 / tpt evaluations per 8
+// pods instead of 8; and up to 4 waves (on different SIMDs) hold it, wave
+// tidx of tshare taking the 8-pod blocks b with b mod tshare == tidx. (A
+// partial word holding the full cost on one SIMD was 6 % of config C:
+// 100,000 rows 323 us, 99,840 rows 303 us, profiles/r03zd_tail.json.)
+template <int KW, int NW, bool GEN, bool TAIL>
+__device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt, uint32_t tpt, uint32_t tshare,
+                                            uint32_t tidx, const uint2 *pinfo, uint32_t np, uint32_t lane, u64 *lds) {
+    const uint32_t seg_shift = tpt == 8u ? 3u : tpt == 4u ? 4u : 5u;  // log2(64 / tpt)
     for (uint32_t pb = 0; pb < np; pb += 64) {
         const uint32_t nblk = min(64u, np - pb);
         // the block's pods, one per lane: A and digit | tolerates << 4
@@ -199,6 +227,20 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const uint2 *pi
                     h = max(h, GEN ? word_scan(match10(W[k], q[t]), W[k].hb + q[t].A) : word_fast(W[k], q[t]));
                 r[t] = h;
             }
+            if (TAIL && ((pb + j) >> 3) % tshare == tidx) {  // wave-uniform
+                const uint32_t seg = lane >> seg_shift;
+                for (uint32_t e = 0; e < 8u; e += tpt) {
+                    // lanes of segment seg: pod j + e + seg of the block (past nblk: A 0 and
+                    // class 14, which no row matches, so h stays 0)
+                    const int src = (int)(j + e + seg) << 2;
+                    const Pod qt = pod_bits((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)a_l),
+                                            (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)info_l));
+                    const uint32_t h = GEN ? word_scan(match10(Wt, qt), Wt.hb + qt.A) : word_fast(Wt, qt);
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        if ((uint32_t)t >= e && (uint32_t)t < e + tpt) r[t] = max(r[t], seg == (uint32_t)t - e ? h : 0u);
+                }
+            }
             const uint32_t u = reduce8(r, lane);
             const uint32_t pi = j + rev3(lane >> 3);  // lanes 8k: pod pi of the block
             const bool mine = (lane & 7u) == 0u && pi < nblk;
@@ -212,7 +254,7 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const uint2 *pi
                 const uint32_t t = rev3(l >> 3);
                 const Pod qs = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
                                         (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
-                const u64 v = pod_slow<KW, NW>(W, qs);
+                const u64 v = pod_slow<KW, NW>(W, Wt, TAIL && ((pb + j) >> 3) % tshare == tidx, qs);
                 if (lane == 0 && v) atomicMax(&lds[pb + j + t], v);
             }
         }
@@ -225,7 +267,35 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const uint2 *pi
 // 12.5k-row shard dealt over 4 waves gave them 2, 2, 2 and 1 words, and the
 // SIMD that hosts the short waves idled), and the per-pod reduction is paid
 // once per 7 words instead of once per 2.
-template <int KW>
+// Pods per evaluation of a workgroup's packed last word (sweep_range): 8, 4 or
+// 2 for a last word of <= 8, 16, 32 groups, 0 when it stays a full word. ng
+// groups over `waves` waves. Packed only where that lowers the busiest SIMD's
+// load (waves w and w + 4 share a SIMD): words per SIMD, in sixteenths, with
+// and without it (100,000 rows over 16 waves: 14 -> 13.06; 50,010 over 8: 7
+// either way, and packing cost 1 %).
+__host__ __device__ inline uint32_t tail_pods(uint32_t ng, uint32_t waves) {
+    if (!MS_TAIL_PACK || ng == 0) return 0u;
+    const uint32_t wlast = (ng + 63u) / 64u - 1u, tail_n = ng - wlast * 64u;
+    const uint32_t tpt = tail_n <= 8u ? 8u : tail_n <= 16u ? 4u : tail_n <= 32u ? 2u : 0u;
+    if (!tpt) return 0u;
+    const uint32_t wv_t = wlast % waves;
+    const uint32_t tshare = (uint32_t)MS_TAIL_SHARE < waves - wv_t ? (uint32_t)MS_TAIL_SHARE : waves - wv_t;
+    uint32_t L[4] = {0, 0, 0, 0};
+    for (uint32_t w = 0; w < waves && w <= wlast; ++w) L[w & 3u] += 16u * ((wlast - w) / waves + 1u);
+    auto mx = [&] {
+        const uint32_t a = L[0] > L[1] ? L[0] : L[1], b = L[2] > L[3] ? L[2] : L[3];
+        return a > b ? a : b;
+    };
+    const uint32_t m0 = mx();
+    L[wv_t & 3u] -= 16u;
+    const uint32_t eps = ((tpt == 8u ? 4u : tpt == 4u ? 8u : 12u) + tshare - 1u) / tshare;
+    for (uint32_t i = 0; i < tshare; ++i) L[(wv_t + i) & 3u] += eps;
+    return mx() < m0 ? tpt : 0u;
+}
+
+// TP: the packed-last-word path is compiled in (launch_sweep_pp picks it only
+// for shapes tail_pods packs; the others run the plain form).
+template <int KW, bool TP>
 __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
@@ -245,18 +315,27 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
 
     // the wave's groups, dealt round-robin over the workgroup's waves so their
     // word counts differ by at most one: word k of lane l is group
-    // g0 + (k * waves + wv) * 64 + l
+    // g0 + (k * waves + wv) * 64 + l. The workgroup's last word, when it holds
+    // T <= 32 groups, is packed instead (sweep_range): its wave loads group
+    // (lane mod 64/tpt) of it into Wt.
     const uint32_t waves = blockDim.x >> 6;
     const uint32_t g0 = blockIdx.y * waves * 64u * KW;
-    Word W[KW];
+    const uint32_t ng = min(n_groups - g0, waves * 64u * KW);  // (blockIdx.y < gy: g0 < n_groups)
+    const uint32_t wlast = (ng + 63u) / 64u - 1u, tail_n = ng - wlast * 64u;
+    uint32_t tpt = TP ? tail_pods(ng, waves) : 0u;
+    const uint32_t wv_t = wlast % waves, tshare = min((uint32_t)MS_TAIL_SHARE, waves - wv_t);  // its waves
+    const bool owner = wv == wv_t;     // it is this wave's last word in the dealing
+    if (wv < wv_t || wv >= wv_t + tshare) tpt = 0u;  // wave-uniform
+    Word W[KW], Wt;
     int nw = 0;
     bool over = false;
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
-        const uint32_t gw = g0 + (k * waves + wv) * 64u;
+        const uint32_t wi = k * waves + wv;
+        const uint32_t gw = g0 + wi * 64u;
         const uint32_t g = gw + lane;
-        const bool in = g < n_groups;
-        if (gw < n_groups) nw = k + 1;  // wave-uniform
+        const bool in = g < n_groups && !(tpt && owner && wi == wlast);
+        if (gw < n_groups && !(tpt && owner && wi == wlast)) nw = k + 1;  // wave-uniform
         W[k].d0 = in ? planes[kPlaneD0 * gstride + g] : 0u;
         W[k].d1 = in ? planes[kPlaneD1 * gstride + g] : 0u;
         W[k].d2 = in ? planes[kPlaneD2 * gstride + g] : 0u;
@@ -267,17 +346,41 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
         // more than 3 present rows of one digit in a group: the fast slots cannot hold them
         over = over || (in && planes[kPlaneOver * gstride + g] != 0u);
     }
+    {
+        const uint32_t gi = tpt ? lane & ((64u / tpt) - 1u) : 0u;
+        const uint32_t g = g0 + wlast * 64u + gi;
+        const bool in = tpt && gi < tail_n;
+        Wt.d0 = in ? planes[kPlaneD0 * gstride + g] : 0u;
+        Wt.d1 = in ? planes[kPlaneD1 * gstride + g] : 0u;
+        Wt.d2 = in ? planes[kPlaneD2 * gstride + g] : 0u;
+        Wt.d3 = in ? planes[kPlaneD3 * gstride + g] : 0u;
+        Wt.sched = in ? planes[kPlaneSched * gstride + g] : 0u;
+        Wt.pres = in ? planes[kPlanePresent * gstride + g] : 0u;
+        Wt.hb = (node_base + g * kGroupRows) * kG24;
+        over = over || (in && planes[kPlaneOver * gstride + g] != 0u);
+    }
     const bool gen = __ballot(over) != 0;
     __syncthreads();
-    if (np) {
-        switch (nw * 2 + (gen ? 1 : 0)) {  // wave-uniform
-#define MS_PP_CASE(N)                                                                     \
-    case 2 * N:                                                                           \
-        if constexpr (N <= KW) sweep_range<KW, (N <= KW ? N : KW), false>(W, pinfo, np, lane, lds); \
-        break;                                                                            \
-    case 2 * N + 1:                                                                       \
-        if constexpr (N <= KW) sweep_range<KW, (N <= KW ? N : KW), true>(W, pinfo, np, lane, lds);  \
+    if (np && (nw || tpt)) {
+        switch (nw * 4 + (gen ? 2 : 0) + (tpt ? 1 : 0)) {  // wave-uniform
+#define MS_PP_CASE(N)                                                                                       \
+    case 4 * N:                                                                                             \
+        if constexpr (N <= KW && N > 0)                                                                     \
+            sweep_range<KW, (N <= KW ? N : KW), false, false>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds); \
+        break;                                                                                              \
+    case 4 * N + 1:                                                                                         \
+        if constexpr (N <= KW)                                                                              \
+            sweep_range<KW, (N <= KW ? N : KW), false, true>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);  \
+        break;                                                                                              \
+    case 4 * N + 2:                                                                                         \
+        if constexpr (N <= KW && N > 0)                                                                     \
+            sweep_range<KW, (N <= KW ? N : KW), true, false>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);  \
+        break;                                                                                              \
+    case 4 * N + 3:                                                                                         \
+        if constexpr (N <= KW)                                                                              \
+            sweep_range<KW, (N <= KW ? N : KW), true, true>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);   \
         break;
+            MS_PP_CASE(0)
             MS_PP_CASE(1)
             MS_PP_CASE(2)
             MS_PP_CASE(3)
@@ -427,7 +530,7 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
         if (!keys) return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sweep_nunn_pp<kPpWords>, grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
+        hipLaunchKernelGGL((k_sweep_nunn_pp<kPpWords, false>), grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
                            t, 0);
         e = hipGetLastError();
@@ -441,12 +544,18 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     const uint32_t lds = chunk * (sizeof(u64) + sizeof(uint2));
     unsigned long long *kk = results ? nullptr : keys;
     const int cm = results ? commit : 0;
-    if (KW == (uint32_t)kPpWordsSmall)
-        hipExtLaunchKernelGGL(k_sweep_nunn_pp<kPpWordsSmall>, grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes,
-                              t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm);
-    else
-        hipExtLaunchKernelGGL(k_sweep_nunn_pp<kPpWords>, grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes,
-                              t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm);
+    const bool tp = tail_pods(n_groups, W) != 0u;  // (gy == 1: the workgroup holds every group)
+#define MS_PP_LAUNCH(KWV, TPV)                                                                                     \
+    hipExtLaunchKernelGGL((k_sweep_nunn_pp<KWV, TPV>), grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes, t.gcap, \
+                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm)
+    if (KW == (uint32_t)kPpWordsSmall) {
+        if (tp) MS_PP_LAUNCH(kPpWordsSmall, true);
+        else MS_PP_LAUNCH(kPpWordsSmall, false);
+    } else {
+        if (tp) MS_PP_LAUNCH(kPpWords, true);
+        else MS_PP_LAUNCH(kPpWords, false);
+    }
+#undef MS_PP_LAUNCH
     return hipGetLastError();
 }
 
