@@ -267,17 +267,24 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt,
 // 12.5k-row shard dealt over 4 waves gave them 2, 2, 2 and 1 words, and the
 // SIMD that hosts the short waves idled), and the per-pod reduction is paid
 // once per 7 words instead of once per 2.
-// Pods per evaluation of a workgroup's packed last word (sweep_range): 8, 4 or
-// 2 for a last word of <= 8, 16, 32 groups, 0 when it stays a full word. ng
+// Pods per evaluation of a workgroup's packed last word (sweep_range): 8 for a
+// last word of <= 8 groups, 0 when it stays a full word (sweep_range also
+// takes 4 and 2: 16 and 32 groups). ng
 // groups over `waves` waves. Packed only where that lowers the busiest SIMD's
-// load (waves w and w + 4 share a SIMD): words per SIMD, in sixteenths, with
-// and without it (100,000 rows over 16 waves: 14 -> 13.06; 50,010 over 8: 7
-// either way, and packing cost 1 %).
+// load (waves w and w + 4 of a workgroup share a SIMD): words per SIMD, in
+// sixteenths, with and without it (100,000 rows over 16 waves: 14 -> 13.06;
+// 50,010 over 8: 7 either way, and packing cost 1 %).
 __host__ __device__ inline uint32_t tail_pods(uint32_t ng, uint32_t waves) {
     if (!MS_TAIL_PACK || ng == 0) return 0u;
     const uint32_t wlast = (ng + 63u) / 64u - 1u, tail_n = ng - wlast * 64u;
-    const uint32_t tpt = tail_n <= 8u ? 8u : tail_n <= 16u ? 4u : tail_n <= 32u ? 2u : 0u;
+    // (8 pods per evaluation only: 2 per evaluation, 17 groups left over a
+    // 6,250-row wave, cost more than the full word, profiles/r03zk_tail_pack_ab.txt)
+    const uint32_t tpt = tail_n <= 8u ? 8u : 0u;
     if (!tpt) return 0u;
+    // up to 4 waves: several workgroups share a CU and the hardware rotates
+    // their waves over the SIMDs (profiles/r03z_hwid_placement.txt), so every
+    // word saved is saved on every SIMD
+    if (waves <= 4u) return tpt;
     const uint32_t wv_t = wlast % waves;
     const uint32_t tshare = (uint32_t)MS_TAIL_SHARE < waves - wv_t ? (uint32_t)MS_TAIL_SHARE : waves - wv_t;
     uint32_t L[4] = {0, 0, 0, 0};
