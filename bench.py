@@ -207,11 +207,14 @@ def e2e_host(eng, pods_np, n_nodes, world=1, compact=False):
     P = len(pods_np)
     return {"ms_median": ms, "pods_per_s": P / (ms * 1e-3), "evals_per_s": P * n_nodes / (ms * 1e-3),
             "runs": [t * 1e3 for t in ts],
-            "includes": ("ms_schedule_batch_compact: H2D of 8 B pods" if compact else
-                         "ms_schedule_batch: H2D of 40 B pods")
-                        + " (pageable host array), filter+score+selectHost+decode"
+            "includes": ("ms_schedule_batch_compact: 8 B pods copied from the (pageable) host array into pinned "
+                         "memory the kernel reads over PCIe (single shard; a staged H2D with N > 1)" if compact else
+                         "ms_schedule_batch: H2D of 40 B pods (pageable host array)")
+                        + ", filter+score+selectHost+decode"
                         + (", reduce-scatter + all-gather over the communicator" if world > 1 else "")
-                        + ", bind commit, D2H of " + ("8" if compact else "24") + " B results into the host array"}
+                        + ", bind commit, " + ("8 B results written by the kernel to pinned memory and copied into "
+                                               "the host array" if compact else
+                                               "D2H of 24 B results into the host array")}
 
 
 def _cpu_info(threads):

@@ -53,6 +53,8 @@ void free_all(ms_ctx *c) {
                    c->d_merged, c->d_merged_flags, c->d_drow, c->d_top_ext};
     for (void *p : dev)
         if (p) (void)hipFree(p);
+    if (c->h_podz) (void)hipHostFree(c->h_podz);
+    if (c->h_resz) (void)hipHostFree(c->h_resz);
     if (c->h_pods) (void)hipHostFree(c->h_pods);
     if (c->h_res) (void)hipHostFree(c->h_res);
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
@@ -804,6 +806,36 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
+    // Single-shard NU+NN: one launch reading the pods from and writing the
+    // results to pinned host memory (8 B each way per pod over PCIe, no copy
+    // commands, no widen / narrow passes); the host copies the caller's arrays
+    // in and out. MINISCHED_COMPACT_ZC=0: the staged path below (A/B).
+    static const bool zc = [] {
+        const char *e = getenv("MINISCHED_COMPACT_ZC");
+        return !(e && e[0] == '0');
+    }();
+    if (zc && !c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows) {
+        if (n > c->z_cap) {
+            if (c->h_podz) (void)hipHostFree(c->h_podz);
+            if (c->h_resz) (void)hipHostFree(c->h_resz);
+            c->h_podz = nullptr;
+            c->h_resz = nullptr;
+            c->z_cap = 0;
+            if (hipHostMalloc((void **)&c->h_podz, sizeof(ms_pod_compact) * n, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&c->h_resz, sizeof(ms_result_compact) * n, hipHostMallocDefault) != hipSuccess)
+                return fail(c, MS_E_OOM, "compact pinned staging");
+            c->z_cap = n;
+        }
+        const hipStream_t s = c->stream;
+        MS_HIP(c, hipStreamSynchronize(s));  // (no earlier call still reads h_podz)
+        std::memcpy(c->h_podz, pods, sizeof(ms_pod_compact) * n);
+        ++c->ctx_seq;  // binds write the table on the context stream
+        MS_HIP(c, launch_sweep_pp_compact(c->t, c->rows_dev, c->h_podz, n, seed32_of(c->cfg.seed), c->h_resz,
+                                          c->present_dev, c->num_cus, s));
+        MS_HIP(c, hipStreamSynchronize(s));
+        std::memcpy(out, c->h_resz, sizeof(ms_result_compact) * n);
+        return MS_OK;
+    }
     rc = c->comm ? comm_stage(c, n) : ensure_stage(c, n);
     if (rc) return rc;
     if (n > c->compact_cap) {

@@ -79,6 +79,9 @@ struct ms_ctx {
     hipEvent_t ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
+    ms_pod_compact *h_podz = nullptr;      // pinned compact pods / results the compact cycle's
+    ms_result_compact *h_resz = nullptr;   // kernel reads and writes over PCIe (zero-copy)
+    uint32_t z_cap = 0;
     // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
     ms_seq_cand *d_merged = nullptr;
     uint32_t *d_merged_flags = nullptr;

@@ -158,6 +158,13 @@ hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
                            int num_cus, hipStream_t s, int commit = 0, hipEvent_t done = nullptr);
+// The compact host-array cycle (ms_schedule_batch_compact) in one launch, rows
+// <= kPpMaxFusedRows: pods are ms_pod_compact records and results
+// ms_result_compact, both in pinned host memory the kernel reads and writes
+// over PCIe (no copy launches, no widen / narrow passes); binds committed.
+hipError_t launch_sweep_pp_compact(const NodeTable &t, uint32_t n_rows, const ms_pod_compact *pods, uint32_t n_pods,
+                                   uint32_t seed32, ms_result_compact *results, uint32_t present, int num_cus,
+                                   hipStream_t s);
 // (done, optional: recorded after the sweep, by its own dispatch when it is
 // one launch: no separate event packet on s)
 // Rows one K1 pp workgroup holds (16 waves x 64 lanes x 4 groups of 30):

@@ -183,8 +183,11 @@ __device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Word &Wt, boo
 // Pod p of a workgroup's chunk as the prologue leaves it in LDS: x = A =
 // tb_pod(seed32, ordinal), y = class bits (digit, 14 for a non-digit name, |
 // tolerates << 4) | name digit byte << 8.
-__device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, uint32_t p, uint32_t seed32) {
-    const uint2 pr = *reinterpret_cast<const uint2 *>(pods + p);  // ordinal, digit, tolerates
+// pstride: bytes per pod record (sizeof(ms_pod_rec), or 8 for ms_pod_compact,
+// its first 8 bytes).
+__device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, uint32_t p, uint32_t seed32,
+                                           uint32_t pstride) {
+    const uint2 pr = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(pods) + (size_t)p * pstride);
     const int dig = (int)(int8_t)(pr.y & 0xFFu);
     const uint32_t info = ((uint32_t)dig <= 9u ? (uint32_t)dig : 14u) | (((pr.y >> 8) & 0xFFu) ? 16u : 0u);
     return make_uint2(tb_pod(seed32, pr.x), info | ((pr.y & 0xFFu) << 8));
@@ -306,7 +309,8 @@ template <int KW, bool TP>
 __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
-    int atomic_keys, ms_result *__restrict__ results, uint32_t present, NodeTable tab, int commit) {
+    int atomic_keys, ms_result *__restrict__ results, uint32_t present, NodeTable tab, int commit,
+    uint32_t pstride, ms_result_compact *__restrict__ resc) {
     // LDS: one combine slot per pod of the chunk, then the chunk's pod entries
     extern __shared__ u64 lds[];
     uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk);
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
         lds[i] = 0;
-        pinfo[i] = pod_entry(pods, pbeg + i, seed32);
+        pinfo[i] = pod_entry(pods, pbeg + i, seed32, pstride);
     }
 
     // the wave's groups, dealt round-robin over the workgroup's waves so their
@@ -414,13 +418,29 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
             if (!atomic_keys) keys[pbeg + i] = key;
             else if (key) atomicMax(&keys[pbeg + i], key);
         }
-        if (results) {
+        if (results || resc) {
             const ms_result r = decode_key(key, (int8_t)(pe.y >> 8), nullptr, 0, present);
-            results[pbeg + i] = r;
+            if (results) {
+                results[pbeg + i] = r;
+            } else {  // the compact record, straight into the caller's (pinned host) array
+                ms_result_compact rc;
+                rc.node = r.node;
+                rc.score = (uint16_t)r.score;
+                rc.code = (uint8_t)r.code;
+                rc.plugin_mask = (uint8_t)r.plugin_mask;
+                resc[pbeg + i] = rc;
+            }
             // assume-on-select in the same launch (ms_schedule_batch / the sequential
             // NU+NN cycle): NodeInfo.AddPod on the winner, which this context owns
-            // (one workgroup holds all its rows)
-            if (commit && r.code == MS_CODE_SUCCESS) add_pod(tab, (uint32_t)r.node - tab.base, pods[pbeg + i], +1);
+            // (one workgroup holds all its rows); a compact pod requests nothing
+            if (commit && r.code == MS_CODE_SUCCESS) {
+                if (resc) {
+                    const ms_pod_rec z = {};
+                    add_pod(tab, (uint32_t)r.node - tab.base, z, +1);
+                } else {
+                    add_pod(tab, (uint32_t)r.node - tab.base, pods[pbeg + i], +1);
+                }
+            }
         }
     }
 }
@@ -485,9 +505,10 @@ hipError_t launch_build_planes(const NodeTable &t, const NodeDelta *d_deltas, ui
 // MINISCHED_PP_CHUNK overrides the chunk (tuning).
 constexpr uint32_t kPpMaxChunk = 2048;
 
-hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                           uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
-                           int num_cus, hipStream_t s, int commit, hipEvent_t done) {
+namespace {
+hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                         uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present, int num_cus,
+                         hipStream_t s, int commit, hipEvent_t done, uint32_t pstride, ms_result_compact *resc) {
     if (n_pods == 0) return done ? hipEventRecord(done, s) : hipSuccess;
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
@@ -534,12 +555,12 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     if (gy > 1) {
         // several workgroups per chunk: combine keys with atomicMax, then decode
         // (done: an event record after the last of these launches)
-        if (!keys) return hipErrorInvalidValue;
+        if (!keys || resc) return hipErrorInvalidValue;
         hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * n_pods, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_sweep_nunn_pp<kPpWords, false>), grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
-                           t, 0);
+                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr);
         e = hipGetLastError();
         if (e == hipSuccess && results) e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
         if (e == hipSuccess && results && commit) e = launch_apply_binds(t, pods, n_pods, results, s);
@@ -549,12 +570,12 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     // done: recorded by the dispatch itself (hipExtLaunchKernel's stop event: no
     // separate event packet between this sweep and the next launch on s)
     const uint32_t lds = chunk * (sizeof(u64) + sizeof(uint2));
-    unsigned long long *kk = results ? nullptr : keys;
-    const int cm = results ? commit : 0;
+    unsigned long long *kk = (results || resc) ? nullptr : keys;
+    const int cm = (results || resc) ? commit : 0;
     const bool tp = tail_pods(n_groups, W) != 0u;  // (gy == 1: the workgroup holds every group)
 #define MS_PP_LAUNCH(KWV, TPV)                                                                                     \
     hipExtLaunchKernelGGL((k_sweep_nunn_pp<KWV, TPV>), grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes, t.gcap, \
-                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm)
+                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc)
     if (KW == (uint32_t)kPpWordsSmall) {
         if (tp) MS_PP_LAUNCH(kPpWordsSmall, true);
         else MS_PP_LAUNCH(kPpWordsSmall, false);
@@ -564,6 +585,23 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
     }
 #undef MS_PP_LAUNCH
     return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
+                           int num_cus, hipStream_t s, int commit, hipEvent_t done) {
+    return sweep_pp_impl(t, n_rows, pods, n_pods, seed32, keys, results, present, num_cus, s, commit, done,
+                         (uint32_t)sizeof(ms_pod_rec), nullptr);
+}
+
+hipError_t launch_sweep_pp_compact(const NodeTable &t, uint32_t n_rows, const ms_pod_compact *pods, uint32_t n_pods,
+                                   uint32_t seed32, ms_result_compact *results, uint32_t present, int num_cus,
+                                   hipStream_t s) {
+    static_assert(sizeof(ms_pod_compact) == 8 && sizeof(ms_result_compact) == 8, "compact records");
+    if (n_rows > kPpMaxFusedRows || !results) return hipErrorInvalidValue;
+    return sweep_pp_impl(t, n_rows, reinterpret_cast<const ms_pod_rec *>(pods), n_pods, seed32, nullptr, nullptr,
+                         present, num_cus, s, 1, nullptr, (uint32_t)sizeof(ms_pod_compact), results);
 }
 
 }  // namespace msgpu
