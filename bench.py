@@ -26,10 +26,11 @@ Scaling (--scaling, default strong): config C as BASELINE.json states it —
 100k/N rows, decode of its 100k/N pods). --scaling weak: every GPU brings its
 own 100k-pod batch (N x 100k pods per step), a labelled extra.
 
-Extra fields (rank 0): pods/s per SURVEY §8(d) — ms_schedule_batch on host
-arrays (H2D of the pods, the cycle, bind commit, D2H of the results; 1
-warm-up, median of 5; with N > 1 the collective host call over the
-communicator) — as the top-level `pods_per_s`, the device-resident rate as
+Extra fields (rank 0): pods/s per SURVEY §8(d) — ms_schedule_batch_compact on
+host arrays (8 B pods in, the cycle, bind commit, 8 B results out; single
+shard: one launch over pinned host memory; 1 warm-up, median of 5; with N > 1
+the collective host call over the communicator; `e2e`: ms_schedule_batch with
+40/24 B records) — as the top-level `pods_per_s`, the device-resident rate as
 `device_pods_per_s`, the VALU-issue roofline of the timed kernel with its HBM
 figures, and the CPU baseline (oracle, OpenMP, on the box's host cores).
 
