@@ -452,6 +452,27 @@ def _pods_with_zero_hash(seed, n_nodes, want=4):
     return out
 
 
+@pytest.mark.parametrize("rows", [99_870, 25_020, 130, 50_010])
+@pytest.mark.parametrize("layout", ["cycle", "iid"])
+def test_pp_packed_last_word(oracle, rows, layout):
+    # K1 pp packs a workgroup's last lane word of <= 8 groups (8 pods per evaluation,
+    # shared by up to 4 waves) where that lowers the busiest SIMD's load: 99,870 rows
+    # (16 waves, 1 group left over), 25,020 (4 waves), 130 (one wave, one word);
+    # 50,010 rows stay unpacked. i.i.d. digits take the bit-scan form, non-digit pods
+    # and tiny clusters the exact slow path, both over the packed word.
+    seed = 31 if layout == "cycle" else 32
+    rng = np.random.default_rng(seed)
+    nr = synth.nodes(rows, seed=seed)
+    if layout == "iid":
+        nr["name_digit"] = rng.integers(0, 10, rows)
+    pr = synth.pods(2_500, seed=seed)
+    pr["tolerates_unschedulable"][::5] = 1
+    pr["name_digit"][::97] = -1
+    o = oracle.schedule_nunn_omp(nr, pr, seed=seed) if rows > 1000 else oracle.schedule(nr, pr, seed=seed)
+    with engine_with(nr, seed=seed) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+
+
 def test_pp_zero_hash_winner(oracle):
     # K1 pp treats a wave maximum of 0 as "no score-10 row here" and redoes the pod
     # exactly: a pod whose only feasible score-10 node hashes to exactly 0 must still
