@@ -821,8 +821,10 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
             c->h_podz = nullptr;
             c->h_resz = nullptr;
             c->z_cap = 0;
-            if (hipHostMalloc((void **)&c->h_podz, sizeof(ms_pod_compact) * n, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&c->h_resz, sizeof(ms_result_compact) * n, hipHostMallocDefault) != hipSuccess)
+            // coherent (fine-grained): the kernel's reads see this call's host copy and
+            // its writes reach host memory with no cache maintenance between calls
+            if (hipHostMalloc((void **)&c->h_podz, sizeof(ms_pod_compact) * n, hipHostMallocCoherent) != hipSuccess ||
+                hipHostMalloc((void **)&c->h_resz, sizeof(ms_result_compact) * n, hipHostMallocCoherent) != hipSuccess)
                 return fail(c, MS_E_OOM, "compact pinned staging");
             c->z_cap = n;
         }

@@ -304,6 +304,23 @@ def test_compact_records(oracle, plugin_set, n_pods):
             e.schedule_compact(_lib.compact_pods(pr[:3]))
 
 
+def test_compact_repeated_calls(oracle):
+    # successive compact calls on one context with different pods (the pinned staging is
+    # reused, and regrown for a larger call): every call equals the oracle, binds accumulate
+    nr = synth.nodes(7000, seed=41)
+    total = np.zeros(7000, dtype=np.int64)
+    with engine_with(nr, seed=41) as e:
+        for k, n in enumerate((5000, 1200, 30_000, 3)):
+            pr = synth.pods(n, seed=41, start=k * 100_000)
+            pr["tolerates_unschedulable"][::9] = 1
+            o = oracle.schedule(nr, pr, seed=41)
+            r = e.schedule_compact(_lib.compact_pods(pr))
+            for k_res, k_or in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")):
+                assert np.array_equal(r[k_res].astype(np.int64), o[k_or].astype(np.int64)), (n, k_res)
+            total += np.bincount(o["node"][o["code"] == 0], minlength=7000)
+        assert np.array_equal(e.read(0, 7000)["pod_count"], total)
+
+
 def test_commit_uncommit(oracle):
     nr = synth.nodes(10, seed=2, resources=True)
     pr = synth.pods(1, seed=2, resources=True)
