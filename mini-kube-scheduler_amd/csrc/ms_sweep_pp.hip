@@ -572,13 +572,14 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     const uint32_t lds = chunk * (sizeof(u64) + sizeof(uint2));
     unsigned long long *kk = (results || resc) ? nullptr : keys;
     const int cm = (results || resc) ? commit : 0;
-    const bool tp = tail_pods(n_groups, W) != 0u;  // (gy == 1: the workgroup holds every group)
+    // (gy == 1: the workgroup holds every group; the 8-word form stays unpacked: its
+    // packed instantiation needs 117 VGPRs, half the waves per SIMD it sizes for)
+    const bool tp = KW == (uint32_t)kPpWords && tail_pods(n_groups, W) != 0u;
 #define MS_PP_LAUNCH(KWV, TPV)                                                                                     \
     hipExtLaunchKernelGGL((k_sweep_nunn_pp<KWV, TPV>), grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes, t.gcap, \
                           n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc)
     if (KW == (uint32_t)kPpWordsSmall) {
-        if (tp) MS_PP_LAUNCH(kPpWordsSmall, true);
-        else MS_PP_LAUNCH(kPpWordsSmall, false);
+        MS_PP_LAUNCH(kPpWordsSmall, false);
     } else {
         if (tp) MS_PP_LAUNCH(kPpWords, true);
         else MS_PP_LAUNCH(kPpWords, false);
