@@ -5,9 +5,9 @@ TAG=${1:-r03zh}
 mkdir -p gpurun_out/$TAG
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 T="timeout -k 10"
-$T 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "nunn or pp or fuzz or config_c or config_d or sharded or smoke or parity" > gpurun_out/$TAG/tests.log 2>&1
+$T 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "nunn or pp or fuzz or config_c or sharded or parity" > gpurun_out/$TAG/tests.log 2>&1
 rc=$?; tail -1 gpurun_out/$TAG/tests.log; [ $rc -eq 0 ] || exit $rc
-export PROBE_ROWS=100000,99840,50010,25000 PROBE_STEPS=200
+export PROBE_ROWS=100000,25000,25020,6250,50000 PROBE_STEPS=200
 L=$PWD/mini-kube-scheduler_amd/minisched_amd
 for r in 1 2; do
   for v in t0 def; do
