@@ -584,6 +584,11 @@ __device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_
 // where the lane = row form paid a sort plus four wave-wide max extractions
 // per (pod, tile) on top of its evaluations.
 constexpr uint32_t kTpPods = 16;
+#ifndef MS_TP_UNROLL
+#define MS_TP_UNROLL 2  // row blocks unrolled in sweep_tp_task (A/B)
+#endif
+#define MS_PRAGMA(x) _Pragma(#x)
+#define MS_UNROLL(n) MS_PRAGMA(unroll n)
 
 __device__ __forceinline__ void tile_keys_store(u64 *dst, uint32_t j, const u64 (&k)[4]) {
     *dst = j == 0 ? k[0] : j == 1 ? k[1] : j == 2 ? k[2] : k[3];
@@ -675,7 +680,7 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     const DRow *d = rows + part;  // the tile's rows, staged in LDS
     u64 k[4] = {0ull, 0ull, 0ull, 0ull};
     // rows 4 at a time (LDS reads issued together at the top of each block)
-#pragma unroll 2
+    MS_UNROLL(MS_TP_UNROLL)
     for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
         u64 x[4];
 #pragma unroll
