@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 3
+#define MS_ABI_VERSION 4
 
 /* ---- return codes -------------------------------------------------------- */
 #define MS_OK 0
@@ -173,6 +173,26 @@ int ms_destroy(ms_ctx *ctx);
  * thread when ctx is NULL). Never NULL. */
 const char *ms_last_error(const ms_ctx *ctx);
 int ms_get_info(const ms_ctx *ctx, ms_info *out);
+
+/* Host-side phase times of the last ms_schedule_batch / ms_schedule_batch_compact
+ * call on ctx (diagnostics: where a slow host call spent its wall time). ns[]
+ * is indexed by MS_PH_*; every phase is host wall time inside the call, and
+ * the phases sum to ns[MS_PH_TOTAL] up to the bookkeeping between them. */
+#define MS_CALL_PHASES 8
+enum {
+    MS_PH_TOTAL = 0,      /* the whole call                                            */
+    MS_PH_LOCK_FLUSH = 1, /* scheduling lock + drain of queued node deltas              */
+    MS_PH_STAGE_IN = 2,   /* pods host -> staging / H2D enqueue (pageable: runtime copy) */
+    MS_PH_LAUNCH = 3,     /* kernel launches of the cycle (and collectives)             */
+    MS_PH_STAGE_OUT = 4,  /* D2H enqueue / results staging -> caller's array            */
+    MS_PH_WAIT = 5,       /* blocked in stream synchronisation                          */
+    MS_PH_ALLOC = 6,      /* (re)allocation of staging buffers                          */
+    MS_PH_CHUNKS = 7      /* number of copy/cycle chunks (a count, not ns)              */
+};
+typedef struct ms_call_profile {
+    uint64_t ns[MS_CALL_PHASES];
+} ms_call_profile;
+int ms_last_call_profile(const ms_ctx *ctx, ms_call_profile *out);
 
 /* ---- node deltas (informer Add/Update/Delete, eventhandler.go:60-76) ------
  * Enqueued under a mutex (safe from informer goroutines while another thread

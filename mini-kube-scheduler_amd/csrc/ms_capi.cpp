@@ -455,7 +455,7 @@ uint32_t e2e_chunks(uint32_t n) {
     return std::max(1u, std::min(k, n / kE2eMinChunk));
 }
 
-int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *out, uint32_t parts) {
+int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *out, uint32_t parts, CallClock &ck) {
     const hipStream_t s = c->stream;
     if (!c->copy_stream) {
         MS_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
@@ -463,32 +463,40 @@ int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *o
             MS_HIP(c, hipEventCreateWithFlags(&c->ev_copy[i], hipEventDisableTiming));
             MS_HIP(c, hipEventCreateWithFlags(&c->ev_cyc[i], hipEventDisableTiming));
         }
+        ck.lap(MS_PH_ALLOC);
     }
     const hipStream_t cs = c->copy_stream;
     const uint32_t per = cdiv(n, parts);
     auto beg = [&](uint32_t i) { return std::min(n, i * per); };
     auto cnt = [&](uint32_t i) { return beg(i + 1) - beg(i); };
+    ck.count(MS_PH_CHUNKS, parts);
     MS_HIP(c, hipMemcpyAsync(c->d_pods, pods, sizeof(ms_pod_rec) * cnt(0), hipMemcpyHostToDevice, s));
+    ck.lap(MS_PH_STAGE_IN);
     for (uint32_t i = 0; i < parts; ++i) {
         if (i > 0) MS_HIP(c, hipStreamWaitEvent(s, c->ev_copy[i], 0));
         int rc = select_locked(c, cnt(i), c->d_pods + beg(i), c->d_res + beg(i), s, 1);
         if (rc) return rc;
         MS_HIP(c, hipEventRecord(c->ev_cyc[i], s));
+        ck.lap(MS_PH_LAUNCH);
         if (i + 1 < parts) {
             MS_HIP(c, hipMemcpyAsync(c->d_pods + beg(i + 1), pods + beg(i + 1), sizeof(ms_pod_rec) * cnt(i + 1),
                                      hipMemcpyHostToDevice, cs));
             MS_HIP(c, hipEventRecord(c->ev_copy[i + 1], cs));
+            ck.lap(MS_PH_STAGE_IN);
         }
         if (i > 0) {
             MS_HIP(c, hipStreamWaitEvent(cs, c->ev_cyc[i - 1], 0));
             MS_HIP(c, hipMemcpyAsync(out + beg(i - 1), c->d_res + beg(i - 1), sizeof(ms_result) * cnt(i - 1),
                                      hipMemcpyDeviceToHost, cs));
+            ck.lap(MS_PH_STAGE_OUT);
         }
     }
     MS_HIP(c, hipMemcpyAsync(out + beg(parts - 1), c->d_res + beg(parts - 1), sizeof(ms_result) * cnt(parts - 1),
                              hipMemcpyDeviceToHost, s));
+    ck.lap(MS_PH_STAGE_OUT);
     MS_HIP(c, hipStreamSynchronize(cs));
     MS_HIP(c, hipStreamSynchronize(s));
+    ck.lap(MS_PH_WAIT);
     return MS_OK;
 }
 
@@ -637,6 +645,12 @@ int ms_destroy(ms_ctx *c) {
 
 const char *ms_last_error(const ms_ctx *c) { return c ? c->err.c_str() : g_create_err.c_str(); }
 
+int ms_last_call_profile(const ms_ctx *c, ms_call_profile *out) {
+    if (!valid_ctx(c) || !out) return MS_E_INVAL;
+    for (int i = 0; i < MS_CALL_PHASES; ++i) out->ns[i] = c->prof[i];
+    return MS_OK;
+}
+
 int ms_get_info(const ms_ctx *c, ms_info *out) {
     if (!valid_ctx(c) || !out) return MS_E_INVAL;
     ms_ctx *m = const_cast<ms_ctx *>(c);
@@ -735,10 +749,12 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     if (mode != MS_MODE_BATCHED && mode != MS_MODE_SEQUENTIAL) return fail(c, MS_E_INVAL, "unknown mode");
     if (n_pods == 0) return MS_OK;
     std::lock_guard<std::mutex> g(c->sched_mu);
+    CallClock ck(c);
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
-    if (c->comm) return comm_schedule_host(c, n_pods, pods, mode, out);  // node-sharded over the communicator
+    ck.lap(MS_PH_LOCK_FLUSH);
+    if (c->comm) return comm_schedule_host(c, n_pods, pods, mode, out, &ck);  // node-sharded over the communicator
     const hipStream_t s = c->stream;
     ++c->ctx_seq;  // binds below write the table on the context stream
     uint32_t B = c->batch_cap;
@@ -747,6 +763,7 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
         // its binds lands: one pass over the whole call (header contract)
         rc = ensure_stage(c, n_pods);
         if (rc) return rc;
+        ck.lap(MS_PH_ALLOC);
         B = n_pods;
     }
     // Host arrays go straight to the device (the runtime's own pageable-copy
@@ -762,10 +779,11 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, hipStreamSynchronize(s));  // h_pods / h_res free to reuse
+        ck.lap(MS_PH_WAIT);
         const bool seq_full = (mode == MS_MODE_SEQUENTIAL && c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA);
         const uint32_t parts = (pageable && plugins_stateless(c)) ? e2e_chunks(nb) : 1u;
         if (parts > 1) {  // (NU+NN / NA: binds never change a later pod's keys, so chunks equal one batch)
-            rc = schedule_chunked(c, pods + s0, nb, out + s0, parts);
+            rc = schedule_chunked(c, pods + s0, nb, out + s0, parts, ck);
             if (rc) return rc;
             continue;
         }
@@ -775,6 +793,8 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
             std::memcpy(c->h_pods, pods + s0, sizeof(ms_pod_rec) * nb);
             MS_HIP(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
         }
+        ck.count(MS_PH_CHUNKS);
+        ck.lap(MS_PH_STAGE_IN);
         if (seq_full) {
             rc = run_sequential(c, nb, c->d_pods, c->d_res, s);
             if (rc) return rc;
@@ -784,13 +804,18 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
             rc = select_locked(c, nb, c->d_pods, c->d_res, s, 1);
             if (rc) return rc;
         }
+        ck.lap(MS_PH_LAUNCH);
         if (pageable) {
             MS_HIP(c, hipMemcpyAsync(out + s0, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
+            ck.lap(MS_PH_STAGE_OUT);
             MS_HIP(c, hipStreamSynchronize(s));
+            ck.lap(MS_PH_WAIT);
         } else {
             MS_HIP(c, hipMemcpyAsync(c->h_res, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
             MS_HIP(c, hipStreamSynchronize(s));
+            ck.lap(MS_PH_WAIT);
             std::memcpy(out + s0, c->h_res, sizeof(ms_result) * nb);
+            ck.lap(MS_PH_STAGE_OUT);
         }
     }
     return MS_OK;
@@ -803,9 +828,12 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
         return fail(c, MS_E_INVAL, "ms_schedule_batch_compact: the resource-aware set needs ms_schedule_batch");
     if (n == 0) return MS_OK;
     std::lock_guard<std::mutex> g(c->sched_mu);
+    CallClock ck(c);
+    ck.count(MS_PH_CHUNKS);
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
+    ck.lap(MS_PH_LOCK_FLUSH);
     // Single-shard NU+NN: one launch reading the pods from and writing the
     // results to pinned host memory (8 B each way per pod over PCIe, no copy
     // commands, no widen / narrow passes); the host copies the caller's arrays
@@ -827,15 +855,21 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
                 hipHostMalloc((void **)&c->h_resz, sizeof(ms_result_compact) * n, hipHostMallocCoherent) != hipSuccess)
                 return fail(c, MS_E_OOM, "compact pinned staging");
             c->z_cap = n;
+            ck.lap(MS_PH_ALLOC);
         }
         const hipStream_t s = c->stream;
         MS_HIP(c, hipStreamSynchronize(s));  // (no earlier call still reads h_podz)
+        ck.lap(MS_PH_WAIT);
         std::memcpy(c->h_podz, pods, sizeof(ms_pod_compact) * n);
+        ck.lap(MS_PH_STAGE_IN);
         ++c->ctx_seq;  // binds write the table on the context stream
         MS_HIP(c, launch_sweep_pp_compact(c->t, c->rows_dev, c->h_podz, n, seed32_of(c->cfg.seed), c->h_resz,
                                           c->present_dev, c->num_cus, s));
+        ck.lap(MS_PH_LAUNCH);
         MS_HIP(c, hipStreamSynchronize(s));
+        ck.lap(MS_PH_WAIT);
         std::memcpy(out, c->h_resz, sizeof(ms_result_compact) * n);
+        ck.lap(MS_PH_STAGE_OUT);
         return MS_OK;
     }
     rc = c->comm ? comm_stage(c, n) : ensure_stage(c, n);
@@ -851,9 +885,11 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
             return fail(c, MS_E_OOM, "compact staging");
         c->compact_cap = n;
     }
+    ck.lap(MS_PH_ALLOC);
     const hipStream_t s = c->stream;
     // 8 B per pod in and out over PCIe; widened / narrowed on the device
     MS_HIP(c, hipMemcpyAsync(c->d_podc, pods, sizeof(ms_pod_compact) * n, hipMemcpyHostToDevice, s));
+    ck.lap(MS_PH_STAGE_IN);
     MS_HIP(c, launch_pods_widen(c->d_podc, n, c->d_pods, s));
     if (c->comm) {
         rc = comm_cycle_staged(c, n, mode);
@@ -863,8 +899,11 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
     }
     if (rc) return rc;
     MS_HIP(c, launch_results_narrow(c->d_res, n, c->d_resc, s));
+    ck.lap(MS_PH_LAUNCH);
     MS_HIP(c, hipMemcpyAsync(out, c->d_resc, sizeof(ms_result_compact) * n, hipMemcpyDeviceToHost, s));
+    ck.lap(MS_PH_STAGE_OUT);
     MS_HIP(c, hipStreamSynchronize(s));
+    ck.lap(MS_PH_WAIT);
     return MS_OK;
 }
 

@@ -54,6 +54,17 @@
 
 #include "ms_ctx.h"
 
+// The RCCL entry points. `make comm-loopback` (tests only) builds this file with
+// -DMS_COMM_LOOPBACK against an in-process rendezvous of G contexts on one GPU
+// (ms_comm_loopback.h), so the world > 1 code below runs on a 1-GPU box; the
+// product library calls RCCL itself.
+#ifdef MS_COMM_LOOPBACK
+#include "ms_comm_loopback.h"
+#define CCL(fn) lb_##fn
+#else
+#define CCL(fn) fn
+#endif
+
 namespace msgpu {
 
 namespace {
@@ -121,7 +132,7 @@ namespace {
     do {                                                                                          \
         ncclResult_t r_ = (call);                                                                 \
         if (r_ != ncclSuccess)                                                                    \
-            return fail((c), MS_E_RCCL, std::string(#call) + ": " + ncclGetErrorString(r_));      \
+            return fail((c), MS_E_RCCL, std::string(#call) + ": " + CCL(ncclGetErrorString)(r_));      \
     } while (0)
 
 void free_slot(ShardSlot &sl) {
@@ -267,18 +278,18 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     host_tick(m, 2, tp);  // events to the collective stream
     ncclResult_t r = ncclSuccess;
     if (ps == MS_PLUGINS_NU_NN) {  // the keys alone: one call, no group
-        r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
+        r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
     } else {
-        r = ncclGroupStart();
-        if (r == ncclSuccess) r = ncclReduceScatter(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
+        r = CCL(ncclGroupStart)();
+        if (r == ncclSuccess) r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
         if (r == ncclSuccess && ps == MS_PLUGINS_NU_NRF_NN_LA)  // 0/1 bytes: uint8 MAX = OR
-            r = ncclReduceScatter(sl.flags, sl.flags_mine, (size_t)per * 4, ncclUint8, ncclMax, m.comm, m.cs);
+            r = CCL(ncclReduceScatter)(sl.flags, sl.flags_mine, (size_t)per * 4, ncclUint8, ncclMax, m.comm, m.cs);
         if (r == ncclSuccess && ps == MS_PLUGINS_NU_NN_NA)  // anchors < 2^21: uint32 MAX
-            r = ncclReduceScatter(sl.flags, sl.flags_mine, per, ncclUint32, ncclMax, m.comm, m.cs);
-        const ncclResult_t r2 = ncclGroupEnd();
+            r = CCL(ncclReduceScatter)(sl.flags, sl.flags_mine, per, ncclUint32, ncclMax, m.comm, m.cs);
+        const ncclResult_t r2 = CCL(ncclGroupEnd)();
         if (r == ncclSuccess) r = r2;
     }
-    if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sharded reduce-scatter: ") + ncclGetErrorString(r));
+    if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sharded reduce-scatter: ") + CCL(ncclGetErrorString)(r));
     host_tick(m, 3, tp);  // the grouped reduce-scatter
     MS_HIP(c, hipEventRecord(m.ev_comb[si], m.cs));
     Pending p{si, n, 0, 0, pods, results};
@@ -344,12 +355,12 @@ int seq_sharded_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result 
             MS_HIP(c, launch_seq_window_in(pods, n, m.ctl, m.win_pods, W, s));
             rc = seq_candidates_locked(c, W, m.win_pods, m.cands, m.sflags, s);
             if (rc) return rc;
-            ncclResult_t e = ncclGroupStart();
-            if (e == ncclSuccess) e = ncclAllGather(m.cands, m.cands_all, cand_bytes, ncclUint8, m.comm, s);
-            if (e == ncclSuccess) e = ncclAllGather(m.sflags, m.sflags_all, W, ncclUint32, m.comm, s);
-            const ncclResult_t e2 = ncclGroupEnd();
+            ncclResult_t e = CCL(ncclGroupStart)();
+            if (e == ncclSuccess) e = CCL(ncclAllGather)(m.cands, m.cands_all, cand_bytes, ncclUint8, m.comm, s);
+            if (e == ncclSuccess) e = CCL(ncclAllGather)(m.sflags, m.sflags_all, W, ncclUint32, m.comm, s);
+            const ncclResult_t e2 = CCL(ncclGroupEnd)();
             if (e == ncclSuccess) e = e2;
-            if (e != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sequential all-gather: ") + ncclGetErrorString(e));
+            if (e != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sequential all-gather: ") + CCL(ncclGetErrorString)(e));
             MS_HIP(c, launch_seq_validate_rep(c->t, W, m.win_pods, seed32, (uint32_t)m.world, m.cands_all, m.sflags_all,
                                               m.merged, m.merged_flags, m.win_res, m.ctl + 2, s, m.ctl + 1));
             MS_HIP(c, launch_seq_window_out(m.win_res, m.ctl, results, n, s));
@@ -379,7 +390,7 @@ int batched_all_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result 
     if (rc) return rc;
     // (a rank whose slice is short or empty sends entries past n: never read)
     const size_t bytes = (size_t)per * sizeof(ms_result);
-    MS_NCCL(c, ncclAllGather(reinterpret_cast<char *>(stage) + (size_t)m.rank * bytes, stage, bytes, ncclUint8, m.comm, s));
+    MS_NCCL(c, CCL(ncclAllGather)(reinterpret_cast<char *>(stage) + (size_t)m.rank * bytes, stage, bytes, ncclUint8, m.comm, s));
     if (commit) MS_HIP(c, launch_apply_binds(c->t, pods, n, stage, s));  // NodeInfo.AddPod on this shard's winners
     return MS_OK;
 }
@@ -414,7 +425,7 @@ void comm_free(ms_ctx *c) {
     if (m->cs) (void)hipStreamSynchronize(m->cs);
     if (m->ds) (void)hipStreamSynchronize(m->ds);
     (void)hipDeviceSynchronize();
-    if (m->comm) (void)ncclCommDestroy(m->comm);
+    if (m->comm) (void)CCL(ncclCommDestroy)(m->comm);
     for (uint32_t i = 0; i < kPipeMax; ++i) {
         free_slot(m->slot[i]);
         if (m->ev_swept[i]) (void)hipEventDestroy(m->ev_swept[i]);
@@ -454,15 +465,21 @@ int comm_stage(ms_ctx *c, uint32_t n) {
     return ensure_stage(c, std::max<uint32_t>(n, per * (uint32_t)m.world));
 }
 
-int comm_schedule_host(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, int32_t mode, ms_result *out) {
+int comm_schedule_host(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, int32_t mode, ms_result *out, CallClock *ck) {
     const hipStream_t s = c->stream;
     int rc = comm_stage(c, n);
     if (rc) return rc;
+    ck->lap(MS_PH_ALLOC);
+    ck->count(MS_PH_CHUNKS);
     MS_HIP(c, hipMemcpyAsync(c->d_pods, pods, sizeof(ms_pod_rec) * n, hipMemcpyHostToDevice, s));
+    ck->lap(MS_PH_STAGE_IN);
     rc = comm_cycle_staged(c, n, mode);
     if (rc) return rc;
+    ck->lap(MS_PH_LAUNCH);
     MS_HIP(c, hipMemcpyAsync(out, c->d_res, sizeof(ms_result) * n, hipMemcpyDeviceToHost, s));
+    ck->lap(MS_PH_STAGE_OUT);
     MS_HIP(c, hipStreamSynchronize(s));
+    ck->lap(MS_PH_WAIT);
     return MS_OK;
 }
 
@@ -481,6 +498,49 @@ int comm_schedule_device(ms_ctx *c, uint32_t n, const ms_pod_rec *pods_dev, ms_r
     return MS_OK;
 }
 
+namespace {
+
+// The communicator's streams and events, then the rendezvous of the ranks.
+int comm_setup(ms_ctx *c, CommState &m, const ms_comm_id *id, int32_t rank, int32_t world) {
+    // The collective and decode streams get the highest priority: high-priority
+    // streams are served by hardware queues of their own, so the caller's
+    // (sweep) stream can never share a queue with them and serialise a
+    // reduce-scatter or a decode behind the next sweep; their short kernels are
+    // dispatched ahead of the sweep's pending workgroups. MINISCHED_COMM_PRIO=0:
+    // normal priority (A/B).
+    int lo = 0, hi = 0;
+    MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    const char *cp = getenv("MINISCHED_COMM_PRIO");
+    const int cprio = (cp && cp[0] == '0') ? 0 : hi;
+    MS_HIP(c, hipStreamCreateWithPriority(&m.cs, hipStreamNonBlocking, cprio));
+    // (MINISCHED_SHARD_STREAMS=2 only) two sweep streams; MINISCHED_SWEEP_PRIO=1
+    // creates them with the highest priority (A/B: the collectives then fell behind)
+    if (m.two_streams) {
+        const char *pe = getenv("MINISCHED_SWEEP_PRIO");
+        const int sprio = (pe && atoi(pe) == 1) ? hi : 0;
+        for (hipStream_t &q : m.ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, sprio));
+    }
+    MS_HIP(c, hipStreamCreateWithPriority(&m.ds, hipStreamNonBlocking, cprio));
+    MS_HIP(c, hipEventCreateWithFlags(&m.ev_ds, hipEventDisableTiming));
+    for (uint32_t i = 0; i < kPipeMax; ++i) {
+        MS_HIP(c, hipEventCreateWithFlags(&m.ev_swept[i], hipEventDisableTiming));
+        MS_HIP(c, hipEventCreateWithFlags(&m.ev_comb[i], hipEventDisableTiming));
+    }
+    MS_HIP(c, hipEventCreateWithFlags(&m.ev_drained, hipEventDisableTiming));
+    MS_HIP(c, hipEventCreateWithFlags(&m.ev_in, hipEventDisableTiming));
+    MS_HIP(c, hipEventCreateWithFlags(&m.ev_ctx, hipEventDisableTiming));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id->internal, sizeof(uid));
+    const ncclResult_t r = CCL(ncclCommInitRank)(&m.comm, world, uid, rank);
+    if (r != ncclSuccess) {
+        m.comm = nullptr;
+        return fail(c, MS_E_RCCL, std::string("ncclCommInitRank: ") + CCL(ncclGetErrorString)(r));
+    }
+    return MS_OK;
+}
+
+}  // namespace
+
 }  // namespace msgpu
 
 using namespace msgpu;
@@ -490,8 +550,8 @@ extern "C" {
 int ms_comm_id_create(ms_comm_id *out) {
     if (!out) return MS_E_INVAL;
     ncclUniqueId id;
-    const ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) return fail(nullptr, MS_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    const ncclResult_t r = CCL(ncclGetUniqueId)(&id);
+    if (r != ncclSuccess) return fail(nullptr, MS_E_RCCL, std::string("ncclGetUniqueId: ") + CCL(ncclGetErrorString)(r));
     std::memcpy(out->internal, &id, sizeof(id));
     return MS_OK;
 }
@@ -512,43 +572,13 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     m->group = std::min(m->group, m->depth);
     if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->two_streams = atoi(e) == 2;
     if (const char *e = getenv("MINISCHED_HOST_PROF")) m->host_prof = atoi(e) == 1;
-    c->comm = m;  // (comm_free releases a partial state)
-    // The collective and decode streams get the highest priority: high-priority
-    // streams are served by hardware queues of their own, so the caller's
-    // (sweep) stream can never share a queue with them and serialise a
-    // reduce-scatter or a decode behind the next sweep; their short kernels are
-    // dispatched ahead of the sweep's pending workgroups. MINISCHED_COMM_PRIO=0:
-    // normal priority (A/B).
-    int lo = 0, hi = 0;
-    MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const char *cp = getenv("MINISCHED_COMM_PRIO");
-    const int cprio = (cp && cp[0] == '0') ? 0 : hi;
-    MS_HIP(c, hipStreamCreateWithPriority(&m->cs, hipStreamNonBlocking, cprio));
-    // (MINISCHED_SHARD_STREAMS=2 only) two sweep streams; MINISCHED_SWEEP_PRIO=1
-    // creates them with the highest priority (A/B: the collectives then fell behind)
-    if (m->two_streams) {
-        const char *pe = getenv("MINISCHED_SWEEP_PRIO");
-        const int sprio = (pe && atoi(pe) == 1) ? hi : 0;
-        for (hipStream_t &q : m->ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, sprio));
-    }
-    MS_HIP(c, hipStreamCreateWithPriority(&m->ds, hipStreamNonBlocking, cprio));
-    MS_HIP(c, hipEventCreateWithFlags(&m->ev_ds, hipEventDisableTiming));
-    for (uint32_t i = 0; i < kPipeMax; ++i) {
-        MS_HIP(c, hipEventCreateWithFlags(&m->ev_swept[i], hipEventDisableTiming));
-        MS_HIP(c, hipEventCreateWithFlags(&m->ev_comb[i], hipEventDisableTiming));
-    }
-    MS_HIP(c, hipEventCreateWithFlags(&m->ev_drained, hipEventDisableTiming));
-    MS_HIP(c, hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
-    MS_HIP(c, hipEventCreateWithFlags(&m->ev_ctx, hipEventDisableTiming));
-    ncclUniqueId uid;
-    std::memcpy(&uid, id->internal, sizeof(uid));
-    const ncclResult_t r = ncclCommInitRank(&m->comm, world, uid, rank);
-    if (r != ncclSuccess) {
-        m->comm = nullptr;
-        comm_free(c);
-        return fail(c, MS_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    }
-    return MS_OK;
+    // Attached before the streams exist (MS_HIP reports through the context);
+    // every failure below goes through comm_free, so a context is either joined
+    // or left without a communicator, never half-built.
+    c->comm = m;
+    const int rc = comm_setup(c, *m, id, rank, world);
+    if (rc != MS_OK) comm_free(c);
+    return rc;
 }
 
 int ms_sharded_slice(const ms_ctx *c, uint32_t n, uint32_t *first, uint32_t *count) {

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
 #include <mutex>
 #include <string>
@@ -110,6 +111,9 @@ struct ms_ctx {
     // until ms_comm_init
     msgpu::CommState *comm = nullptr;
 
+    // host phase times of the last ms_schedule_batch(_compact) call (ms_last_call_profile)
+    uint64_t prof[MS_CALL_PHASES] = {};
+
     std::string err;
 };
 
@@ -126,6 +130,31 @@ int fail(ms_ctx *c, int code, const std::string &msg);
     } while (0)
 
 inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// Host wall time of a host-array call split into MS_PH_* phases: lap(ph) adds
+// the time since the previous lap to phase ph; the destructor records the
+// call's total (every return path of the call).
+class CallClock {
+  public:
+    using Clock = std::chrono::steady_clock;
+    explicit CallClock(ms_ctx *c) : c_(c), t0_(Clock::now()), t_(t0_) {
+        for (uint64_t &v : c_->prof) v = 0;
+    }
+    ~CallClock() { c_->prof[MS_PH_TOTAL] = ns(t0_, Clock::now()); }
+    void lap(int ph) {
+        const auto now = Clock::now();
+        c_->prof[ph] += ns(t_, now);
+        t_ = now;
+    }
+    void count(int ph, uint64_t k = 1) { c_->prof[ph] += k; }
+
+  private:
+    static uint64_t ns(Clock::time_point a, Clock::time_point b) {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+    }
+    ms_ctx *c_;
+    Clock::time_point t0_, t_;
+};
 
 constexpr uint32_t kTopKCands = 4;  // ms_seq_cand entries per pod and shard (the validator's top-K)
 
@@ -147,7 +176,8 @@ int seq_candidates_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev
 void comm_free(ms_ctx *c);
 // ms_schedule_batch / ms_schedule_sequential_device on a context joined to a
 // communicator (callers hold sched_mu; deltas flushed)
-int comm_schedule_host(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode, ms_result *out);
+int comm_schedule_host(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_t mode, ms_result *out,
+                       CallClock *ck);
 // the same on pods already staged in c->d_pods (comm_stage(n) first), results in c->d_res
 int comm_stage(ms_ctx *c, uint32_t n_pods);
 int comm_cycle_staged(ms_ctx *c, uint32_t n_pods, int32_t mode);

@@ -17,6 +17,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # MINISCHED_LIB selects another build of the same ABI (e.g. the MS_STAMPS
 # diagnostic library); the default is the production library.
 LIB_PATH = os.environ.get("MINISCHED_LIB") or os.path.join(HERE, "libminisched_gpu.so")
+# TEST-ONLY build (`make comm-loopback`): ms_comm.cpp's RCCL calls replaced by an
+# in-process rendezvous, so G contexts driven by G host threads form a world-G
+# communicator on one GPU (tests/test_gpu_loopback.py). Never the product path.
+LOOPBACK_LIB_PATH = os.path.join(HERE, "libminisched_gpu_loopback.so")
 
 # ---- constants (minisched_gpu.h) -------------------------------------------
 MS_OK = 0
@@ -122,6 +126,13 @@ class ms_config(ctypes.Structure):
     ]
 
 
+CALL_PHASES = ("total", "lock_flush", "stage_in", "launch", "stage_out", "wait", "alloc", "chunks")  # MS_PH_*
+
+
+class ms_call_profile(ctypes.Structure):
+    _fields_ = [("ns", ctypes.c_uint64 * len(CALL_PHASES))]
+
+
 class ms_info(ctypes.Structure):
     _fields_ = [
         ("max_nodes", ctypes.c_uint32),
@@ -156,6 +167,7 @@ SIGNATURES = {
     "ms_destroy": (ctypes.c_int, [_vp]),
     "ms_last_error": (ctypes.c_char_p, [_vp]),
     "ms_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(ms_info)]),
+    "ms_last_call_profile": (ctypes.c_int, [_vp, ctypes.POINTER(ms_call_profile)]),
     "ms_nodes_upsert": (ctypes.c_int, [_vp, _u32, _vp, _vp]),
     "ms_nodes_delete": (ctypes.c_int, [_vp, _u32, _vp]),
     "ms_nodes_flush": (ctypes.c_int, [_vp]),
@@ -189,14 +201,15 @@ class DecodeJob(ctypes.Structure):  # ms_decode_job
 
 assert ctypes.sizeof(DecodeJob) == 40
 
-_LIB: Optional[ctypes.CDLL] = None
+_LIBS: dict = {}
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Loads the HIP library (fails loudly when it was not built)."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
+    """Loads the HIP library (fails loudly when it was not built). Each path is
+    its own handle (RTLD_LOCAL), so a test can hold the product library and the
+    loopback build side by side."""
+    if path in _LIBS:
+        return _LIBS[path]
     if not os.path.exists(path):
         raise RuntimeError(
             f"{path} is missing: build it with `make -C mini-kube-scheduler_amd` "
@@ -217,7 +230,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _LIB = lib
+    if hasattr(lib, "lb_collectives_issued"):  # the loopback build only
+        lib.lb_collectives_issued.restype = ctypes.c_ulonglong
+        lib.lb_collectives_issued.argtypes = []
+    _LIBS[path] = lib
     return lib
 
 
@@ -231,10 +247,10 @@ def _ptr(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
-def comm_id_create() -> bytes:
+def comm_id_create(lib: Optional[ctypes.CDLL] = None) -> bytes:
     """A new communicator id (rank 0 creates it and ships the bytes to every rank)."""
     out = ms_comm_id()
-    lib = load()
+    lib = lib or load()
     rc = lib.ms_comm_id_create(ctypes.byref(out))
     if rc != MS_OK:
         raise MSError("ms_comm_id_create", rc, lib.ms_last_error(None).decode())
@@ -259,8 +275,9 @@ class Engine:
         device: int = 0,
         max_batch: int = 1 << 16,
         score_weights=(0, 0),
+        lib: Optional[ctypes.CDLL] = None,
     ):
-        self.lib = load()
+        self.lib = lib or load()
         cfg = ms_config(device, plugin_set, max_nodes, node_base, max_batch, (ctypes.c_uint16 * 2)(*score_weights), seed)
         h = ctypes.c_void_p()
         rc = self.lib.ms_create(ctypes.byref(cfg), ctypes.byref(h))
@@ -294,6 +311,13 @@ class Engine:
         out = ms_info()
         self._check("ms_get_info", self.lib.ms_get_info(self.h, ctypes.byref(out)))
         return out
+
+    def last_call_profile(self) -> dict:
+        """Host phase times of the last ms_schedule_batch(_compact) call: microseconds
+        per MS_PH_* phase (chunks: a count)."""
+        out = ms_call_profile()
+        self._check("ms_last_call_profile", self.lib.ms_last_call_profile(self.h, ctypes.byref(out)))
+        return {k: (int(out.ns[i]) if k == "chunks" else out.ns[i] * 1e-3) for i, k in enumerate(CALL_PHASES)}
 
     def upsert(self, ordinals: np.ndarray, recs: np.ndarray):
         o = np.ascontiguousarray(ordinals, dtype=np.uint32)

@@ -69,7 +69,7 @@ def test_library_links_rccl():
 
 def test_abi_version_and_no_device_error_path():
     lib = _lib.load()
-    assert lib.ms_abi_version() == 3
+    assert lib.ms_abi_version() == 4
     if _lib.device_count() > 0:
         pytest.skip("a device is visible; the no-device path is exercised on CPU hosts")
     cfg = _lib.ms_config(0, 0, 16, 0, 64, (ctypes.c_uint16 * 2)(), 1)
@@ -116,3 +116,22 @@ def test_comm_id_create_on_host():
     # rank receives its 128 bytes out of band (sharded.init_comm broadcasts them)
     a, b = _lib.comm_id_create(), _lib.comm_id_create()
     assert len(a) == len(b) == _lib.COMM_ID_BYTES and a != b
+
+
+def test_loopback_build_is_test_only():
+    # `make comm-loopback`: the same ABI with ms_comm.cpp's RCCL calls replaced by an
+    # in-process rendezvous (tests/test_gpu_loopback.py); it links no RCCL, and the
+    # product library exports none of its symbols
+    assert os.path.exists(_lib.LOOPBACK_LIB_PATH), "make -C mini-kube-scheduler_amd comm-loopback"
+    dyn = subprocess.run(["readelf", "-d", _lib.LOOPBACK_LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "librccl.so" not in dyn
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LOOPBACK_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert set(re.findall(r" T (ms_\w+)", out)) == set(declared_functions())
+    assert "lb_ncclReduceScatter" in out and "lb_collectives_issued" in out
+    prod = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout
+    assert "lb_" not in prod
+    und = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert "ncclReduceScatter" in und and "ncclAllGather" in und
