@@ -61,6 +61,13 @@ BYTES_PER_EVAL = {"NU+NN": 2, "NU+NRF+NN+LA": 58}
 # SIMD at 8 waves/SIMD (tools/ubench/valu_rates.hip, profiles/r02c_valu_rates.txt).
 VALU_PEAK_NOMINAL = 256 * 4 * 2.4e9 / 4
 VALU_PEAK_MEASURED = 256 * 4 / 1.75e-9
+# MI355X_MICROARCH.md (lines 54, 473): a wave64 VALU op issues over 2 cycles on a
+# SIMD-32, i.e. 1.229e12 wave-instructions/s chip-wide. No instruction this
+# kernel uses reached it in our microbenchmark (~4.2 cycles each at 8 waves per
+# SIMD, profiles/r02c_valu_rates.txt), so `frac` stays against the 4-cycle
+# rate and `frac_vs_guide_peak` reports the guide's figure beside it.
+VALU_PEAK_GUIDE = 256 * 4 * 2.4e9 / 2
+VALU_RATES_UBENCH = "tools/ubench/valu_rates.hip -> profiles/r02c_valu_rates.txt"
 PP_KERNEL = "k_sweep_nunn_pp"
 
 
@@ -111,7 +118,10 @@ def cpu_baseline(n_nodes, seed, target_s):
 
     from minisched_amd import synth
 
-    threads = min(16, os.cpu_count() or 1)  # the box's CPU share is 16
+    from minisched_amd.hostinfo import cpu_share
+
+    share = cpu_share()  # the affinity mask, capped by the cgroup CPU quota
+    threads = share["threads"]
     nr = synth.nodes(n_nodes, seed=seed)
     n_probe = 1024
     probe = synth.pods(n_probe, seed=seed)
@@ -135,6 +145,9 @@ def cpu_baseline(n_nodes, seed, target_s):
         "pods_per_s": n_pods / dt,
         "cpu_model": cpu_model(),
         "nproc": os.cpu_count(),
+        "affinity_cpus": share["affinity"],
+        "cgroup_quota_cpus": share["quota"],
+        "threads_rule": "len(os.sched_getaffinity(0)), capped by the cgroup CPU quota (minisched_amd/hostinfo.py)",
         "faithful_1t": faithful,
     }
 
@@ -197,17 +210,20 @@ def e2e_host(eng, pods_np, n_nodes, world=1, compact=False):
         out = np.zeros(len(pods_np), dtype=_lib.RESULT)
         call = lambda: eng.schedule(pods_np, _lib.MODE_BATCHED, out=out)  # noqa: E731
     call()
-    ts = []
+    ts, phases = [], []
     for _ in range(5):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         call()
         ts.append(time.perf_counter() - t0)
+        # host phase times inside the call (ms_last_call_profile, us)
+        phases.append({k: round(v, 1) if k != "chunks" else v for k, v in eng.last_call_profile().items()})
     ms = float(np.median(ts)) * 1e3
     P = len(pods_np)
     return {"ms_median": ms, "pods_per_s": P / (ms * 1e-3), "evals_per_s": P * n_nodes / (ms * 1e-3),
-            "runs": [t * 1e3 for t in ts],
+            "runs": [t * 1e3 for t in ts], "max_over_median": max(ts) / float(np.median(ts)),
+            "phases_us": phases,
             "includes": ("ms_schedule_batch_compact: 8 B pods copied from the (pageable) host array into pinned "
                          "memory the kernel reads over PCIe (single shard; a staged H2D with N > 1)" if compact else
                          "ms_schedule_batch: H2D of 40 B pods (pageable host array)")
@@ -256,7 +272,9 @@ def other_configs(args, dev, stream):
 
     from minisched_amd import _lib, synth
 
-    threads = min(16, os.cpu_count() or 1)
+    from minisched_amd.hostinfo import cpu_threads
+
+    threads = cpu_threads()
     out = {}
     sync = torch.cuda.synchronize
 
@@ -372,10 +390,13 @@ def other_configs(args, dev, stream):
             "bound": "valu", "kernel": "k_seq_step",
             "achieved": valu / step_s, "peak": VALU_PEAK_NOMINAL, "unit": "wave-instr/s",
             "frac": valu / step_s / VALU_PEAK_NOMINAL,
+            "frac_vs_guide_peak": valu / step_s / VALU_PEAK_GUIDE,
             "valu_insts_per_launch": valu, "kernel_ms_rocprof": step_s * 1e3,
             "validator_ns_per_pod": pj.get("validator_ns_per_pod"),
             "validator_frac_of_step": pj.get("validator_frac_of_step"),
             "traffic": pj.get("step_hbm_bytes"),
+            "fetch_bytes_per_step": pj.get("step_FETCH_SIZE_KB", 0) * 1024 * 2 or None,  # (gfx950 x2 read correction)
+            "write_bytes_per_step": pj.get("step_WRITE_SIZE_KB", 0) * 1024 or None,
             "hbm": {"algorithmic_bytes_per_eval": BYTES_PER_EVAL["NU+NRF+NN+LA"],
                     "algorithmic_GBps": N * P * BYTES_PER_EVAL["NU+NRF+NN+LA"] / med / 1e9},
             "profile": os.path.relpath(args.profile_json_e, ROOT),
@@ -518,6 +539,10 @@ def main():
             "unit": "wave-instr/s",
             "frac": (valu / kernel_s) / VALU_PEAK_NOMINAL if valu else None,
             "frac_of_measured_ceiling": (valu / kernel_s) / VALU_PEAK_MEASURED if valu else None,
+            "peak_guide": VALU_PEAK_GUIDE,
+            "frac_vs_guide_peak": (valu / kernel_s) / VALU_PEAK_GUIDE if valu else None,
+            "peak_note": "peak = 4-cycle wave64 issue (the measured rate of every instruction K1 uses, "
+                         + VALU_RATES_UBENCH + "); peak_guide = the guide's 2-cycle wave64 rate",
             "traffic": traffic,
             "kernel": PP_KERNEL,
             "kernel_ms": kernel_ms,

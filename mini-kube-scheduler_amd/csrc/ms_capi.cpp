@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -500,6 +501,97 @@ int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *o
     return MS_OK;
 }
 
+// Pinned coherent staging of compact records (the compact cycle's kernel reads
+// the pods from and writes the results to it over PCIe), grown to n.
+int ensure_zc(ms_ctx *c, uint32_t n) {
+    if (n <= c->z_cap) return MS_OK;
+    if (c->h_podz) (void)hipHostFree(c->h_podz);
+    if (c->h_resz) (void)hipHostFree(c->h_resz);
+    c->h_podz = nullptr;
+    c->h_resz = nullptr;
+    c->z_cap = 0;
+    // coherent (fine-grained): the kernel's reads see this call's host copy and
+    // its writes reach host memory with no cache maintenance between calls
+    if (hipHostMalloc((void **)&c->h_podz, sizeof(ms_pod_compact) * n, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_resz, sizeof(ms_result_compact) * n, hipHostMallocCoherent) != hipSuccess)
+        return fail(c, MS_E_OOM, "compact pinned staging");
+    c->z_cap = n;
+    return MS_OK;
+}
+
+// The single-shard NU+NN cycle of a host-array call without runtime (pageable)
+// copies: chunk by chunk, the host writes the 8-B compact records K1 reads into
+// pinned coherent memory (narrowing 40-B ms_pod_rec, or copying compact ones),
+// the compact cycle kernel (one launch per chunk, binds included) reads them
+// and writes 8-B results there over PCIe, and the host moves chunk i-1's
+// results into the caller's array (widening to ms_result, or copying) while
+// chunk i runs. For ms_schedule_batch the pageable copies this replaces cost
+// 0.59 ms at config C (the blocking D2H alone ~0.42 ms of host time) and once
+// took 7.3 ms (BENCH_r03 e2e.runs[4]; the A/B rerun caught a 6.7 ms pageable
+// H2D in the call's stage_in phase, profiles/r04b_e2e_zc_ab.txt);
+// MINISCHED_PAGEABLE_E2E=1 restores them (A/B). Chunks: one per 128k pods, at
+// most 4 (config C's 100k pods: one; 4 chunks of 25k pods cost as much kernel
+// time as their overlap saved, 0.448 vs 0.451 ms, and 0.402 vs 0.370 ms for
+// compact records). MINISCHED_ZC_PARTS overrides the chunk count (1..4).
+constexpr uint32_t kZcMinChunk = 131072;
+template <typename PodIn, typename ResOut>
+int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock &ck) {
+    static_assert(sizeof(ms_pod_compact) <= sizeof(PodIn), "compact pod = the first 8 B of a pod record");
+    const hipStream_t s = c->stream;
+    int rc = ensure_zc(c, n);
+    if (rc) return rc;
+    if (!c->ev_cyc[0]) {
+        for (int i = 0; i < 4; ++i) MS_HIP(c, hipEventCreateWithFlags(&c->ev_cyc[i], hipEventDisableTiming));
+    }
+    ck.lap(MS_PH_ALLOC);
+    MS_HIP(c, hipStreamSynchronize(s));  // (no earlier call still reads h_podz)
+    ck.lap(MS_PH_WAIT);
+    static const uint32_t parts_env = [] {
+        const char *e = getenv("MINISCHED_ZC_PARTS");
+        return e ? (uint32_t)std::min(4, std::max(1, atoi(e))) : 0u;
+    }();
+    const uint32_t parts = parts_env ? std::min(parts_env, std::max(1u, n)) : std::max(1u, std::min(4u, n / kZcMinChunk));
+    const uint32_t per = cdiv(n, parts);
+    auto beg = [&](uint32_t i) { return std::min(n, i * per); };
+    auto move_out = [&](uint32_t i) {
+        const ms_result_compact *r = c->h_resz;
+        if constexpr (std::is_same<ResOut, ms_result_compact>::value) {
+            std::memcpy(out + beg(i), r + beg(i), sizeof(ms_result_compact) * (beg(i + 1) - beg(i)));
+        } else {
+            for (uint32_t j = beg(i); j < beg(i + 1); ++j) {
+                const ms_result_compact x = r[j];
+                out[j] = ms_result{x.node, (int32_t)x.code, (int64_t)x.score, (uint32_t)x.plugin_mask, 0u};
+            }
+        }
+    };
+    ++c->ctx_seq;  // binds write the table on the context stream
+    ck.count(MS_PH_CHUNKS, parts);
+    for (uint32_t i = 0; i < parts; ++i) {
+        ms_pod_compact *z = c->h_podz;
+        if constexpr (std::is_same<PodIn, ms_pod_compact>::value) {
+            std::memcpy(z + beg(i), pods + beg(i), sizeof(ms_pod_compact) * (beg(i + 1) - beg(i)));
+        } else {
+            for (uint32_t j = beg(i); j < beg(i + 1); ++j) std::memcpy(&z[j], &pods[j], sizeof(ms_pod_compact));
+        }
+        ck.lap(MS_PH_STAGE_IN);
+        MS_HIP(c, launch_sweep_pp_compact(c->t, c->rows_dev, c->h_podz + beg(i), beg(i + 1) - beg(i),
+                                          seed32_of(c->cfg.seed), c->h_resz + beg(i), c->present_dev, c->num_cus, s));
+        MS_HIP(c, hipEventRecord(c->ev_cyc[i], s));
+        ck.lap(MS_PH_LAUNCH);
+        if (i > 0) {
+            MS_HIP(c, hipEventSynchronize(c->ev_cyc[i - 1]));
+            ck.lap(MS_PH_WAIT);
+            move_out(i - 1);
+            ck.lap(MS_PH_STAGE_OUT);
+        }
+    }
+    MS_HIP(c, hipEventSynchronize(c->ev_cyc[parts - 1]));
+    ck.lap(MS_PH_WAIT);
+    move_out(parts - 1);
+    ck.lap(MS_PH_STAGE_OUT);
+    return MS_OK;
+}
+
 // This shard's speculative top-4 candidates with records, and its filter flags,
 // for a batch of at most MS_SEQ_SHARD_BATCH_MAX pods (ms_seq_candidates_device;
 // the in-library node-sharded sequential cycle).
@@ -755,6 +847,12 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     if (rc) return rc;
     ck.lap(MS_PH_LOCK_FLUSH);
     if (c->comm) return comm_schedule_host(c, n_pods, pods, mode, out, &ck);  // node-sharded over the communicator
+    static const bool zc_e2e = [] {
+        const char *e = getenv("MINISCHED_PAGEABLE_E2E");
+        return !(e && e[0] == '1');
+    }();
+    if (zc_e2e && !c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows)
+        return schedule_zc(c, pods, n_pods, out, ck);  // (NU+NN: both modes are the batched cycle + binds)
     const hipStream_t s = c->stream;
     ++c->ctx_seq;  // binds below write the table on the context stream
     uint32_t B = c->batch_cap;
@@ -829,7 +927,6 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
     if (n == 0) return MS_OK;
     std::lock_guard<std::mutex> g(c->sched_mu);
     CallClock ck(c);
-    ck.count(MS_PH_CHUNKS);
     MS_HIP(c, hipSetDevice(c->cfg.device));
     int rc = flush_locked(c);
     if (rc) return rc;
@@ -842,36 +939,8 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
         const char *e = getenv("MINISCHED_COMPACT_ZC");
         return !(e && e[0] == '0');
     }();
-    if (zc && !c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows) {
-        if (n > c->z_cap) {
-            if (c->h_podz) (void)hipHostFree(c->h_podz);
-            if (c->h_resz) (void)hipHostFree(c->h_resz);
-            c->h_podz = nullptr;
-            c->h_resz = nullptr;
-            c->z_cap = 0;
-            // coherent (fine-grained): the kernel's reads see this call's host copy and
-            // its writes reach host memory with no cache maintenance between calls
-            if (hipHostMalloc((void **)&c->h_podz, sizeof(ms_pod_compact) * n, hipHostMallocCoherent) != hipSuccess ||
-                hipHostMalloc((void **)&c->h_resz, sizeof(ms_result_compact) * n, hipHostMallocCoherent) != hipSuccess)
-                return fail(c, MS_E_OOM, "compact pinned staging");
-            c->z_cap = n;
-            ck.lap(MS_PH_ALLOC);
-        }
-        const hipStream_t s = c->stream;
-        MS_HIP(c, hipStreamSynchronize(s));  // (no earlier call still reads h_podz)
-        ck.lap(MS_PH_WAIT);
-        std::memcpy(c->h_podz, pods, sizeof(ms_pod_compact) * n);
-        ck.lap(MS_PH_STAGE_IN);
-        ++c->ctx_seq;  // binds write the table on the context stream
-        MS_HIP(c, launch_sweep_pp_compact(c->t, c->rows_dev, c->h_podz, n, seed32_of(c->cfg.seed), c->h_resz,
-                                          c->present_dev, c->num_cus, s));
-        ck.lap(MS_PH_LAUNCH);
-        MS_HIP(c, hipStreamSynchronize(s));
-        ck.lap(MS_PH_WAIT);
-        std::memcpy(out, c->h_resz, sizeof(ms_result_compact) * n);
-        ck.lap(MS_PH_STAGE_OUT);
-        return MS_OK;
-    }
+    if (zc && !c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows)
+        return schedule_zc(c, pods, n, out, ck);
     rc = c->comm ? comm_stage(c, n) : ensure_stage(c, n);
     if (rc) return rc;
     if (n > c->compact_cap) {

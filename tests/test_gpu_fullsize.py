@@ -17,12 +17,13 @@ import numpy as np
 import pytest
 
 from minisched_amd import _lib, synth
+from minisched_amd.hostinfo import cpu_threads
 from minisched_amd._lib import MODE_BATCHED, MODE_SEQUENTIAL, PLUGINS_NU_NN, PLUGINS_NU_NRF_NN_LA, Engine
 
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-THREADS = 16  # the GPU box's CPU share
+THREADS = cpu_threads()  # the affinity mask, capped by the cgroup quota
 
 
 def assert_same(res, o, tag=""):

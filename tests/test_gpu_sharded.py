@@ -442,7 +442,9 @@ def _sharded_c(oracle, n_nodes, n_pods, G, seed=1):
 
     nr = synth.nodes(n_nodes, seed=seed)
     pr = synth.pods(n_pods, seed=seed)
-    o = oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=16)
+    from minisched_amd.hostinfo import cpu_threads
+
+    o = oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=cpu_threads())
     dev = torch.device("cuda:0")
     s = torch.cuda.Stream(device=dev)
     sp = s.cuda_stream
