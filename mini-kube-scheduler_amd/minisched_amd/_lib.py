@@ -28,11 +28,13 @@ MS_E_INVAL, MS_E_HIP, MS_E_RCCL, MS_E_OOM, MS_E_CAPACITY, MS_E_NODEV = -1, -2, -
 PLUGINS_NU_NN = 0
 PLUGINS_NU_NRF_NN_LA = 1
 PLUGINS_NU_NN_NA = 2
+PLUGINS_NU_TT_NN = 3
 MODE_BATCHED = 0
 MODE_SEQUENTIAL = 1
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE = 0, 1, 2
 MASK_NODE_UNSCHEDULABLE = 1
 MASK_NODE_RESOURCES_FIT = 2
+MASK_TAINT_TOLERATION = 4
 MAX_ORDINAL = 0xFFFFD  # keys 0 / 1 are reserved (no feasible node)
 
 ERRNAMES = {
@@ -53,7 +55,7 @@ NODE_REC = np.dtype(
         ("_pad0", "u1"),
         ("allowed_pods", "<i4"),
         ("pod_count", "<i4"),
-        ("_pad1", "<i4"),
+        ("taints", "<u4"),  # MS_PLUGINS_NU_TT_NN: bits 0-7 NoSchedule/NoExecute ids, 8-15 PreferNoSchedule
         ("alloc_milli_cpu", "<i8"),
         ("alloc_memory", "<i8"),
         ("req_milli_cpu", "<i8"),

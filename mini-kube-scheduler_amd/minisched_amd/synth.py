@@ -26,7 +26,21 @@ GiB = 1 << 30
 # column streams
 S_NODE_UNSCHED, S_POD_TOL, S_NODE_CPU, S_NODE_MEM, S_POD_NOREQ, S_POD_CPU, S_POD_MEM = 1, 2, 3, 4, 5, 6, 7
 S_NODE_ZONE, S_POD_ZONE, S_POD_ZWEIGHT = 8, 9, 10
+S_NODE_HARD, S_NODE_SOFT, S_POD_TOLH, S_POD_TOLS = 11, 12, 13, 14
 N_ZONES = 8
+# MS_PLUGINS_NU_TT_NN taint universe of the synthetic clusters: 3 NoSchedule /
+# NoExecute taint ids (bits 0-2 of ms_node_rec.taints) and 6 PreferNoSchedule
+# ids (bits 8-13)
+N_HARD_TAINTS, N_SOFT_TAINTS = 3, 6
+
+
+def _bits(seed: int, stream: int, start: int, n: int, nbits: int, per_mille: int) -> np.ndarray:
+    """Per record a mask of nbits independent bits, each set with probability per_mille / 1000."""
+    m = np.zeros(n, dtype=np.uint32)
+    for b in range(nbits):
+        u = stream_u64(seed, stream * 16 + b, start, n)
+        m |= ((u % np.uint64(1000)) < np.uint64(per_mille)).astype(np.uint32) << np.uint32(b)
+    return m
 
 DEFAULT_MILLI_CPU_REQUEST = 100  # k8s@v1.22.0 pkg/scheduler/util/non_zero.go
 DEFAULT_MEMORY_REQUEST = 200 * MiB
@@ -46,9 +60,12 @@ def stream_u64(seed: int, stream: int, start: int, n: int) -> np.ndarray:
         return mix64(state + k * GOLDEN)
 
 
-def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False) -> np.ndarray:
+def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False,
+          taints: bool = False) -> np.ndarray:
     """Node records for ordinals [start, start+n). zones: topology zone labels
-    for MS_PLUGINS_NU_NN_NA (value ids 1..8, 5 % of nodes unlabelled)."""
+    for MS_PLUGINS_NU_NN_NA (value ids 1..8, 5 % of nodes unlabelled). taints:
+    for MS_PLUGINS_NU_TT_NN, each NoSchedule taint id on 4 % of nodes and each
+    PreferNoSchedule id on 30 %."""
     rec = np.zeros(n, dtype=NODE_REC)
     i = np.arange(start, start + n, dtype=np.int64)
     rec["name_digit"] = (i % 10).astype(np.uint8)
@@ -64,12 +81,19 @@ def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones:
     if zones:
         u = stream_u64(seed, S_NODE_ZONE, start, n)
         rec["zone"] = np.where(u % np.uint64(100) < np.uint64(5), 0, 1 + (u >> np.uint64(8)) % np.uint64(N_ZONES))
+    if taints:
+        rec["taints"] = _bits(seed, S_NODE_HARD, start, n, N_HARD_TAINTS, 40) | (
+            _bits(seed, S_NODE_SOFT, start, n, N_SOFT_TAINTS, 300) << np.uint32(8))
     return rec
 
 
-def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False) -> np.ndarray:
+def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False,
+         taints: bool = False) -> np.ndarray:
     """Pod records for ordinals [start, start+n). zones: 70 % of pods carry one
-    preferred zone term (zone 1..8, weight 1..100) for MS_PLUGINS_NU_NN_NA."""
+    preferred zone term (zone 1..8, weight 1..100) for MS_PLUGINS_NU_NN_NA.
+    taints: MS_PLUGINS_NU_TT_NN tolerated taint ids (each with probability
+    0.3), in the bytes that set shares with the NodeAffinity term
+    (tol_hard = pref_zone, tol_soft = pref_weight, minisched_gpu.h)."""
     rec = np.zeros(n, dtype=POD_REC)
     j = np.arange(start, start + n, dtype=np.int64)
     rec["ordinal"] = j.astype(np.uint32)
@@ -90,7 +114,18 @@ def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: 
         w = stream_u64(seed, S_POD_ZWEIGHT, start, n)
         rec["pref_zone"] = np.where(u % np.uint64(10) < np.uint64(7), 1 + (u >> np.uint64(8)) % np.uint64(N_ZONES), 0)
         rec["pref_weight"] = np.where(rec["pref_zone"] > 0, 1 + w % np.uint64(100), 0)
+    if taints:
+        set_tolerations(rec, _bits(seed, S_POD_TOLH, start, n, N_HARD_TAINTS, 300),
+                        _bits(seed, S_POD_TOLS, start, n, N_SOFT_TAINTS, 300))
     return rec
+
+
+def set_tolerations(rec: np.ndarray, tol_hard, tol_soft) -> None:
+    """MS_PLUGINS_NU_TT_NN: bit t of tol_hard / tol_soft = some toleration of the
+    pod tolerates NoSchedule / PreferNoSchedule taint id t (ms_pod_rec.tol_hard,
+    .tol_soft: the bytes of the NodeAffinity term)."""
+    rec["pref_zone"] = np.asarray(tol_hard, dtype=np.uint8)
+    rec["pref_weight"] = np.asarray(tol_soft, dtype=np.uint8)
 
 
 # BASELINE.md §3

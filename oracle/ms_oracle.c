@@ -402,3 +402,138 @@ int msor_schedule_na(const msor_nodes *nd, const msor_pods *pd, int64_t w_nn, in
     free(na);
     return 0;
 }
+
+/* ---- TaintToleration + the in-loop reverse normalise hook ------------------ */
+
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/tainttoleration/taint_toleration.go
+ * Filter: v1helper.FindMatchingUntoleratedTaint over the node's taints with
+ * effect NoSchedule or NoExecute -> UnschedulableAndUnresolvable. Taints are
+ * ids of the cluster's taint universe; the toleration match (v1 ToleratesTaint)
+ * is evaluated per (pod, taint id) on the host, as the Filter evaluates it per
+ * call. */
+static int tt_rejects(uint32_t taints, uint8_t tol_hard) { return (taints & 0xFFu & ~(uint32_t)tol_hard) != 0; }
+
+/* Score: countIntolerableTaintsPreferNoSchedule — the node's PreferNoSchedule
+ * taints no PreferNoSchedule-or-empty-effect toleration of the pod tolerates
+ * (getAllTolerationPreferNoSchedule). */
+static int64_t tt_raw(uint32_t taints, uint8_t tol_soft) {
+    return (int64_t)__builtin_popcount((taints >> 8) & 0xFFu & ~(uint32_t)tol_soft);
+}
+
+/* DefaultNormalizeScore(100, reverse=true) as one value map: the whole list is
+ * rewritten with the same map at every step of the loop. */
+static int64_t tt_map(int64_t m, int64_t v) { return m == 0 ? 100 : 100 - (100 * v) / m; }
+
+/* Closed form of the loop (msor_tt_inloop, literal = 0). The loop normalises
+ * the whole F-entry list after writing entry k; entries > k are still the
+ * zeros of createPluginToNodeScores (minisched.go:327-334) and are rewritten
+ * like every other. Every step applies one map v -> 100 - floor(100 v / M_k)
+ * (M_k = the list maximum; all 100 when M_k = 0) to every entry, the entries
+ * not yet scored included (they stay equal: one "future" value u). With counts
+ * <= 8 the list holds both 0 and 100 after step 2 (step 0 leaves the first
+ * entry at 0 and u at 100, or both at 100 when c0 = 0; then step 1 or 2 makes
+ * a 0 and keeps a 100), so every later step before the last has M_k = 100 and
+ * is the flip v -> 100 - v: entry j >= 3 is written at step j as c_j, mapped to
+ * 100 - c_j, and flipped F-2-j more times before the last step. The last step
+ * (no future entry left) is the one map with M = the list's maximum. */
+static void tt_closed(const int64_t *c, uint32_t F, int64_t *out) {
+    if (F <= 4) { /* (small lists: the loop itself) */
+        int64_t s[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < F; ++k) {
+            s[k] = c[k];
+            msor_default_normalize(100, 1, s, F);
+        }
+        for (uint32_t k = 0; k < F; ++k) out[k] = s[k];
+        return;
+    }
+    int64_t s[3], u = 0; /* entries 0..2 and the future value after step 2 */
+    for (uint32_t k = 0; k < 3; ++k) {
+        s[k] = c[k];
+        int64_t m = u;
+        for (uint32_t i = 0; i <= k; ++i) m = s[i] > m ? s[i] : m;
+        for (uint32_t i = 0; i <= k; ++i) s[i] = tt_map(m, s[i]);
+        u = tt_map(m, u);
+    }
+    const int nf_odd = (int)((F - 4) & 1u); /* flips of steps 3..F-2 */
+    int64_t m_last = c[F - 1];
+    for (uint32_t j = 0; j + 1 < F; ++j) {
+        int64_t p;
+        if (j < 3) p = nf_odd ? 100 - s[j] : s[j];
+        else p = ((F - 2 - j) & 1u) ? c[j] : 100 - c[j];
+        out[j] = p;
+        if (p > m_last) m_last = p;
+    }
+    for (uint32_t j = 0; j + 1 < F; ++j) out[j] = tt_map(m_last, out[j]);
+    out[F - 1] = tt_map(m_last, c[F - 1]);
+}
+
+int msor_tt_inloop(const int64_t *c, uint32_t F, int literal, int64_t *out) {
+    for (uint32_t k = 0; k < F; ++k)
+        if (c[k] < 0 || c[k] > 8) return -1;
+    if (!literal) {
+        tt_closed(c, F, out);
+        return 0;
+    }
+    /* minisched.go:164-185: Score writes entry k, NormalizeScore rewrites the
+     * whole list (entries > k still 0) */
+    for (uint32_t k = 0; k < F; ++k) out[k] = 0;
+    for (uint32_t k = 0; k < F; ++k) {
+        out[k] = c[k];
+        msor_default_normalize(100, 1, out, F);
+    }
+    return 0;
+}
+
+int msor_schedule_tt(const msor_nodes *nd, const msor_pods *pd, int literal, uint64_t seed,
+                     uint32_t node_base, int32_t *out_node, int64_t *out_score, int32_t *out_code,
+                     uint32_t *out_mask, uint64_t *out_key) {
+    if (!nd || !pd || !nd->flags || !nd->digit || !nd->taints || !pd->ordinal || !pd->digit || !pd->tol ||
+        !pd->tol_hard || !pd->tol_soft)
+        return -1;
+    if ((uint64_t)node_base + nd->n >= 0xFFFFFu) return -1;
+    const uint32_t cap = nd->n ? nd->n : 1;
+    uint32_t *feas = (uint32_t *)malloc(sizeof(uint32_t) * cap);
+    int64_t *cnt = (int64_t *)malloc(sizeof(int64_t) * cap);
+    int64_t *tt = (int64_t *)malloc(sizeof(int64_t) * cap);
+    if (!feas || !cnt || !tt) { free(feas); free(cnt); free(tt); return -1; }
+    for (uint32_t j = 0; j < pd->n; ++j) {
+        /* RunFilterPlugins (minisched.go:115-151): NU then TT, first failure per node */
+        uint32_t F = 0, mask = 0;
+        for (uint32_t i = 0; i < nd->n; ++i) {
+            if (nd->flags[i] & MSOR_NODE_ABSENT) continue;
+            if (nu_rejects(nd->flags[i], pd->tol[j])) { mask |= MSOR_MASK_NU; continue; }
+            if (tt_rejects(nd->taints[i], pd->tol_hard[j])) { mask |= MSOR_MASK_TT; continue; }
+            cnt[F] = tt_raw(nd->taints[i], pd->tol_soft[j]);
+            feas[F++] = i;
+        }
+        int32_t node = -1, code;
+        int64_t score = 0;
+        uint64_t best = 0;
+        if (F == 0) {
+            code = MSOR_CODE_UNSCHEDULABLE;
+        } else if (pd->digit[j] < 0) { /* NodeNumber.Score fails at the first node (:170-172) */
+            code = MSOR_CODE_ERROR;
+        } else {
+            msor_tt_inloop(cnt, F, literal, tt);
+            const uint32_t ph = msor_pod_hash(seed, pd->ordinal[j]);
+            for (uint32_t k = 0; k < F; ++k) { /* sum (:187-196) and selectHost (:304-325) */
+                const uint32_t ord = node_base + feas[k];
+                const uint64_t key = msor_key(nn_score(pd->digit[j], nd->digit[feas[k]]) + tt[k],
+                                              msor_tb_hash(ph, ord), ord);
+                if (key > best) best = key;
+            }
+            code = MSOR_CODE_SUCCESS;
+            node = (int32_t)(0xFFFFFu - (uint32_t)(best & 0xFFFFFu));
+            score = (int64_t)(best >> 52);
+        }
+        if (out_node) out_node[j] = node;
+        if (out_score) out_score[j] = score;
+        if (out_code) out_code[j] = code;
+        if (out_mask) out_mask[j] = code == MSOR_CODE_UNSCHEDULABLE ? mask : 0;
+        if (out_key) out_key[j] = code == MSOR_CODE_SUCCESS ? best : 0;
+    }
+    free(feas);
+    free(cnt);
+    free(tt);
+    return 0;
+}

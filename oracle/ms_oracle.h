@@ -27,6 +27,8 @@ extern "C" {
 #define MSOR_PLUGINS_NU_NN 0        /* Filter[NodeUnschedulable], Score[NodeNumber]          */
 #define MSOR_PLUGINS_NU_NRF_NN_LA 1 /* Filter[NU, NodeResourcesFit], Score[NN, LeastAllocated] */
 #define MSOR_PLUGINS_NU_NN_NA 2     /* Filter[NU], Score[NN, NodeAffinity + DefaultNormalizeScore] */
+#define MSOR_PLUGINS_NU_TT_NN 3     /* Filter[NU, TaintToleration], Score[NN, TaintToleration +
+                                       DefaultNormalizeScore(reverse=true)]                 */
 
 #define MSOR_MODE_BATCHED 0    /* every pod against the same node state          */
 #define MSOR_MODE_SEQUENTIAL 1 /* queue order, assume-on-select NodeInfo.AddPod   */
@@ -37,6 +39,7 @@ extern "C" {
 
 #define MSOR_MASK_NU (1u << 0)
 #define MSOR_MASK_NRF (1u << 1)
+#define MSOR_MASK_TT (1u << 2)
 
 #define MSOR_NODE_UNSCHEDULABLE 0x01u
 #define MSOR_NODE_ABSENT 0x80u
@@ -51,6 +54,9 @@ typedef struct {
     int64_t *req_cpu, *req_mem;     /* Requested.MilliCPU / .Memory                */
     int64_t *nz_cpu, *nz_mem;       /* NonZeroRequested.MilliCPU / .Memory         */
     const uint8_t *zone;            /* zone label value id, 0 = none (NU_NN_NA)   */
+    /* taint ids of the cluster's taint universe (NU_TT_NN): bits 0-7 taints with
+     * effect NoSchedule or NoExecute, bits 8-15 taints with effect PreferNoSchedule */
+    const uint32_t *taints;
 } msor_nodes;
 
 typedef struct {
@@ -60,6 +66,9 @@ typedef struct {
     const uint8_t *tol;      /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
     const int64_t *req_cpu, *req_mem, *nz_cpu, *nz_mem; /* may be NULL for NU_NN */
     const uint8_t *pref_zone, *pref_weight; /* one preferred zone term (NU_NN_NA)  */
+    /* NU_TT_NN: bit t set when some toleration of the pod tolerates taint id t
+     * (v1 ToleratesTaint, host-side): tol_hard over bits 0-7, tol_soft over 8-15 */
+    const uint8_t *tol_hard, *tol_soft;
 } msor_pods;
 
 uint32_t msor_fmix32(uint32_t h);
@@ -118,6 +127,23 @@ int msor_schedule_na(const msor_nodes *nodes, const msor_pods *pods, int64_t w_n
 
 /* upstream k8s@v1.22.0 pkg/scheduler/framework/plugins/helper/normalize_score.go */
 void msor_default_normalize(int64_t max_priority, int reverse, int64_t *scores, uint32_t n);
+
+/* MSOR_PLUGINS_NU_TT_NN, batched (stateless). Filter plugins in order
+ * [NodeUnschedulable, TaintToleration]; score plugins [NodeNumber,
+ * TaintToleration] with TaintToleration's ScoreExtensions =
+ * DefaultNormalizeScore(MaxNodeScore=100, reverse=true), run by RunScorePlugins
+ * on the WHOLE list after every node (minisched.go:164-185). literal=1 runs
+ * that loop as written (O(F^2) per pod); literal=0 its closed form
+ * (msor_tt_inloop). FitError mask bits: NU, TT (MSOR_MASK_TT). */
+int msor_schedule_tt(const msor_nodes *nodes, const msor_pods *pods, int literal, uint64_t seed,
+                     uint32_t node_base, int32_t *out_node, int64_t *out_score, int32_t *out_code,
+                     uint32_t *out_mask, uint64_t *out_key);
+
+/* The TaintToleration list after RunScorePlugins' in-loop hook: raw counts
+ * c[0..F) (each in 0..8) in LIST order -> final normalised scores out[0..F).
+ * literal=1: the loop as written; literal=0: the closed form.
+ * Returns 0, or -1 when a count is out of range. */
+int msor_tt_inloop(const int64_t *c, uint32_t F, int literal, int64_t *out);
 
 #ifdef __cplusplus
 }

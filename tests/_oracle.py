@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_LIB = os.path.join(ORACLE_DIR, "libmsoracle.so")
 
-PLUGINS_NU_NN, PLUGINS_NU_NRF_NN_LA, PLUGINS_NU_NN_NA = 0, 1, 2
+PLUGINS_NU_NN, PLUGINS_NU_NRF_NN_LA, PLUGINS_NU_NN_NA, PLUGINS_NU_TT_NN = 0, 1, 2, 3
 MODE_BATCHED, MODE_SEQUENTIAL = 0, 1
 
 
@@ -34,6 +34,7 @@ class msor_nodes(ctypes.Structure):
             "nz_cpu",
             "nz_mem",
             "zone",
+            "taints",
         )
     ]
 
@@ -41,7 +42,8 @@ class msor_nodes(ctypes.Structure):
 class msor_pods(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32)] + [
         (f, ctypes.c_void_p)
-        for f in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem", "pref_zone", "pref_weight")
+        for f in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem", "pref_zone", "pref_weight",
+                  "tol_hard", "tol_soft")
     ]
 
 
@@ -93,6 +95,16 @@ def lib():
             ctypes.c_uint64,
             ctypes.c_uint32,
         ] + [ctypes.c_void_p] * 5
+        L.msor_schedule_tt.restype = ctypes.c_int
+        L.msor_schedule_tt.argtypes = [
+            ctypes.POINTER(msor_nodes),
+            ctypes.POINTER(msor_pods),
+            ctypes.c_int,
+            ctypes.c_uint64,
+            ctypes.c_uint32,
+        ] + [ctypes.c_void_p] * 5
+        L.msor_tt_inloop.restype = ctypes.c_int
+        L.msor_tt_inloop.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
         L.msor_default_normalize.restype = None
         L.msor_default_normalize.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32]
         L.msor_schedule_nunn_names.restype = ctypes.c_int
@@ -135,6 +147,7 @@ class NodeCols:
         self.nz_cpu = _col(recs["nonzero_milli_cpu"], np.int64)
         self.nz_mem = _col(recs["nonzero_memory"], np.int64)
         self.zone = _col(recs["zone"], np.uint8)
+        self.taints = _col(recs["taints"], np.uint32)
 
     def struct(self):
         return msor_nodes(
@@ -153,6 +166,7 @@ class NodeCols:
                     "nz_cpu",
                     "nz_mem",
                     "zone",
+                    "taints",
                 )
             ],
         )
@@ -169,9 +183,12 @@ def _pod_cols(pods):
         nz_mem=_col(pods["nonzero_memory"], np.int64),
         pref_zone=_col(pods["pref_zone"], np.uint8),
         pref_weight=_col(pods["pref_weight"], np.uint8),
+        # (NU_TT_NN: the same two bytes carry the tolerated taint ids, minisched_gpu.h)
+        tol_hard=_col(pods["pref_zone"], np.uint8),
+        tol_soft=_col(pods["pref_weight"], np.uint8),
     )
     st = msor_pods(len(pods), *[_p(cols[k]) for k in ("ordinal", "digit", "tol", "req_cpu", "req_mem", "nz_cpu", "nz_mem",
-                                                      "pref_zone", "pref_weight")])
+                                                      "pref_zone", "pref_weight", "tol_hard", "tol_soft")])
     return cols, st
 
 
@@ -215,6 +232,30 @@ def schedule_na(node_recs, pods, weights=(1, 1), literal=True, seed=1, node_base
     )
     assert rc == 0, "oracle rejected its arguments"
     return o
+
+
+def schedule_tt(node_recs, pods, literal=True, seed=1, node_base=0):
+    """MSOR_PLUGINS_NU_TT_NN (batched): literal=True runs RunScorePlugins' in-loop
+    reverse NormalizeScore as written (O(F^2) per pod), False its closed form."""
+    L = lib()
+    cols = NodeCols(node_recs)
+    nst = cols.struct()
+    pc, pst = _pod_cols(pods)
+    o = _outs(len(pods))
+    rc = L.msor_schedule_tt(
+        ctypes.byref(nst), ctypes.byref(pst), 1 if literal else 0, seed, node_base,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),
+    )
+    assert rc == 0, "oracle rejected its arguments"
+    return o
+
+
+def tt_inloop(counts, literal=True):
+    """The TaintToleration list after the in-loop reverse normalise hook."""
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    out = np.zeros(max(1, len(c)), dtype=np.int64)
+    assert lib().msor_tt_inloop(_p(c), len(c), 1 if literal else 0, _p(out)) == 0
+    return out[: len(c)]
 
 
 def default_normalize(scores, max_priority=100, reverse=False):
