@@ -59,6 +59,16 @@ extern "C" {
  * ScoreExtensions = DefaultNormalizeScore(MaxNodeScore, reverse=false), run by
  * RunScorePlugins' in-loop hook (minisched.go:178-183) exactly as written]. */
 #define MS_PLUGINS_NU_NN_NA 2
+/* Filter[NU, TaintToleration]; Score[NN, TaintToleration with ScoreExtensions =
+ * DefaultNormalizeScore(MaxNodeScore, reverse=true), run by RunScorePlugins'
+ * in-loop hook exactly as written]. Taints are ids of a cluster-wide universe
+ * the shim assigns: ms_node_rec.taints bits 0-7 = NoSchedule / NoExecute taint
+ * ids on the node, bits 8-15 = PreferNoSchedule ids; ms_pod_rec bytes
+ * pref_zone / pref_weight carry tol_hard / tol_soft: bit t set when some
+ * toleration of the pod tolerates taint id t (v1 ToleratesTaint; for
+ * PreferNoSchedule ids only tolerations with that or an empty effect can).
+ * (k8s@v1.22.0 plugins/tainttoleration/taint_toleration.go, restated.) */
+#define MS_PLUGINS_NU_TT_NN 3
 
 /* ---- modes --------------------------------------------------------------- */
 #define MS_MODE_BATCHED 0    /* all pods of the call see the same node state               */
@@ -75,6 +85,7 @@ extern "C" {
 /* ms_result.plugin_mask = FitError Diagnosis.UnschedulablePlugins */
 #define MS_MASK_NODE_UNSCHEDULABLE (1u << 0) /* "NodeUnschedulable" */
 #define MS_MASK_NODE_RESOURCES_FIT (1u << 1) /* "NodeResourcesFit"  */
+#define MS_MASK_TAINT_TOLERATION (1u << 2)   /* "TaintToleration"   */
 
 #define MS_MAX_ORDINAL 0xFFFFDu /* (keys 0 and 1 are reserved: no feasible node) */
 
@@ -88,7 +99,8 @@ typedef struct ms_node_rec {
     uint8_t _pad0;
     int32_t allowed_pods;  /* NodeInfo.Allocatable.AllowedPodNumber                 */
     int32_t pod_count;     /* len(NodeInfo.Pods)                                    */
-    int32_t _pad1;
+    uint32_t taints;       /* MS_PLUGINS_NU_TT_NN: taint ids (bits 0-7 NoSchedule /
+                              NoExecute, bits 8-15 PreferNoSchedule); else ignored  */
     int64_t alloc_milli_cpu, alloc_memory;     /* NodeInfo.Allocatable             */
     int64_t req_milli_cpu, req_memory;         /* NodeInfo.Requested               */
     int64_t nonzero_milli_cpu, nonzero_memory; /* NodeInfo.NonZeroRequested        */
@@ -100,7 +112,9 @@ typedef struct ms_pod_rec {
     int8_t name_digit;               /* last char of pod name as 0..9; -1 = not     */
     uint8_t tolerates_unschedulable; /* TolerationsTolerateTaint(unschedulable:NoSchedule) */
     /* MS_PLUGINS_NU_NN_NA: one PreferredSchedulingTerm {weight, zone In [pref_zone]}
-     * (NodeAffinity.Score = weight when the node's zone label matches); 0 = none */
+     * (NodeAffinity.Score = weight when the node's zone label matches); 0 = none.
+     * MS_PLUGINS_NU_TT_NN: pref_zone = tol_hard, pref_weight = tol_soft (the
+     * tolerated NoSchedule / PreferNoSchedule taint ids, see the plugin set). */
     uint8_t pref_zone;
     uint8_t pref_weight;             /* 1..100 (API validation of the term weight)  */
     int64_t req_milli_cpu, req_memory;         /* Fit PreFilter request              */
@@ -313,6 +327,26 @@ int ms_seq_candidates_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pod
 int ms_seq_validate_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
                            const ms_seq_cand *cands_all_dev, const uint32_t *flags_all_dev, ms_result *results_dev,
                            uint32_t *n_done_dev, void *stream);
+/* ---- node-sharded MS_PLUGINS_NU_TT_NN ---------------------------------------
+ * TaintToleration's in-loop reverse normalisation makes a node's score depend
+ * on its rank among the pod's feasible nodes in LIST order, so shards do not
+ * combine by a MAX. Instead every shard writes, per pod, a summary of its
+ * nodes (MS_TT_SUMMARY_BYTES, opaque: feasible count, filter flags, the first
+ * three and the last feasible node, the best node per (raw count, rank
+ * parity) class); summaries of consecutive shards merge associatively, and
+ * the decode applies the closed form of the loop and selectHost.
+ *   1. ms_tt_summaries_device: this shard's summaries (summaries_dev: n_pods x
+ *      MS_TT_SUMMARY_BYTES);
+ *   2. the caller gathers them shard-major (summaries_all[s][p], shards in
+ *      ordinal order = LIST order);
+ *   3. ms_tt_decode_device: the merge over the n_shards shards and each pod's
+ *      result (no bind commit). */
+#define MS_TT_SUMMARY_BYTES 192u
+int ms_tt_summaries_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, void *summaries_dev,
+                           void *stream);
+int ms_tt_decode_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                        const void *summaries_all_dev, ms_result *results_dev, void *stream);
+
 /* Whole exact sequential cycle on device-resident pods (single shard; on a
  * context joined to a communicator, the node-sharded cycle below). */
 int ms_schedule_sequential_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev,

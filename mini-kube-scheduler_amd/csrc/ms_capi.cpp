@@ -51,7 +51,7 @@ void free_all(ms_ctx *c) {
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
                    c->d_podc, c->d_resc,
-                   c->d_merged, c->d_merged_flags, c->d_drow, c->d_top_ext};
+                   c->d_merged, c->d_merged_flags, c->d_drow, c->d_top_ext, c->t.taints, c->d_tt};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_podz) (void)hipHostFree(c->h_podz);
@@ -371,10 +371,47 @@ int ensure_stage(ms_ctx *c, uint32_t n) {
     return MS_OK;
 }
 
+// MS_PLUGINS_NU_TT_NN: summary scratch for n pods' row segments.
+int ensure_tt(ms_ctx *c, uint32_t n) {
+    const size_t need = (size_t)tt_segments(c->rows_dev) * n * MS_TT_SUMMARY_BYTES;
+    if (need <= c->tt_bytes) return MS_OK;
+    if (c->d_tt) (void)hipFree(c->d_tt);
+    c->d_tt = nullptr;
+    c->tt_bytes = 0;
+    if (hipMalloc(&c->d_tt, need) != hipSuccess) return fail(c, MS_E_OOM, "TaintToleration summaries");
+    c->tt_bytes = need;
+    return MS_OK;
+}
+
+// The batch's per-pod summaries of every row segment, merged in LIST order into
+// out (this shard's summary), or finalised into results (the single-shard
+// cycle; commit: the winners' NodeInfo.AddPod). Chunks of batch_cap pods.
+int tt_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *out, ms_result *results, int commit,
+                    hipStream_t s) {
+    const uint32_t B = c->batch_cap, segs = tt_segments(c->rows_dev);
+    int rc = ensure_tt(c, std::min(B, n_pods));
+    if (rc) return rc;
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, launch_tt_sweep(c->t, c->rows_dev, d_pods + s0, nb, seed32, c->d_tt, s));
+        MS_HIP(c, launch_tt_combine(c->d_tt, nb, segs, d_pods + s0, nb, seed32,
+                                    out ? static_cast<char *>(out) + (size_t)s0 * MS_TT_SUMMARY_BYTES : nullptr,
+                                    out ? nullptr : results + s0, c->t, commit, s));
+    }
+    return MS_OK;
+}
+
+int tt_summaries_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *out, hipStream_t s) {
+    return tt_cycle_locked(c, n_pods, d_pods, out, nullptr, 0, s);
+}
+
 // This shard's keys (and filter flags for the resource-aware set) for a batch.
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
                  hipStream_t s, hipEvent_t done) {
     const uint32_t seed32 = seed32_of(c->cfg.seed);
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN)
+        return fail(c, MS_E_INVAL, "TaintToleration shards combine by summaries (ms_tt_summaries_device), not keys");
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NN) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
                                   c->num_cus, s, 0, done));
@@ -413,6 +450,12 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
                   int commit = 0, hipEvent_t done = nullptr) {
     const uint32_t B = c->batch_cap;
     const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN;
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // (stateless: binds in the combine launch)
+        int rc = tt_cycle_locked(c, n_pods, d_pods, nullptr, d_res, commit, s);
+        if (rc) return rc;
+        if (done) MS_HIP(c, hipEventRecord(done, s));
+        return MS_OK;
+    }
     if (fused && c->rows_dev <= kPpMaxFusedRows) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32_of(c->cfg.seed), nullptr, d_res,
                                   c->present_dev, c->num_cus, s, commit, done));
@@ -637,7 +680,7 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     if (!cfg || !out) return fail(nullptr, MS_E_INVAL, "ms_create: null argument");
     *out = nullptr;
     if (cfg->plugin_set != MS_PLUGINS_NU_NN && cfg->plugin_set != MS_PLUGINS_NU_NRF_NN_LA &&
-        cfg->plugin_set != MS_PLUGINS_NU_NN_NA)
+        cfg->plugin_set != MS_PLUGINS_NU_NN_NA && cfg->plugin_set != MS_PLUGINS_NU_TT_NN)
         return fail(nullptr, MS_E_INVAL, "ms_create: unknown plugin_set");
     const uint32_t w0 = cfg->score_weight[0] ? cfg->score_weight[0] : 1u;
     const uint32_t w1 = cfg->score_weight[1] ? cfg->score_weight[1] : 1u;
@@ -683,6 +726,7 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     bool ok = hipMalloc((void **)&t.flags, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.digit, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.zone, n + kColumnPad) == hipSuccess &&
+              hipMalloc((void **)&t.taints, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.alloc_cpu, n * 8) == hipSuccess &&
@@ -1052,6 +1096,8 @@ int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, con
     MS_HIP(c, hipSetDevice(c->cfg.device));
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA && n_pods && !flags_dev)
         return fail(c, MS_E_INVAL, "ms_decode_device: the NodeAffinity anchors (flags) are required for this plugin set");
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN)
+        return fail(c, MS_E_INVAL, "ms_decode_device: TaintToleration shards decode summaries (ms_tt_decode_device)");
     MS_HIP(c, decode_for(c, pods_dev, n_pods, reinterpret_cast<const unsigned long long *>(keys_dev), flags_dev,
                          present_nodes, results_dev, pick_stream(c, stream)));
     return MS_OK;
@@ -1060,6 +1106,8 @@ int ms_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, con
 int ms_decode_device_jobs(ms_ctx *c, uint32_t n_jobs, const ms_decode_job *jobs, uint32_t present_nodes,
                           void *stream) {
     if (!valid_ctx(c) || n_jobs > MS_DECODE_MAX_JOBS || (n_jobs && !jobs)) return MS_E_INVAL;
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN)
+        return fail(c, MS_E_INVAL, "ms_decode_device_jobs: TaintToleration shards decode summaries (ms_tt_decode_device)");
     for (uint32_t i = 0; i < n_jobs; ++i)
         if (jobs[i].n_pods && (!jobs[i].pods || !jobs[i].keys || !jobs[i].results)) return MS_E_INVAL;
     if (n_jobs == 0) return MS_OK;
@@ -1169,6 +1217,36 @@ int ms_seq_validate_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_de
         return MS_OK;
     }
     return chain_back(c, s);
+}
+
+int ms_tt_summaries_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, void *summaries_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !summaries_dev))) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_TT_NN)
+        return fail(c, MS_E_INVAL, "ms_tt_summaries_device: the TaintToleration plugin set only");
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);
+    if (rc) return rc;
+    rc = tt_summaries_locked(c, n_pods, pods_dev, summaries_dev, s);
+    if (rc) return rc;
+    return chain_back(c, s);
+}
+
+int ms_tt_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                        const void *summaries_all_dev, ms_result *results_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !summaries_all_dev || !results_dev))) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_TT_NN)
+        return fail(c, MS_E_INVAL, "ms_tt_decode_device: the TaintToleration plugin set only");
+    if (n_shards == 0) return fail(c, MS_E_INVAL, "ms_tt_decode_device: no shards");
+    if (n_pods == 0) return MS_OK;
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    MS_HIP(c, launch_tt_combine(summaries_all_dev, n_pods, n_shards, pods_dev, n_pods, seed32_of(c->cfg.seed), nullptr,
+                                results_dev, c->t, 0, pick_stream(c, stream)));
+    return MS_OK;
 }
 
 }  // extern "C"

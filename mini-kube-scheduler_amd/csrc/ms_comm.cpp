@@ -78,6 +78,9 @@ struct ShardSlot {
     unsigned long long *keys = nullptr;       // G x cap: this shard's maxima, pod order
     unsigned long long *keys_mine = nullptr;  // cap: the cluster's maxima of this rank's slice
     uint32_t *flags = nullptr, *flags_mine = nullptr;
+    // MS_PLUGINS_NU_TT_NN: this shard's per-pod summaries (G x cap, pod order) and
+    // the slice's summaries from every shard (G x cap, shard order) after the all-to-all
+    void *summ = nullptr, *summ_mine = nullptr;
     uint32_t cap = 0;       // pods per slice the buffers hold
     bool used = false;      // a batch went through this slot
     uint64_t dec_gen = 0;   // the drain that decoded its last batch
@@ -136,7 +139,7 @@ namespace {
     } while (0)
 
 void free_slot(ShardSlot &sl) {
-    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine};
+    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.summ, sl.summ_mine};
     for (void *q : p)
         if (q) (void)hipFree(q);
     sl = ShardSlot{};
@@ -152,7 +155,10 @@ int slot_ensure(ms_ctx *c, ShardSlot &sl, uint32_t per) {
     if (hipMalloc((void **)&sl.keys, G * cap * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&sl.keys_mine, cap * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&sl.flags, G * cap * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess) {
+        hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess ||
+        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN &&
+         (hipMalloc(&sl.summ, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess ||
+          hipMalloc(&sl.summ_mine, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess))) {
         free_slot(sl);
         return fail(c, MS_E_OOM, "sharded combine buffers");
     }
@@ -175,7 +181,14 @@ int drain_locked(ms_ctx *c, size_t k) {
     k = std::min(k, m.pending.size());
     if (k == 0) return MS_OK;
     MS_HIP(c, hipStreamWaitEvent(s, m.ev_comb[m.pending[k - 1].slot], 0));  // collectives run in issue order
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // the slice's G summaries merged in shard (LIST) order
+        for (size_t i = 0; i < k; ++i) {
+            const Pending &p = m.pending[i];
+            const ShardSlot &sl = m.slot[p.slot];
+            MS_HIP(c, launch_tt_combine(sl.summ_mine, cdiv(p.n, (uint32_t)m.world), (uint32_t)m.world, p.pods + p.first,
+                                        p.count, seed32_of(c->cfg.seed), nullptr, p.results, c->t, 0, s));
+        }
+    } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
         for (size_t i = 0; i < k; ++i) {
             const Pending &p = m.pending[i];
             const ShardSlot &sl = m.slot[p.slot];
@@ -263,7 +276,12 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     const int ps = c->cfg.plugin_set;
     // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
     // packet between consecutive sweeps on X)
-    rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X, m.ev_swept[si]);
+    if (ps == MS_PLUGINS_NU_TT_NN) {  // per-pod summaries of this shard's nodes, no keys
+        rc = tt_summaries_locked(c, n, pods, sl.summ, X);
+        if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
+    } else {
+        rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X, m.ev_swept[si]);
+    }
     if (rc) return rc;
     host_tick(m, 1, tp);  // the sweep launch
     m.reads_outstanding = true;
@@ -279,6 +297,10 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     ncclResult_t r = ncclSuccess;
     if (ps == MS_PLUGINS_NU_NN) {  // the keys alone: one call, no group
         r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
+    } else if (ps == MS_PLUGINS_NU_TT_NN) {
+        // summaries do not combine by MAX: every rank sends each rank its pod slice's
+        // summaries ([q][per] in pod order) and receives its slice's from every shard
+        r = CCL(ncclAllToAll)(sl.summ, sl.summ_mine, (size_t)per * MS_TT_SUMMARY_BYTES, ncclUint8, m.comm, m.cs);
     } else {
         r = CCL(ncclGroupStart)();
         if (r == ncclSuccess) r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
@@ -289,7 +311,7 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
         const ncclResult_t r2 = CCL(ncclGroupEnd)();
         if (r == ncclSuccess) r = r2;
     }
-    if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sharded reduce-scatter: ") + CCL(ncclGetErrorString)(r));
+    if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("sharded combine: ") + CCL(ncclGetErrorString)(r));
     host_tick(m, 3, tp);  // the grouped reduce-scatter
     MS_HIP(c, hipEventRecord(m.ev_comb[si], m.cs));
     Pending p{si, n, 0, 0, pods, results};

@@ -34,6 +34,8 @@ ncclResult_t lb_ncclReduceScatter(const void *sendbuff, void *recvbuff, size_t r
                                   ncclRedOp_t op, ncclComm_t comm, hipStream_t stream);
 ncclResult_t lb_ncclAllGather(const void *sendbuff, void *recvbuff, size_t sendcount, ncclDataType_t datatype,
                               ncclComm_t comm, hipStream_t stream);
+ncclResult_t lb_ncclAllToAll(const void *sendbuff, void *recvbuff, size_t count, ncclDataType_t datatype,
+                             ncclComm_t comm, hipStream_t stream);
 ncclResult_t lb_ncclGroupStart();
 ncclResult_t lb_ncclGroupEnd();
 const char *lb_ncclGetErrorString(ncclResult_t result);

@@ -19,7 +19,7 @@ constexpr int kMaxRanks = 16;
 constexpr auto kJoinTimeout = std::chrono::seconds(120);
 
 struct Post {
-    int kind = 0;  // 1 reduce-scatter, 2 all-gather
+    int kind = 0;  // 1 reduce-scatter, 2 all-gather, 3 all-to-all
     const void *send = nullptr;
     void *recv = nullptr;
     size_t count = 0;
@@ -118,13 +118,20 @@ ncclResult_t collective(Comm *c, const Post &p, hipStream_t st) {
         if (es == 1) e = launch_max<uint8_t>(s, G, base, p.count, p.recv, st);
         else if (es == 4) e = launch_max<uint32_t>(s, G, base, p.count, p.recv, st);
         else e = launch_max<unsigned long long>(s, G, base, p.count, p.recv, st);
-    } else {  // all-gather: rank j's send buffer into block j of this rank's recv
+    } else if (p.kind == 2) {  // all-gather: rank j's send buffer into block j of this rank's recv
         const size_t bytes = p.count * es;
         for (int j = 0; j < G && e == hipSuccess; ++j) {
             char *dst = static_cast<char *>(p.recv) + (size_t)j * bytes;
             if (dst != g.post[j].send && bytes)  // (in place: this rank's own block is already there)
                 e = hipMemcpyAsync(dst, g.post[j].send, bytes, hipMemcpyDeviceToDevice, st);
         }
+    } else {  // all-to-all: block r of rank j's send buffer into block j of this rank's recv
+        const size_t bytes = p.count * es;
+        for (int j = 0; j < G && e == hipSuccess; ++j)
+            if (bytes)
+                e = hipMemcpyAsync(static_cast<char *>(p.recv) + (size_t)j * bytes,
+                                   static_cast<const char *>(g.post[j].send) + (size_t)r * bytes, bytes,
+                                   hipMemcpyDeviceToDevice, st);
     }
     if (e != hipSuccess) return ncclUnhandledCudaError;
     if (hipEventRecord(g.ev_done[r], st) != hipSuccess) return ncclUnhandledCudaError;
@@ -223,6 +230,19 @@ ncclResult_t lb_ncclAllGather(const void *sendbuff, void *recvbuff, size_t sendc
     p.send = sendbuff;
     p.recv = recvbuff;
     p.count = sendcount;
+    p.dt = datatype;
+    return collective(c, p, stream);
+}
+
+ncclResult_t lb_ncclAllToAll(const void *sendbuff, void *recvbuff, size_t count, ncclDataType_t datatype,
+                             ncclComm_t comm, hipStream_t stream) {
+    Comm *c = reinterpret_cast<Comm *>(comm);
+    if (!c || dt_size(datatype) == 0) return ncclInvalidArgument;
+    Post p;
+    p.kind = 3;
+    p.send = sendbuff;
+    p.recv = recvbuff;
+    p.count = count;
     p.dt = datatype;
     return collective(c, p, stream);
 }

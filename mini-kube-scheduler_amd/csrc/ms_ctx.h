@@ -83,6 +83,9 @@ struct ms_ctx {
     ms_pod_compact *h_podz = nullptr;      // pinned compact pods / results the compact cycle's
     ms_result_compact *h_resz = nullptr;   // kernel reads and writes over PCIe (zero-copy)
     uint32_t z_cap = 0;
+    // MS_PLUGINS_NU_TT_NN: segment summaries of the sweep (tt_bytes allocated)
+    void *d_tt = nullptr;
+    size_t tt_bytes = 0;
     // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
     ms_seq_cand *d_merged = nullptr;
     uint32_t *d_merged_flags = nullptr;
@@ -165,6 +168,8 @@ int order_after_ctx_stream(ms_ctx *c, hipStream_t s);
 int chain_back(ms_ctx *c, hipStream_t s, bool recorded = false);
 int ensure_tiles(ms_ctx *c, uint32_t n_tiles);
 int ensure_stage(ms_ctx *c, uint32_t n);
+// MS_PLUGINS_NU_TT_NN: this shard's merged per-pod summaries (MS_TT_SUMMARY_BYTES each) into out
+int tt_summaries_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *out, hipStream_t s);
 bool plugins_stateless(const ms_ctx *c);
 // done (optional): recorded on s after the sweep (by the K1 dispatch itself when it is one launch)
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,

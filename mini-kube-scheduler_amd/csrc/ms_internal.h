@@ -35,6 +35,7 @@ struct NodeTable {
     uint8_t *flags;
     uint8_t *digit;
     uint8_t *zone;  // zone label value id (MS_PLUGINS_NU_NN_NA), 0 = none
+    uint32_t *taints;  // taint ids (MS_PLUGINS_NU_TT_NN): bits 0-7 NoSchedule/NoExecute, 8-15 PreferNoSchedule
     int32_t *allowed_pods;
     int32_t *pod_count;
     int64_t *alloc_cpu, *alloc_mem;
@@ -263,6 +264,17 @@ uint32_t seq_max_rows();
 hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *keys,
                          const uint32_t *flags, uint32_t present_nodes, ms_result *out, hipStream_t s,
                          const uint32_t *present_dev = nullptr);
+// MS_PLUGINS_NU_TT_NN (ms_taint.hip): per-pod summaries of LIST-ordered row
+// segments (tt_segments(n_rows) of them, segment s at summaries[s * n_pods + p],
+// MS_TT_SUMMARY_BYTES each), and their merge: n_segs summaries per pod (segment
+// s at in[s * stride + p]) into out[p] (merged summary) or, with out null,
+// results[p] (commit: NodeInfo.AddPod on winners this table owns).
+uint32_t tt_segments(uint32_t n_rows, uint32_t *seg_rows = nullptr);
+hipError_t launch_tt_sweep(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           uint32_t seed32, void *summaries, hipStream_t s);
+hipError_t launch_tt_combine(const void *in, uint32_t stride, uint32_t n_segs, const ms_pod_rec *pods, uint32_t n_pods,
+                             uint32_t seed32, void *out, ms_result *results, const NodeTable &t, int commit,
+                             hipStream_t s);
 // One launch decoding several batches' pod slices, each with a device-side present flag.
 constexpr uint32_t kMaxSliceJobs = 8;
 struct SliceJob {

@@ -2097,6 +2097,7 @@ __global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uin
         t.flags[r] = kNodeAbsent;
         t.digit[r] = 0xFF;
         t.zone[r] = 0;
+        t.taints[r] = 0;
         t.allowed_pods[r] = 0;
         t.pod_count[r] = 0;
         t.alloc_cpu[r] = t.alloc_mem[r] = 0;
@@ -2107,6 +2108,7 @@ __global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uin
     t.flags[r] = x.rec.unschedulable ? kNodeUnschedulable : 0;
     t.digit[r] = x.rec.name_digit <= 9 ? x.rec.name_digit : 0xFF;
     t.zone[r] = x.rec.zone;
+    t.taints[r] = x.rec.taints & 0xFFFFu;
     t.allowed_pods[r] = x.rec.allowed_pods;
     t.pod_count[r] = x.rec.pod_count;
     t.alloc_cpu[r] = x.rec.alloc_milli_cpu;
@@ -2123,6 +2125,7 @@ __global__ void k_init_table(NodeTable t) {
     t.flags[r] = kNodeAbsent;
     t.digit[r] = 0xFF;
     t.zone[r] = 0;
+    t.taints[r] = 0;
     t.allowed_pods[r] = 0;
     t.pod_count[r] = 0;
     t.alloc_cpu[r] = t.alloc_mem[r] = 0;
@@ -2139,6 +2142,7 @@ __global__ void k_read_rows(NodeTable t, uint32_t first, uint32_t n, ms_node_rec
     x.unschedulable = (f & kNodeUnschedulable) ? 1 : 0;
     x.name_digit = t.digit[r];
     x.zone = t.zone[r];
+    x.taints = t.taints[r];
     x.allowed_pods = (f & kNodeAbsent) ? -1 : t.allowed_pods[r];
     x.pod_count = t.pod_count[r];
     x.alloc_milli_cpu = t.alloc_cpu[r];

@@ -101,6 +101,7 @@ SEQ_CAND = np.dtype(
     ]
 )
 SEQ_TOPK = 4
+TT_SUMMARY_BYTES = 192  # MS_TT_SUMMARY_BYTES
 SEQ_SHARD_BATCH_MAX = 256
 SEQ_MAX_SHARDS = 16
 assert NODE_REC.itemsize == 64 and POD_REC.itemsize == 40 and RESULT.itemsize == 24 and SEQ_CAND.itemsize == 72
@@ -186,6 +187,8 @@ SIGNATURES = {
     "ms_select_batch_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_seq_candidates_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "ms_seq_validate_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "ms_tt_summaries_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_tt_decode_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp]),
     "ms_comm_id_create": (ctypes.c_int, [ctypes.POINTER(ms_comm_id)]),
     "ms_comm_init": (ctypes.c_int, [_vp, ctypes.POINTER(ms_comm_id), _i32, _i32]),
     "ms_sharded_slice": (ctypes.c_int, [_vp, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
@@ -418,6 +421,17 @@ class Engine:
         self._check("ms_seq_validate_device",
                     self.lib.ms_seq_validate_device(self.h, n_pods, pods_dev, n_shards, cands_all_dev, flags_all_dev,
                                                     results_dev, n_done_dev, stream or None))
+
+    def tt_summaries_device(self, n_pods, pods_dev, summaries_dev, stream=0):
+        """Node-sharded TaintToleration set, step 1: this shard's per-pod summaries."""
+        self._check("ms_tt_summaries_device",
+                    self.lib.ms_tt_summaries_device(self.h, n_pods, pods_dev, summaries_dev, stream or None))
+
+    def tt_decode_device(self, n_pods, pods_dev, n_shards, summaries_all_dev, results_dev, stream=0):
+        """Step 3: merge the shards' summaries (shard-major, LIST order) and decode."""
+        self._check("ms_tt_decode_device",
+                    self.lib.ms_tt_decode_device(self.h, n_pods, pods_dev, n_shards, summaries_all_dev, results_dev,
+                                                 stream or None))
 
     # ---- in-library multi-GPU (a communicator per job) -------------------------
     def comm_init(self, comm_id: bytes, rank: int, world: int):

@@ -79,7 +79,7 @@ def flags_op_for(plugin_set: int) -> Optional[str]:
     from . import _lib
 
     return {_lib.PLUGINS_NU_NN: None, _lib.PLUGINS_NU_NRF_NN_LA: FLAGS_BYTES,
-            _lib.PLUGINS_NU_NN_NA: FLAGS_U32}[plugin_set]
+            _lib.PLUGINS_NU_NN_NA: FLAGS_U32, _lib.PLUGINS_NU_TT_NN: None}[plugin_set]
 
 
 def combine_scatter_(keys, keys_out, flags=None, flags_out=None, group=None, async_op=False, flags_op=FLAGS_BYTES):
@@ -265,6 +265,12 @@ class ShardedCycle:
             raise ValueError("this plugin set needs its flags combined (filter bytes / NodeAffinity anchors)")
         # in-library node-sharded cycle when the engine has a communicator
         self._library = (split == "nodes" and _has_comm(engine)) if library is None else library
+        from . import _lib
+
+        if (engine.plugin_set == _lib.PLUGINS_NU_TT_NN and split == "nodes" and world > 1
+                and not self._library):
+            raise ValueError("TaintToleration node shards combine by summaries: join a communicator "
+                             "(init_comm) or use ms_tt_summaries_device / ms_tt_decode_device")
         if self._library:
             self.a, n_mine = engine.sharded_slice(n_pods)
             self.b = self.a + n_mine

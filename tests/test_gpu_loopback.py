@@ -112,6 +112,7 @@ def _sharded_cycle(lib, nr, pr, G, plugin_set, seed, steps=6, uneven=False, dead
             assert (first, first + count) == sharded.pod_slice(len(pr), r, G)
             pods = torch.from_numpy(host_pods).to(dev)
             res = torch.full((max(1, count) * 24,), 0xAB, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()  # (the copy and the fill ran on torch's stream, not the library's)
             s = torch.cuda.Stream(device=dev) if caller_stream else None
             sp = s.cuda_stream if s is not None else 0
             for _ in range(steps):  # more than the pipeline depth: slots are reused after their decodes
@@ -133,22 +134,25 @@ def _oracle_for(oracle, nr, pr, plugin_set, seed, dead=()):
         nr["allowed_pods"][np.asarray(dead)] = -1  # oracle: absent from the node list
     if plugin_set == _lib.PLUGINS_NU_NN_NA:
         return oracle.schedule_na(nr, pr, seed=seed, literal=False)
+    if plugin_set == _lib.PLUGINS_NU_TT_NN:
+        return oracle.schedule_tt(nr, pr, seed=seed, literal=False)
     if plugin_set == _lib.PLUGINS_NU_NN:
         return oracle.schedule_nunn_omp(nr, pr, seed=seed, threads=cpu_threads())
     return oracle.schedule(nr, pr, plugin_set=plugin_set, seed=seed)
 
 
-@pytest.mark.parametrize("plugin_set", [0, 1, 2])
+@pytest.mark.parametrize("plugin_set", [0, 1, 2, 3])
 @pytest.mark.parametrize("G,uneven", [(2, False), (3, True), (4, False), (8, True)])
 def test_loopback_sharded_cycle(lb, oracle, plugin_set, G, uneven):
-    # every plugin set's combine (keys; filter bytes; NodeAffinity anchors) at world G,
+    # every plugin set's combine (keys; filter bytes; NodeAffinity anchors; TaintToleration
+    # summaries through the all-to-all) at world G,
     # pods not divisible by G (3001), uneven shards, deleted nodes on one shard and a
     # shard with every node deleted (it contributes key 0 / empty flags)
     seed = 300 + 10 * G + plugin_set
-    res_set, zones = plugin_set == 1, plugin_set == 2
+    res_set, zones, taints = plugin_set == 1, plugin_set == 2, plugin_set == 3
     n = 9000
-    nr = synth.nodes(n, seed=seed, resources=res_set, zones=zones)
-    pr = synth.pods(3001, seed=seed, resources=res_set, zones=zones)
+    nr = synth.nodes(n, seed=seed, resources=res_set, zones=zones, taints=taints)
+    pr = synth.pods(3001, seed=seed, resources=res_set, zones=zones, taints=taints)
     pr["name_digit"][::17] = -1
     cuts = _cuts(n, G, uneven)
     dead = list(range(cuts[0][0], cuts[0][1])) + list(range(cuts[-1][0], cuts[-1][1], 3))
@@ -215,16 +219,16 @@ def _check_tables(cuts, got, cols, tag):
             raise AssertionError(f"{tag}: node table column {k_dev} differs after the binds")
 
 
-@pytest.mark.parametrize("plugin_set,mode", [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0), (2, 1)])
+@pytest.mark.parametrize("plugin_set,mode", [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0), (2, 1), (3, 0), (3, 1)])
 def test_loopback_schedule_batch(lb, oracle, plugin_set, mode):
     # ms_schedule_batch on joined contexts (world 3, uneven shards): every rank returns
     # every pod's result (the all-gather of the slices / the replicated validator), and
     # each shard commits only its own nodes' binds
     G, seed = 3, 400 + 2 * plugin_set + mode
-    res_set, zones = plugin_set == 1, plugin_set == 2
+    res_set, zones, taints = plugin_set == 1, plugin_set == 2, plugin_set == 3
     n_nodes, n_pods = (1200, 7001) if res_set else (5000, 4001)
-    nr = synth.nodes(n_nodes, seed=seed, resources=res_set, zones=zones)
-    pr = synth.pods(n_pods, seed=seed, resources=res_set, zones=zones)
+    nr = synth.nodes(n_nodes, seed=seed, resources=res_set, zones=zones, taints=taints)
+    pr = synth.pods(n_pods, seed=seed, resources=res_set, zones=zones, taints=taints)
     pr["name_digit"][::23] = -1
     if plugin_set == 1:
         o = (oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed) if mode == 1
@@ -274,6 +278,7 @@ def _sequential_ranks(lb, nr, pr, G, seed, uneven=False):
         try:
             pods = torch.from_numpy(host_pods).to(dev)
             res = torch.zeros(len(pr) * 24, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()  # (the copy and the fill ran on torch's stream, not s)
             s = torch.cuda.Stream(device=dev)
             e.schedule_sequential_device(len(pr), pods.data_ptr(), res.data_ptr(), s.cuda_stream)
             s.synchronize()
@@ -336,6 +341,7 @@ def test_loopback_mismatched_collectives_fail_cleanly(lb):
             dev = torch.device("cuda:0")
             pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
             res = torch.zeros(n * 24, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
             with pytest.raises(_lib.MSError) as ei:
                 e.sharded_submit(n, pods.data_ptr(), res.data_ptr(), 0)
                 e.sharded_drain(0)
