@@ -326,6 +326,9 @@ class Engine:
 
     def upsert(self, ordinals: np.ndarray, recs: np.ndarray):
         o = np.ascontiguousarray(ordinals, dtype=np.uint32)
+        recs = np.asarray(recs)
+        if recs.dtype.names and "_pad1" in recs.dtype.names and recs.dtype.itemsize == NODE_REC.itemsize:
+            recs = np.ascontiguousarray(recs).view(NODE_REC)  # (ABI 3 records: `taints` was `_pad1`)
         r = np.ascontiguousarray(recs, dtype=NODE_REC)
         assert len(o) == len(r)
         self._check("ms_nodes_upsert", self.lib.ms_nodes_upsert(self.h, len(o), _ptr(o), _ptr(r)))

@@ -132,10 +132,22 @@ def _col(a, dtype):
     return np.array(a, dtype=dtype, copy=True, order="C")
 
 
+def _node_view(recs):
+    """Round-3 fixtures store the node records with `_pad1` where `taints` now
+    sits (same bytes, always 0 there): read them as the current layout."""
+    recs = np.asarray(recs)
+    if recs.dtype.names and "taints" not in recs.dtype.names and recs.dtype.itemsize == 64:
+        from minisched_amd import _lib
+
+        recs = np.ascontiguousarray(recs).view(_lib.NODE_REC)
+    return recs
+
+
 class NodeCols:
     """SoA copy of node records (the oracle mutates resource columns in place)."""
 
     def __init__(self, recs):
+        recs = _node_view(recs)
         self.flags = _col(np.where(recs["allowed_pods"] < 0, 0x80, 0) | (recs["unschedulable"] & 1), np.uint8)
         self.digit = _col(np.where(recs["name_digit"] <= 9, recs["name_digit"], 0xFF), np.uint8)
         self.allowed_pods = _col(recs["allowed_pods"], np.int32)
