@@ -384,21 +384,23 @@ int ms_comm_id_create(ms_comm_id *out);
 int ms_comm_init(ms_ctx *ctx, const ms_comm_id *id, int32_t rank, int32_t world);
 
 /* Pipelined node-sharded batched cycle on device-resident pods (the bench's
- * and a service loop's step). ms_sharded_submit orders after the work already
- * on `stream` (the pods), sweeps this shard on one of the context's two sweep
- * streams (consecutive batches alternate, so one sweep's ramp and tail overlap
- * the next), runs the grouped reduce-scatter on the collective stream and,
- * once more than the pipeline depth (4) batches are in flight, decodes the
- * oldest ones on the context's decode stream: batch k's collective overlaps
- * the sweeps of the following batches. ms_sharded_drain decodes every
- * remaining batch and makes `stream` wait for all decodes. results_dev
- * receives this rank's pod slice [first, first + count) of the batch
- * (ms_sharded_slice) and is complete once the stream work of a later
- * ms_sharded_drain completes; pods_dev and results_dev must stay valid until
- * then. Every rank submits the same batches in the same order. No binds are
- * committed (stateless: NU+NN, NodeAffinity; for the resource-aware set each
- * batch sees the state of its submit). Deltas and binds issued meanwhile wait
- * for the sweeps in flight. */
+ * and a service loop's step). ms_sharded_submit sweeps this shard on `stream`
+ * (after the work already there: the pods), runs the batch's collective on the
+ * context's collective stream (the grouped reduce-scatter; for
+ * MS_PLUGINS_NU_TT_NN an all-to-all of the per-pod summaries) and, once more
+ * than the pipeline depth (4) batches are in flight, decodes the oldest ones
+ * on the context's decode stream: batch k's collective overlaps the sweeps of
+ * the following batches. ms_sharded_drain decodes every remaining batch and
+ * makes `stream` wait for all decodes. results_dev receives this rank's pod
+ * slice [first, first + count) of the batch (ms_sharded_slice) and is
+ * complete once the stream work of a later ms_sharded_drain completes.
+ * pods_dev must stay valid AND UNMODIFIED until then: the decode of a batch
+ * reads its pods (name digit, ordinal) up to `depth` submits later, so a loop
+ * that refills pod buffers rotates at least depth + 1 of them.
+ * Every rank submits the same batches in the same order. No binds are
+ * committed (stateless: NU+NN, NodeAffinity, TaintToleration; for the
+ * resource-aware set each batch sees the state of its submit). Deltas and
+ * binds issued meanwhile wait for the sweeps in flight. */
 int ms_sharded_slice(const ms_ctx *ctx, uint32_t n_pods, uint32_t *first, uint32_t *count);
 int ms_sharded_submit(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
                       void *stream);

@@ -252,20 +252,25 @@ uint32_t OrdinalAllocator::LowestAny() {
 
 uint32_t OrdinalAllocator::Allocate(int digit) {
     uint32_t o;
-    if (digit >= 0 && digit <= 9 && !free_[digit].empty()) {
+    const uint64_t spread = kSpreadSlack + 2ull * (live_ + 1ull);  // (skewed name digits)
+    if (digit >= 0 && digit <= 9 && !free_[digit].empty() && *free_[digit].begin() < spread) {
         o = *free_[digit].begin();
         free_[digit].erase(free_[digit].begin());
-    } else if (digit >= 0 && digit <= 9 && next_[digit] < cap_) {
+    } else if (digit >= 0 && digit <= 9 && next_[digit] < cap_ && next_[digit] < spread) {
         o = next_[digit];
         next_[digit] += 10;
     } else {
-        o = LowestAny();  // no digit, or the digit's residue is full
+        o = LowestAny();  // no digit, the digit's residue is full, or its slot is too far out
     }
+    ++live_;
     high_ = std::max(high_, o + 1);
     return o;
 }
 
-void OrdinalAllocator::Release(uint32_t o) { free_[o % 10].insert(o); }
+void OrdinalAllocator::Release(uint32_t o) {
+    free_[o % 10].insert(o);
+    if (live_) --live_;
+}
 
 uint32_t OrdinalAllocator::HighWater() const { return high_; }
 

@@ -206,8 +206,14 @@ ms_pod_rec EncodePod(const v1::Pod &pod, uint32_t ordinal);
 // ordinal of any residue. When a digit's residue is full up to the capacity,
 // its nodes take the lowest free ordinal of any residue (correct, on the
 // kernel's bit-scan path).
+// Digit-aligned ordinals, within a bounded spread: a digit-aligned slot is taken
+// only while it stays below kSpreadSlack + 2 x (live nodes + 1); past that (e.g.
+// every node name ending in '0', which digit alignment would spread over 10x
+// the ordinals) the lowest free ordinal of any residue is used, so the sweep
+// extent (HighWater) stays within about twice the live node count.
 class OrdinalAllocator {
    public:
+    static constexpr uint32_t kSpreadSlack = 300;  // 10 groups of 30 ordinals
     explicit OrdinalAllocator(uint32_t capacity);
     uint32_t Allocate(int digit);  // digit 0..9, or -1; throws std::length_error when full
     void Release(uint32_t ordinal);
@@ -216,6 +222,7 @@ class OrdinalAllocator {
    private:
     uint32_t LowestAny();
     uint32_t cap_;
+    uint32_t live_ = 0;
     uint32_t next_[10];            // lowest never-used ordinal of residue d
     std::set<uint32_t> free_[10];  // released ordinals per residue
     uint32_t high_ = 0;

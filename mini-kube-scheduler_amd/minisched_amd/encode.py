@@ -170,7 +170,11 @@ class DigitOrdinals:
     ordinals hold at most 3 nodes of one digit whatever the informer Add order
     (the layout K1 pp's fast hash slots cover). Names without a digit, and
     digits whose residue is full up to the capacity, take the lowest free
-    ordinal of any residue."""
+    ordinal of any residue; so does a digit whose aligned slot lies past
+    SPREAD_SLACK + 2 x (live nodes + 1) (skewed name digits would otherwise
+    spread the table over up to 10x the ordinals)."""
+
+    SPREAD_SLACK = 300
 
     def __init__(self, capacity: int):
         import heapq  # noqa: F401  (free lists are min-heaps)
@@ -179,6 +183,7 @@ class DigitOrdinals:
         self.next = list(range(10))
         self.free: List[List[int]] = [[] for _ in range(10)]
         self.high = 0
+        self.live = 0
 
     def _lowest_any(self) -> int:
         import heapq
@@ -199,13 +204,15 @@ class DigitOrdinals:
     def allocate(self, digit: int) -> int:
         import heapq
 
-        if 0 <= digit <= 9 and self.free[digit]:
+        spread = self.SPREAD_SLACK + 2 * (self.live + 1)
+        if 0 <= digit <= 9 and self.free[digit] and self.free[digit][0] < spread:
             o = heapq.heappop(self.free[digit])
-        elif 0 <= digit <= 9 and self.next[digit] < self.cap:
+        elif 0 <= digit <= 9 and self.next[digit] < self.cap and self.next[digit] < spread:
             o = self.next[digit]
             self.next[digit] += 10
         else:
             o = self._lowest_any()
+        self.live += 1
         self.high = max(self.high, o + 1)
         return o
 
@@ -213,3 +220,4 @@ class DigitOrdinals:
         import heapq
 
         heapq.heappush(self.free[ordinal % 10], ordinal)
+        self.live = max(0, self.live - 1)

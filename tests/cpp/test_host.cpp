@@ -11,6 +11,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <set>
 #include <vector>
 
 #include "minisched.h"
@@ -137,6 +138,11 @@ static void cpu_tests() {
             threw = true;
         }
         CHECK(threw && full.HighWater() == 12);
+        // skewed digits: aligned slots only within kSpreadSlack + 2 x (live + 1), then dense
+        OrdinalAllocator sk(100000);
+        std::set<uint32_t> seen;
+        for (int i = 0; i < 5000; ++i) seen.insert(sk.Allocate(0));
+        CHECK(seen.size() == 5000 && sk.HighWater() <= 2 * 5000 + OrdinalAllocator::kSpreadSlack + 2);
     });
     run("queue: FIFO, backoff 1 s, event matching (queue.go)", [] {
         FakeClock clk;

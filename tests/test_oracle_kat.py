@@ -295,3 +295,9 @@ def test_digit_ordinals_allocator():
     assert sorted(full.allocate(5) for _ in range(12)) == list(range(12))
     with pytest.raises(OverflowError):
         full.allocate(5)
+    # skewed digits (every name ends in 0): aligned slots only within the spread
+    # bound, then dense; the sweep extent stays ~2x the node count, not 10x
+    sk = encode.DigitOrdinals(100_000)
+    got = [sk.allocate(0) for _ in range(5000)]
+    assert len(set(got)) == 5000 and sk.high <= 2 * 5000 + sk.SPREAD_SLACK + 2
+    assert got[:30] == list(range(0, 300, 10))  # aligned while within the bound
