@@ -402,6 +402,33 @@ def other_configs(args, dev, stream):
             "profile": os.path.relpath(args.profile_json_e, ROOT),
         }
     out["E"] = line
+    del pods, res
+
+    # ---- TT (not a BASELINE config): TaintToleration filter + the in-loop
+    # reverse-normalised score (MS_PLUGINS_NU_TT_NN), 50k nodes x 100k pods, batched
+    N, P = 50_000, 100_000
+    nr, pr = synth.nodes(N, seed=args.seed, taints=True), synth.pods(P, seed=args.seed, taints=True)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    with _lib.Engine(max_nodes=N, plugin_set=_lib.PLUGINS_NU_TT_NN, seed=args.seed, device=dev.index) as e:
+        e.upsert(np.arange(N), nr)
+        e.flush()
+        med, ts = _median_time(lambda: e.select_batch_device(P, pods.data_ptr(), res.data_ptr()), sync=sync)
+        got = res.cpu().numpy().view(_lib.RESULT)
+    n_pre = 2_000
+    t0 = time.perf_counter()
+    o = _oracle.schedule_tt(nr, pr[:n_pre], literal=False, seed=args.seed)
+    cpu_tt = time.perf_counter() - t0
+    out["TT"] = {
+        "workload": "TT (extension, not a BASELINE config): 50000 nodes x 100000 pods, NU+TaintToleration filters, "
+                    "NN + TaintToleration score with the in-loop reverse DefaultNormalizeScore, batched",
+        "ms": med * 1e3, "runs_ms": [t * 1e3 for t in ts], "evals_per_s": N * P / med, "pods_per_s": P / med,
+        "parity_vs_oracle_prefix": bool(np.array_equal(got["node"][:n_pre], o["node"])
+                                        and np.array_equal(got["code"][:n_pre], o["code"])),
+        "cpu_baseline": dict(value=N * n_pre / cpu_tt, unit="pod×node evals/s", kind="port",
+                             sample=f"oracle msor_schedule_tt closed form (1 thread), first {n_pre} pods "
+                                    f"({cpu_tt:.2f} s)", pods_per_s=n_pre / cpu_tt, **_cpu_info(1)),
+    }
     return out
 
 

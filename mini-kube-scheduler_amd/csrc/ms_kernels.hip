@@ -1016,6 +1016,26 @@ __device__ __forceinline__ void lds_dma16(void *dst, const void *src, uint32_t n
 #endif
 }
 
+// The same copy issued by nthreads threads (tid < nthreads) of a workgroup:
+// more loads in flight than one wave can hold (the step's idle validator
+// waves help the validating wave's prologue). The caller waits and barriers.
+__device__ __forceinline__ void lds_dma16_wg(void *dst, const void *src, uint32_t n16, uint32_t n_units, uint32_t tid,
+                                             uint32_t nthreads) {
+    if (n16 == 0) return;
+    const uint4 *g = reinterpret_cast<const uint4 *>(src);
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (uint32_t u = tid; u < n_units; u += nthreads) {
+#ifdef MS_NO_LDS_DMA
+        d[u] = g[min(u, n16 - 1)];
+#else
+        // (global_load_lds writes lane i's 16 B at the wave's base + 16 i: the
+        // wave-uniform base is d + u - lane)
+        __builtin_amdgcn_global_load_lds((global_void_t *)(g + min(u, n16 - 1)), (lds_void_t *)(d + (u - (tid & 63u))),
+                                         16, 0, 0);
+#endif
+    }
+}
+
 // Entry k (wave-divergent) of a register-held top-4 list, without the dynamic
 // register indexing that would put the list in scratch.
 __device__ __forceinline__ u64 pick4(const u64 (&e)[kTopK], int k) {
@@ -1313,8 +1333,37 @@ struct SeqArgs {
     uint32_t *stats;
 };
 
+// The validator's LDS tables cleared by nthreads threads: touched-node map,
+// per-slot bind counts, claim buckets.
+__device__ __forceinline__ void validate_clear(SeqShared &S, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < (uint32_t)kMapCap / 4; i += nthreads) reinterpret_cast<uint4 *>(S.map)[i] = make_uint4(0, 0, 0, 0);
+    static_assert(kSeqSlots % 16 == 0, "bound[] is cleared 16 slots per lane");
+    for (uint32_t i = tid; i < (uint32_t)kSeqSlots / 16; i += nthreads)
+        reinterpret_cast<uint4 *>(S.bound)[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = tid; i < (uint32_t)kClaimCap / 4; i += nthreads)
+        reinterpret_cast<uint4 *>(S.claim)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+
+// The validator's bulk prologue copies (the batch's top-4 records, ranks
+// 4..7, the stale nodes' records: up to ~85 KB) issued by every thread of the
+// workgroup; the caller waits for them and barriers before validate_batch
+// (wg_dma = true) runs on one wave. Same units and layout as validate_batch's
+// own copies.
+__device__ __forceinline__ void validate_prologue_wg(SeqShared &S, const SeqArgs &va, uint32_t tid, uint32_t nthreads) {
+    const uint32_t n_pods = va.n_pods;
+    if (n_pods > (uint32_t)kSeqBatch) return;
+    validate_clear(S, tid, nthreads);
+    lds_dma16_wg(&S.rec[0][0], va.top4_recs, n_pods * kTopK * kRecF / 2, kSeqBatch * kTopK * kRecF / 2, tid, nthreads);
+    if (va.top_ext)
+        lds_dma16_wg(&S.top_ext[0][0], va.top_ext, n_pods * kTopK / 2, kSeqBatch * kTopK / 2, tid, nthreads);
+    if (va.prev_in) {
+        const uint32_t units = (va.carry ? kPrevCap : kSeqBatch) * kRecF / 2;
+        lds_dma16_wg(&S.rec[kPrevSlot0][0], va.prev_recs_in, units, units, tid, nthreads);
+    }
+}
+
 template <int J>  // tile lists per lane: n_tiles <= 64 * J
-__device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, uint32_t lane) {
+__device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, uint32_t lane, bool wg_dma = false) {
     const NodeTable &t = va.t;
     const uint32_t n_rows = va.n_rows, n_pods = va.n_pods, seed32 = va.seed32, n_tiles = va.n_tiles;
     const ms_pod_rec *__restrict__ pods = va.pods;
@@ -1350,11 +1399,13 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                       kRecU * 64 * 16 == kPrevSlot0 * kRecF * 8 && kPrevU * 64 * 16 == kPrevCap * kRecF * 8 &&
                       kSpecU * 64 == kSeqBatch,
                   "prologue copies tile the LDS arrays exactly");
-    lds_dma16<kRecU>(&S.rec[0][0], top4_recs, n_pods * kTopK * kRecF / 2, lane);
-    if (va.top_ext) lds_dma16<kTopU>(&S.top_ext[0][0], va.top_ext, n_pods * kTopK / 2, lane);
-    if (prev_in) {  // (a writer without carry left at most kSeqBatch entries)
-        if (carry) lds_dma16<kPrevU>(&S.rec[kPrevSlot0][0], prev_recs_in, kPrevCap * kRecF / 2, lane);
-        else lds_dma16<kPrevU / 2>(&S.rec[kPrevSlot0][0], prev_recs_in, kSeqBatch * kRecF / 2, lane);
+    if (!wg_dma) {  // (else the whole workgroup issued these copies: validate_prologue_wg)
+        lds_dma16<kRecU>(&S.rec[0][0], top4_recs, n_pods * kTopK * kRecF / 2, lane);
+        if (va.top_ext) lds_dma16<kTopU>(&S.top_ext[0][0], va.top_ext, n_pods * kTopK / 2, lane);
+        if (prev_in) {  // (a writer without carry left at most kSeqBatch entries)
+            if (carry) lds_dma16<kPrevU>(&S.rec[kPrevSlot0][0], prev_recs_in, kPrevCap * kRecF / 2, lane);
+            else lds_dma16<kPrevU / 2>(&S.rec[kPrevSlot0][0], prev_recs_in, kSeqBatch * kRecF / 2, lane);
+        }
     }
     const uint32_t n_pod_u = n_pods * (uint32_t)sizeof(ms_pod_rec) / 8, n_top_u = n_pods * kTopK / 2;
     uint2 vpod[kPodU];
@@ -1376,11 +1427,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 #pragma unroll
         for (int k = 0; k < kPrevW; ++k) vprow[k] = prev_in ? prev_in[min(lane + 64u * k, (uint32_t)kPrevWords - 1)] : 0u;
     }
-    for (uint32_t i = lane; i < (uint32_t)kMapCap / 4; i += 64) reinterpret_cast<uint4 *>(S.map)[i] = make_uint4(0, 0, 0, 0);
-    static_assert(kSeqSlots % 16 == 0, "bound[] is cleared 16 slots per lane");
-    for (uint32_t i = lane; i < (uint32_t)kSeqSlots / 16; i += 64) reinterpret_cast<uint4 *>(S.bound)[i] = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = lane; i < (uint32_t)kClaimCap / 4; i += 64)
-        reinterpret_cast<uint4 *>(S.claim)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (!wg_dma) validate_clear(S, lane, 64u);
     if (lane == 0) S.n_out = 0;
     {
         uint2 *dp = reinterpret_cast<uint2 *>(S.pods);
@@ -1752,7 +1799,16 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
     const u64 t_begin = __builtin_amdgcn_s_memrealtime();
 #endif
     if (blockIdx.x == 0) {
-        if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x);
+        // the bulk prologue copies by all W waves (MS_WG_PROLOGUE=0: by the validating wave alone, A/B)
+#ifndef MS_WG_PROLOGUE
+#define MS_WG_PROLOGUE 1
+#endif
+        if (MS_WG_PROLOGUE && va.n_pods) {
+            validate_prologue_wg(S, va, threadIdx.x, 64u * W);
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        }
+        if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x, MS_WG_PROLOGUE != 0);
 #ifdef MS_VSTAMPS
         if (threadIdx.x == 0 && va.n_pods)
             atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 9, __builtin_amdgcn_s_memrealtime() - t_begin);
