@@ -124,6 +124,15 @@ struct CommState {
     ms_seq_cand *cands = nullptr, *cands_all = nullptr, *merged = nullptr;
     uint32_t *sflags = nullptr, *sflags_all = nullptr, *merged_flags = nullptr;
     uint64_t seq_windows = 0, seq_rounds = 0;
+    // coalesced submits: a NU+NN submission whose sweep waits to share the next one's launch
+    struct Stash {
+        bool on = false;
+        uint32_t n = 0, si = 0;
+        const ms_pod_rec *pods = nullptr;
+        ms_result *results = nullptr;
+        hipStream_t X = nullptr;
+    } stash;
+    bool coalesce = true;
     // MINISCHED_HOST_PROF=1: host time of ms_sharded_submit's phases (ns), printed at ms_destroy
     bool host_prof = false;
     uint64_t hp[6] = {0, 0, 0, 0, 0, 0}, hp_calls = 0;
@@ -214,9 +223,13 @@ int drain_locked(ms_ctx *c, size_t k) {
 }
 
 // Everything pending decoded; then `s` waits for the decode stream.
+int flush_stash(ms_ctx *c);
+
 int drain_to(ms_ctx *c, hipStream_t s) {
     CommState &m = *c->comm;
-    int rc = drain_locked(c, m.pending.size());
+    int rc = flush_stash(c);  // (a coalesced submission waiting for a partner)
+    if (rc) return rc;
+    rc = drain_locked(c, m.pending.size());
     if (rc) return rc;
     MS_HIP(c, hipEventRecord(m.ev_ds, m.ds));
     MS_HIP(c, hipStreamWaitEvent(s, m.ev_ds, 0));
@@ -231,21 +244,26 @@ inline void host_tick(CommState &m, int i, HostClock::time_point &t) {
     t = now;
 }
 
-int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
+// Submissions whose sweep can share a launch with the next one: NU+NN K1
+// sweeps of a shard one workgroup holds, on one sweep stream.
+bool coalescable(const ms_ctx *c) {
+    const CommState &m = *c->comm;
+    return m.coalesce && !m.two_streams && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows;
+}
+
+// The sweep stream and slot of the next submission (the slot's buffers sized
+// for n pods), ordered after: the caller's stream (its pods), the context
+// stream when it wrote the table since (deltas, binds), and the slot's
+// previous collective (it read the keys this sweep overwrites).
+int prepare_locked(ms_ctx *c, uint32_t n, hipStream_t s, uint32_t &si, hipStream_t &X) {
     CommState &m = *c->comm;
-    int rc = MS_OK;
-    HostClock::time_point tp = m.host_prof ? HostClock::now() : HostClock::time_point();
-    if (m.host_prof) ++m.hp_calls;
     const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
-    const uint32_t si = (uint32_t)(m.submitted % (m.depth + 1));
+    si = (uint32_t)(m.submitted % (m.depth + 1));
     const int xi = (int)(m.submitted & 1u);
-    const hipStream_t X = m.two_streams ? m.ss[xi] : s;
+    X = m.two_streams ? m.ss[xi] : s;
     ShardSlot &sl = m.slot[si];
-    rc = slot_ensure(c, sl, per);
+    int rc = slot_ensure(c, sl, per);
     if (rc) return rc;
-    // the sweep stream after: the caller's stream (its pods), the context stream
-    // when it wrote the table since (deltas, binds), the slot's previous
-    // collective (it read the keys this sweep overwrites)
     if (X != s) {
         MS_HIP(c, hipEventRecord(m.ev_in, s));
         MS_HIP(c, hipStreamWaitEvent(X, m.ev_in, 0));
@@ -259,35 +277,38 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     }
     // the slot's previous collective (submission k - depth - 1) read the keys
     // this sweep overwrites. Collectives complete in issue order, so one wait
-    // covers all older ones: wait for submission k - 2's (two steps old,
-    // normally done, and never the one the previous sweep feeds) and skip the
-    // next waits it covers.
+    // covers all older ones: wait for submission k - L's and skip the next
+    // waits it covers. L = 2 (two steps old, normally done, and never the one
+    // the previous sweep feeds); with coalesced submits L = 3: k is the first
+    // of a pair (then k - 1 and k - 2 are the previous pair, whose collectives
+    // follow the previous launch) or k - 3's wait is already on X.
     if (sl.used) {
         const uint64_t k = m.submitted, prev = k - (m.depth + 1);
-        if (m.two_streams || m.depth + 1 < 3) {
+        const uint32_t L = coalescable(c) ? 3u : 2u;
+        if (m.two_streams || m.depth + 1 <= L) {
             MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[si], 0));
         } else if (m.x_stream != X || m.x_comb_seen <= prev) {
             m.x_stream = X;
-            MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[(k - 2) % (m.depth + 1)], 0));
-            m.x_comb_seen = k - 1;
+            MS_HIP(c, hipStreamWaitEvent(X, m.ev_comb[(k - L) % (m.depth + 1)], 0));
+            m.x_comb_seen = k - L + 1;
         }
     }
-    host_tick(m, 0, tp);  // ordering of the sweep stream
+    ++m.submitted;
+    return MS_OK;
+}
+
+// The collective of slot si's batch on the collective stream, after the sweep
+// event ev (that recorded the batch's sweep) and the drain that decoded the
+// slot's previous batch; then the batch joins the pending list (and the oldest
+// are decoded once more than `depth` wait).
+int collective_locked(ms_ctx *c, uint32_t si, hipEvent_t ev, uint32_t n, const ms_pod_rec *pods, ms_result *results,
+                      HostClock::time_point &tp) {
+    CommState &m = *c->comm;
+    ShardSlot &sl = m.slot[si];
+    const uint32_t G = (uint32_t)m.world, per = cdiv(n, G);
     const int ps = c->cfg.plugin_set;
-    // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
-    // packet between consecutive sweeps on X)
-    if (ps == MS_PLUGINS_NU_TT_NN) {  // per-pod summaries of this shard's nodes, no keys
-        rc = tt_summaries_locked(c, n, pods, sl.summ, X);
-        if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
-    } else {
-        rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X, m.ev_swept[si]);
-    }
-    if (rc) return rc;
-    host_tick(m, 1, tp);  // the sweep launch
-    m.reads_outstanding = true;
-    // the collective after the sweep, and after the drain that decoded the
-    // slot's previous batch (it read keys_mine); one wait covers a whole drain
-    MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_swept[si], 0));
+    // one wait covers a whole drain
+    if (ev) MS_HIP(c, hipStreamWaitEvent(m.cs, ev, 0));
     if (sl.used && sl.dec_gen > m.cs_drain_seen) {
         MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_drained, 0));
         m.cs_drain_seen = m.drains;
@@ -317,10 +338,75 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     Pending p{si, n, 0, 0, pods, results};
     slice_of(m, n, p.first, p.count);
     m.pending.push_back(p);
-    ++m.submitted;
+    int rc = MS_OK;
     if (m.pending.size() > m.depth) rc = drain_locked(c, std::min<size_t>(m.group, m.pending.size()));
     host_tick(m, 4, tp);  // bookkeeping + drains
     return rc;
+}
+
+// The stashed submission's sweep alone, then its collective.
+int flush_stash(ms_ctx *c) {
+    CommState &m = *c->comm;
+    if (!m.stash.on) return MS_OK;
+    const CommState::Stash st = m.stash;
+    m.stash.on = false;
+    HostClock::time_point tp = m.host_prof ? HostClock::now() : HostClock::time_point();
+    int rc = sweep_locked(c, st.n, st.pods, m.slot[st.si].keys, nullptr, st.X, m.ev_swept[st.si]);
+    if (rc) return rc;
+    m.reads_outstanding = true;
+    return collective_locked(c, st.si, m.ev_swept[st.si], st.n, st.pods, st.results, tp);
+}
+
+int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
+    CommState &m = *c->comm;
+    HostClock::time_point tp = m.host_prof ? HostClock::now() : HostClock::time_point();
+    if (m.host_prof) ++m.hp_calls;
+    const bool co = coalescable(c);
+    if (!co) {
+        int rc = flush_stash(c);
+        if (rc) return rc;
+    }
+    uint32_t si = 0;
+    hipStream_t X = nullptr;
+    int rc = prepare_locked(c, n, s, si, X);
+    if (rc) return rc;
+    host_tick(m, 0, tp);  // ordering of the sweep stream
+    if (co && (!m.stash.on || m.stash.X != X)) {
+        // Coalesced submits (MINISCHED_SHARD_COALESCE=0 turns it off): this
+        // batch's sweep waits for the next submission (or a drain / table
+        // writer) and then shares ONE K1 launch with it, so the launch's ramp
+        // and drain (~7.5 us at a 12.5k-row shard, tools/probe_fixed.py) are
+        // paid once per two batches. Its collective starts after both sweeps.
+        rc = flush_stash(c);
+        if (rc) return rc;
+        m.stash = CommState::Stash{true, n, si, pods, results, X};
+        return MS_OK;
+    }
+    ShardSlot &sl = m.slot[si];
+    if (co) {  // the stashed batch and this one in one launch
+        const CommState::Stash st = m.stash;
+        m.stash.on = false;
+        MS_HIP(c, launch_sweep_pp2(c->t, c->rows_dev, st.pods, st.n, m.slot[st.si].keys, pods, n, sl.keys,
+                                   seed32_of(c->cfg.seed), c->present_dev, c->num_cus, X, m.ev_swept[si]));
+        host_tick(m, 1, tp);  // the sweep launch
+        m.reads_outstanding = true;
+        rc = collective_locked(c, st.si, m.ev_swept[si], st.n, st.pods, st.results, tp);
+        if (rc) return rc;
+        return collective_locked(c, si, nullptr, n, pods, results, tp);  // (cs already waits for the sweep)
+    }
+    const int ps = c->cfg.plugin_set;
+    // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
+    // packet between consecutive sweeps on X)
+    if (ps == MS_PLUGINS_NU_TT_NN) {  // per-pod summaries of this shard's nodes, no keys
+        rc = tt_summaries_locked(c, n, pods, sl.summ, X);
+        if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
+    } else {
+        rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X, m.ev_swept[si]);
+    }
+    if (rc) return rc;
+    host_tick(m, 1, tp);  // the sweep launch
+    m.reads_outstanding = true;
+    return collective_locked(c, si, m.ev_swept[si], n, pods, results, tp);
 }
 
 // Sequential-window buffers for windows of w pods.
@@ -426,6 +512,10 @@ void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world) {
 
 int comm_fence_reads(ms_ctx *c, hipStream_t writer) {
     CommState *m = c->comm;
+    if (m && m->stash.on) {  // the stashed batch's sweep reads the table before this writer
+        const int rc = flush_stash(c);
+        if (rc) return rc;
+    }
     if (!m || !m->reads_outstanding) return 0;
     // every sweep in flight is the newest of its slot (a slot is swept again only
     // after the collective that read its previous sweep): wait for each slot's
@@ -594,6 +684,7 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     m->group = std::min(m->group, m->depth);
     if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->two_streams = atoi(e) == 2;
     if (const char *e = getenv("MINISCHED_HOST_PROF")) m->host_prof = atoi(e) == 1;
+    if (const char *e = getenv("MINISCHED_SHARD_COALESCE")) m->coalesce = atoi(e) != 0;
     // Attached before the streams exist (MS_HIP reports through the context);
     // every failure below goes through comm_free, so a context is either joined
     // or left without a communicator, never half-built.

@@ -159,6 +159,12 @@ hipError_t launch_init_table(const NodeTable &t, hipStream_t s);
 hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present,
                            int num_cus, hipStream_t s, int commit = 0, hipEvent_t done = nullptr);
+// Two shard sweeps (keys only, rows <= kPpMaxFusedRows) in ONE launch: the
+// per-launch ramp and drain are paid once for both batches (ms_sharded_submit
+// coalesces consecutive submits). done: recorded after both.
+hipError_t launch_sweep_pp2(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods1, uint32_t n1,
+                            unsigned long long *keys1, const ms_pod_rec *pods2, uint32_t n2, unsigned long long *keys2,
+                            uint32_t seed32, uint32_t present, int num_cus, hipStream_t s, hipEvent_t done);
 // The compact host-array cycle (ms_schedule_batch_compact) in one launch, rows
 // <= kPpMaxFusedRows: pods are ms_pod_compact records and results
 // ms_result_compact, both in pinned host memory the kernel reads and writes

@@ -303,20 +303,33 @@ __host__ __device__ inline uint32_t tail_pods(uint32_t ng, uint32_t waves) {
     return mx() < m0 ? tpt : 0u;
 }
 
+// A second batch swept by the same launch (shard sweeps with key output only:
+// ms_sharded_submit coalesces two consecutive submits into one launch, paying
+// the per-launch ramp and drain once). Workgroups nblk1.. take its chunks.
+struct PpJob2 {
+    const ms_pod_rec *pods;  // nullptr: one batch
+    u64 *keys;
+    uint32_t n_pods, nblk1;
+};
+
 // TP: the packed-last-word path is compiled in (launch_sweep_pp picks it only
 // for shapes tail_pods packs; the others run the plain form).
 template <int KW, bool TP>
 __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
-    const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys,
+    const ms_pod_rec *__restrict__ pods1, uint32_t n_pods1, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys1,
     int atomic_keys, ms_result *__restrict__ results, uint32_t present, NodeTable tab, int commit,
-    uint32_t pstride, ms_result_compact *__restrict__ resc) {
+    uint32_t pstride, ms_result_compact *__restrict__ resc, PpJob2 j2) {
     // LDS: one combine slot per pod of the chunk, then the chunk's pod entries
     extern __shared__ u64 lds[];
     uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk);
     const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t pbeg = blockIdx.x * chunk;
+    const bool second = j2.pods && blockIdx.x >= j2.nblk1;  // (workgroup-uniform)
+    const ms_pod_rec *__restrict__ pods = second ? j2.pods : pods1;
+    const uint32_t n_pods = second ? j2.n_pods : n_pods1;
+    u64 *__restrict__ keys = second ? j2.keys : keys1;
+    const uint32_t pbeg = (second ? blockIdx.x - j2.nblk1 : blockIdx.x) * chunk;
     const uint32_t pend = min(n_pods, pbeg + chunk);
     const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
@@ -508,18 +521,24 @@ constexpr uint32_t kPpMaxChunk = 2048;
 namespace {
 hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                          uint32_t seed32, unsigned long long *keys, ms_result *results, uint32_t present, int num_cus,
-                         hipStream_t s, int commit, hipEvent_t done, uint32_t pstride, ms_result_compact *resc) {
-    if (n_pods == 0) return done ? hipEventRecord(done, s) : hipSuccess;
+                         hipStream_t s, int commit, hipEvent_t done, uint32_t pstride, ms_result_compact *resc,
+                         const ms_pod_rec *pods2 = nullptr, uint32_t n_pods2 = 0, unsigned long long *keys2 = nullptr) {
+    if (n_pods == 0 && n_pods2 == 0) return done ? hipEventRecord(done, s) : hipSuccess;
+    // (two batches: shard sweeps into keys, one workgroup holding every row)
+    const uint32_t n_all = n_pods + (pods2 ? n_pods2 : 0u);
     if (!t.planes) return hipErrorInvalidValue;
     const uint32_t n_groups = cdiv(n_rows, kGroupRows);
     // small shards with many pods: KW = 8, one single-wave workgroup per pod
     // chunk holds every row. It needs enough pods per wave to balance whole
     // waves over the SIMDs: 12.5k rows x 800k pods 347 vs 412 us, but x 100k
-    // pods 58.8 vs 52.7 us (profiles/r03_pp_words_ab.txt). MINISCHED_PP_WORDS
-    // = 4 / 8 forces a form (A/B).
+    // pods 58.8 vs 52.7 us (profiles/r03_pp_words_ab.txt): a line through the
+    // two crosses near 160k pods, and a coalesced pair of 100k-pod batches
+    // (200k) still ran faster at KW = 4 (53.5 vs 54.5 us per batch,
+    // profiles/r04f_coalesce_probe.txt), so the form switches at 1024 pods per
+    // CU. MINISCHED_PP_WORDS = 4 / 8 forces a form (A/B).
     const char *wenv = getenv("MINISCHED_PP_WORDS");
     const uint32_t cus_ = (uint32_t)(num_cus > 0 ? num_cus : 256);
-    bool small = n_groups <= kPpSmallGroups && n_pods >= 512u * cus_ && !getenv("MINISCHED_PP_WAVES");
+    bool small = n_groups <= kPpSmallGroups && n_all >= 1024u * cus_ && !getenv("MINISCHED_PP_WAVES");
     if (wenv) small = n_groups <= kPpSmallGroups && atoi(wenv) == 8;
     const uint32_t KW = small ? (uint32_t)kPpWordsSmall : (uint32_t)kPpWords;
     const uint32_t waves_needed = std::max(1u, cdiv(n_groups, 64u * KW));
@@ -539,7 +558,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // a full one -- exact chunks ran 11% slower at 25k rows, r02k_ab_chunk.txt)
     auto chunk_for = [&](uint32_t per_cu) {
         const uint32_t resident = std::max(1u, per_cu * cus / gy);
-        return cdiv(cdiv(n_pods, resident), 8) * 8;
+        return cdiv(cdiv(n_all, resident), 8) * 8;
     };
     uint32_t chunk = chunk_for(std::max(1u, 32u / W));  // one round at 32 waves per CU
     // Half as many workgroups (16 waves per CU, 4 per SIMD still saturate VALU
@@ -551,7 +570,10 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     if (32u / W > 1u && chunk_for(std::max(1u, 16u / W)) <= 1024u) chunk = chunk_for(std::max(1u, 16u / W));
     if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
-    const dim3 grid(cdiv(n_pods, chunk), gy);
+    const uint32_t nblk1 = cdiv(n_pods, chunk);
+    const dim3 grid(nblk1 + (pods2 ? cdiv(n_pods2, chunk) : 0u), gy);
+    const PpJob2 j2 = {pods2, reinterpret_cast<u64 *>(keys2), n_pods2, nblk1};
+    if (pods2 && (gy > 1 || results || resc || !keys || !keys2)) return hipErrorInvalidValue;
     if (gy > 1) {
         // several workgroups per chunk: combine keys with atomicMax, then decode
         // (done: an event record after the last of these launches)
@@ -560,7 +582,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_sweep_nunn_pp<kPpWords, false>), grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
-                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr);
+                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr, PpJob2{});
         e = hipGetLastError();
         if (e == hipSuccess && results) e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
         if (e == hipSuccess && results && commit) e = launch_apply_binds(t, pods, n_pods, results, s);
@@ -577,7 +599,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     const bool tp = KW == (uint32_t)kPpWords && tail_pods(n_groups, W) != 0u;
 #define MS_PP_LAUNCH(KWV, TPV)                                                                                     \
     hipExtLaunchKernelGGL((k_sweep_nunn_pp<KWV, TPV>), grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes, t.gcap, \
-                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc)
+                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc, j2)
     if (KW == (uint32_t)kPpWordsSmall) {
         MS_PP_LAUNCH(kPpWordsSmall, false);
     } else {
@@ -594,6 +616,14 @@ hipError_t launch_sweep_pp(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
                            int num_cus, hipStream_t s, int commit, hipEvent_t done) {
     return sweep_pp_impl(t, n_rows, pods, n_pods, seed32, keys, results, present, num_cus, s, commit, done,
                          (uint32_t)sizeof(ms_pod_rec), nullptr);
+}
+
+hipError_t launch_sweep_pp2(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods1, uint32_t n1,
+                            unsigned long long *keys1, const ms_pod_rec *pods2, uint32_t n2, unsigned long long *keys2,
+                            uint32_t seed32, uint32_t present, int num_cus, hipStream_t s, hipEvent_t done) {
+    if (n_rows > kPpMaxFusedRows) return hipErrorInvalidValue;
+    return sweep_pp_impl(t, n_rows, pods1, n1, seed32, keys1, nullptr, present, num_cus, s, 0, done,
+                         (uint32_t)sizeof(ms_pod_rec), nullptr, pods2, n2, keys2);
 }
 
 hipError_t launch_sweep_pp_compact(const NodeTable &t, uint32_t n_rows, const ms_pod_compact *pods, uint32_t n_pods,

@@ -357,6 +357,47 @@ def test_library_sharded_cycle_1rank(oracle, plugin_set):
     _same(res, o, 0, len(pr), "library cycle")
 
 
+@pytest.mark.parametrize("coalesce,words", [("1", ""), ("0", ""), ("1", "8"), ("1", "4")])
+def test_library_submit_coalescing(oracle, monkeypatch, coalesce, words):
+    # Consecutive NU+NN submits share one K1 launch (ms_comm.cpp submit_locked's
+    # stash): distinct pod batches of distinct sizes, an odd count (the last one
+    # swept alone at the drain), and a node delta between two submits (the
+    # stashed sweep must read the table BEFORE the delta, as submitted). Both
+    # K1 forms for small shards (MINISCHED_PP_WORDS: 8 = one wave holds every
+    # row, chosen above 1024 pods per CU; 4) under the two-batch launch.
+    import torch
+
+    from minisched_amd import _lib
+
+    monkeypatch.setenv("MINISCHED_SHARD_COALESCE", coalesce)
+    if words:
+        monkeypatch.setenv("MINISCHED_PP_WORDS", words)
+    nr = synth.nodes(5000, seed=81)
+    batches = [synth.pods(n, seed=81 + i) for i, n in enumerate((700, 1200, 333, 2048, 901))]
+    nr2 = nr.copy()
+    nr2["unschedulable"][::5] ^= 1  # the delta: NodeUnschedulable flips, NodeNumber digits move
+    nr2["name_digit"][::7] = (nr2["name_digit"][::7] + 3) % 10
+    want = [oracle.schedule(nr if i < 3 else nr2, p, seed=81) for i, p in enumerate(batches)]
+    dev = torch.device("cuda:0")
+    e = _comm_engine(nr, 0, 81)
+    try:
+        s = torch.cuda.Stream(device=dev)
+        pods = [torch.from_numpy(p.view(np.uint8).copy()).to(dev) for p in batches]
+        res = [torch.zeros(len(p) * _lib.RESULT.itemsize, dtype=torch.uint8, device=dev) for p in batches]
+        torch.cuda.synchronize()
+        for i in range(5):
+            if i == 3:  # (batch 2 is stashed here when coalescing: 0+1 shared a launch)
+                e.upsert(np.arange(5000), nr2)
+                e.flush()
+            e.sharded_submit(len(batches[i]), pods[i].data_ptr(), res[i].data_ptr(), s.cuda_stream)
+        e.sharded_drain(s.cuda_stream)
+        s.synchronize()
+        for i in range(5):
+            _same(res[i].cpu().numpy().view(_lib.RESULT), want[i], 0, len(batches[i]), f"batch {i}")
+    finally:
+        e.close()
+
+
 def test_library_schedule_batch_1rank(oracle):
     # ms_schedule_batch on a communicator: every pod's result on every rank (all-gather of
     # the slices), binds committed on the rank's own shard; NU+NN batched and sequential,

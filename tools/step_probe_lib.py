@@ -7,7 +7,8 @@ slice decode on the decode stream) exactly as ShardedCycle does, K steps
 between HIP events, then ms_sharded_drain. With one rank the reduce-scatter is
 a copy and the slice is all 100k pods (a G-rank slice is 100k/G), so this
 slightly over-counts the decode. MINISCHED_SHARD_STREAMS=1 (set per variant)
-puts every sweep on one stream.
+puts every sweep on one stream; MINISCHED_SHARD_COALESCE=0 gives each submit
+its own sweep launch (default: two consecutive submits share one K1 launch).
 """
 import json
 import os
@@ -34,10 +35,14 @@ def main():
     variants = os.environ.get("PROBE_VARIANTS", "")
     variants = [v.split(":") for v in variants.split(",")] if variants else \
         [("1", st) for st in os.environ.get("PROBE_STREAMS", "2,1").split(",")]
-    for prio, streams in variants * int(os.environ.get("PROBE_REPEAT", "1")):
+    # PROBE_COALESCE "1,0": MINISCHED_SHARD_COALESCE per variant (two submits' sweeps in one launch)
+    coal = os.environ.get("PROBE_COALESCE", "1").split(",")
+    variants = [(p_, st, co) for p_, st in variants for co in coal]
+    for prio, streams, co in variants * int(os.environ.get("PROBE_REPEAT", "1")):
         os.environ["MINISCHED_SHARD_STREAMS"] = streams
+        os.environ["MINISCHED_SHARD_COALESCE"] = co
         os.environ["MINISCHED_SWEEP_PRIO"] = prio
-        streams = f"{streams}p{prio}"
+        streams = f"{streams}p{prio}" + ("" if co == "1" else "c0")
         for G in [int(g) for g in os.environ.get("PROBE_G", "1,2,4,8,16").split(",")]:
             lo, hi = sharded.shard_bounds(N, G - 1, G)
             eng = _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=1)
