@@ -709,10 +709,12 @@ __device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t til
 
 // The transposed sweep of one tile by a workgroup of W waves: every thread
 // stages the tile's rows, then wave w takes pod groups w, w + W, ..
-// (block-uniform control flow: every wave reaches both barriers).
+// (block-uniform control flow: every wave reaches both barriers). Returns the
+// wave's groups (bit i: its i-th group) outside the binary64 form's range,
+// which sweep_tp_redo then takes in the lane = row form.
 template <int W>
-__device__ __forceinline__ void sweep_tp_tile(const SweepArgs &a, uint32_t tile, DRow *rows, uint32_t wave,
-                                              uint32_t lane) {
+__device__ __forceinline__ uint32_t sweep_tp_tile(const SweepArgs &a, uint32_t tile, DRow *rows, uint32_t wave,
+                                                  uint32_t lane) {
     __syncthreads();  // the previous tile's readers are done
     const uint4 *src = reinterpret_cast<const uint4 *>(a.t.drow + (size_t)tile * kFullWaveTile);
     uint4 *dst = reinterpret_cast<uint4 *>(rows);
@@ -720,12 +722,17 @@ __device__ __forceinline__ void sweep_tp_tile(const SweepArgs &a, uint32_t tile,
     for (uint32_t i = threadIdx.x; i < kVec; i += 64u * W) dst[i] = src[i];
     __syncthreads();
     const TileBits tb = tile_bits(rows, lane);
-    // groups outside the binary64 form's range (bit i: the wave's i-th group;
-    // a batch holds at most kSeqBatch <= 256 pods, i.e. 16 groups)
+    // (a batch holds at most kSeqBatch <= 256 pods, i.e. 16 groups)
     uint32_t redo = 0;
     for (uint32_t grp = wave, i = 0; grp * kTpPods < a.n_pods; grp += W, ++i)
         if (!sweep_tp_task(a, tile, grp, lane, rows, tb)) redo |= 1u << i;
-    // (a separate loop: the lane = row form's registers do not add to the transposed form's)
+    return redo;
+}
+
+// The groups sweep_tp_tile left (bit i: the wave's i-th group), lane = row form.
+template <int W>
+__device__ __forceinline__ void sweep_tp_redo(const SweepArgs &a, uint32_t tile, uint32_t redo, uint32_t wave,
+                                              uint32_t lane) {
     for (uint32_t grp = wave, i = 0; redo; grp += W, ++i)
         if (redo & (1u << i)) {
             redo &= ~(1u << i);
@@ -737,7 +744,8 @@ constexpr int kTpWaves = 8;  // standalone transposed sweep: 8 waves x 16 pods =
 
 __global__ __launch_bounds__(64 * kTpWaves) void k_sweep_tp_topk(SweepArgs a) {
     __shared__ DRow rows[kFullWaveTile];
-    sweep_tp_tile<kTpWaves>(a, blockIdx.x, rows, threadIdx.x >> 6, lane_id());
+    const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+    sweep_tp_redo<kTpWaves>(a, blockIdx.x, sweep_tp_tile<kTpWaves>(a, blockIdx.x, rows, wave, lane), wave, lane);
 }
 
 __global__ __launch_bounds__(kFullThreads) void k_sweep_full_topk(SweepArgs a) {
@@ -962,7 +970,9 @@ struct SeqShared {
     WalkResult walkres[16];          // and each one's winner
 };
 static_assert(sizeof(SeqShared) <= 160 * 1024, "validator LDS");
-static_assert(sizeof(SeqShared) >= kFullWaveTile * sizeof(DRow), "a sweep workgroup stages a tile in it");
+constexpr uint32_t kTpDeferCap = 32;  // deferred (tile, groups) entries per sweep wave (k_seq_step)
+static_assert(sizeof(SeqShared) >= kFullWaveTile * sizeof(DRow) + 16u * kTpDeferCap * sizeof(uint32_t),  // (W <= 16)
+              "a sweep workgroup stages a tile in it, and its waves' deferred lists after it");
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t row) { return (row * kGolden32) >> (32 - kMapBits); }
 __device__ __forceinline__ uint32_t claim_hash(uint32_t row) { return (row * 0x85EBCA6Bu) >> (32 - kClaimBits); }
@@ -1818,8 +1828,27 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
     if (sw.t.drow && sw.fast) {  // transposed form: a tile per workgroup, its rows in the validator's (idle) LDS
         DRow *rows = reinterpret_cast<DRow *>(&S);
-        for (uint32_t tile = blockIdx.x - 1; tile < sw.n_tiles; tile += gridDim.x - 1)
-            sweep_tp_tile<W>(sw, tile, rows, wave, lane);
+        // Groups outside the binary64 range are taken after the tile loop, listed
+        // per wave in LDS past the staged rows: with the lane = row fallback
+        // inline, its registers made the loop's invariants spill (28 B per lane,
+        // 4.1 MB of scratch writes per config E step, a reload wait per tile).
+        uint32_t *defer = reinterpret_cast<uint32_t *>(rows + kFullWaveTile) + wave * kTpDeferCap;
+        uint32_t nd = 0;
+        bool over = false;
+        for (uint32_t tile = blockIdx.x - 1; tile < sw.n_tiles; tile += gridDim.x - 1) {
+            const uint32_t r = sweep_tp_tile<W>(sw, tile, rows, wave, lane);  // (wave-uniform)
+            if (r) {
+                if (nd < kTpDeferCap) defer[nd++] = tile << 16 | r;
+                else over = true;
+            }
+        }
+        for (uint32_t i = 0; i < nd; ++i) sweep_tp_redo<W>(sw, defer[i] >> 16, defer[i] & 0xFFFFu, wave, lane);
+        if (over) {  // (more deferred tiles than the list holds: every group of every tile, exactly)
+            uint32_t all = 0;
+            for (uint32_t grp = wave, i = 0; grp * kTpPods < sw.n_pods; grp += W, ++i) all |= 1u << i;
+            for (uint32_t tile = blockIdx.x - 1; tile < sw.n_tiles; tile += gridDim.x - 1)
+                sweep_tp_redo<W>(sw, tile, all, wave, lane);
+        }
     } else {
         for (uint32_t task = (blockIdx.x - 1) * W + wave; task < n_tasks; task += (gridDim.x - 1) * W)
             sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
@@ -2088,8 +2117,11 @@ __global__ void k_seq_window_in(const ms_pod_rec *__restrict__ pods, uint32_t n,
     const uint32_t cur = min(ctl[0], n);
     const uint32_t live = min(w, n - cur);
     for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) {
-        ms_pod_rec z = {};
-        win[i] = i < live ? pods[cur + i] : z;
+        // 8-byte words (a struct select put the record on the stack)
+        const uint2 *src = reinterpret_cast<const uint2 *>(pods + cur + min(i, live ? live - 1u : 0u));
+        uint2 *dst = reinterpret_cast<uint2 *>(win + i);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(ms_pod_rec) / 8); ++k) dst[k] = i < live ? src[k] : make_uint2(0u, 0u);
     }
     if (threadIdx.x == 0) ctl[1] = live;
 }
