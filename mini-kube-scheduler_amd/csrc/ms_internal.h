@@ -82,7 +82,10 @@ enum : uint32_t {
     kPlaneD3,
     kPlaneSched,    // present && !Spec.Unschedulable
     kPlanePresent,  // present (not tombstoned)
-    kPlaneOver,     // 1 if the group holds more than 3 present rows of one digit (K1 pp's scan path)
+    kPlaneOver,     // bit 0: the group holds more than 3 present rows of one digit (K1 pp's scan path);
+                    // bit 1: some present row's digit is not its ordinal mod 10 (no fixed-slot path)
+    kPlaneDigitPres,   // present && the name ends in a digit
+    kPlaneDigitSched,  // present && !Spec.Unschedulable && the name ends in a digit
     kPlanes
 };
 

@@ -9,8 +9,9 @@
 //   selectHost       :304-325 (rand.Intn tie-break -> rule r3, minisched_gpu.h)
 //
 // Bit-sliced evaluation. The node table keeps, per group of 30 consecutive
-// rows, six bit planes (ms_internal.h kPlane*): the four bits of each row's
-// name digit (15 = no digit), "present and schedulable" and "present". A lane
+// rows, bit planes (ms_internal.h kPlane*): the four bits of each row's
+// name digit (15 = no digit), "present and schedulable" and "present" (and
+// both restricted to digit names, plus a per-group flag word). A lane
 // holds up to kPpWords groups in registers. For one pod and one group:
 //   F = tolerates ? present : schedulable                     (NodeUnschedulable, 30 rows)
 //   m = F & XNOR(d0, pod bit 0) & .. & XNOR(d3, pod bit 3)    (NodeNumber's 10, 30 rows)
@@ -26,6 +27,11 @@
 // feasible row of the wave scores 10: the wave's maximum is then 0 and the pod
 // is redone by the exact slow path (every feasible row hashed, explicit
 // found flags), which also covers non-digit pods.
+// Fixed-slot form (word_fix): where every present digit-named row of a
+// wave's groups has digit == ordinal mod 10 (the digit-aligned allocator's
+// layout, and the synthetic clusters'), the pod's digit can only sit at three
+// known slots, so the per-pod mask is one v_bitop3 and the slots need no
+// search: 24 VALU per pod and group instead of 31, same keys bit for bit.
 //
 // Grid: a workgroup holds ALL of the context's rows (up to 16 waves x 64 lanes
 // x kPpWords groups = 122,880 rows; more rows split over grid.y and combine
@@ -71,6 +77,7 @@ constexpr uint32_t kPpSmallGroups = 64u * kPpWordsSmall;  // 15,360 rows
 struct Word {
     uint32_t d0, d1, d2, d3;  // digit bit planes
     uint32_t sched, pres;     // present & schedulable, present
+    uint32_t dsched, dpres;   // the same restricted to rows whose name ends in a digit
     uint32_t hb;              // (ordinal of the group's row 0) * kG24
 };
 
@@ -79,6 +86,11 @@ struct Pod {
     uint32_t A;               // tb_pod(seed32, ordinal)
     uint32_t s0, s1, s2, s3;  // digit bit i as 0 / ~0 (non-digit pods: 14, which no node has)
     uint32_t tol;             // tolerates node.kubernetes.io/unschedulable: 0 / ~0
+    // fixed-slot form (groups whose rows' digits equal their ordinals mod 10):
+    // the three slots of the pod's digit, p0 = (digit - node_base) mod 10, p0 + 10,
+    // p0 + 20 (non-digit pods: 30, a bit no group sets), and A + p_j * kG24
+    uint32_t p0, p1, p2;
+    uint32_t A0, A1, A2;
 };
 
 #define MS_BITOP3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
@@ -132,7 +144,8 @@ __device__ __forceinline__ uint32_t word_scan(uint32_t m, uint32_t hbA) {
     return h;
 }
 
-__device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
+// base10: node_base mod 10 (the fixed slots; 0 when unused).
+__device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info, uint32_t base10 = 0) {
     Pod q;
     q.A = A;
     q.s0 = (info & 1u) ? ~0u : 0u;
@@ -140,7 +153,39 @@ __device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
     q.s2 = (info & 4u) ? ~0u : 0u;
     q.s3 = (info & 8u) ? ~0u : 0u;
     q.tol = (info & 16u) ? ~0u : 0u;
+    const uint32_t d = info & 15u;
+    const bool dig = d <= 9u;
+    q.p0 = dig ? (d + 10u - base10) % 10u : 30u;
+    q.p1 = dig ? q.p0 + 10u : 30u;
+    q.p2 = dig ? q.p0 + 20u : 30u;
+    q.A0 = A + q.p0 * kG24;
+    q.A1 = q.A0 + 10u * kG24;
+    q.A2 = q.A0 + 20u * kG24;
     return q;
+}
+
+// Fixed-slot form: in a group where every present row's name digit is its
+// ordinal mod 10 (the digit-aligned allocator's layout, ms_nodes_upsert docs),
+// the rows of the pod's digit can only sit at slots p0, p0 + 10, p0 + 20, and
+// such a row scores NodeNumber's 10 exactly when its name ends in a digit. So
+// the filter-and-score mask of the group is ONE v_bitop3 over the digit-name
+// planes (NodeUnschedulable with the toleration, as feasible()), and the
+// three candidates need no slot search: each hash input is hb + A_j, zeroed by
+// its slot's bit (v_bfe_i32 gives 0 / ~0; mix32(0) = 0, the empty value).
+__device__ __forceinline__ uint32_t match_fix(const Word &w, const Pod &q) {
+    return MS_BITOP3(w.dpres, w.dsched, q.tol, kSelect);
+}
+
+__device__ __forceinline__ uint32_t word_fix(const Word &w, const Pod &q) {
+    const uint32_t m = match_fix(w, q);
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_sbfe((int)m, (int)q.p0, 1);
+    const uint32_t k1 = (uint32_t)__builtin_amdgcn_sbfe((int)m, (int)q.p1, 1);
+    const uint32_t k2 = (uint32_t)__builtin_amdgcn_sbfe((int)m, (int)q.p2, 1);
+    uint32_t x0 = (w.hb + q.A0) & k0, x1 = (w.hb + q.A1) & k1, x2 = (w.hb + q.A2) & k2;
+    // (opaque: left visible, the compiler folds the AND into a v_bitop3 with the
+    // first xor-shift and pays a separate shift for it, one VALU more per slot)
+    asm("" : "+v"(x0), "+v"(x1), "+v"(x2));
+    return max(max(mix32(x0), mix32(x1)), mix32(x2));
 }
 
 // Exact evaluation of one pod over the wave's NW groups, with explicit found
@@ -149,13 +194,16 @@ __device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
 // 0 when no row of the wave is feasible.
 // tail: the wave's packed last word (below) is evaluated here like a full one:
 // its groups repeat in every lane segment, and repeats leave the max unchanged.
-template <int KW, int NW>
+// FIX: the wave's words are digit-aligned (word_fix): the score-10 rows are
+// the fixed slots' digit-name rows.
+template <int KW, int NW, bool FIX>
 __device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Word &Wt, bool tail, const Pod &q) {
     uint32_t h = 0;
     bool found = false;
+    const uint32_t cmask = (1u << q.p0) | (1u << q.p1) | (1u << q.p2);  // (non-digit pods: bit 30, never set)
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
-        const uint32_t m = match10(W[k], q);
+        const uint32_t m = FIX ? match_fix(W[k], q) & cmask : match10(W[k], q);
         found = found || m != 0;
         h = max(h, word_scan(m, W[k].hb + q.A));
     }
@@ -202,9 +250,16 @@ __device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, 
 // tidx of tshare taking the 8-pod blocks b with b mod tshare == tidx. (A
 // partial word holding the full cost on one SIMD was 6 % of config C:
 // 100,000 rows 323 us, 99,840 rows 303 us, profiles/r03zd_tail.json.)
-template <int KW, int NW, bool GEN, bool TAIL>
+// MODE: kModeFast (three slots found by bit scans, word_fast), kModeGen (some
+// group of the wave holds more than 3 rows of a digit: the bit-scan loop),
+// kModeFix (every group of the wave is digit-aligned: word_fix).
+constexpr int kModeFast = 0, kModeGen = 1, kModeFix = 2;
+
+template <int KW, int NW, int MODE, bool TAIL>
 __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt, uint32_t tpt, uint32_t tshare,
-                                            uint32_t tidx, const uint2 *pinfo, uint32_t np, uint32_t lane, u64 *lds) {
+                                            uint32_t tidx, const uint2 *pinfo, uint32_t np, uint32_t lane, u64 *lds,
+                                            uint32_t base10) {
+    constexpr bool GEN = MODE == kModeGen;
     const uint32_t seg_shift = tpt == 8u ? 3u : tpt == 4u ? 4u : 5u;  // log2(64 / tpt)
     for (uint32_t pb = 0; pb < np; pb += 64) {
         const uint32_t nblk = min(64u, np - pb);
@@ -220,14 +275,16 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt,
 #pragma unroll
             for (int t = 0; t < 8; ++t)
                 q[t] = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
-                                (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
+                                (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)), base10);
             uint32_t r[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 uint32_t h = 0;
 #pragma unroll
                 for (int k = 0; k < NW; ++k)
-                    h = max(h, GEN ? word_scan(match10(W[k], q[t]), W[k].hb + q[t].A) : word_fast(W[k], q[t]));
+                    h = max(h, MODE == kModeGen ? word_scan(match10(W[k], q[t]), W[k].hb + q[t].A)
+                               : MODE == kModeFix ? word_fix(W[k], q[t])
+                                                  : word_fast(W[k], q[t]));
                 r[t] = h;
             }
             if (TAIL && ((pb + j) >> 3) % tshare == tidx) {  // wave-uniform
@@ -256,8 +313,8 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt,
                 redo &= redo - 1ull;
                 const uint32_t t = rev3(l >> 3);
                 const Pod qs = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
-                const u64 v = pod_slow<KW, NW>(W, Wt, TAIL && ((pb + j) >> 3) % tshare == tidx, qs);
+                                        (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)), base10);
+                const u64 v = pod_slow<KW, NW, MODE == kModeFix>(W, Wt, TAIL && ((pb + j) >> 3) % tshare == tidx, qs);
                 if (lane == 0 && v) atomicMax(&lds[pb + j + t], v);
             }
         }
@@ -319,7 +376,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods1, uint32_t n_pods1, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys1,
     int atomic_keys, ms_result *__restrict__ results, uint32_t present, NodeTable tab, int commit,
-    uint32_t pstride, ms_result_compact *__restrict__ resc, PpJob2 j2) {
+    uint32_t pstride, ms_result_compact *__restrict__ resc, PpJob2 j2, int fix_ok) {
     // LDS: one combine slot per pod of the chunk, then the chunk's pod entries
     extern __shared__ u64 lds[];
     uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk);
@@ -352,7 +409,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     if (wv < wv_t || wv >= wv_t + tshare) tpt = 0u;  // wave-uniform
     Word W[KW], Wt;
     int nw = 0;
-    bool over = false;
+    bool over = false, misaligned = false;
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
         const uint32_t wi = k * waves + wv;
@@ -366,9 +423,13 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
         W[k].d3 = in ? planes[kPlaneD3 * gstride + g] : 0u;
         W[k].sched = in ? planes[kPlaneSched * gstride + g] : 0u;
         W[k].pres = in ? planes[kPlanePresent * gstride + g] : 0u;
+        W[k].dsched = in ? planes[kPlaneDigitSched * gstride + g] : 0u;
+        W[k].dpres = in ? planes[kPlaneDigitPres * gstride + g] : 0u;
         W[k].hb = (node_base + g * kGroupRows) * kG24;
+        const uint32_t ov = in ? planes[kPlaneOver * gstride + g] : 0u;
         // more than 3 present rows of one digit in a group: the fast slots cannot hold them
-        over = over || (in && planes[kPlaneOver * gstride + g] != 0u);
+        over = over || (ov & 1u) != 0u;
+        misaligned = misaligned || (ov & 2u) != 0u;
     }
     {
         const uint32_t gi = tpt ? lane & ((64u / tpt) - 1u) : 0u;
@@ -381,29 +442,28 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
         Wt.sched = in ? planes[kPlaneSched * gstride + g] : 0u;
         Wt.pres = in ? planes[kPlanePresent * gstride + g] : 0u;
         Wt.hb = (node_base + g * kGroupRows) * kG24;
-        over = over || (in && planes[kPlaneOver * gstride + g] != 0u);
+        Wt.dsched = Wt.dpres = 0u;  // (the packed word always takes word_fast / word_scan)
+        over = over || (in && (planes[kPlaneOver * gstride + g] & 1u) != 0u);
     }
     const bool gen = __ballot(over) != 0;
+    // every word of the wave digit-aligned (MINISCHED_PP_FIX=0 at launch: never)
+    const int mode = gen ? kModeGen : (fix_ok && __ballot(misaligned) == 0) ? kModeFix : kModeFast;
+    const uint32_t base10 = node_base % 10u;
     __syncthreads();
     if (np && (nw || tpt)) {
-        switch (nw * 4 + (gen ? 2 : 0) + (tpt ? 1 : 0)) {  // wave-uniform
-#define MS_PP_CASE(N)                                                                                       \
-    case 4 * N:                                                                                             \
-        if constexpr (N <= KW && N > 0)                                                                     \
-            sweep_range<KW, (N <= KW ? N : KW), false, false>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds); \
-        break;                                                                                              \
-    case 4 * N + 1:                                                                                         \
-        if constexpr (N <= KW)                                                                              \
-            sweep_range<KW, (N <= KW ? N : KW), false, true>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);  \
-        break;                                                                                              \
-    case 4 * N + 2:                                                                                         \
-        if constexpr (N <= KW && N > 0)                                                                     \
-            sweep_range<KW, (N <= KW ? N : KW), true, false>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);  \
-        break;                                                                                              \
-    case 4 * N + 3:                                                                                         \
-        if constexpr (N <= KW)                                                                              \
-            sweep_range<KW, (N <= KW ? N : KW), true, true>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);   \
+        switch (nw * 6 + mode * 2 + (tpt ? 1 : 0)) {  // wave-uniform
+#define MS_PP_CASE1(N, M, T)                                                                                     \
+    case 6 * N + 2 * M + T:                                                                                      \
+        if constexpr (N <= KW && (N > 0 || T))                                                                   \
+            sweep_range<KW, (N <= KW ? N : KW), M, T>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds, base10); \
         break;
+#define MS_PP_CASE(N)        \
+    MS_PP_CASE1(N, 0, false) \
+    MS_PP_CASE1(N, 0, true)  \
+    MS_PP_CASE1(N, 1, false) \
+    MS_PP_CASE1(N, 1, true)  \
+    MS_PP_CASE1(N, 2, false) \
+    MS_PP_CASE1(N, 2, true)
             MS_PP_CASE(0)
             MS_PP_CASE(1)
             MS_PP_CASE(2)
@@ -414,6 +474,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
             MS_PP_CASE(7)
             MS_PP_CASE(8)
 #undef MS_PP_CASE
+#undef MS_PP_CASE1
             default:
                 break;  // no groups in this wave
         }
@@ -460,7 +521,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
 
 // Bit planes of one 30-row group from the SoA columns (flags, digit).
 __device__ __forceinline__ void build_group(const NodeTable &t, uint32_t g) {
-    uint32_t d[4] = {0, 0, 0, 0}, sched = 0, pres = 0;
+    uint32_t d[4] = {0, 0, 0, 0}, sched = 0, pres = 0, isdig = 0, misal = 0;
     for (uint32_t s = 0; s < kGroupRows; ++s) {
         const uint32_t r = g * kGroupRows + s;
         if (r >= t.cap) break;
@@ -471,9 +532,13 @@ __device__ __forceinline__ void build_group(const NodeTable &t, uint32_t g) {
         if (!(f & kNodeAbsent)) {
             pres |= 1u << s;
             if (!(f & kNodeUnschedulable)) sched |= 1u << s;
+            if (v <= 9u) {
+                isdig |= 1u << s;
+                if (v != (t.base + r) % 10u) misal = 2u;  // digit != ordinal mod 10
+            }
         }
     }
-    uint32_t over = 0;
+    uint32_t over = misal;
 #pragma unroll
     for (int v = 0; v < 10; ++v) {
         const uint32_t m = pres & ((v & 1) ? d[0] : ~d[0]) & ((v & 2) ? d[1] : ~d[1]) & ((v & 4) ? d[2] : ~d[2]) &
@@ -481,6 +546,8 @@ __device__ __forceinline__ void build_group(const NodeTable &t, uint32_t g) {
         over |= __popc(m) > 3 ? 1u : 0u;
     }
     const uint32_t st = t.gcap;
+    t.planes[kPlaneDigitPres * st + g] = pres & isdig;
+    t.planes[kPlaneDigitSched * st + g] = sched & isdig;
     t.planes[kPlaneOver * st + g] = over;
     t.planes[kPlaneD0 * st + g] = d[0];
     t.planes[kPlaneD1 * st + g] = d[1];
@@ -572,6 +639,11 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
     const uint32_t nblk1 = cdiv(n_pods, chunk);
     const dim3 grid(nblk1 + (pods2 ? cdiv(n_pods2, chunk) : 0u), gy);
+    // the fixed-slot form for digit-aligned waves (MINISCHED_PP_FIX=0: off, A/B)
+    static const int fix_ok = [] {
+        const char *e = getenv("MINISCHED_PP_FIX");
+        return e ? (atoi(e) != 0 ? 1 : 0) : 1;
+    }();
     const PpJob2 j2 = {pods2, reinterpret_cast<u64 *>(keys2), n_pods2, nblk1};
     if (pods2 && (gy > 1 || results || resc || !keys || !keys2)) return hipErrorInvalidValue;
     if (gy > 1) {
@@ -582,7 +654,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_sweep_nunn_pp<kPpWords, false>), grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
-                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr, PpJob2{});
+                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr, PpJob2{}, fix_ok);
         e = hipGetLastError();
         if (e == hipSuccess && results) e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
         if (e == hipSuccess && results && commit) e = launch_apply_binds(t, pods, n_pods, results, s);
@@ -599,7 +671,8 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     const bool tp = KW == (uint32_t)kPpWords && tail_pods(n_groups, W) != 0u;
 #define MS_PP_LAUNCH(KWV, TPV)                                                                                     \
     hipExtLaunchKernelGGL((k_sweep_nunn_pp<KWV, TPV>), grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes, t.gcap, \
-                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc, j2)
+                          n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc, j2, \
+                          fix_ok)
     if (KW == (uint32_t)kPpWordsSmall) {
         MS_PP_LAUNCH(kPpWordsSmall, false);
     } else {

@@ -165,6 +165,36 @@ def test_nunn_edge_cases(oracle):
         assert e.info().present_nodes == 5000
 
 
+@pytest.mark.parametrize("node_base", [0, 7, 33_333, 999_990])
+@pytest.mark.parametrize("layout", ["aligned", "one_misaligned", "names", "sparse"])
+def test_fixed_slot_form(oracle, node_base, layout):
+    # K1's fixed-slot form (ms_sweep_pp.hip word_fix): waves whose groups are
+    # digit-aligned (digit == ordinal mod 10 for every present digit-named row)
+    # take three known slots per pod; a single misaligned group sends its wave
+    # back to the slot search. Shard offsets not divisible by 10 move the slots
+    # (node_base mod 10), non-digit node names and pods, unschedulable rows,
+    # tolerations and tombstones keep their meaning; every layout equals the oracle.
+    n = 40_000 if node_base < 999_000 else 1_000
+    nr = synth.nodes(n, seed=11, start=node_base)
+    pr = synth.pods(3001, seed=11)
+    pr["name_digit"][::13] = -1
+    pr["tolerates_unschedulable"][::5] = 1
+    rng = np.random.default_rng(node_base + len(layout))
+    if layout == "one_misaligned":
+        nr["name_digit"][12_345 % n] = (nr["name_digit"][12_345 % n] + 1) % 10
+    elif layout == "names":  # non-digit names stay aligned (they never match)
+        nr["name_digit"][rng.integers(0, n, n // 7)] = 0xFF
+    elif layout == "sparse":  # most rows deleted: groups with one or two present rows
+        nr["allowed_pods"][rng.random(n) < 0.9] = -1
+    o = oracle.schedule(nr, pr, seed=11, node_base=node_base)
+    with engine_with(nr, seed=11, node_base=node_base) as e:
+        if layout == "sparse":
+            gone = np.flatnonzero(nr["allowed_pods"] < 0) + node_base
+            e.delete(gone.astype(np.uint32))
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+    assert (o["code"] == 0).sum() > 0
+
+
 def test_config_b_exact_sequential(oracle):
     # BASELINE config B: 5k nodes x 10k pods, NU+NN, exact sequential
     nr = synth.nodes(5000, seed=1)
