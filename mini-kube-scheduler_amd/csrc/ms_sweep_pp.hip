@@ -144,8 +144,8 @@ __device__ __forceinline__ uint32_t word_scan(uint32_t m, uint32_t hbA) {
     return h;
 }
 
-// base10: node_base mod 10 (the fixed slots; 0 when unused).
-__device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info, uint32_t base10 = 0) {
+// info: the pod entry's class bits (pod_entry), the fixed slot p0 in bits 16-20.
+__device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info) {
     Pod q;
     q.A = A;
     q.s0 = (info & 1u) ? ~0u : 0u;
@@ -153,11 +153,10 @@ __device__ __forceinline__ Pod pod_bits(uint32_t A, uint32_t info, uint32_t base
     q.s2 = (info & 4u) ? ~0u : 0u;
     q.s3 = (info & 8u) ? ~0u : 0u;
     q.tol = (info & 16u) ? ~0u : 0u;
-    const uint32_t d = info & 15u;
-    const bool dig = d <= 9u;
-    q.p0 = dig ? (d + 10u - base10) % 10u : 30u;
-    q.p1 = dig ? q.p0 + 10u : 30u;
-    q.p2 = dig ? q.p0 + 20u : 30u;
+    q.p0 = (info >> 16) & 31u;  // (30 for a non-digit pod: p1 = p2 = 30 too)
+    const uint32_t step = q.p0 < 10u ? 10u : 0u;
+    q.p1 = q.p0 + step;
+    q.p2 = q.p1 + step;
     q.A0 = A + q.p0 * kG24;
     q.A1 = q.A0 + 10u * kG24;
     q.A2 = q.A0 + 20u * kG24;
@@ -230,15 +229,18 @@ __device__ __forceinline__ u64 pod_slow(const Word (&W)[KW], const Word &Wt, boo
 
 // Pod p of a workgroup's chunk as the prologue leaves it in LDS: x = A =
 // tb_pod(seed32, ordinal), y = class bits (digit, 14 for a non-digit name, |
-// tolerates << 4) | name digit byte << 8.
+// tolerates << 4) | name digit byte << 8 | the fixed slot p0 << 16 ((digit -
+// node_base) mod 10, 30 for a non-digit name: word_fix).
 // pstride: bytes per pod record (sizeof(ms_pod_rec), or 8 for ms_pod_compact,
 // its first 8 bytes).
 __device__ __forceinline__ uint2 pod_entry(const ms_pod_rec *__restrict__ pods, uint32_t p, uint32_t seed32,
-                                           uint32_t pstride) {
+                                           uint32_t pstride, uint32_t base10) {
     const uint2 pr = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(pods) + (size_t)p * pstride);
     const int dig = (int)(int8_t)(pr.y & 0xFFu);
-    const uint32_t info = ((uint32_t)dig <= 9u ? (uint32_t)dig : 14u) | (((pr.y >> 8) & 0xFFu) ? 16u : 0u);
-    return make_uint2(tb_pod(seed32, pr.x), info | ((pr.y & 0xFFu) << 8));
+    const bool isd = (uint32_t)dig <= 9u;
+    const uint32_t info = (isd ? (uint32_t)dig : 14u) | (((pr.y >> 8) & 0xFFu) ? 16u : 0u);
+    const uint32_t p0 = isd ? ((uint32_t)dig + 10u - base10) % 10u : 30u;
+    return make_uint2(tb_pod(seed32, pr.x), info | ((pr.y & 0xFFu) << 8) | (p0 << 16));
 }
 
 // One wave sweeps the chunk's pods [0, np) through its NW words into lds[p].
@@ -257,25 +259,24 @@ constexpr int kModeFast = 0, kModeGen = 1, kModeFix = 2;
 
 template <int KW, int NW, int MODE, bool TAIL>
 __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt, uint32_t tpt, uint32_t tshare,
-                                            uint32_t tidx, const uint2 *pinfo, uint32_t np, uint32_t lane, u64 *lds,
-                                            uint32_t base10) {
+                                            uint32_t tidx, const uint2 *pinfo, uint32_t np, uint32_t lane, u64 *lds) {
     constexpr bool GEN = MODE == kModeGen;
     const uint32_t seg_shift = tpt == 8u ? 3u : tpt == 4u ? 4u : 5u;  // log2(64 / tpt)
     for (uint32_t pb = 0; pb < np; pb += 64) {
         const uint32_t nblk = min(64u, np - pb);
         // the block's pods, one per lane: A and digit | tolerates << 4
-        uint32_t a_l = 0, info_l = 14u;
+        uint32_t a_l = 0, info_l = 14u | (30u << 16);  // (lanes past the block: no row matches)
         if (lane < nblk) {
             const uint2 e = pinfo[pb + lane];
             a_l = e.x;
-            info_l = e.y & 0xFFu;
+            info_l = e.y;
         }
         for (uint32_t j = 0; j < nblk; j += 8) {
             Pod q[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t)
                 q[t] = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
-                                (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)), base10);
+                                (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
             uint32_t r[8];
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
@@ -313,7 +314,7 @@ __device__ __forceinline__ void sweep_range(const Word (&W)[KW], const Word &Wt,
                 redo &= redo - 1ull;
                 const uint32_t t = rev3(l >> 3);
                 const Pod qs = pod_bits((uint32_t)__builtin_amdgcn_readlane((int)a_l, (int)(j + t)),
-                                        (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)), base10);
+                                        (uint32_t)__builtin_amdgcn_readlane((int)info_l, (int)(j + t)));
                 const u64 v = pod_slow<KW, NW, MODE == kModeFix>(W, Wt, TAIL && ((pb + j) >> 3) % tshare == tidx, qs);
                 if (lane == 0 && v) atomicMax(&lds[pb + j + t], v);
             }
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
         lds[i] = 0;
-        pinfo[i] = pod_entry(pods, pbeg + i, seed32, pstride);
+        pinfo[i] = pod_entry(pods, pbeg + i, seed32, pstride, node_base % 10u);
     }
 
     // the wave's groups, dealt round-robin over the workgroup's waves so their
@@ -448,14 +449,13 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const bool gen = __ballot(over) != 0;
     // every word of the wave digit-aligned (MINISCHED_PP_FIX=0 at launch: never)
     const int mode = gen ? kModeGen : (fix_ok && __ballot(misaligned) == 0) ? kModeFix : kModeFast;
-    const uint32_t base10 = node_base % 10u;
     __syncthreads();
     if (np && (nw || tpt)) {
         switch (nw * 6 + mode * 2 + (tpt ? 1 : 0)) {  // wave-uniform
 #define MS_PP_CASE1(N, M, T)                                                                                     \
     case 6 * N + 2 * M + T:                                                                                      \
         if constexpr (N <= KW && (N > 0 || T))                                                                   \
-            sweep_range<KW, (N <= KW ? N : KW), M, T>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds, base10); \
+            sweep_range<KW, (N <= KW ? N : KW), M, T>(W, Wt, tpt, tshare, wv - wv_t, pinfo, np, lane, lds);         \
         break;
 #define MS_PP_CASE(N)        \
     MS_PP_CASE1(N, 0, false) \
@@ -635,6 +635,13 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // near 2k) it was 1.3% slower, at 12.5k rows x 800k pods (784) 1.6% faster
     // (profiles/r02zb_ab_chunk_half.jsonl).
     if (32u / W > 1u && chunk_for(std::max(1u, 16u / W)) <= 1024u) chunk = chunk_for(std::max(1u, 16u / W));
+    // Workgroups of at most 8 waves (shards up to 61,440 rows): at most 56 pods each
+    // with the fixed-slot form, whose shorter words leave the per-8-pod reduction
+    // and the scalar pod work exposed at 4 waves per SIMD; more, smaller
+    // workgroups hide them (100k pods: 12.5k rows 44.3 -> 43.7 us, 25k 73.3 -> 71.0,
+    // 50k 133.0 -> 127.0; 50k x 1M pods neutral; 16-wave workgroups lose,
+    // profiles/r04n_shard_shapes.txt, r04o_d_chunk.txt).
+    if (!small && W <= 8u) chunk = std::min(chunk, 56u);
     if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
     const uint32_t nblk1 = cdiv(n_pods, chunk);
