@@ -635,13 +635,11 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // near 2k) it was 1.3% slower, at 12.5k rows x 800k pods (784) 1.6% faster
     // (profiles/r02zb_ab_chunk_half.jsonl).
     if (32u / W > 1u && chunk_for(std::max(1u, 16u / W)) <= 1024u) chunk = chunk_for(std::max(1u, 16u / W));
-    // Workgroups of at most 8 waves (shards up to 61,440 rows): at most 56 pods each
-    // with the fixed-slot form, whose shorter words leave the per-8-pod reduction
-    // and the scalar pod work exposed at 4 waves per SIMD; more, smaller
-    // workgroups hide them (100k pods: 12.5k rows 44.3 -> 43.7 us, 25k 73.3 -> 71.0,
-    // 50k 133.0 -> 127.0; 50k x 1M pods neutral; 16-wave workgroups lose,
-    // profiles/r04n_shard_shapes.txt, r04o_d_chunk.txt).
-    if (!small && W <= 8u) chunk = std::min(chunk, 56u);
+    // (Chunks of <= 56 pods for <= 8-wave workgroups sped the shard sweep alone up,
+    // 12.5k rows 44.3 -> 43.7 us, 25k 73.3 -> 71.0, 50k 133.0 -> 127.0, but slowed the
+    // pipelined sharded step, whose collective and decode kernels then interleave with
+    // a multi-round sweep: 74.6 -> 77.7 us at 25k, 136.3 -> 140 at 50k;
+    // profiles/r04n_shard_shapes.txt, r04p_chunk56_probe.json. Not kept.)
     if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
     const uint32_t nblk1 = cdiv(n_pods, chunk);
