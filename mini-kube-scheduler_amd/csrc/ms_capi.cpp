@@ -29,7 +29,7 @@ thread_local std::string g_create_err;
 
 // validator counters: u32[6] (overflow, re-swept tiles, recomputes, pods, speculation misses,
 // list scans), then u64[4] phase cycles in the MS_VSTAMPS diagnostic build
-constexpr size_t kStatsBytes = 128;
+constexpr size_t kStatsBytes = 256;
 
 }  // namespace
 
@@ -757,7 +757,7 @@ int ms_destroy(ms_ctx *c) {
     if (!c) return MS_E_INVAL;
 #ifdef MS_VSTAMPS
     {
-        uint32_t st[32] = {};
+        uint32_t st[64] = {};
         (void)hipSetDevice(c->cfg.device);
         (void)hipStreamSynchronize(c->stream);
         if (hipMemcpy(st, c->d_overflow, kStatsBytes, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -765,12 +765,14 @@ int ms_destroy(ms_ctx *c) {
             std::fprintf(stderr,
                          "MS_VSTAMPS pods=%u slow=%u tile_scans=%u misses=%u recomputes=%u resweeps=%u rounds=%u cycles: prologue=%llu "
                          "group=%llu prologue_loads=%llu slow=%llu rounds=%llu epilogue=%llu first_slow=%llu round_cand=%llu "
-                         "round_claim=%llu | step waves (10 ns): validator=%llu sweep_sum=%llu sweep_waves=%llu\n",
+                         "round_claim=%llu | step waves (10 ns): validator=%llu sweep_sum=%llu sweep_waves=%llu | epilogue "
+                         "parts: counters=%llu compaction=%llu writeback=%llu\n",
                          st[3], st[5], st[6], st[4], st[2], st[1], st[7], (unsigned long long)cy[0], (unsigned long long)cy[1],
                          (unsigned long long)cy[2], (unsigned long long)cy[3], (unsigned long long)cy[4],
                          (unsigned long long)cy[5], (unsigned long long)cy[6], (unsigned long long)cy[7],
                          (unsigned long long)cy[8], (unsigned long long)cy[9], (unsigned long long)cy[10],
-                         (unsigned long long)cy[11]);
+                         (unsigned long long)cy[11], (unsigned long long)cy[12], (unsigned long long)cy[13],
+                         (unsigned long long)cy[14]);
         }
     }
 #endif

@@ -1285,9 +1285,9 @@ __device__ __forceinline__ u64 readlane_u64(u64 v, uint32_t l) {
 // over the batch, land in stats[8..] (u64), printed at ms_destroy.
 #ifdef MS_VSTAMPS
 struct VStamps {
-    u64 prev, acc[9];
+    u64 prev, acc[12];  // [9..11]: epilogue parts (counters, compaction, write-back), stored at stats u64 [12..14]
 };
-#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0, 0, 0, 0}};
+#define MS_VST_DECL VStamps vst = {__builtin_amdgcn_s_memtime(), {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}};
 #define MS_VST(i)                                               \
     do {                                                        \
         __builtin_amdgcn_sched_barrier(0);                      \
@@ -1733,6 +1733,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         atomicAdd(&stats[7], ctr.rounds);
 #endif
     }
+    MS_VST(9);
     // the bound slots (not a dead copy or an untouched stale node), compacted
     // with ballots into bl[], then written back one slot per lane
     uint32_t n_bl = 0;
@@ -1751,6 +1752,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    MS_VST(10);
     for (uint32_t o = lane; o < n_bl; o += 64) {
         const int64_t *r = S.rec[S.bl[o]];
         const uint32_t row = (uint32_t)r[F_ROW];
@@ -1767,6 +1769,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     if (lane == 0) S.n_out = n_bl;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    MS_VST(11);
     if (prev_out) {
         // carried: the previous batch's own binds that this batch did not bind again
         const uint32_t n_own = S.n_out;
@@ -1784,8 +1787,10 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     }
 #ifdef MS_VSTAMPS
     MS_VST(5);
-    if (lane == 0)
+    if (lane == 0) {
         for (int i = 0; i < 9; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i, vst.acc[i]);
+        for (int i = 9; i < 12; ++i) atomicAdd(reinterpret_cast<u64 *>(stats + 8) + i + 3, vst.acc[i]);
+    }
 #endif
 }
 
