@@ -614,8 +614,13 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // 16-wave workgroups (the groups are dealt round-robin, so every wave holds
     // 3 or 4 words), shards of 257..2048 groups at least 4 waves
     // (profiles/r02c_ab.json, r02j_ab_shard_waves.jsonl)
+    // Shards needing exactly 2 waves (257..512 groups) keep 2: with the fixed-slot
+    // form's shorter words the 4-wave split (2, 2, 2, 1 words at 12.5k rows) paid the
+    // per-8-pod reduction twice as often; the pipelined G = 8 step went 46.1 -> 43.9 us
+    // (profiles/r04t_g8_w2.txt; the slot-search form was 53.7 -> 53.0, r04f).
     uint32_t W = 1;
-    if (waves_needed > 1)
+    if (waves_needed == 2) W = 2;
+    else if (waves_needed > 1)
         while (W < std::max(4u, waves_needed) && W < (uint32_t)kPpMaxWaves) W *= 2;
     if (const char *w = getenv("MINISCHED_PP_WAVES")) W = (uint32_t)std::min(16, std::max(1, atoi(w)));
     if (!keys) W = std::max(W, std::min<uint32_t>(kPpMaxWaves, waves_needed));  // no scratch: one workgroup per chunk
