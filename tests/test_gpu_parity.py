@@ -195,6 +195,25 @@ def test_fixed_slot_form(oracle, node_base, layout):
     assert (o["code"] == 0).sum() > 0
 
 
+@pytest.mark.parametrize("n_nodes,layout", [(7_711, "aligned"), (12_500, "aligned"), (15_360, "aligned"),
+                                             (12_500, "misaligned"), (12_500, "overfull")])
+def test_two_wave_shards(oracle, n_nodes, layout):
+    # 257..512 row groups take 2-wave workgroups (ms_sweep_pp.hip geometry): the
+    # G = 8 shard of config C (12,500 rows) and the bounds of the range, with the
+    # fixed-slot form, the slot search (one misaligned row) and the bit-scan
+    # loop (more than 3 rows of a digit in a group).
+    nr = synth.nodes(n_nodes, seed=21, start=87_500)
+    if layout == "misaligned":
+        nr["name_digit"][6_001] = (nr["name_digit"][6_001] + 3) % 10
+    elif layout == "overfull":
+        nr["name_digit"][3_000:3_030] = 4
+    pr = synth.pods(20_000, seed=21)
+    pr["name_digit"][::11] = -1
+    o = oracle.schedule(nr, pr, seed=21, node_base=87_500)
+    with engine_with(nr, seed=21, node_base=87_500) as e:
+        assert_same(e.schedule(pr, MODE_BATCHED), o)
+
+
 def test_config_b_exact_sequential(oracle):
     # BASELINE config B: 5k nodes x 10k pods, NU+NN, exact sequential
     nr = synth.nodes(5000, seed=1)
