@@ -278,9 +278,57 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     const size_t prev_words = 2 + seq_prev_cap(), prev_fields = (size_t)seq_prev_cap() * seq_rec_fields();
     const size_t cells_per_set = (size_t)SB * n_tiles, recs_per_set = (size_t)SB * seq_topk() * seq_rec_fields();
     const char *pipe_env = getenv("MINISCHED_SEQ_PIPE");
+    if (pipe_env && std::string(pipe_env) == "fused2") {
+        // Single stream, depth 2 (MINISCHED_SEQ_PIPE=fused2, A/B; not the default:
+        // the deeper speculation doubled the recomputes and re-swept 18x the tiles,
+        // 54.9 vs 45.9 ms at config E, 48.2 ms at its best batch of 64,
+        // profiles/r04w_e_fused2_ab.txt). Step k = ONE launch validating batch
+        // k, merging batch k+1 (its tile lists came from step k-1) and sweeping
+        // batch k+2, so no merge launch sits between steps. Batch k's
+        // speculation predates batches k-1 and k-2 (carry: the prev lists hold
+        // both); three tile-list sets (validation k may re-scan its own lists
+        // while sweep k+2 writes), two merge-output sets.
+        auto tiles = [&](uint32_t k, unsigned long long *&tk, uint32_t *&tf) {
+            tk = c->d_tile_keys + cells_per_set * seq_topk() * (k % 3u);
+            tf = c->d_tile_flags + cells_per_set * (k % 3u);
+        };
+        auto out_top = [&](uint32_t k) { return c->d_top4 + (size_t)SB * seq_topk() * (k & 1u); };
+        auto out_ext = [&](uint32_t k) { return top_ext ? top_ext + (size_t)SB * seq_topk() * (k & 1u) : nullptr; };
+        const uint32_t nb0 = std::min(B, n_pods), nb1 = n_pods > B ? std::min(B, n_pods - B) : 0u;
+        unsigned long long *tk = nullptr;
+        uint32_t *tf = nullptr;
+        tiles(0, tk, tf);
+        MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, tk, tf, n_tiles, s));
+        MS_HIP(c, launch_topk_merge(tk, tf, nb0, n_tiles, out_top(0), c->d_spec, c->d_spec_flags, tq, c->d_top4_rec,
+                                    s, out_ext(0)));
+        if (nb1) {
+            tiles(1, tk, tf);
+            MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods + B, nb1, seed32, tk, tf, n_tiles, s));
+        }
+        uint32_t k = 0;
+        for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
+            const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
+            const uint32_t s1 = s0 + B, n1 = s1 < n_pods ? std::min(B, n_pods - s1) : 0u;
+            const uint32_t s2 = s1 + B, n2 = s2 < n_pods ? std::min(B, n_pods - s2) : 0u;
+            unsigned long long *tk0, *tk1, *tk2;
+            uint32_t *tf0, *tf1, *tf2;
+            tiles(k, tk0, tf0);
+            tiles(k + 1, tk1, tf1);
+            tiles(k + 2, tk2, tf2);
+            SeqMerge mg = {tk1, tf1, n1, out_top(k + 1), c->d_spec + SB * nxt, out_ext(k + 1),
+                           c->d_spec_flags + SB * nxt, c->d_top4_rec + recs_per_set * nxt};
+            MS_HIP(c, launch_seq_step(tq, rows, n_tiles, seed32, d_pods + s0, nb, tk0, tf0, c->d_spec + SB * cur,
+                                      c->d_spec_flags + SB * cur, out_top(k), c->d_top4_rec + recs_per_set * cur,
+                                      k ? c->d_prev + prev_words * nxt : nullptr,
+                                      k ? c->d_prev_rec + prev_fields * nxt : nullptr, c->d_prev + prev_words * cur,
+                                      c->d_prev_rec + prev_fields * cur, d_res + s0, c->d_overflow,
+                                      n2 ? d_pods + s2 : nullptr, n2, tk2, tf2, c->num_cus, s, out_ext(k), &mg, 1));
+        }
+        return MS_OK;
+    }
     if (!pipe_env || std::string(pipe_env) == "fused") {
-        // Single stream (default): step k = one launch validating batch k while
-        // sweeping batch k+1 (launch_seq_step), then batch k+1's top-4 merge.
+        // Single stream, depth 1 (default): step k = one launch validating batch
+        // k while sweeping batch k+1 (launch_seq_step), then batch k+1's top-4 merge.
         // No cross-stream hand-off (each cost ~12 us per batch, and a
         // validation launched beside a sweep waited for a SIMD to drain);
         // batch k+1 treats batch k's binds as stale.

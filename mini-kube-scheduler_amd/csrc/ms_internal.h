@@ -235,9 +235,21 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
                                const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
                                ms_result *results, uint32_t *stats, hipStream_t s,
                                const unsigned long long *top_ext = nullptr);
-// One single-stream step: validate batch k (n_pods, carry 0: batch k's sweep
-// ran beside batch k-1's validation) while sweeping batch k+1 (n_next pods,
-// tile lists only; launch_topk_merge follows). Either count may be 0.
+// A merge inside a step (launch_seq_step): batch k+1's tile lists -> its
+// global top-4, speculative winner, flags, records, ranks 4..7 (launch_topk_merge's outputs).
+struct SeqMerge {
+    const unsigned long long *tile_keys;
+    const uint32_t *tile_flags;
+    uint32_t n_pods;
+    unsigned long long *top, *spec, *ext;
+    uint32_t *spec_flags;
+    int64_t *recs;
+};
+// One single-stream step: validate batch k (n_pods) while sweeping the next
+// batch (n_next pods, tile lists only) and, with merge, merging the batch in
+// between (depth 2: carry 1, batch k's speculation predates batches k-1 and
+// k-2). Without merge (depth 1, carry 0), launch_topk_merge follows the step.
+// Any count may be 0.
 hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles, uint32_t seed32,
                            const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *tile_keys,
                            const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
@@ -245,7 +257,8 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s, const unsigned long long *top_ext = nullptr);
+                           hipStream_t s, const unsigned long long *top_ext = nullptr,
+                           const SeqMerge *merge = nullptr, int carry = 0);
 // Node-sharded sequential mode (minisched_gpu.h ms_seq_*): this shard's top-4
 // candidates with records + all-tile filter flags per pod, from the top-4 merge
 // output; and the replicated validation over the shards' gathered lists

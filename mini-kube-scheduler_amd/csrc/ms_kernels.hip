@@ -875,14 +875,12 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
 // gets the batch-start records of the four entries for the in-order validator.
 // ext (optional): ranks 4..7 at ext[p * 4 + r - 4] and the number of certified
 // ranks (4..8) in bits 28-31 of spec_flags (merge_pod_lists).
+// One pod's merge by one wave (k_topk_merge, and k_seq_step's merge workgroups).
 template <int J>
-__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
-                                                   const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
-                                                   uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
-                                                   uint32_t *__restrict__ spec_flags, NodeTable t,
-                                                   int64_t *__restrict__ recs, u64 *__restrict__ ext) {
-    const uint32_t p = blockIdx.x, lane = threadIdx.x;
-    if (p >= n_pods) return;
+__device__ __forceinline__ void merge_pod(const u64 *__restrict__ tile_keys, const uint32_t *__restrict__ tile_flags,
+                                          uint32_t p, uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
+                                          uint32_t *__restrict__ spec_flags, const NodeTable &t,
+                                          int64_t *__restrict__ recs, u64 *__restrict__ ext, uint32_t lane) {
     u64 out;
     uint32_t f, cert = 0;
     if (ext) {
@@ -899,6 +897,28 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
         spec_flags[p] = f | (cert << 28);
     }
 }
+
+template <int J>
+__global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_keys,
+                                                   const uint32_t *__restrict__ tile_flags, uint32_t n_pods,
+                                                   uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
+                                                   uint32_t *__restrict__ spec_flags, NodeTable t,
+                                                   int64_t *__restrict__ recs, u64 *__restrict__ ext) {
+    const uint32_t p = blockIdx.x;
+    if (p >= n_pods) return;
+    merge_pod<J>(tile_keys, tile_flags, p, n_tiles, top, spec, spec_flags, t, recs, ext, threadIdx.x);
+}
+
+// Batch k+1's merge inside step k (the depth-2 fused pipeline, run_sequential):
+// its tile lists were written by step k-1, so the merge workgroups need no wait.
+struct MergeArgs {
+    const u64 *tile_keys;
+    const uint32_t *tile_flags;
+    uint32_t n_pods, n_tiles;
+    u64 *top, *spec, *ext;
+    uint32_t *spec_flags;
+    int64_t *recs;
+};
 
 // ----------------------------------------------------------------------------
 // Exact sequential engine, in-order half: ONE wave walks the batch in queue
@@ -1808,7 +1828,8 @@ __global__ __launch_bounds__(64) void k_validate_seq(SeqArgs va) {
 // which its validation treats as stale (prev lists). W waves per workgroup:
 // the most that fit the validator's VGPRs at one workgroup per CU.
 template <int J, int W>
-__global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks) {
+__global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks, MergeArgs mg,
+                                                     uint32_t merge_wgs) {
     __shared__ SeqShared S;
 #ifdef MS_VSTAMPS  // wave durations (s_memrealtime, 100 MHz): u64 stats[8+9] validator, [8+10] sweep waves, [8+11] their count
     const u64 t_begin = __builtin_amdgcn_s_memrealtime();
@@ -1831,6 +1852,14 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         return;
     }
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    if (blockIdx.x <= merge_wgs) {  // workgroups 1 .. merge_wgs: batch k+1's merge, a pod per wave
+        const uint32_t p = (blockIdx.x - 1) * W + wave;
+        if (p < mg.n_pods)
+            merge_pod<J>(mg.tile_keys, mg.tile_flags, p, mg.n_tiles, mg.top, mg.spec, mg.spec_flags, va.t, mg.recs,
+                         mg.ext, lane);
+        return;
+    }
+    const uint32_t sb = blockIdx.x - 1 - merge_wgs, sg = gridDim.x - 1 - merge_wgs;  // sweep workgroup, count
     if (sw.t.drow && sw.fast) {  // transposed form: a tile per workgroup, its rows in the validator's (idle) LDS
         DRow *rows = reinterpret_cast<DRow *>(&S);
         // Groups outside the binary64 range are taken after the tile loop, listed
@@ -1840,7 +1869,7 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         uint32_t *defer = reinterpret_cast<uint32_t *>(rows + kFullWaveTile) + wave * kTpDeferCap;
         uint32_t nd = 0;
         bool over = false;
-        for (uint32_t tile = blockIdx.x - 1; tile < sw.n_tiles; tile += gridDim.x - 1) {
+        for (uint32_t tile = sb; tile < sw.n_tiles; tile += sg) {
             const uint32_t r = sweep_tp_tile<W>(sw, tile, rows, wave, lane);  // (wave-uniform)
             if (r) {
                 if (nd < kTpDeferCap) defer[nd++] = tile << 16 | r;
@@ -1851,15 +1880,14 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         if (over) {  // (more deferred tiles than the list holds: every group of every tile, exactly)
             uint32_t all = 0;
             for (uint32_t grp = wave, i = 0; grp * kTpPods < sw.n_pods; grp += W, ++i) all |= 1u << i;
-            for (uint32_t tile = blockIdx.x - 1; tile < sw.n_tiles; tile += gridDim.x - 1)
-                sweep_tp_redo<W>(sw, tile, all, wave, lane);
+            for (uint32_t tile = sb; tile < sw.n_tiles; tile += sg) sweep_tp_redo<W>(sw, tile, all, wave, lane);
         }
     } else {
-        for (uint32_t task = (blockIdx.x - 1) * W + wave; task < n_tasks; task += (gridDim.x - 1) * W)
+        for (uint32_t task = sb * W + wave; task < n_tasks; task += sg * W)
             sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
     }
 #ifdef MS_VSTAMPS
-    if (lane == 0 && (blockIdx.x - 1) * W + wave < n_tasks) {
+    if (lane == 0 && sb * W + wave < n_tasks) {
         atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 10, __builtin_amdgcn_s_memrealtime() - t_begin);
         atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 11, 1ull);
     }
@@ -2423,14 +2451,14 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s, const unsigned long long *top_ext) {
-    if (n_pods == 0 && n_next == 0) return hipSuccess;
+                           hipStream_t s, const unsigned long long *top_ext, const SeqMerge *merge, int carry) {
+    if (n_pods == 0 && n_next == 0 && !(merge && merge->n_pods)) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
         (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
         return hipErrorInvalidValue;
     const SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
                         spec,     spec_flags,   top4,    top4_recs,  top_ext, n_tiles, prev_in, prev_recs_in,
-                        prev_out, prev_recs_out, 0,      results,    stats};
+                        prev_out, prev_recs_out, carry,  results,    stats};
     // tasks: (tile, chunk of next pods) pairs, sized to fit one pass of the
     // sweep workgroups (one per CU beside the validator's)
     const uint32_t cus = (uint32_t)(num_cus > 1 ? num_cus : 256);
@@ -2443,8 +2471,18 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     const SweepArgs sw = {t,       n_rows,         next_pods,       n_next,  chunk,
                           seed32,  next_tile_keys, next_tile_flags, n_tiles, seq_fast()};
     const uint32_t n_tasks = n_next ? n_tiles * cdiv(n_next, chunk) : 0u;
-    const uint32_t grid = n_tasks ? 1u + std::min(cus - 1, tp ? n_tiles : cdiv(n_tasks, W)) : 1u;
-#define MS_STEP(JJ, WW) hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks)
+    // merge workgroups (a pod per wave) between the validator's and the sweep's
+    MergeArgs mg = {};
+    uint32_t merge_wgs = 0;
+    if (merge && merge->n_pods) {
+        mg = {merge->tile_keys, merge->tile_flags, merge->n_pods, n_tiles, merge->top, merge->spec, merge->ext,
+              merge->spec_flags, merge->recs};
+        merge_wgs = cdiv(merge->n_pods, W);
+    }
+    const uint32_t room = cus > 1u + merge_wgs ? cus - 1u - merge_wgs : 1u;
+    const uint32_t grid = 1u + merge_wgs + (n_tasks ? std::min(room, tp ? n_tiles : cdiv(n_tasks, W)) : 0u);
+#define MS_STEP(JJ, WW) \
+    hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, mg, merge_wgs)
     if (J == 1) MS_STEP(1, 12);
     else if (J == 2) MS_STEP(2, 12);
     else if (J == 4) MS_STEP(4, 12);

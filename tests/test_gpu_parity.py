@@ -393,12 +393,13 @@ def test_chunked_batches(oracle):
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
 
 
-@pytest.mark.parametrize("pipe", ["fused", "2", "1", "0"])
+@pytest.mark.parametrize("pipe", ["fused2", "fused", "2", "1", "0"])
 @pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
 def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch, pipe):
     # speculative batch boundaries must not change placements: 50 nodes (one
     # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted); the
-    # default single-stream steps (validation k beside the sweep of k+1), and
+    # default single-stream steps (validation k beside the sweep of k+1, merge
+    # launched after; "fused2": beside the merge of k+1 and the sweep of k+2), and
     # two streams with the speculation overlapping two validations (2), one
     # (1) or none (0); 256 is clamped to the validator's 128
     monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
