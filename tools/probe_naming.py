@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""K1 pp at config C on three node-naming layouts.
+"""K1 pp at config C on node-naming layouts (skewed digits).
 
   cycling : node{i} at ordinal i (digit = i % 10, the synthetic default)
   iid     : digits i.i.d. uniform 0..9 (names unrelated to ordinals)
@@ -7,6 +7,8 @@
   iid_allocated : the iid names, ordinals from the digit-aligned allocator
             (encode.DigitOrdinals, the host mirror's OrdinalAllocator) in Add
             order; the table spans the allocator's high-water mark (holes absent)
+  skew_allocated / skew_dense : 70 % of the names end in 0, allocator ordinals
+            (bounded spread) / ordinals in Add order (PROBE_LAYOUTS=a,b selects)
 
 Each: mean device time of the fused single-launch cycle (ms_select_batch_device)
 over K launches, the fraction of 30-row groups whose "over" plane is set (the
@@ -40,7 +42,27 @@ def layouts(n, seed):
     allocated = np.zeros(alloc.high, dtype=base.dtype)
     allocated["allowed_pods"] = -1  # never added: absent from the LIST
     allocated[ords] = iid
-    return {"cycling": base, "iid": iid, "perm": perm, "iid_allocated": allocated}
+    # skewed names (70 % end in 0): the allocator keeps digit-aligned ordinals only
+    # within its bounded spread of the dense frontier, else the lowest free one
+    skew = base.copy()
+    skew["name_digit"] = np.where(rng.random(n) < 0.7, 0, rng.integers(0, 10, n)).astype(np.uint8)
+    alloc2 = encode.DigitOrdinals(2 * n)
+    ords2 = np.array([alloc2.allocate(int(d)) for d in skew["name_digit"]])
+    skew_alloc = np.zeros(alloc2.high, dtype=base.dtype)
+    skew_alloc["allowed_pods"] = -1
+    skew_alloc[ords2] = skew
+    out = {"cycling": base, "iid": iid, "perm": perm, "iid_allocated": allocated, "skew_allocated": skew_alloc,
+           "skew_dense": skew}
+    only = os.environ.get("PROBE_LAYOUTS")
+    return {k: v for k, v in out.items() if not only or k in only.split(",")}
+
+
+def misaligned_frac(nr):
+    """Groups the fixed-slot form cannot take: a present digit-named row whose digit
+    is not its ordinal mod 10."""
+    ok = (nr["allowed_pods"] < 0) | (nr["name_digit"] > 9) | (nr["name_digit"] == np.arange(len(nr)) % 10)
+    g = len(ok) // 30
+    return float((~ok[: g * 30].reshape(g, 30).all(1)).mean())
 
 
 def over_frac(nr):
@@ -85,7 +107,7 @@ def main():
         o = _oracle.schedule_nunn_omp(nr, pr, seed=1, threads=16)
         ok = all(np.array_equal(got[a].astype(np.int64), o[b].astype(np.int64))
                  for a, b in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")))
-        out[name] = {"ms": ms, "rows": rows, "evals_per_s": N * P / (ms * 1e-3), "over_group_frac": over_frac(nr),
+        out[name] = {"ms": ms, "rows": rows, "evals_per_s": N * P / (ms * 1e-3), "over_group_frac": over_frac(nr), "misaligned_group_frac": misaligned_frac(nr),
                      "parity": ok, "oracle_s": time.perf_counter() - t0}
         print(name, json.dumps(out[name]), flush=True)
     print(json.dumps(out))
