@@ -17,7 +17,7 @@
 //   F, the filter flags, the first three and the last feasible node
 //   (c, NodeNumber match, tie-break hash), and per class (c, rank parity) of the
 //   other feasible nodes the best (NodeNumber match, hash) pair;
-// summaries of consecutive segments merge associatively (tt_merge: ranks of
+// summaries of consecutive segments merge associatively (tt_merge_into: ranks of
 // the later segment shift by the earlier one's F), so row segments of one
 // context and node shards of several GPUs combine the same way, and the
 // finalisation (tt_finalize) applies the closed form and selectHost's argmax.
@@ -31,9 +31,13 @@ namespace {
 
 constexpr int kTtClasses = 18;  // c in 0..8 x rank parity
 constexpr uint32_t kTtThreads = 256;   // pods per sweep workgroup (one per lane)
-constexpr uint32_t kTtTile = 2048;     // rows staged in LDS per pass
+#ifndef MS_TT_TILE
+#define MS_TT_TILE 1024
+#endif
+constexpr uint32_t kTtTile = MS_TT_TILE;  // rows staged in LDS per pass (2048 -> 1024: 8.24 -> 6.92 ms at 50k x 100k)
 constexpr uint32_t kTtSegRows = 2048;  // minimum rows per segment
 constexpr uint32_t kTtMaxSegs = 16;
+constexpr uint32_t kTtCombineThreads = 128;  // k_tt_combine: one pod per thread, its running summary in LDS
 
 // Segment summary of one pod (MS_TT_SUMMARY_BYTES). Special entries pack
 // c << 40 | NodeNumber match << 32 | hash; class entries match << 32 | hash.
@@ -57,13 +61,15 @@ __device__ __forceinline__ void cls_put(TtSummary &r, uint32_t c, uint32_t par, 
     r.occ |= 1u << k;
 }
 
-// b follows a in LIST order.
-__device__ __forceinline__ TtSummary tt_merge(const TtSummary &a, const TtSummary &b) {
-    TtSummary r = a;
-    r.n = a.n + b.n;
-    r.flags = a.flags | b.flags;
+// r <- r merged with b, b following r in LIST order (in place: r lives in LDS
+// in k_tt_combine, where its dynamically indexed classes need no scratch).
+__device__ __forceinline__ void tt_merge_into(TtSummary &r, const TtSummary &b) {
+    const uint32_t an = r.n;
+    const u64 alast = r.last;
+    r.n = an + b.n;
+    r.flags |= b.flags;
     // b's classes, their parity shifted by a.n
-    const uint32_t sh = a.n & 1u;
+    const uint32_t sh = an & 1u;
 #pragma unroll
     for (int k = 0; k < kTtClasses; ++k)
         if ((b.occ >> k) & 1u) cls_put(r, (uint32_t)k >> 1, ((uint32_t)k & 1u) ^ sh, b.cls[k]);
@@ -73,11 +79,10 @@ __device__ __forceinline__ TtSummary tt_merge(const TtSummary &a, const TtSummar
         if (g + 1u == r.n) r.last = e;
         if (g >= 3u && g + 1u < r.n) cls_put(r, ent_c(e), g & 1u, ent_key(e));
     };
-    if (a.n > 3u && a.n - 1u >= 3u) place(a.last, a.n - 1u);  // (a's first three kept their ranks)
-    for (uint32_t i = 0; i < 3u && i < b.n; ++i) place(b.first[i], a.n + i);
-    if (b.n > 3u) place(b.last, a.n + b.n - 1u);
-    if (b.n == 0u) r.last = a.last;
-    return r;
+    if (an > 3u) place(alast, an - 1u);  // (a's first three kept their ranks)
+    for (uint32_t i = 0; i < 3u && i < b.n; ++i) place(b.first[i], an + i);
+    if (b.n > 3u) place(b.last, an + b.n - 1u);
+    if (b.n == 0u) r.last = alast;
 }
 
 __device__ __forceinline__ int32_t tt_map(int32_t m, int32_t v) { return m == 0 ? 100 : 100 - (100 * v) / m; }
@@ -168,12 +173,15 @@ __device__ __forceinline__ uint32_t row_word(const NodeTable &t, uint32_t r) {
 }
 
 // grid (pod blocks, segments): lane = pod, rows of the segment streamed through
-// LDS in LIST order; the pod's per-class bests live in LDS (dynamic class index).
+// LDS in LIST order; the pod's per-class best hashes live in LDS (dynamic class
+// index), their NodeNumber match bits in a register.
 __global__ __launch_bounds__(kTtThreads) void k_tt_sweep(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
                                                          const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
                                                          uint32_t seed32, TtSummary *__restrict__ out) {
     __shared__ uint32_t tile[kTtTile];
-    __shared__ u64 cls[kTtClasses][kTtThreads];
+    // per-class best: the hash in LDS, the NodeNumber match bit in a register
+    // (bit k of clsm), so the workgroup's LDS is 22 KB (7 per CU)
+    __shared__ uint32_t clsh[kTtClasses][kTtThreads];
     const uint32_t tid = threadIdx.x;
     const uint32_t p = blockIdx.x * kTtThreads + tid;
     const uint32_t seg = blockIdx.y;
@@ -184,7 +192,7 @@ __global__ __launch_bounds__(kTtThreads) void k_tt_sweep(NodeTable t, uint32_t n
     const uint32_t tolu = pod.tolerates_unschedulable ? 1u : 0u;
     const uint32_t tolh = pod.pref_zone, tols = pod.pref_weight;  // tol_hard / tol_soft (minisched_gpu.h)
     const uint32_t pd = pod.name_digit >= 0 && pod.name_digit <= 9 ? (uint32_t)pod.name_digit : 14u;
-    uint32_t n = 0, flags = 0, occ = 0;
+    uint32_t n = 0, flags = 0, occ = 0, clsm = 0;
     u64 f0 = 0, f1 = 0, f2 = 0, last = 0;
     for (uint32_t base = r0; base < r1; base += kTtTile) {
         const uint32_t nt = min(kTtTile, r1 - base);
@@ -208,8 +216,11 @@ __global__ __launch_bounds__(kTtThreads) void k_tt_sweep(NodeTable t, uint32_t n
             const u64 e = ((u64)c << 40) | ((u64)nn << 32) | tb_hash(A, ord);
             if (n >= 4u) {  // the previous feasible node (rank n-1 >= 3) is not the last: into its class
                 const uint32_t k = 2u * ent_c(last) + ((n - 1u) & 1u);
-                const u64 v = ent_key(last);
-                if (!((occ >> k) & 1u) || v > cls[k][tid]) cls[k][tid] = v;
+                const uint32_t vm = (uint32_t)(last >> 32) & 1u, vh = (uint32_t)last, om = (clsm >> k) & 1u;
+                if (!((occ >> k) & 1u) || vm > om || (vm == om && vh > clsh[k][tid])) {
+                    clsh[k][tid] = vh;
+                    clsm = (clsm & ~(1u << k)) | (vm << k);
+                }
                 occ |= 1u << k;
             }
             f0 = n == 0u ? e : f0;
@@ -229,7 +240,8 @@ __global__ __launch_bounds__(kTtThreads) void k_tt_sweep(NodeTable t, uint32_t n
     o.first[1] = f1;
     o.first[2] = f2;
     o.last = last;
-    for (int k = 0; k < kTtClasses; ++k) o.cls[k] = ((occ >> k) & 1u) ? cls[k][tid] : 0ull;
+    for (int k = 0; k < kTtClasses; ++k)
+        o.cls[k] = ((occ >> k) & 1u) ? ((u64)((clsm >> k) & 1u) << 32 | clsh[k][tid]) : 0ull;
 }
 
 // Per pod: the merge of n_segs summaries in LIST order (segment s at
@@ -238,10 +250,12 @@ __global__ __launch_bounds__(kTtThreads) void k_tt_sweep(NodeTable t, uint32_t n
 __global__ void k_tt_combine(const TtSummary *__restrict__ in, uint32_t stride, uint32_t n_segs,
                              const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t seed32,
                              TtSummary *__restrict__ out, ms_result *__restrict__ results, NodeTable t, int commit) {
+    __shared__ TtSummary acc[kTtCombineThreads];
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pods) return;
-    TtSummary r = in[p];
-    for (uint32_t s = 1; s < n_segs; ++s) r = tt_merge(r, in[(size_t)s * stride + p]);
+    TtSummary &r = acc[threadIdx.x];
+    r = in[p];
+    for (uint32_t s = 1; s < n_segs; ++s) tt_merge_into(r, in[(size_t)s * stride + p]);
     if (out) {
         out[p] = r;
         return;
@@ -280,7 +294,7 @@ hipError_t launch_tt_combine(const void *in, uint32_t stride, uint32_t n_segs, c
                              hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     if (n_segs == 0 || (!out && !results)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_tt_combine, dim3(cdiv(n_pods, 128)), dim3(128), 0, s, static_cast<const TtSummary *>(in), stride,
+    hipLaunchKernelGGL(k_tt_combine, dim3(cdiv(n_pods, kTtCombineThreads)), dim3(kTtCombineThreads), 0, s, static_cast<const TtSummary *>(in), stride,
                        n_segs, pods, n_pods, seed32, static_cast<TtSummary *>(out), results, t, commit);
     return hipGetLastError();
 }
