@@ -19,6 +19,18 @@ __device__ __forceinline__ u64 make_key(uint32_t score, uint32_t h, uint32_t ord
     return ((u64)hi << 32) | lo;
 }
 
+// Full 64-lane sum (the same row_shr / row_bcast scan as wave_max_u32_dpp; an
+// out-of-row source reads 0, the identity); wave-uniform result from lane 63.
+__device__ __forceinline__ uint32_t wave_sum_u32_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Full 64-lane unsigned max; result is wave-uniform (read from lane 63).
 __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1

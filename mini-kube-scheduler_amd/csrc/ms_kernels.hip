@@ -1741,17 +1741,19 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         }
         MS_VST(1);
     }
-    // counters, then every touched node's record goes back to the table
-    if (ctr.recompute) atomicAdd(&stats[2], ctr.recompute);
-    if (lane == 0) {
-        atomicAdd(&stats[1], ctr.resweep);
-        atomicAdd(&stats[3], n_pods);
-        atomicAdd(&stats[4], ctr.miss);
-        atomicAdd(&stats[5], ctr.slow);
-        atomicAdd(&stats[6], ctr.scan);
+    // counters (one atomic instruction: lane i adds counter i + 1; the recomputes
+    // are per lane, the rest wave-uniform), then every touched node's record
+    // goes back to the table
+    {
+        const uint32_t rsum = wave_sum_u32_dpp(ctr.recompute);
+        const uint32_t v = lane == 0 ? ctr.resweep : lane == 1 ? rsum : lane == 2 ? n_pods : lane == 3 ? ctr.miss
+                           : lane == 4 ? ctr.slow : lane == 5 ? ctr.scan : lane == 6 ? ctr.rounds : 0u;
 #ifdef MS_VSTAMPS
-        atomicAdd(&stats[7], ctr.rounds);
+        constexpr uint32_t kCounters = 7;
+#else
+        constexpr uint32_t kCounters = 6;
 #endif
+        if (lane < kCounters && v) atomicAdd(&stats[1 + lane], v);
     }
     MS_VST(9);
     // the bound slots (not a dead copy or an untouched stale node), compacted
