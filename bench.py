@@ -87,9 +87,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the e2e measurements and configs B, D, E")
     ap.add_argument("--no-configs", action="store_true", help="skip configs B, D, E (device + CPU baselines)")
-    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r04r_pmc_C.json"),
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r04z_pmc_C.json"),
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
-    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r04r_pmc_E.json"),
+    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r04z_pmc_E.json"),
                     help="rocprofv3 counter summary of config E's step kernel (tools/profile_e.sh)")
     return ap.parse_args()
 
