@@ -400,7 +400,13 @@ int ms_comm_init(ms_ctx *ctx, const ms_comm_id *id, int32_t rank, int32_t world)
  * Every rank submits the same batches in the same order. No binds are
  * committed (stateless: NU+NN, NodeAffinity, TaintToleration; for the
  * resource-aware set each batch sees the state of its submit). Deltas and
- * binds issued meanwhile wait for the sweeps in flight. */
+ * binds issued meanwhile wait for the sweeps in flight. For MS_PLUGINS_NU_NN
+ * two consecutive submits on one stream share ONE sweep launch: a submission's
+ * sweep may be enqueued only by the next submit (or by a drain, a node delta
+ * flush or any other call on the context, which sweep it alone first), so
+ * the stream carries its work only after that call; its collective and the
+ * order of collectives are unchanged (MINISCHED_SHARD_COALESCE=0: one launch
+ * per submit). */
 int ms_sharded_slice(const ms_ctx *ctx, uint32_t n_pods, uint32_t *first, uint32_t *count);
 int ms_sharded_submit(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, ms_result *results_dev,
                       void *stream);
