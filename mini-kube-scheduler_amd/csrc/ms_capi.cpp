@@ -620,11 +620,13 @@ int ensure_zc(ms_ctx *c, uint32_t n) {
 // 0.59 ms at config C (the blocking D2H alone ~0.42 ms of host time) and once
 // took 7.3 ms (BENCH_r03 e2e.runs[4]; the A/B rerun caught a 6.7 ms pageable
 // H2D in the call's stage_in phase, profiles/r04b_e2e_zc_ab.txt);
-// MINISCHED_PAGEABLE_E2E=1 restores them (A/B). Chunks: one per 128k pods, at
-// most 4 (config C's 100k pods: one; 4 chunks of 25k pods cost as much kernel
-// time as their overlap saved, 0.448 vs 0.451 ms, and 0.402 vs 0.370 ms for
-// compact records). MINISCHED_ZC_PARTS overrides the chunk count (1..4).
-constexpr uint32_t kZcMinChunk = 131072;
+// MINISCHED_PAGEABLE_E2E=1 restores them (A/B). Chunks: one per 50k pods, at
+// most 4. With the fixed-slot K1 (shorter kernels) config C's 100k pods in 2
+// chunks overlap the host copies: 0.320 vs 0.328 ms compact, 0.362 vs 0.403 ms
+// with 40/24-B records (profiles/r04zb_zc_parts.txt; 3 chunks 0.325 / 0.364;
+// round 3, slot-search K1: 4 chunks of 25k cost as much kernel time as their
+// overlap saved). MINISCHED_ZC_PARTS overrides the chunk count (1..4).
+constexpr uint32_t kZcMinChunk = 50000;
 template <typename PodIn, typename ResOut>
 int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock &ck) {
     static_assert(sizeof(ms_pod_compact) <= sizeof(PodIn), "compact pod = the first 8 B of a pod record");
