@@ -1,7 +1,8 @@
 """Randomised parity: clusters and pod queues far from the synthetic configs.
 
 Each case draws a cluster from its own seeded generator: digit layouts that
-cycle, are i.i.d. or use two digits only (the K1 bit-scan path), nodes
+cycle, follow the ordinal (K1's fixed-slot form), are i.i.d. or use two digits
+only (the K1 bit-scan path), nodes
 without a name digit, unschedulable fractions up to 60 %, tiny pod caps,
 capacities from 0 to 2^48 (the int64 LeastAllocated form above 2^41),
 pre-existing Requested up to 1.5x Allocatable, tombstoned nodes; pods with
@@ -10,6 +11,8 @@ tolerations. The HIP path (through the C ABI) must equal the oracle pod by pod,
 and after sequential binds the node table must equal the oracle's columns.
 A failure names its case; the case index is the generator seed.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -29,15 +32,17 @@ def need_gpu():
         pytest.fail("gpu test collected on a host without a visible device")
 
 
-def rand_nodes(rng, n, resources):
+def rand_nodes(rng, n, resources, base=0):
     rec = np.zeros(n, dtype=NODE_REC)
-    layout = rng.integers(0, 3)
+    layout = rng.integers(0, 4)
     if layout == 0:
         d = np.arange(n) % 10
     elif layout == 1:
         d = rng.integers(0, 10, n)
-    else:
+    elif layout == 2:
         d = rng.choice(rng.integers(0, 10, 2), n)
+    else:  # digit = ordinal mod 10 (the allocator's layout: K1's fixed-slot form)
+        d = (base + np.arange(n)) % 10
     d = np.where(rng.random(n) < 0.05, 0xFF, d)
     rec["name_digit"] = d.astype(np.uint8)
     rec["unschedulable"] = (rng.random(n) < rng.random() * 0.6).astype(np.uint8)
@@ -117,12 +122,12 @@ def test_fuzz_resource_batched(oracle, case):
         assert_same(e.schedule(pr, MODE_BATCHED), o)
 
 
-@pytest.mark.parametrize("case", range(48))
+@pytest.mark.parametrize("case", range(int(os.environ.get("MINISCHED_FUZZ_NUNN", "48"))))  # (extended runs: more)
 def test_fuzz_nunn(oracle, case):
     rng = np.random.default_rng(3000 + case)
     n, p = int(rng.integers(1, 40_000)), int(rng.integers(1, 3000))
     base = int(rng.integers(0, 1 << 19))
-    nr, pr = rand_nodes(rng, n, False), rand_pods(rng, p, False)
+    nr, pr = rand_nodes(rng, n, False, base), rand_pods(rng, p, False)
     seed = int(rng.integers(0, 1 << 40))
     cols = oracle.NodeCols(nr)
     with engine_with(nr, seed=seed, node_base=base) as e:
