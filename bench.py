@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip configs B, D, E (device + CPU baselines)")
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r04z_pmc_C.json"),
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
+    ap.add_argument("--profile-shard-prefix", default=os.path.join(ROOT, "profiles", "r04zh_pmc_shard"),
+                    help="N > 1: per-shard K1 counters <prefix><rows>.json (tools/profile_shards.sh)")
     ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r04z_pmc_E.json"),
                     help="rocprofv3 counter summary of config E's step kernel (tools/profile_e.sh)")
     return ap.parse_args()
@@ -556,7 +558,9 @@ def main():
         value = float(P) * float(N) * args.steps / elapsed
         algo_bytes = kernel_evals * BYTES_PER_EVAL[plugins]
         kernel_s = kernel_ms * 1e-3
-        pj = load_profile(args.profile_json, hi - lo, P) if world == 1 else None
+        # N > 1: this rank's shard sweep, counters of the same shard shape (tools/profile_shards.sh)
+        prof_path = args.profile_json if world == 1 else f"{args.profile_shard_prefix}{hi - lo}.json"
+        pj = load_profile(prof_path, hi - lo, P)
         valu = pj.get("SQ_INSTS_VALU") if pj else None
         traffic = pj.get("hbm_bytes_per_launch") if pj else None
         roofline = {
@@ -578,7 +582,7 @@ def main():
             "kernel_ms_rocprof": (pj.get("kernel_avg_ns_rocprof") or 0) * 1e-6 if pj else None,
             "valu_insts_per_launch": valu,
             "lane_valu_per_pair": valu * 64 / kernel_evals if valu else None,
-            "profile": os.path.relpath(args.profile_json, ROOT) if pj else None,
+            "profile": os.path.relpath(prof_path, ROOT) if pj else None,
             "hbm": {
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "algorithmic_GBps": algo_bytes / kernel_s / 1e9,
