@@ -191,7 +191,10 @@ int ms_get_info(const ms_ctx *ctx, ms_info *out);
 /* Host-side phase times of the last ms_schedule_batch / ms_schedule_batch_compact
  * call on ctx (diagnostics: where a slow host call spent its wall time). ns[]
  * is indexed by MS_PH_*; every phase is host wall time inside the call, and
- * the phases sum to ns[MS_PH_TOTAL] up to the bookkeeping between them. */
+ * the phases sum to ns[MS_PH_TOTAL] up to the bookkeeping between them.
+ * Thread-safe like the other entry points: it takes the scheduling lock, so
+ * it waits for a call in progress on another thread and never returns a
+ * partly written profile. */
 #define MS_CALL_PHASES 8
 enum {
     MS_PH_TOTAL = 0,      /* the whole call                                            */

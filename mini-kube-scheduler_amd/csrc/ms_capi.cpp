@@ -66,13 +66,15 @@ void free_all(ms_ctx *c) {
         if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
     }
     if (c->ev_seq) (void)hipEventDestroy(c->ev_seq);
+    if (c->ev_tt) (void)hipEventDestroy(c->ev_tt);
     if (c->copy_stream) {
         (void)hipStreamSynchronize(c->copy_stream);
         (void)hipStreamDestroy(c->copy_stream);
-        for (int i = 0; i < 4; ++i) {
-            if (c->ev_copy[i]) (void)hipEventDestroy(c->ev_copy[i]);
-            if (c->ev_cyc[i]) (void)hipEventDestroy(c->ev_cyc[i]);
-        }
+    }
+    // (the zero-copy path creates ev_cyc without a copy stream)
+    for (int i = 0; i < 4; ++i) {
+        if (c->ev_copy[i]) (void)hipEventDestroy(c->ev_copy[i]);
+        if (c->ev_cyc[i]) (void)hipEventDestroy(c->ev_cyc[i]);
     }
     if (c->seq_stream) {
         (void)hipStreamSynchronize(c->seq_stream);
@@ -439,6 +441,9 @@ int tt_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *
     const uint32_t B = c->batch_cap, segs = tt_segments(c->rows_dev);
     int rc = ensure_tt(c, std::min(B, n_pods));
     if (rc) return rc;
+    if (!c->ev_tt) MS_HIP(c, hipEventCreateWithFlags(&c->ev_tt, hipEventDisableTiming));
+    // the previous cycle's sweep/combine on another stream still owns d_tt
+    if (c->tt_stream && c->tt_stream != s) MS_HIP(c, hipStreamWaitEvent(s, c->ev_tt, 0));
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
@@ -447,6 +452,8 @@ int tt_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *
                                     out ? static_cast<char *>(out) + (size_t)s0 * MS_TT_SUMMARY_BYTES : nullptr,
                                     out ? nullptr : results + s0, c->t, commit, s));
     }
+    MS_HIP(c, hipEventRecord(c->ev_tt, s));
+    c->tt_stream = s;
     return MS_OK;
 }
 
@@ -547,16 +554,25 @@ uint32_t e2e_chunks(uint32_t n) {
     return std::max(1u, std::min(k, n / kE2eMinChunk));
 }
 
+// The per-chunk events of the host-array paths, each created once whichever
+// path (zero-copy or chunked copies) runs first (no leak when a
+// context switches paths); copies: also the copy-stream events.
+int ensure_chunk_events(ms_ctx *c, bool copies) {
+    for (int i = 0; i < 4; ++i) {
+        if (!c->ev_cyc[i]) MS_HIP(c, hipEventCreateWithFlags(&c->ev_cyc[i], hipEventDisableTiming));
+        if (copies && !c->ev_copy[i]) MS_HIP(c, hipEventCreateWithFlags(&c->ev_copy[i], hipEventDisableTiming));
+    }
+    return MS_OK;
+}
+
 int schedule_chunked(ms_ctx *c, const ms_pod_rec *pods, uint32_t n, ms_result *out, uint32_t parts, CallClock &ck) {
     const hipStream_t s = c->stream;
     if (!c->copy_stream) {
         MS_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-        for (int i = 0; i < 4; ++i) {
-            MS_HIP(c, hipEventCreateWithFlags(&c->ev_copy[i], hipEventDisableTiming));
-            MS_HIP(c, hipEventCreateWithFlags(&c->ev_cyc[i], hipEventDisableTiming));
-        }
         ck.lap(MS_PH_ALLOC);
     }
+    int erc = ensure_chunk_events(c, true);
+    if (erc) return erc;
     const hipStream_t cs = c->copy_stream;
     const uint32_t per = cdiv(n, parts);
     auto beg = [&](uint32_t i) { return std::min(n, i * per); };
@@ -633,9 +649,8 @@ int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock
     const hipStream_t s = c->stream;
     int rc = ensure_zc(c, n);
     if (rc) return rc;
-    if (!c->ev_cyc[0]) {
-        for (int i = 0; i < 4; ++i) MS_HIP(c, hipEventCreateWithFlags(&c->ev_cyc[i], hipEventDisableTiming));
-    }
+    rc = ensure_chunk_events(c, false);
+    if (rc) return rc;
     ck.lap(MS_PH_ALLOC);
     MS_HIP(c, hipStreamSynchronize(s));  // (no earlier call still reads h_podz)
     ck.lap(MS_PH_WAIT);
@@ -835,6 +850,9 @@ const char *ms_last_error(const ms_ctx *c) { return c ? c->err.c_str() : g_creat
 
 int ms_last_call_profile(const ms_ctx *c, ms_call_profile *out) {
     if (!valid_ctx(c) || !out) return MS_E_INVAL;
+    // CallClock writes prof under sched_mu while a call runs: read it under the
+    // same lock, so a concurrent reader never sees a torn profile
+    std::lock_guard<std::mutex> g(const_cast<ms_ctx *>(c)->sched_mu);
     for (int i = 0; i < MS_CALL_PHASES; ++i) out->ns[i] = c->prof[i];
     return MS_OK;
 }

@@ -86,6 +86,12 @@ struct ms_ctx {
     // MS_PLUGINS_NU_TT_NN: segment summaries of the sweep (tt_bytes allocated)
     void *d_tt = nullptr;
     size_t tt_bytes = 0;
+    // d_tt is one scratch for every TT cycle of the context: a cycle on another
+    // stream than the previous one waits for ev_tt, recorded after that one's
+    // combine (node-sharded submits run on caller / sweep streams that are not
+    // chained through the context stream)
+    hipEvent_t ev_tt = nullptr;
+    hipStream_t tt_stream = nullptr;
     // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
     ms_seq_cand *d_merged = nullptr;
     uint32_t *d_merged_flags = nullptr;

@@ -12,6 +12,11 @@ Only the fields the in-scope plugins read cross the boundary:
                   topology.kubernetes.io/zone label and the pod's one preferred
                   NodeAffinity term {weight, zone In [value]}, as value ids that
                   one ZoneIds table assigns on both sides (0 = none).
+  * taints / tol_hard, tol_soft — MS_PLUGINS_NU_TT_NN: the node's Spec.Taints
+                  as taint ids that one TaintIds table assigns (at most 8
+                  NoSchedule/NoExecute and 8 PreferNoSchedule taints in the
+                  cluster), and per pod the ids some toleration tolerates
+                  (Toleration.ToleratesTaint, restated below).
 Quantities are already integers here: cpu in millicores, memory in bytes.
 """
 from __future__ import annotations
@@ -26,6 +31,9 @@ from ._lib import NODE_REC, POD_REC
 TAINT_NODE_UNSCHEDULABLE = "node.kubernetes.io/unschedulable"
 ZONE_LABEL = "topology.kubernetes.io/zone"
 TAINT_EFFECT_NO_SCHEDULE = "NoSchedule"
+TAINT_EFFECT_NO_EXECUTE = "NoExecute"
+TAINT_EFFECT_PREFER_NO_SCHEDULE = "PreferNoSchedule"
+TAINT_IDS_PER_KIND = 8  # ms_node_rec.taints: bits 0-7 hard, 8-15 PreferNoSchedule
 DEFAULT_MILLI_CPU_REQUEST = 100
 DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
 
@@ -36,6 +44,13 @@ def name_digit(name: str) -> int:
         raise ValueError("empty object name (the reference would panic slicing name[-1:])")
     c = name[-1]
     return ord(c) - 48 if "0" <= c <= "9" else -1
+
+
+@dataclass(frozen=True)
+class Taint:
+    key: str
+    value: str = ""
+    effect: str = TAINT_EFFECT_NO_SCHEDULE
 
 
 @dataclass
@@ -88,6 +103,76 @@ class Node:
     unschedulable: bool = False
     allocatable: Dict[str, int] = field(default_factory=dict)  # cpu (milli), memory (bytes), pods
     labels: Dict[str, str] = field(default_factory=dict)
+    taints: List[Taint] = field(default_factory=list)
+
+
+class TaintIds:
+    """Taint -> id, shared by node and pod encoding (the shim's map for
+    MS_PLUGINS_NU_TT_NN, minisched_gpu.h). Filter taints (NoSchedule and
+    NoExecute: TaintToleration.Filter's filterPredicate) take ids 0..7 in
+    ms_node_rec.taints bits 0-7; PreferNoSchedule taints (the ones Score counts,
+    countIntolerableTaintsPreferNoSchedule) take ids 0..7 in bits 8-15. A taint
+    is identified by (key, value, effect): Toleration.ToleratesTaint reads
+    exactly those three. A ninth taint of one kind raises OverflowError: the
+    device form (and the closed form of the in-loop reverse normaliser, whose
+    raw counts must stay <= 8) holds no more, so such a cluster must not be
+    scheduled with this plugin set. Taints with any other effect are ignored
+    by both plugins and get no id. (k8s@v1.22.0
+    plugins/tainttoleration/taint_toleration.go, restated.)"""
+
+    def __init__(self):
+        self.hard: Dict[Taint, int] = {}
+        self.soft: Dict[Taint, int] = {}
+
+    def id_of(self, t: Taint) -> Tuple[Optional[str], int]:
+        """("hard" | "soft" | None, id) of taint t, assigning a new id on first sight."""
+        if t.effect in (TAINT_EFFECT_NO_SCHEDULE, TAINT_EFFECT_NO_EXECUTE):
+            table, kind = self.hard, "hard"
+        elif t.effect == TAINT_EFFECT_PREFER_NO_SCHEDULE:
+            table, kind = self.soft, "soft"
+        else:
+            return None, -1
+        if t not in table:
+            if len(table) >= TAINT_IDS_PER_KIND:
+                raise OverflowError(f"more than {TAINT_IDS_PER_KIND} distinct {kind} taints in the cluster: "
+                                    "MS_PLUGINS_NU_TT_NN cannot encode it")
+            table[t] = len(table)
+        return kind, table[t]
+
+    def node_bits(self, taints: List[Taint]) -> int:
+        """ms_node_rec.taints of a node's Spec.Taints. Taints are unique per
+        (key, effect) on a node (API validation), so bit counts equal entry
+        counts; a duplicate raises."""
+        seen = set()
+        bits = 0
+        for t in taints:
+            if (t.key, t.effect) in seen:
+                raise ValueError(f"duplicate taint {t.key}:{t.effect} on one node (API validation)")
+            seen.add((t.key, t.effect))
+            kind, i = self.id_of(t)
+            if kind == "hard":
+                bits |= 1 << i
+            elif kind == "soft":
+                bits |= 1 << (8 + i)
+        return bits
+
+    def pod_masks(self, tolerations: List["Toleration"]) -> Tuple[int, int]:
+        """(tol_hard, tol_soft): bit t set when some toleration tolerates taint
+        id t. Filter: FindMatchingUntoleratedTaint over the hard taints with all
+        tolerations. Score: the tolerations with an empty or PreferNoSchedule
+        effect (getAllTolerationPreferNoSchedule) against the PreferNoSchedule
+        taints; ToleratesTaint's own effect check makes that prefilter a no-op.
+        Pods must be encoded after every node of the cluster (the ids a pod's
+        masks refer to are the ones assigned so far)."""
+        hard = soft = 0
+        for t, i in self.hard.items():
+            if any(toleration_tolerates(x, t.key, t.value, t.effect) for x in tolerations):
+                hard |= 1 << i
+        pref = [x for x in tolerations if x.effect in ("", TAINT_EFFECT_PREFER_NO_SCHEDULE)]
+        for t, i in self.soft.items():
+            if any(toleration_tolerates(x, t.key, t.value, t.effect) for x in pref):
+                soft |= 1 << i
+        return hard, soft
 
 
 class ZoneIds:
@@ -131,10 +216,17 @@ def pod_requests(p: Pod):
     return rc, rm, nc, nm
 
 
-def pod_records(pods: List[Pod], zone_ids: Optional[ZoneIds] = None) -> np.ndarray:
+def pod_records(pods: List[Pod], zone_ids: Optional[ZoneIds] = None,
+                taint_ids: Optional[TaintIds] = None) -> np.ndarray:
+    """taint_ids (MS_PLUGINS_NU_TT_NN): pref_zone / pref_weight carry the pod's
+    tol_hard / tol_soft masks instead of a NodeAffinity term."""
     rec = np.zeros(len(pods), dtype=POD_REC)
     for i, p in enumerate(pods):
-        if p.preferred_zone is not None:
+        if taint_ids is not None:
+            if p.preferred_zone is not None:
+                raise ValueError("MS_PLUGINS_NU_TT_NN records carry tolerations, not a NodeAffinity term")
+            rec[i]["pref_zone"], rec[i]["pref_weight"] = taint_ids.pod_masks(p.tolerations)
+        elif p.preferred_zone is not None:
             zone, weight = p.preferred_zone
             if not 1 <= weight <= 100:
                 raise ValueError("PreferredSchedulingTerm weight must be in 1..100 (API validation)")
@@ -149,9 +241,12 @@ def pod_records(pods: List[Pod], zone_ids: Optional[ZoneIds] = None) -> np.ndarr
     return rec
 
 
-def node_records(nodes: List[Node], zone_ids: Optional[ZoneIds] = None) -> np.ndarray:
+def node_records(nodes: List[Node], zone_ids: Optional[ZoneIds] = None,
+                 taint_ids: Optional[TaintIds] = None) -> np.ndarray:
     rec = np.zeros(len(nodes), dtype=NODE_REC)
     for i, n in enumerate(nodes):
+        if taint_ids is not None:
+            rec[i]["taints"] = taint_ids.node_bits(n.taints)
         if ZONE_LABEL in n.labels:
             rec[i]["zone"] = (zone_ids or ZoneIds())(n.labels[ZONE_LABEL])
         d = name_digit(n.name)

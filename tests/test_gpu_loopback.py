@@ -167,6 +167,51 @@ def test_loopback_sharded_cycle(lb, oracle, plugin_set, G, uneven):
     assert covered == len(pr)
 
 
+@pytest.mark.parametrize("mode", ["two_sweep_streams", "alternating_caller_streams"])
+def test_loopback_tt_distinct_batches_concurrent_streams(lb, oracle, monkeypatch, mode):
+    # TaintToleration submits share the context's segment-summary
+    # scratch. With two sweep streams (MINISCHED_SHARD_STREAMS=2), or consecutive
+    # submits on different caller streams, two batches' sweeps could run at once on
+    # it; each submit here carries a DIFFERENT pod batch into its own result buffer,
+    # so an unordered overlap shows up as a wrong result
+    import torch
+
+    if mode == "two_sweep_streams":
+        monkeypatch.setenv("MINISCHED_SHARD_STREAMS", "2")
+    G, seed, n, nb, steps = 2, 707, 6000, 1500, 6
+    nr = synth.nodes(n, seed=seed, taints=True)
+    pr = synth.pods(nb * steps, seed=seed, taints=True)
+    o = _oracle_for(oracle, nr, pr, _lib.PLUGINS_NU_TT_NN, seed)
+    cuts = _cuts(n, G)
+    cid = _lib.comm_id_create(lb)
+    dev = torch.device("cuda:0")
+    host_pods = pr.view(np.uint8).copy()
+
+    def rank_fn(r):
+        lo, hi = cuts[r]
+        e = _joined(lb, cid, r, G, nr, lo, hi, _lib.PLUGINS_NU_TT_NN, seed)
+        try:
+            first, count = e.sharded_slice(nb)
+            pods = torch.from_numpy(host_pods).to(dev)
+            res = [torch.full((max(1, count) * 24,), 0xAB, dtype=torch.uint8, device=dev) for _ in range(steps)]
+            torch.cuda.synchronize()
+            ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
+            for k in range(steps):
+                s = ss[k % 2] if mode == "alternating_caller_streams" else ss[0]
+                e.sharded_submit(nb, pods.data_ptr() + 40 * nb * k, res[k].data_ptr(), s.cuda_stream)
+            for s in ss:
+                e.sharded_drain(s.cuda_stream)
+            torch.cuda.synchronize()
+            return first, count, [x.cpu().numpy().view(_lib.RESULT)[:count].copy() for x in res]
+        finally:
+            e.close()
+
+    got = run_ranks(G, rank_fn)
+    for r, (first, count, res) in enumerate(got):
+        for k in range(steps):
+            _same(res[k], o, nb * k + first, nb * k + first + count, f"TT {mode} rank {r} batch {k}")
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_loopback_config_c_full(lb, oracle, G):
     # config C at full size (100k nodes x 100k pods) through the library's pipelined
