@@ -434,6 +434,42 @@ def other_configs(args, dev, stream):
     return out
 
 
+def slice_parity(n_nodes, seed, pods_np, a, b, res, threads, prefix=1024):
+    """Checker, after the timed region: this rank's decoded pod slice [a, b) of
+    the last timed batch against the oracle's OpenMP result over the WHOLE
+    cluster (all n_nodes, every shard), on a prefix of the slice. Never on the
+    measured path (the N > 1 line verifies itself)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle  # checker only
+
+    from minisched_amd import synth
+
+    k = int(min(prefix, b - a))
+    if k <= 0:
+        return {"ok": True, "n": 0}
+    o = _oracle.schedule_nunn_omp(synth.nodes(n_nodes, seed=seed), pods_np[a:a + k], seed=seed, threads=threads)
+    ok = all(np.array_equal(np.asarray(res[x][:k]).astype(np.int64), np.asarray(o[y]).astype(np.int64))
+             for x, y in (("node", "node"), ("code", "code"), ("score", "score"), ("plugin_mask", "mask")))
+    return {"ok": bool(ok), "n": k}
+
+
+RANK_FIELDS = ("rank", "comm_rank", "comm_world", "wall_s", "device_ms_per_step", "kernel_ms", "parity_ok",
+               "parity_pods", "slice_first", "slice_end", "pods_scheduled")
+
+
+def gather_rows(row, world, dev):
+    """Every rank's RANK_FIELDS row on every rank (one all-gather, after the timed region)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return [list(row)]
+    t = torch.tensor(row, dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
 def load_profile(path, n_local, n_pods):
     try:
         pj = json.load(open(path))
@@ -484,7 +520,17 @@ def main():
     # gloo rehearsals keep the Python combine
     use_lib = world > 1 and split == "nodes" and backend == "nccl"
     if use_lib:
-        sharded.init_comm(eng)
+        try:
+            sharded.init_comm(eng)
+        except _lib.MSError as ex:  # fail loudly: a timed line without the RCCL path would be meaningless
+            print(f"bench.py rank {rank}/{world}: ms_comm_init failed ({_lib.ERRNAMES.get(ex.code, ex.code)}): {ex}",
+                  file=sys.stderr, flush=True)
+            raise SystemExit(3 if ex.code == _lib.MS_E_RCCL else 4)
+        inf = eng.info()
+        if (inf.comm_rank, inf.comm_world) != (rank, world):
+            print(f"bench.py rank {rank}: the communicator reports rank {inf.comm_rank} of {inf.comm_world}, "
+                  f"expected {rank} of {world}", file=sys.stderr, flush=True)
+            raise SystemExit(3)
     present = sharded.present_total(eng) if split == "nodes" and not use_lib else None
 
     pods_np = synth.pods(P, seed=args.seed)
@@ -517,6 +563,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_rank = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -543,6 +590,23 @@ def main():
     else:
         kernel_ms = timed(cyc.step, stream, reps)
         kernel_evals = float(cyc.b - cyc.a) * float(hi - lo)
+
+    # self-verification (after the timed region): the rank's communicator, its own
+    # step times and the parity of its decoded slice; gathered to rank 0
+    from minisched_amd.hostinfo import cpu_threads
+
+    inf = eng.info()
+    chk = slice_parity(N, args.seed, pods_np, cyc.a, cyc.b, res, max(1, cpu_threads() // max(1, world)))
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
+    rows = gather_rows([rank, inf.comm_rank, inf.comm_world if use_lib else -1, elapsed_rank, step_dev_ms, kernel_ms,
+                        1.0 if chk["ok"] else 0.0, chk["n"], cyc.a, cyc.b,
+                        int((res["code"] == _lib.CODE_SUCCESS).sum())], world, coll_dev)
+    per_rank = [{k: (int(v) if k not in ("wall_s", "device_ms_per_step", "kernel_ms") else v)
+                 for k, v in zip(RANK_FIELDS, r)} for r in rows]
+    for r in per_rank:
+        r["parity_ok"] = bool(r["parity_ok"])
+        r["ms_per_step"] = r.pop("wall_s") * 1e3 / args.steps
+    parity_all = all(r["parity_ok"] for r in per_rank)
 
     extras = {}
     if not args.no_extras:
@@ -627,6 +691,19 @@ def main():
             "pods_scheduled": ok,
             "roofline": roofline,
             "cpu_baseline": None,
+            # each rank's communicator (RCCL rank / world as the
+            # library reports them; -1 without the in-library communicator), its own
+            # wall and device step times, its sweep kernel time, and the parity of its
+            # decoded slice against the oracle over the whole cluster (a prefix of the
+            # slice, checked after the timed region)
+            "verify": {
+                "backend": backend if world > 1 else None,
+                "in_library_rccl": bool(cyc.library),
+                "parity_ok_all_ranks": parity_all,
+                "parity_check": "oracle msor_schedule_nunn_omp over all nodes, first <= 1024 pods of each rank's "
+                                "decoded slice of the last timed batch (node, code, score, plugin mask)",
+                "per_rank": per_rank,
+            },
         }
         line.update(extras)
         if world == 1 and not args.no_cpu_baseline:
@@ -640,6 +717,10 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if not parity_all:
+        print(f"bench.py rank {rank}: decoded results differ from the oracle "
+              f"({[r['rank'] for r in per_rank if not r['parity_ok']]})", file=sys.stderr, flush=True)
+        raise SystemExit(5)
 
 
 if __name__ == "__main__":

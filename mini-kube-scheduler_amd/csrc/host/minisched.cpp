@@ -250,26 +250,49 @@ uint32_t OrdinalAllocator::LowestAny() {
     return best;
 }
 
-uint32_t OrdinalAllocator::Allocate(int digit) {
-    uint32_t o;
-    const uint64_t spread = kSpreadSlack + 2ull * (live_ + 1ull);  // (skewed name digits)
-    if (digit >= 0 && digit <= 9 && !free_[digit].empty() && *free_[digit].begin() < spread) {
-        o = *free_[digit].begin();
+bool OrdinalAllocator::Skewed() const {
+    const uint32_t mx = *std::max_element(count_, count_ + 10);
+    return live_ >= kSkewMinLive && 100ull * mx > (uint64_t)kSkewBreakEvenX10 * live_;
+}
+
+// (live_ and count_ already include the node being placed)
+uint32_t OrdinalAllocator::Pick(int digit) {
+    const bool has = digit >= 0 && digit <= 9;
+    const uint64_t spread = kSpreadSlack + 2ull * live_;  // (skewed name digits)
+    if (Skewed()) return LowestAny();                     // dense: cheaper than any aligned spread
+    if (has && !free_[digit].empty() && *free_[digit].begin() < spread) {
+        const uint32_t o = *free_[digit].begin();
         free_[digit].erase(free_[digit].begin());
-    } else if (digit >= 0 && digit <= 9 && next_[digit] < cap_ && next_[digit] < spread) {
-        o = next_[digit];
-        next_[digit] += 10;
-    } else {
-        o = LowestAny();  // no digit, the digit's residue is full, or its slot is too far out
+        return o;
     }
+    if (has && next_[digit] < cap_ && next_[digit] < spread) {
+        const uint32_t o = next_[digit];
+        next_[digit] += 10;
+        return o;
+    }
+    return LowestAny();  // no digit, the digit's residue is full, or its slot is too far out
+}
+
+uint32_t OrdinalAllocator::Allocate(int digit) {
+    const bool has = digit >= 0 && digit <= 9;
+    if (has) ++count_[digit];
     ++live_;
+    uint32_t o;
+    try {
+        o = Pick(digit);
+    } catch (...) {  // (full: the shares stay as they were)
+        --live_;
+        if (has) --count_[digit];
+        throw;
+    }
     high_ = std::max(high_, o + 1);
     return o;
 }
 
-void OrdinalAllocator::Release(uint32_t o) {
+void OrdinalAllocator::Release(uint32_t o, int digit) {
     free_[o % 10].insert(o);
     if (live_) --live_;
+    if (digit >= 0 && digit <= 9 && count_[digit]) --count_[digit];
 }
 
 uint32_t OrdinalAllocator::HighWater() const { return high_; }
@@ -314,7 +337,7 @@ void Scheduler::OnNodeDelete(const v1::Node &node) {  // eventhandler.go:51-56
     if (ms_nodes_delete(ctx_, 1, &o) != MS_OK) throw std::runtime_error(ms_last_error(ctx_));
     ordinal_.erase(it);
     names_[o].clear();
-    ordinals_.Release(o);
+    ordinals_.Release(o, NameDigit(node.name));
     nodes_.erase(node.name);
     usage_.erase(node.name);
     if (Gvk(framework::kNode) & framework::Delete)

@@ -214,15 +214,24 @@ ms_pod_rec EncodePod(const v1::Pod &pod, uint32_t ordinal);
 class OrdinalAllocator {
    public:
     static constexpr uint32_t kSpreadSlack = 300;  // 10 groups of 30 ordinals
+    // Skew fallback (encode.DigitOrdinals in lockstep): with at
+    // least kSkewMinLive live nodes and 10 x the largest digit share above 2.6
+    // (100 x max count > kSkewBreakEvenX10 x live), an aligned table costs more
+    // to sweep than a dense one on the bit-scan path, so allocations go dense.
+    static constexpr uint32_t kSkewMinLive = 100;
+    static constexpr uint32_t kSkewBreakEvenX10 = 26;
     explicit OrdinalAllocator(uint32_t capacity);
     uint32_t Allocate(int digit);  // digit 0..9, or -1; throws std::length_error when full
-    void Release(uint32_t ordinal);
+    void Release(uint32_t ordinal, int digit);  // digit: the released node's name digit
     uint32_t HighWater() const;    // 1 + the highest ordinal ever handed out (0 if none)
+    bool Skewed() const;           // allocations currently go dense
 
    private:
     uint32_t LowestAny();
+    uint32_t Pick(int digit);
     uint32_t cap_;
     uint32_t live_ = 0;
+    uint32_t count_[10] = {};      // live nodes per name digit
     uint32_t next_[10];            // lowest never-used ordinal of residue d
     std::set<uint32_t> free_[10];  // released ordinals per residue
     uint32_t high_ = 0;

@@ -267,9 +267,21 @@ class DigitOrdinals:
     digits whose residue is full up to the capacity, take the lowest free
     ordinal of any residue; so does a digit whose aligned slot lies past
     SPREAD_SLACK + 2 x (live nodes + 1) (skewed name digits would otherwise
-    spread the table over up to 10x the ordinals)."""
+    spread the table over up to 10x the ordinals).
+
+    Skew fallback: alignment pays only while the table it
+    builds is cheaper to sweep than a dense one. An aligned table spans
+    ~10 x (largest digit share) x live rows, all on K1's fast path; a dense one
+    spans live rows on the bit-scan path, which costs ~2.6x per row at config C
+    (0.68 vs 0.264 ms, profiles/r04x_naming_*.log). So once SKEW_MIN_LIVE nodes
+    are live and 10 x the largest digit share of the live nodes (this one
+    included) exceeds SKEW_BREAK_EVEN = 2.6 (integer form: 100 x max count >
+    26 x live), every allocation takes the lowest free ordinal of any residue.
+    release() needs the node's digit to keep the shares current."""
 
     SPREAD_SLACK = 300
+    SKEW_MIN_LIVE = 100
+    SKEW_BREAK_EVEN_X10 = 26  # 10 x (10 x largest share) threshold, 2.6 in integers
 
     def __init__(self, capacity: int):
         import heapq  # noqa: F401  (free lists are min-heaps)
@@ -279,6 +291,7 @@ class DigitOrdinals:
         self.free: List[List[int]] = [[] for _ in range(10)]
         self.high = 0
         self.live = 0
+        self.count = [0] * 10  # live nodes per name digit
 
     def _lowest_any(self) -> int:
         import heapq
@@ -296,23 +309,44 @@ class DigitOrdinals:
             self.next[bd] += 10
         return best
 
-    def allocate(self, digit: int) -> int:
-        import heapq
+    def skewed(self) -> bool:
+        """True when the live digit mix makes a dense table cheaper than an aligned one."""
+        return self.live >= self.SKEW_MIN_LIVE and 100 * max(self.count) > self.SKEW_BREAK_EVEN_X10 * self.live
 
-        spread = self.SPREAD_SLACK + 2 * (self.live + 1)
-        if 0 <= digit <= 9 and self.free[digit] and self.free[digit][0] < spread:
-            o = heapq.heappop(self.free[digit])
-        elif 0 <= digit <= 9 and self.next[digit] < self.cap and self.next[digit] < spread:
-            o = self.next[digit]
-            self.next[digit] += 10
-        else:
-            o = self._lowest_any()
+    def allocate(self, digit: int) -> int:
+        has_digit = 0 <= digit <= 9
+        if has_digit:
+            self.count[digit] += 1
         self.live += 1
+        try:
+            o = self._pick(digit, has_digit)
+        except OverflowError:  # (full: the shares stay as they were)
+            self.live -= 1
+            if has_digit:
+                self.count[digit] -= 1
+            raise
         self.high = max(self.high, o + 1)
         return o
 
-    def release(self, ordinal: int) -> None:
+    def _pick(self, digit: int, has_digit: bool) -> int:
+        import heapq
+
+        spread = self.SPREAD_SLACK + 2 * self.live
+        if self.skewed():
+            return self._lowest_any()
+        if has_digit and self.free[digit] and self.free[digit][0] < spread:
+            return heapq.heappop(self.free[digit])
+        if has_digit and self.next[digit] < self.cap and self.next[digit] < spread:
+            o = self.next[digit]
+            self.next[digit] += 10
+            return o
+        return self._lowest_any()
+
+    def release(self, ordinal: int, digit: int) -> None:
+        """Frees `ordinal`, held by a node whose name digit is `digit` (0..9, or -1)."""
         import heapq
 
         heapq.heappush(self.free[ordinal % 10], ordinal)
         self.live = max(0, self.live - 1)
+        if 0 <= digit <= 9 and self.count[digit]:
+            self.count[digit] -= 1

@@ -110,9 +110,9 @@ static void cpu_tests() {
         CHECK(got[5] == 10 && got[8] == 9);
         for (size_t i = 0; i < got.size(); ++i)
             if (digits[i] >= 0) CHECK((int)(got[i] % 10) == digits[i]);
-        a.Release(17);
+        a.Release(17, 7);
         CHECK(a.Allocate(7) == 17);  // its residue's hole first
-        a.Release(27);
+        a.Release(27, 7);
         CHECK(a.Allocate(-1) == 2);  // (2 < 27)
         // every 30 consecutive ordinals hold at most 3 of one digit
         OrdinalAllocator b(3000);
@@ -143,6 +143,26 @@ static void cpu_tests() {
         std::set<uint32_t> seen;
         for (int i = 0; i < 5000; ++i) seen.insert(sk.Allocate(0));
         CHECK(seen.size() == 5000 && sk.HighWater() <= 2 * 5000 + OrdinalAllocator::kSpreadSlack + 2);
+        // skew fallback: dense once 100 x max count > 26 x live, live >= 100
+        CHECK(sk.Skewed() && sk.HighWater() <= 5000 + OrdinalAllocator::kSpreadSlack);
+        OrdinalAllocator t(10000);
+        for (int i = 0; i < 100; ++i) (void)t.Allocate(i < 26 ? 0 : 1 + i % 9);
+        CHECK(!t.Skewed());  // 26 % of one digit
+        (void)t.Allocate(0);
+        CHECK(t.Skewed());   // 27 of 101
+        // 70 % zeros: the table stays ~n rows
+        OrdinalAllocator s70(100000);
+        std::vector<std::pair<uint32_t, int>> held;
+        uint64_t y = 777;
+        for (int i = 0; i < 20000; ++i) {
+            y = y * 6364136223846793005ull + 1442695040888963407ull;
+            const int d = ((y >> 33) % 100) < 70 ? 0 : (int)((y >> 40) % 10);
+            held.push_back({s70.Allocate(d), d});
+        }
+        CHECK(s70.Skewed() && s70.HighWater() <= 20000 + OrdinalAllocator::kSpreadSlack);
+        for (const auto &h : held)
+            if (h.second == 0) s70.Release(h.first, 0);
+        CHECK(!s70.Skewed() && s70.Allocate(3) % 10 == 3);  // alignment back
     });
     run("queue: FIFO, backoff 1 s, event matching (queue.go)", [] {
         FakeClock clk;

@@ -278,9 +278,9 @@ def test_digit_ordinals_allocator():
     a = encode.DigitOrdinals(100)
     got = [a.allocate(d) for d in (7, 7, 7, 3, -1, 0, 7, -1, 9, 3)]
     assert got == [7, 17, 27, 3, 0, 10, 37, 1, 9, 13]
-    a.release(17)
+    a.release(17, 7)
     assert a.allocate(7) == 17
-    a.release(27)
+    a.release(27, 7)
     assert a.allocate(-1) == 2
     rng = np.random.default_rng(5)
     b = encode.DigitOrdinals(12_000)
@@ -301,3 +301,42 @@ def test_digit_ordinals_allocator():
     got = [sk.allocate(0) for _ in range(5000)]
     assert len(set(got)) == 5000 and sk.high <= 2 * 5000 + sk.SPREAD_SLACK + 2
     assert got[:30] == list(range(0, 300, 10))  # aligned while within the bound
+    # ... and dense once SKEW_MIN_LIVE nodes are live
+    assert sk.skewed() and sk.high <= 5000 + sk.SPREAD_SLACK
+
+
+def test_digit_ordinals_skew_fallback():
+    # the switch: 10 x the largest live digit share above 2.6 (integer form
+    # 100 x max count > 26 x live) once SKEW_MIN_LIVE nodes are live -> dense ordinals
+    from minisched_amd import encode
+
+    rng = np.random.default_rng(9)
+    n = 50_000
+    # i.i.d. uniform digits stay aligned: every 30 ordinals hold <= 3 of a digit
+    iid = encode.DigitOrdinals(n + n // 10)
+    dig = np.full(n + n // 10, -2)
+    for d in rng.integers(0, 10, n):
+        dig[iid.allocate(int(d))] = d
+    assert not iid.skewed()
+    w = dig[: (iid.high // 30) * 30].reshape(-1, 30)
+    assert max(int((w == d).sum(1).max()) for d in range(10)) <= 3
+    # 70 % of the names end in 0: dense after the first SKEW_MIN_LIVE nodes, so the
+    # table spans ~n rows, not the bounded spread's ~2n (profiles/r04x_naming_layouts.log)
+    sk = encode.DigitOrdinals(2 * n)
+    digits = np.where(rng.random(n) < 0.7, 0, rng.integers(0, 10, n))
+    ords = [sk.allocate(int(d)) for d in digits]
+    assert sk.skewed() and len(set(ords)) == n and sk.high <= n + sk.SPREAD_SLACK
+    # the threshold itself: 26 % of one digit among 100 live nodes is not skewed, 27 % is
+    t = encode.DigitOrdinals(10_000)
+    for i in range(100):
+        t.allocate(0 if i < 26 else 1 + i % 9)
+    assert max(t.count) == 26 and not t.skewed()
+    t.allocate(0)
+    assert 100 * 27 > 26 * 101 and t.skewed()
+    # releasing skewed nodes brings alignment back
+    for o, d in zip(ords, digits):
+        if d == 0:
+            sk.release(o, 0)
+    assert not sk.skewed()
+    o = sk.allocate(3)
+    assert o % 10 == 3
