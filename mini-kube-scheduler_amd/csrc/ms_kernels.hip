@@ -624,6 +624,94 @@ __device__ __forceinline__ void quad_merge4(u64 (&k)[4], uint32_t &f) {
     f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, CTRL, 0xF, 0xF, false);
 }
 
+// ---- tile-local keys as binary64 (round 5) ---------------------------------
+// Inside one 256-row tile a packed key needs score (11 bits), the 32-bit hash
+// and the row's place in the tile (8 bits): 51 bits. Placed in the mantissa of
+// a double with the exponent of 2^52 (bits 0x433 << 52), every such key is an
+// exactly represented normal number 2^52 + K, ordered like K; an infeasible
+// row is +0.0, below every key. A compare-exchange of the per-lane top-4 sort
+// network is then v_max_f64 + v_min_f64 (2 VALU) instead of a 64-bit compare
+// and four selects (5), and a running max is one v_max_f64 instead of three.
+// Issued as inline asm: in IEEE mode the compiler would quiet (canonicalise)
+// operands it cannot prove canonical before llvm.maxnum, one more v_max_f64
+// per operand; every operand here is +0.0 or a normal number.
+#ifndef MS_TP_F64KEYS
+#define MS_TP_F64KEYS 1
+#endif
+constexpr uint32_t kTkExpHi = 0x43300000u;  // high word of 2^52
+
+__device__ __forceinline__ double fmax64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double fmin64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// K = score << 40 | h << 8 | (255 - place), place = the row's index in its tile.
+// se = score + (kTkExpHi >> 8): the exponent rides in the score word, so the
+// high word is one v_alignbit. reject: the high word is 0 instead, a value
+// (+0.0 or a subnormal) below every key; global_key maps any high word below
+// the exponent's to "no feasible row".
+__device__ __forceinline__ double tile_key(uint32_t se, uint32_t h, uint32_t place, bool reject) {
+    const uint32_t hi = reject ? 0u : __builtin_amdgcn_alignbit(se, h, 24);
+    const uint32_t lo = (h << 8) | (255u - place);
+    return __hiloint2double((int)hi, (int)lo);
+}
+// The global packed key (make_key) of a tile key of tile `tile` (0 stays 0).
+__device__ __forceinline__ u64 global_key(double k, uint32_t tile_ord0) {
+    const uint64_t b = (uint64_t)__double_as_longlong(k);
+    if ((uint32_t)(b >> 32) < kTkExpHi) return 0ull;
+    const uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
+    const uint32_t score = (hi >> 8) & 0x7FFu, h = (hi << 24) | (lo >> 8), place = 255u - (lo & 0xFFu);
+    return make_key(score, h, tile_ord0 + place);
+}
+__device__ __forceinline__ void cswap_desc(double &a, double &b) {
+    const double hi = fmax64(a, b), lo = fmin64(a, b);
+    a = hi;
+    b = lo;
+}
+__device__ __forceinline__ void sort4_desc(double (&x)[4]) {
+    cswap_desc(x[0], x[1]);
+    cswap_desc(x[2], x[3]);
+    cswap_desc(x[0], x[2]);
+    cswap_desc(x[1], x[3]);
+    cswap_desc(x[1], x[2]);
+}
+__device__ __forceinline__ void merge4_desc(double (&k)[4], const double (&s)[4]) {
+    double c0 = fmax64(k[0], s[3]), c1 = fmax64(k[1], s[2]), c2 = fmax64(k[2], s[1]), c3 = fmax64(k[3], s[0]);
+    cswap_desc(c0, c2);
+    cswap_desc(c1, c3);
+    cswap_desc(c0, c1);
+    cswap_desc(c2, c3);
+    k[0] = c0;
+    k[1] = c1;
+    k[2] = c2;
+    k[3] = c3;
+}
+template <int CTRL>
+__device__ __forceinline__ void quad_merge4(double (&k)[4], uint32_t &f) {
+    double o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = __longlong_as_double((long long)dpp_u64<CTRL>((u64)__double_as_longlong(k[j])));
+    merge4_desc(k, o);
+    f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, CTRL, 0xF, 0xF, false);
+}
+
+// eval_tp with the tile-local binary64 key (place: the row's index in its tile).
+__device__ __forceinline__ double eval_tp64(const DRow &x, uint32_t ord, uint32_t place, const PodFast &q) {
+    const bool fit_fail = (q.rc > x.fr_cpu) | (q.rm > x.fr_mem);
+    const bool reject = ((x.rbits & q.rej) != 0) | (fit_fail & !(q.bits & kPfZero));
+    const uint32_t s_cpu = cvt_u32_sat(__builtin_fma(q.nnc, x.r_cpu, x.a_cpu));
+    const uint32_t s_mem = cvt_u32_sat(__builtin_fma(q.nnm, x.r_mem, x.a_mem));
+    // nn + floor(s / 2) = floor((s + 2 nn) / 2); the exponent word added twice before the halving
+    constexpr uint32_t kE2 = kTkExpHi >> 7;
+    const uint32_t nn2 = x.digit == (q.bits & 0x1FFu) ? 20u + kE2 : kE2;
+    return tile_key((s_cpu + s_mem + nn2) >> 1, tb_hash(q.A, ord), place, reject);
+}
+
 // eval_fast for the transposed form, where the pod differs per lane: the
 // static filters from the row's precomputed rbits (one AND + compare), Fit's
 // two compares; the filter flags come from the tile's rbits (TileBits).
@@ -678,6 +766,28 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     const uint32_t row0 = tile * kFullWaveTile + part;
     const uint32_t ord0 = a.t.base + row0;
     const DRow *d = rows + part;  // the tile's rows, staged in LDS
+#if MS_TP_F64KEYS
+    double k[4] = {0.0, 0.0, 0.0, 0.0};
+    MS_UNROLL(MS_TP_UNROLL)
+    for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = eval_tp64(d[4 * (i + u)], ord0 + 4 * (i + u), part + 4 * (i + u), q);
+        sort4_desc(x);
+        merge4_desc(k, x);
+    }
+    const bool tol = (q.bits & kPfTol) != 0;
+    uint32_t f = ((tb.any & kRbUnsched) && !tol ? 1u : 0u) | (tb.all & (tol ? kRbAbsent : kRbBlocked) ? 0u : 0x100u);
+    quad_merge4<0xB1>(k, f);  // quad_perm [1,0,3,2]
+    quad_merge4<0x4E>(k, f);  // quad_perm [2,3,0,1]
+    if (pi < cnt) {
+        const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
+        const double mine = part == 0 ? k[0] : part == 1 ? k[1] : part == 2 ? k[2] : k[3];
+        a.tile_keys[cell * kTopK + part] = global_key(mine, a.t.base + tile * kFullWaveTile);
+        if (part == 0) a.tile_flags[cell] = f;
+    }
+    return true;
+#else
     u64 k[4] = {0ull, 0ull, 0ull, 0ull};
     // rows 4 at a time (LDS reads issued together at the top of each block)
     MS_UNROLL(MS_TP_UNROLL)
@@ -698,6 +808,7 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
         if (part == 0) a.tile_flags[cell] = f;
     }
     return true;
+#endif
 }
 
 // One task of the lane = row sweep: (tile, pod chunk cidx of a.chunk pods).
