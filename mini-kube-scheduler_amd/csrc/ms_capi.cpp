@@ -51,7 +51,8 @@ void free_all(ms_ctx *c) {
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
                    c->d_podc, c->d_resc,
-                   c->d_merged, c->d_merged_flags, c->d_drow, c->d_top_ext, c->t.taints, c->d_tt};
+                   c->d_merged, c->d_merged_flags, c->d_drow, c->d_top_ext, c->t.taints, c->d_tt,
+                   c->d_merge_tags, c->d_merge_ctr};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     if (c->h_podz) (void)hipHostFree(c->h_podz);
@@ -177,6 +178,18 @@ int chain_back(ms_ctx *c, hipStream_t s, bool recorded) {
     return MS_OK;
 }
 
+// The in-step merge's counter: MINISCHED_CTR_FINE=1 allocates it fine-grained
+// (atomics and polls at the memory side, coherent across XCDs without L2
+// maintenance; A/B), else plain device memory.
+hipError_t ctr_alloc(uint32_t **p) {
+    static const bool fine = [] {
+        const char *e = getenv("MINISCHED_CTR_FINE");
+        return e && e[0] == '1';
+    }();
+    if (fine) return hipExtMallocWithFlags((void **)p, 64, hipDeviceMallocFinegrained);
+    return hipMalloc((void **)p, 64);
+}
+
 // Sequential-engine scratch for n_tiles tiles, kSeqBufs batches deep (pipelining).
 int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (!c->seq_stream) {
@@ -190,7 +203,7 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     if (n_tiles <= c->tile_cap) return MS_OK;
     MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
     void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev,
-                   c->d_prev_rec, c->d_drow, c->d_top_ext};
+                   c->d_prev_rec, c->d_drow, c->d_top_ext, c->d_merge_tags, c->d_merge_ctr};
     for (void *q : old)
         if (q) (void)hipFree(q);
     c->d_tile_keys = nullptr;
@@ -203,6 +216,8 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
     c->d_prev_rec = nullptr;
     c->d_drow = nullptr;
     c->d_top_ext = nullptr;
+    c->d_merge_tags = nullptr;
+    c->d_merge_ctr = nullptr;
     c->tile_cap = 0;
     // (ms_seq_candidates_device uses the same buffers for up to kSeqBufs * B pods)
     const size_t B = seq_batch_limit(), NB = kSeqBufs * B, n = NB * n_tiles;
@@ -215,8 +230,11 @@ int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
         hipMalloc((void **)&c->d_prev, 2 * (2 + seq_prev_cap()) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&c->d_prev_rec, 2 * seq_prev_cap() * seq_rec_fields() * sizeof(int64_t)) != hipSuccess ||
         hipMalloc((void **)&c->d_drow, (size_t)n_tiles * kFullWaveTile * sizeof(DRow)) != hipSuccess ||
-        hipMalloc((void **)&c->d_top_ext, NB * seq_topk() * sizeof(unsigned long long)) != hipSuccess)
+        hipMalloc((void **)&c->d_top_ext, NB * seq_topk() * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void **)&c->d_merge_tags, NB * sizeof(uint32_t)) != hipSuccess ||
+        ctr_alloc(&c->d_merge_ctr) != hipSuccess)
         return fail(c, MS_E_OOM, "sequential-engine scratch");
+    MS_HIP(c, hipMemsetAsync(c->d_merge_tags, 0, NB * sizeof(uint32_t), c->stream));
     MS_HIP(c, hipMemsetAsync(c->d_spec, 0, NB * sizeof(unsigned long long), c->stream));
     MS_HIP(c, hipMemsetAsync(c->d_spec_flags, 0, NB * sizeof(uint32_t), c->stream));
     MS_HIP(c, hipStreamSynchronize(c->stream));
@@ -338,13 +356,52 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
         MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, nb0, n_tiles, c->d_top4, c->d_spec,
                                     c->d_spec_flags, tq, c->d_top4_rec, s, top_ext));
-        uint32_t k = 0;
+        // Batch k+1's merge inside step k (default since round 5, "instep"): the sweep
+        // workgroups count themselves done on a device counter, then one wave per
+        // pod merges the tile lists (written through, read L2-bypassing across the
+        // XCDs) while the validator continues; a worker whose bounded wait runs out
+        // leaves its pods untagged and the next validation merges them itself.
+        // With the binary64 tile keys the sweep + merge path fits beside the
+        // validator: config E 44.4 -> 40.5 ms against the merge launch
+        // (profiles/r05c_e_ab.txt, r05f_e_sync_ab.txt). MINISCHED_SEQ_MERGE=launch:
+        // a k_topk_merge launch after each step (A/B); "fallback": the in-step
+        // workers skip (a test hook). Read per call (tests switch it).
+        const char *merge_env = getenv("MINISCHED_SEQ_MERGE");
+        const std::string merge_mode = merge_env ? merge_env : "instep";
+        const bool want_instep = merge_mode == "instep" || merge_mode == "fallback";
+        if (want_instep) MS_HIP(c, hipMemsetAsync(c->d_merge_ctr, 0, sizeof(uint32_t), s));
+        uint32_t k = 0, in_tag = 0, target = 0;
         for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
             const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
             const uint32_t s1 = s0 + B, nn = s1 < n_pods ? std::min(B, n_pods - s1) : 0u;
             unsigned long long *tk = c->d_tile_keys + cells_per_set * seq_topk() * cur;
             unsigned long long *tk1 = c->d_tile_keys + cells_per_set * seq_topk() * nxt;
             uint32_t *tf = c->d_tile_flags + cells_per_set * cur, *tf1 = c->d_tile_flags + cells_per_set * nxt;
+            SeqMergeIO mio;
+            // timeline of steps 200 .. 215 (MS_TIMELINE=<file>; recorded by the
+            // MS_VSTAMPS / MS_TIMELINE_ONLY diagnostic kernels only)
+            static const bool want_tl = getenv("MS_TIMELINE") != nullptr;
+            if (want_tl && !c->d_tl &&
+                hipMalloc((void **)&c->d_tl, (size_t)kTimelineSteps * kTimelineWgs * 8 * 8) == hipSuccess)
+                MS_HIP(c, hipMemsetAsync(c->d_tl, 0, (size_t)kTimelineSteps * kTimelineWgs * 8 * 8, s));
+            mio.tl = c->d_tl;
+            mio.tl_step = k >= 200 ? k - 200 : ~0u;
+            mio.in_tags = c->d_merge_tags + SB * cur;
+            mio.in_tag = in_tag;
+            mio.ctr = c->d_merge_ctr;
+            mio.target = target;
+            const bool in_step = want_instep && seq_step_merges(tq, n_tiles, nn);
+            if (in_step) {
+                if (++c->merge_tag == 0) ++c->merge_tag;  // (0: no tag)
+                mio.top = c->d_top4 + (size_t)SB * seq_topk() * nxt;
+                mio.spec = c->d_spec + SB * nxt;
+                mio.spec_flags = c->d_spec_flags + SB * nxt;
+                mio.recs = c->d_top4_rec + recs_per_set * nxt;
+                mio.ext = top_ext ? top_ext + (size_t)SB * seq_topk() * nxt : nullptr;
+                mio.tags = c->d_merge_tags + SB * nxt;
+                mio.tag = c->merge_tag;
+                mio.skip = merge_mode == "fallback" ? 1 : 0;
+            }
             MS_HIP(c, launch_seq_step(tq, rows, n_tiles, seed32, d_pods + s0, nb, tk, tf, c->d_spec + SB * cur,
                                       c->d_spec_flags + SB * cur, c->d_top4 + (size_t)SB * seq_topk() * cur,
                                       c->d_top4_rec + recs_per_set * cur,
@@ -352,8 +409,10 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
                                       k ? c->d_prev_rec + prev_fields * nxt : nullptr, c->d_prev + prev_words * cur,
                                       c->d_prev_rec + prev_fields * cur, d_res + s0, c->d_overflow,
                                       nn ? d_pods + s1 : nullptr, nn, tk1, tf1, c->num_cus, s,
-                                      top_ext ? top_ext + (size_t)SB * seq_topk() * cur : nullptr));
-            if (nn)
+                                      top_ext ? top_ext + (size_t)SB * seq_topk() * cur : nullptr, nullptr, 0, &mio));
+            target = mio.target;
+            in_tag = in_step ? mio.tag : 0u;
+            if (nn && !in_step)
                 MS_HIP(c, launch_topk_merge(tk1, tf1, nn, n_tiles, c->d_top4 + (size_t)SB * seq_topk() * nxt,
                                             c->d_spec + SB * nxt, c->d_spec_flags + SB * nxt, c->t,
                                             c->d_top4_rec + recs_per_set * nxt, s,
@@ -831,16 +890,33 @@ int ms_destroy(ms_ctx *c) {
                          "MS_VSTAMPS pods=%u slow=%u tile_scans=%u misses=%u recomputes=%u resweeps=%u rounds=%u cycles: prologue=%llu "
                          "group=%llu prologue_loads=%llu slow=%llu rounds=%llu epilogue=%llu first_slow=%llu round_cand=%llu "
                          "round_claim=%llu | step waves (10 ns): validator=%llu sweep_sum=%llu sweep_waves=%llu | epilogue "
-                         "parts: counters=%llu compaction=%llu writeback=%llu\n",
+                         "parts: counters=%llu compaction=%llu writeback=%llu | in-step merge (10 ns, summed from each "
+                         "workgroup's start): swept=%llu waited=%llu merged=%llu workers=%llu wg_counted=%llu\n",
                          st[3], st[5], st[6], st[4], st[2], st[1], st[7], (unsigned long long)cy[0], (unsigned long long)cy[1],
                          (unsigned long long)cy[2], (unsigned long long)cy[3], (unsigned long long)cy[4],
                          (unsigned long long)cy[5], (unsigned long long)cy[6], (unsigned long long)cy[7],
                          (unsigned long long)cy[8], (unsigned long long)cy[9], (unsigned long long)cy[10],
                          (unsigned long long)cy[11], (unsigned long long)cy[12], (unsigned long long)cy[13],
-                         (unsigned long long)cy[14]);
+                         (unsigned long long)cy[14], (unsigned long long)cy[15], (unsigned long long)cy[16],
+                         (unsigned long long)cy[17], (unsigned long long)cy[18], (unsigned long long)cy[19]);
         }
     }
 #endif
+    {
+        const char *tlf = getenv("MS_TIMELINE");
+        if (tlf && c->d_tl) {
+            std::vector<unsigned long long> tl((size_t)kTimelineSteps * kTimelineWgs * 8);
+            if (hipMemcpy(tl.data(), c->d_tl, tl.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                if (FILE *f = std::fopen(tlf, "wb")) {
+                    std::fwrite(tl.data(), 8, tl.size(), f);
+                    std::fclose(f);
+                }
+            }
+            (void)hipFree(c->d_tl);
+            c->d_tl = nullptr;
+        }
+    }
+    if (c->d_tl) (void)hipFree(c->d_tl);
     free_all(c);
     delete c;
     return MS_OK;

@@ -66,6 +66,10 @@ struct ms_ctx {
     unsigned long long *d_top4 = nullptr;  // per-pod global speculative top-4 keys
     int64_t *d_top4_rec = nullptr;         // their batch-start node records (validator layout)
     unsigned long long *d_top_ext = nullptr;  // ranks 4..7 per pod (the validator's slow pods)
+    uint32_t *d_merge_tags = nullptr;         // per pod of both merge-output sets: the in-step merge's tag
+    uint32_t *d_merge_ctr = nullptr;          // the in-step merge's sweep-done counter
+    uint32_t merge_tag = 0;                   // last in-step merge tag issued
+    unsigned long long *d_tl = nullptr;       // MS_VSTAMPS: step timeline (MS_TIMELINE=<file> dumps it at ms_destroy)
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
     int64_t *d_prev_rec = nullptr;         // and their final records (x2)
     DRow *d_drow = nullptr;                // derived rows of the binary64 sweep (tile_cap * kFullWaveTile)

@@ -245,6 +245,32 @@ struct SeqMerge {
     uint32_t *spec_flags;
     int64_t *recs;
 };
+// Batch k+1's merge inside step k at depth 1 (MINISCHED_SEQ_MERGE=instep):
+// once every sweep workgroup of the step has written batch k+1's tile lists
+// (write-through stores, counted on ctr), their waves merge its pods into these
+// buffers (launch_topk_merge's outputs), tagging each merged pod with `tag`.
+// The wait is bounded: a worker that gives up leaves its pods untagged and
+// validation k+1 merges them itself, so a grid that is not co-resident costs
+// time, never correctness. ctr: a u32 zeroed at the run's start; target: the
+// count after the run's earlier in-step merges, advanced by launch_seq_step.
+// in_tags / in_tag: batch k's tags (in_tag 0: batch k was merged by a launch).
+// skip: the workers leave every pod to the fallback (a test hook).
+struct SeqMergeIO {
+    const uint32_t *in_tags = nullptr;
+    uint32_t in_tag = 0;
+    unsigned long long *top = nullptr, *spec = nullptr, *ext = nullptr;
+    uint32_t *spec_flags = nullptr, *tags = nullptr, *ctr = nullptr;
+    int64_t *recs = nullptr;
+    uint32_t tag = 0, target = 0;
+    int skip = 0;
+    // MS_VSTAMPS diagnostic build: per-workgroup timestamps of steps
+    // tl_step < kTimelineSteps (u64 [step][workgroup][8], s_memrealtime)
+    unsigned long long *tl = nullptr;
+    uint32_t tl_step = ~0u;
+};
+constexpr uint32_t kTimelineSteps = 16, kTimelineWgs = 256;
+// Whether launch_seq_step can merge n_next pods in-step (else launch_topk_merge follows).
+bool seq_step_merges(const NodeTable &t, uint32_t n_tiles, uint32_t n_next);
 // One single-stream step: validate batch k (n_pods) while sweeping the next
 // batch (n_next pods, tile lists only) and, with merge, merging the batch in
 // between (depth 2: carry 1, batch k's speculation predates batches k-1 and
@@ -258,7 +284,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
                            hipStream_t s, const unsigned long long *top_ext = nullptr,
-                           const SeqMerge *merge = nullptr, int carry = 0);
+                           const SeqMerge *merge = nullptr, int carry = 0, SeqMergeIO *mio = nullptr);
 // Node-sharded sequential mode (minisched_gpu.h ms_seq_*): this shard's top-4
 // candidates with records + all-tile filter flags per pod, from the top-4 merge
 // output; and the replicated validation over the shards' gathered lists

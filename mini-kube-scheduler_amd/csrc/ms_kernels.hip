@@ -427,6 +427,45 @@ __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
 // keys against the batch-start state (0-terminated when the tile has fewer
 // than K feasible rows) and the tile's filter flags.
 // ----------------------------------------------------------------------------
+// Tile-list stores and loads coherent across the XCDs within one launch
+// (agent-scope relaxed atomics: the store writes through, the load bypasses a
+// possibly stale L2 line). The in-step merge (k_seq_step, SeqMergeIO) reads the
+// lists of sweep workgroups that ran on other XCDs in the same launch.
+// A/B switches of the in-step merge's synchronisation (round 5):
+//   MS_CTR_SCOPE 0: counter add and polls at agent scope (relaxed); 1: system scope
+//   MS_CTR_SLEEP: s_sleep argument between polls (0: spin)
+//   MS_LIST_FENCE 0: tile lists stored / loaded write-through (st_coh / ld_coh);
+//                 1: plain stores, an agent release fence before the count, an
+//                 acquire fence after the wait, plain loads
+#ifndef MS_CTR_SCOPE
+#define MS_CTR_SCOPE 0
+#endif
+#ifndef MS_CTR_SLEEP
+#define MS_CTR_SLEEP 1
+#endif
+#ifndef MS_LIST_FENCE
+#define MS_LIST_FENCE 0
+#endif
+#if MS_CTR_SCOPE
+#define MS_CTR_SCOPE_ID __HIP_MEMORY_SCOPE_SYSTEM
+#else
+#define MS_CTR_SCOPE_ID __HIP_MEMORY_SCOPE_AGENT
+#endif
+typedef __attribute__((address_space(1))) u64 gu64_t;
+typedef __attribute__((address_space(1))) uint32_t gu32_t;
+__device__ __forceinline__ void st_coh(u64 *p, u64 v) {
+    __hip_atomic_store(((gu64_t *)(p)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(((gu32_t *)(p)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 ld_coh(const u64 *p) {
+    return __hip_atomic_load(((const gu64_t *)(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_coh(const uint32_t *p) {
+    return __hip_atomic_load(((const gu32_t *)(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int kTopK = 4;
 constexpr int kTopExt = 8;  // ranks the merge lists for the validator's slow pods (4 beyond the top-4)
 static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
@@ -495,8 +534,8 @@ __device__ __forceinline__ void sweep_topk_group(const Row *x, uint32_t ord0, co
     for (int n = 0; n < NP; ++n) {
         const uint32_t f = (__ballot(nu_any[n] != 0) ? 1u : 0u) | (__ballot(nrf_any[n] != 0) ? 0x100u : 0u);
         const size_t cell = (size_t)(pbeg + i + n) * n_tiles + tile;
-        if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out[n];
-        if (lane == 0) tile_flags[cell] = f;
+        if (lane < (uint32_t)kTopK) st_coh(tile_keys + cell * kTopK + lane, out[n]);
+        if (lane == 0) st_coh(tile_flags + cell, f);
     }
 }
 
@@ -522,6 +561,7 @@ struct SweepArgs {
     uint32_t *tile_flags;
     uint32_t n_tiles;
     uint32_t fast;  // binary64 LeastAllocated where exact (default 1)
+    uint32_t coh;   // an in-step merge reads the lists in the same launch: stores write through (st_coh)
 };
 
 // One wave, lane = row: tile `tile`'s top-4 lists and filter flags for pods
@@ -591,7 +631,7 @@ constexpr uint32_t kTpPods = 16;
 #define MS_UNROLL(n) MS_PRAGMA(unroll n)
 
 __device__ __forceinline__ void tile_keys_store(u64 *dst, uint32_t j, const u64 (&k)[4]) {
-    *dst = j == 0 ? k[0] : j == 1 ? k[1] : j == 2 ? k[2] : k[3];
+    st_coh(dst, j == 0 ? k[0] : j == 1 ? k[1] : j == 2 ? k[2] : k[3]);
 }
 
 __device__ __forceinline__ void sort4_desc(u64 (&x)[4]) {
@@ -783,8 +823,14 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     if (pi < cnt) {
         const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
         const double mine = part == 0 ? k[0] : part == 1 ? k[1] : part == 2 ? k[2] : k[3];
-        a.tile_keys[cell * kTopK + part] = global_key(mine, a.t.base + tile * kFullWaveTile);
-        if (part == 0) a.tile_flags[cell] = f;
+        const u64 g = global_key(mine, a.t.base + tile * kFullWaveTile);
+        if (a.coh && !MS_LIST_FENCE) {  // (launch-uniform)
+            st_coh(a.tile_keys + cell * kTopK + part, g);
+            if (part == 0) st_coh(a.tile_flags + cell, f);
+        } else {
+            a.tile_keys[cell * kTopK + part] = g;
+            if (part == 0) a.tile_flags[cell] = f;
+        }
     }
     return true;
 #else
@@ -805,7 +851,7 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     if (pi < cnt) {
         const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
         tile_keys_store(a.tile_keys + cell * kTopK + part, part, k);
-        if (part == 0) a.tile_flags[cell] = f;
+        if (part == 0) st_coh(a.tile_flags + cell, f);
     }
     return true;
 #endif
@@ -924,7 +970,8 @@ __device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int6
 // cert: how many ranks are exact. A rank past 3 may miss a row when a tile's
 // full list of four was used up before it (its fifth row is not listed), so
 // the ranks after the one that exhausts a full list are not certified.
-template <int J, int R = kTopK>
+// COH: the lists were written in the same launch (ld_coh).
+template <int J, int R = kTopK, bool COH = false>
 __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_keys,
                                                 const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
                                                 uint32_t lane, u64 &out, uint32_t &f, uint32_t *cert_out = nullptr) {
@@ -937,13 +984,21 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
         const uint32_t tt = lane + 64u * j;
         pos[j] = tt < n_tiles ? 0u : (uint32_t)kTopK;
         const uint32_t tc = min(tt, n_tiles - 1);
-        const uint32_t tf = tile_flags[(size_t)p * n_tiles + tc];
-        const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + ((size_t)p * n_tiles + tc) * kTopK);
-        const uint4 a = q[0], b = q[1];
-        e[j][0] = ((u64)a.y << 32) | a.x;
-        e[j][1] = ((u64)a.w << 32) | a.z;
-        e[j][2] = ((u64)b.y << 32) | b.x;
-        e[j][3] = ((u64)b.w << 32) | b.z;
+        const size_t cell = (size_t)p * n_tiles + tc;
+        uint32_t tf;
+        if constexpr (COH) {
+            tf = ld_coh(tile_flags + cell);
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) e[j][k] = ld_coh(tile_keys + cell * kTopK + k);
+        } else {
+            tf = tile_flags[cell];
+            const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
+            const uint4 a = q[0], b = q[1];
+            e[j][0] = ((u64)a.y << 32) | a.x;
+            e[j][1] = ((u64)a.w << 32) | a.z;
+            e[j][2] = ((u64)b.y << 32) | b.x;
+            e[j][3] = ((u64)b.w << 32) | b.z;
+        }
         if (tt < n_tiles && e[j][0] == 0) fl |= tf;
         if (tt < n_tiles) fa |= tf | (e[j][0] != 0 ? 0x100u : 0u);
     }
@@ -987,7 +1042,7 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
 // ext (optional): ranks 4..7 at ext[p * 4 + r - 4] and the number of certified
 // ranks (4..8) in bits 28-31 of spec_flags (merge_pod_lists).
 // One pod's merge by one wave (k_topk_merge, and k_seq_step's merge workgroups).
-template <int J>
+template <int J, bool COH = false>
 __device__ __forceinline__ void merge_pod(const u64 *__restrict__ tile_keys, const uint32_t *__restrict__ tile_flags,
                                           uint32_t p, uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
                                           uint32_t *__restrict__ spec_flags, const NodeTable &t,
@@ -995,10 +1050,10 @@ __device__ __forceinline__ void merge_pod(const u64 *__restrict__ tile_keys, con
     u64 out;
     uint32_t f, cert = 0;
     if (ext) {
-        merge_pod_lists<J, kTopExt>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert);
+        merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert);
         if (lane >= (uint32_t)kTopK && lane < (uint32_t)kTopExt) ext[(size_t)p * kTopK + lane - kTopK] = out;
     } else {
-        merge_pod_lists<J>(tile_keys, tile_flags, p, n_tiles, lane, out, f);
+        merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f);
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
     if (recs && lane < (uint32_t)kTopK) store_merged_rec(t, out, recs + ((size_t)p * kTopK + lane) * kRecF);
@@ -1940,27 +1995,152 @@ __global__ __launch_bounds__(64) void k_validate_seq(SeqArgs va) {
 // cross-stream hand-off: batch k+1's speculation may predate batch k's binds,
 // which its validation treats as stale (prev lists). W waves per workgroup:
 // the most that fit the validator's VGPRs at one workgroup per CU.
+// Batch k+1's in-step merge (SeqMergeIO, depth 1): n = 0 none.
+struct StepMerge {
+    u64 *top, *spec, *ext;
+    uint32_t *spec_flags, *tags, *ctr;
+    int64_t *recs;
+    uint32_t tag, target, n, skip;
+    const uint32_t *in_tags;  // batch k's tags (in_tag 0: merged by a launch, nothing to check)
+    uint32_t in_tag;
+    u64 *tl;                  // MS_VSTAMPS timeline (SeqMergeIO::tl): this step's row, or null
+};
+// MS_VSTAMPS timeline fields per workgroup: 0 start, 1 swept (counted), 2 worker's
+// wait done, 3 worker's merges done, 4 validator done (workgroup 0), 5 tiles swept
+enum { kTlBegin = 0, kTlSwept, kTlWaited, kTlMerged, kTlValidated, kTlTiles };
+constexpr uint64_t kMergeSpinTicks = 10000;  // a worker's wait for the sweep, s_memrealtime (100 MHz): 100 us
+
+// After its sweep a workgroup counts itself done on sm.ctr (its waves' list
+// stores have landed: write-through, so other XCDs read them with ld_coh).
+// Worker wid (wave W-1 of every sweep workgroup first) then waits for all of
+// them and merges pods wid, wid + W * nsw, .. of the next batch, tagging each.
+// The wait is bounded; a worker that gives up leaves its pods untagged and the
+// next step's validation merges them (step_merge_fallback).
+// MS_VSTAMPS (diagnostic build): the merge path's timeline relative to the
+// workgroup's start (s_memrealtime, 10 ns), summed over worker waves at stats
+// u64 [8+15] sweep done, [8+16] counter wait done, [8+17] merges done, [8+18]
+// their count, [8+19] the workgroups' counter add (summed over workgroups).
+template <int J, int W>
+__device__ __forceinline__ void step_merge(const SweepArgs &sw, const StepMerge &sm, uint32_t sb, uint32_t nsw,
+                                           uint32_t wave, uint32_t lane, uint32_t *stats, uint64_t t_begin) {
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    const uint64_t t_swept = __builtin_amdgcn_s_memrealtime();
+    (void)t_swept;
+#endif
+    __builtin_amdgcn_s_waitcnt(0);  // (gfx9: vmcnt covers stores) this wave's lists have landed
+#if MS_LIST_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the lists reach the agent-coherent level
+#endif
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(((gu32_t *)(sm.ctr)), 1u, __ATOMIC_RELAXED, MS_CTR_SCOPE_ID);
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+#ifdef MS_VSTAMPS
+        atomicAdd(reinterpret_cast<u64 *>(stats + 8) + 19, now - t_begin);
+#endif
+        if (sm.tl) sm.tl[blockIdx.x * 8 + kTlSwept] = now;
+#endif
+    }
+    const uint32_t wid = (W - 1 - wave) * nsw + sb;
+    if (wid >= sm.n || sm.skip) return;  // wave-uniform
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(((const gu32_t *)(sm.ctr)), __ATOMIC_RELAXED, MS_CTR_SCOPE_ID));
+        if ((int32_t)(v - sm.target) >= 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kMergeSpinTicks) return;
+        if (MS_CTR_SLEEP) __builtin_amdgcn_s_sleep(MS_CTR_SLEEP);
+    }
+#if MS_LIST_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale lines of the other workgroups' lists
+#endif
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    const uint64_t t_waited = __builtin_amdgcn_s_memrealtime();
+#endif
+    for (uint32_t p = wid; p < sm.n; p += W * nsw) {
+        merge_pod<J, !MS_LIST_FENCE>(sw.tile_keys, sw.tile_flags, p, sw.n_tiles, sm.top, sm.spec, sm.spec_flags, sw.t,
+                                     sm.recs, sm.ext, lane);
+        if (lane == 0) sm.tags[p] = sm.tag;
+    }
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0 && sm.tl) {
+        sm.tl[blockIdx.x * 8 + kTlWaited] = t_waited;
+        sm.tl[blockIdx.x * 8 + kTlMerged] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+#ifdef MS_VSTAMPS
+    if (lane == 0) {
+        u64 *st = reinterpret_cast<u64 *>(stats + 8);
+        atomicAdd(st + 15, t_swept - t_begin);
+        atomicAdd(st + 16, t_waited - t_begin);
+        atomicAdd(st + 17, __builtin_amdgcn_s_memrealtime() - t_begin);
+        atomicAdd(st + 18, 1ull);
+    }
+#else
+    (void)stats;
+    (void)t_begin;
+#endif
+}
+
+// Validation k's check of its batch's in-step merge (workgroup 0, all W waves,
+// before the prologue): pods whose worker gave up are merged here from the tile
+// lists (written by the previous launch). Returns whether any was.
+template <int J, int W>
+__device__ __forceinline__ bool step_merge_fallback(const SeqArgs &va, const StepMerge &sm, bool any, uint32_t wave,
+                                                    uint32_t lane) {
+    if (!__syncthreads_or(any)) return false;
+    for (uint32_t p = wave; p < va.n_pods; p += W)
+        if (sm.in_tags[p] != sm.in_tag) {  // (wave-uniform)
+            merge_pod<J>(va.tile_keys, va.tile_flags, p, va.n_tiles, const_cast<u64 *>(va.top4),
+                         const_cast<u64 *>(va.spec), const_cast<uint32_t *>(va.spec_flags), va.t,
+                         const_cast<int64_t *>(va.top4_recs), const_cast<u64 *>(va.top_ext), lane);
+            if (lane == 0) atomicAdd(&va.stats[40], 1u);  // (u32 40: pods merged by the fallback)
+        }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (no stale L1 lines of the merged entries)
+    __syncthreads();
+    return true;
+}
+
 template <int J, int W>
 __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks, MergeArgs mg,
-                                                     uint32_t merge_wgs) {
+                                                     uint32_t merge_wgs, StepMerge sm) {
     __shared__ SeqShared S;
-#ifdef MS_VSTAMPS  // wave durations (s_memrealtime, 100 MHz): u64 stats[8+9] validator, [8+10] sweep waves, [8+11] their count
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)  // wave durations (s_memrealtime, 100 MHz): u64 stats[8+9] validator, [8+10] sweep waves, [8+11] their count
     const u64 t_begin = __builtin_amdgcn_s_memrealtime();
+    if (sm.tl && threadIdx.x == 0 && blockIdx.x < kTimelineWgs) sm.tl[blockIdx.x * 8 + kTlBegin] = t_begin;
 #endif
     if (blockIdx.x == 0) {
         // the bulk prologue copies by all W waves (MS_WG_PROLOGUE=0: by the validating wave alone, A/B)
 #ifndef MS_WG_PROLOGUE
 #define MS_WG_PROLOGUE 1
 #endif
+        // the tags of an in-step merged batch, loaded beside the prologue's loads
+        const bool check = sm.in_tag != 0u && va.n_pods;
+        uint32_t tg = sm.in_tag;
+        if (check && threadIdx.x < va.n_pods) tg = sm.in_tags[threadIdx.x];
         if (MS_WG_PROLOGUE && va.n_pods) {
             validate_prologue_wg(S, va, threadIdx.x, 64u * W);
             __builtin_amdgcn_s_waitcnt(0);
+            if (check && step_merge_fallback<J, W>(va, sm, tg != sm.in_tag, threadIdx.x >> 6, lane_id())) {
+                validate_prologue_wg(S, va, threadIdx.x, 64u * W);  // again, with the merged entries
+                __builtin_amdgcn_s_waitcnt(0);
+            }
             __syncthreads();
+        } else if (check) {
+            step_merge_fallback<J, W>(va, sm, tg != sm.in_tag, threadIdx.x >> 6, lane_id());
         }
         if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x, MS_WG_PROLOGUE != 0);
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+        if (threadIdx.x == 0 && va.n_pods) {
+            const u64 now = __builtin_amdgcn_s_memrealtime();
 #ifdef MS_VSTAMPS
-        if (threadIdx.x == 0 && va.n_pods)
-            atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 9, __builtin_amdgcn_s_memrealtime() - t_begin);
+            atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 9, now - t_begin);
+#endif
+            if (sm.tl) sm.tl[kTlValidated] = now;
+        }
 #endif
         return;
     }
@@ -1999,6 +2179,11 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         for (uint32_t task = sb * W + wave; task < n_tasks; task += sg * W)
             sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
     }
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (sm.n) step_merge<J, W>(sw, sm, sb, sg, wave, lane, va.stats, t_begin);  // (workgroup-uniform)
+#else
+    if (sm.n) step_merge<J, W>(sw, sm, sb, sg, wave, lane, va.stats, 0);  // (workgroup-uniform)
+#endif
 #ifdef MS_VSTAMPS
     if (lane == 0 && sb * W + wave < n_tasks) {
         atomicAdd(reinterpret_cast<u64 *>(va.stats + 8) + 10, __builtin_amdgcn_s_memrealtime() - t_begin);
@@ -2557,6 +2742,12 @@ hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod
     return hipGetLastError();
 }
 
+// In-step merge (SeqMergeIO): the transposed sweep, a tile per workgroup, all
+// of them resident (one per CU beside the validator's).
+bool seq_step_merges(const NodeTable &t, uint32_t n_tiles, uint32_t n_next) {
+    return n_next && t.drow && seq_fast() && n_tiles <= 64u * kSeqMaxJ;
+}
+
 hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles, uint32_t seed32,
                            const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *tile_keys,
                            const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
@@ -2564,7 +2755,8 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s, const unsigned long long *top_ext, const SeqMerge *merge, int carry) {
+                           hipStream_t s, const unsigned long long *top_ext, const SeqMerge *merge, int carry,
+                           SeqMergeIO *mio) {
     if (n_pods == 0 && n_next == 0 && !(merge && merge->n_pods)) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
         (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
@@ -2581,8 +2773,8 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     if (n_next) chunk = std::min(64u, std::max(8u, cdiv(n_tiles * n_next, (cus - 1) * W)));
     const bool tp = t.drow && seq_fast();
     if (tp) chunk = kTpPods;  // transposed form: a tile per sweep workgroup
-    const SweepArgs sw = {t,       n_rows,         next_pods,       n_next,  chunk,
-                          seed32,  next_tile_keys, next_tile_flags, n_tiles, seq_fast()};
+    SweepArgs sw = {t,       n_rows,         next_pods,       n_next,  chunk,
+                    seed32,  next_tile_keys, next_tile_flags, n_tiles, seq_fast(), 0u};
     const uint32_t n_tasks = n_next ? n_tiles * cdiv(n_next, chunk) : 0u;
     // merge workgroups (a pod per wave) between the validator's and the sweep's
     MergeArgs mg = {};
@@ -2594,8 +2786,33 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     }
     const uint32_t room = cus > 1u + merge_wgs ? cus - 1u - merge_wgs : 1u;
     const uint32_t grid = 1u + merge_wgs + (n_tasks ? std::min(room, tp ? n_tiles : cdiv(n_tasks, W)) : 0u);
+    StepMerge sm = {};
+    if (mio) {
+        sm.in_tags = mio->in_tags;
+        sm.in_tag = mio->in_tags ? mio->in_tag : 0u;
+        if (mio->top && n_next && !merge_wgs && seq_step_merges(t, n_tiles, n_next)) {
+            if (!mio->tags || !mio->ctr || !mio->spec || !mio->spec_flags) return hipErrorInvalidValue;
+            mio->target += grid - 1u;  // every sweep workgroup counts once
+            sm.top = mio->top;
+            sm.spec = mio->spec;
+            sm.ext = mio->ext;
+            sm.spec_flags = mio->spec_flags;
+            sm.tags = mio->tags;
+            sm.ctr = mio->ctr;
+            sm.recs = mio->recs;
+            sm.tag = mio->tag;
+            sm.target = mio->target;
+            sm.n = n_next;
+            sm.skip = mio->skip ? 1u : 0u;
+            sw.coh = 1u;
+        } else if (mio->top) {
+            return hipErrorInvalidValue;  // (the caller asked for an in-step merge seq_step_merges rules out)
+        }
+        if (mio->tl && mio->tl_step < kTimelineSteps && grid <= kTimelineWgs)
+            sm.tl = reinterpret_cast<u64 *>(mio->tl) + (size_t)mio->tl_step * kTimelineWgs * 8;
+    }
 #define MS_STEP(JJ, WW) \
-    hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, mg, merge_wgs)
+    hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, mg, merge_wgs, sm)
     if (J == 1) MS_STEP(1, 12);
     else if (J == 2) MS_STEP(2, 12);
     else if (J == 4) MS_STEP(4, 12);

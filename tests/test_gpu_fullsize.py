@@ -99,6 +99,22 @@ def test_config_e_full():
                                                           minlength=50_000).astype(np.int64))
 
 
+@pytest.mark.parametrize("merge", ["launch", "fallback"])
+def test_config_e_merge_forms(merge, monkeypatch):
+    # config E with batch k+1's merge inside step k ("fallback": the in-step
+    # workers skip and every validation merges its batch itself) equals the fixture
+    monkeypatch.setenv("MINISCHED_SEQ_MERGE", merge)
+    fx = np.load(os.path.join(HERE, "golden", "config_e_full_seed1.npz"))
+    nr = synth.nodes(50_000, seed=1, resources=True)
+    pr = synth.pods(200_000, seed=1, resources=True)
+    o = {k: fx[k] for k in ("node", "code", "score", "mask")}
+    with Engine(max_nodes=50_000, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=1) as e:
+        e.upsert(np.arange(50_000), nr)
+        assert_same(e.schedule(pr, MODE_SEQUENTIAL), o, "E, merge " + merge)
+        assert _table_digest(e.read(0, 50_000)) == str(fx["table_sha256"])
+        assert e.info()._pad == 0
+
+
 def test_nunn_pp_rows_above_one_workgroup(oracle):
     # more rows than one K1 pp workgroup holds (122,880): grid.y workgroups per pod
     # chunk combine with atomicMax, then a separate decode

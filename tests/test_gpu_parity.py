@@ -415,6 +415,26 @@ def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch, pipe):
             assert e.info()._pad == 0
 
 
+@pytest.mark.parametrize("merge", ["launch", "fallback"])
+@pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
+def test_resource_sequential_merge_forms(oracle, monkeypatch, batch, merge):
+    # batch k+1's top-4 merge inside step k (the sweep workgroups merge once all
+    # have written its tile lists), and the fallback where every in-step worker
+    # skips and each validation merges its own batch first
+    monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
+    monkeypatch.setenv("MINISCHED_SEQ_PIPE", "fused")
+    monkeypatch.setenv("MINISCHED_SEQ_MERGE", merge)
+    for n_nodes, n_pods in ((50, 600), (2500, 3000)):
+        seed = 13 * n_nodes + int(batch)
+        nr = synth.nodes(n_nodes, seed=seed, resources=True)
+        pr = synth.pods(n_pods, seed=seed, resources=True)
+        o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed)
+        with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed) as e:
+            assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
+            assert_table_equal(e, o["cols"], n_nodes)
+            assert e.info()._pad == 0
+
+
 @pytest.mark.parametrize("n_nodes", [20_000, 100_000, 140_000])
 def test_resource_sequential_tile_counts(oracle, n_nodes):
     # validator register layouts for 79, 391 and 547 tiles (2, 8 and 16 lists per lane)
