@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 4
+#define MS_ABI_VERSION 5
 
 /* ---- return codes -------------------------------------------------------- */
 #define MS_OK 0
@@ -69,6 +69,16 @@ extern "C" {
  * PreferNoSchedule ids only tolerations with that or an empty effect can).
  * (k8s@v1.22.0 plugins/tainttoleration/taint_toleration.go, restated.) */
 #define MS_PLUGINS_NU_TT_NN 3
+/* Filter[NU]; Score[NN (weight w0), NodeAffinity with SEVERAL preferred terms
+ * (weight w1), ScoreExtensions = DefaultNormalizeScore(MaxNodeScore,
+ * reverse=false) run by the in-loop hook exactly as written]. A pod's terms are
+ * a term set (ms_nam_term_set) registered with ms_nam_term_sets; the pod record
+ * names it by id = pref_zone | pref_weight << 8 (0 = no terms). Raw scores are
+ * sums of matching term weights, up to 400, so the hook rescales earlier
+ * entries whenever a later node's raw score exceeds 100. Terms
+ * test the node's zone label (ms_node_rec.zone) or its second label
+ * (ms_node_rec.label2). */
+#define MS_PLUGINS_NU_NN_NAM 4
 
 /* ---- modes --------------------------------------------------------------- */
 #define MS_MODE_BATCHED 0    /* all pods of the call see the same node state               */
@@ -96,7 +106,9 @@ typedef struct ms_node_rec {
     uint8_t name_digit;    /* last char of node name as 0..9; 0xFF = not a digit     */
     uint8_t zone;          /* value id of the node's topology.kubernetes.io/zone
                               label, 0 = unlabelled (MS_PLUGINS_NU_NN_NA)           */
-    uint8_t _pad0;
+    uint8_t label2;        /* value id of the node's second label (the shim's key,
+                              e.g. node.kubernetes.io/instance-type), 0 = unlabelled
+                              (MS_PLUGINS_NU_NN_NAM term key 1)                      */
     int32_t allowed_pods;  /* NodeInfo.Allocatable.AllowedPodNumber                 */
     int32_t pod_count;     /* len(NodeInfo.Pods)                                    */
     uint32_t taints;       /* MS_PLUGINS_NU_TT_NN: taint ids (bits 0-7 NoSchedule /
@@ -155,7 +167,7 @@ typedef struct ms_config {
     uint32_t max_nodes;  /* node capacity of this context                       */
     uint32_t node_base;  /* global ordinal of local node 0 (shard offset)       */
     uint32_t max_batch;  /* pods per internal chunk of ms_schedule_batch        */
-    /* score plugin weights (MS_PLUGINS_NU_NN_NA only; 0 means 1): [0] NodeNumber,
+    /* score plugin weights (MS_PLUGINS_NU_NN_NA / _NAM only; 0 means 1): [0] NodeNumber,
      * [1] NodeAffinity. The reference sums unweighted ("TODO: plugin weight",
      * minisched.go:186); weights 1/1 reproduce it. w0*10 + w1*100 < 2048. */
     uint16_t score_weight[2];
@@ -349,6 +361,38 @@ int ms_tt_summaries_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_
                            void *stream);
 int ms_tt_decode_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
                         const void *summaries_all_dev, ms_result *results_dev, void *stream);
+
+/* ---- MS_PLUGINS_NU_NN_NAM: several preferred NodeAffinity terms ----------- */
+/* One PreferredSchedulingTerm: its NodeSelectorTerm tests one node label
+ * (key 0: ms_node_rec.zone, 1: ms_node_rec.label2) with operator In [value]
+ * (value id 1..254) or Exists (value 0xFF); weight 1..100, 0 = unused slot. */
+typedef struct ms_pref_term {
+    uint8_t key, value, weight, _pad;
+} ms_pref_term;
+#define MS_NAM_TERMS 4
+typedef struct ms_nam_term_set {
+    ms_pref_term term[MS_NAM_TERMS];
+} ms_nam_term_set; /* 16 bytes */
+/* Registers the context's term sets: pod term set id s (1..n_sets) is
+ * sets[s - 1]; ids above n_sets count as no terms. Copied; replaces the
+ * previous table (stream-ordered after earlier calls). Up to 65535 sets. */
+int ms_nam_term_sets(ms_ctx *ctx, uint32_t n_sets, const ms_nam_term_set *sets);
+/* Node shards (contexts with their own node_base, ordinals = LIST order) of
+ * one MS_PLUGINS_NU_NN_NAM cycle, for a caller with its own collectives:
+ *   1. ms_nam_segment_device: per pod, this shard's rescale composition (an
+ *      opaque MS_NAM_SEG_BYTES record: the composed map of its nodes' in-loop
+ *      rescales on 0..100 and whether a feasible node scored > 0);
+ *   2. the caller gathers them shard-major (segs_all[s][p], shards in ordinal
+ *      order);
+ *   3. ms_nam_keys_device: this shard's packed keys (keys_dev, n_pods x u64) of
+ *      the pods' FINAL scores: its nodes' raw scores through the rescales of
+ *      every later node of the cluster, the first non-zero node of the cluster
+ *      at 100. The element-wise uint64 MAX over the shards is selectHost over
+ *      the cluster; ms_decode_device (flags NULL) turns it into results. */
+#define MS_NAM_SEG_BYTES 104u
+int ms_nam_segment_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, void *seg_dev, void *stream);
+int ms_nam_keys_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                       uint32_t shard_index, const void *segs_all_dev, unsigned long long *keys_dev, void *stream);
 
 /* Whole exact sequential cycle on device-resident pods (single shard; on a
  * context joined to a communicator, the node-sharded cycle below). */

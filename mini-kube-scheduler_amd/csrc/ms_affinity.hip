@@ -1,0 +1,333 @@
+// ms_affinity.hip — plugin set MS_PLUGINS_NU_NN_NAM: Filter[NodeUnschedulable];
+// Score[NodeNumber, NodeAffinity with several preferred terms], NodeAffinity's
+// ScoreExtensions = DefaultNormalizeScore(MaxNodeScore, reverse=false)
+// (k8s@v1.22.0 plugins/nodeaffinity/node_affinity.go, helper/normalize_score.go;
+// restated) run by RunScorePlugins' in-loop hook exactly as written
+// (/root/reference/minisched/minisched.go:164-185).
+//
+// With several terms a raw score (the sum of the matching terms' weights)
+// reaches 400. Once an entry is non-zero the list maximum is 100 after every
+// step, so step i is the identity when r_i <= 100 and otherwise rescales every
+// EARLIER entry by f_{r_i}(v) = floor(100 v / r_i) (entry i ends at 100); the
+// first non-zero node (the anchor) starts at 100. Node j's final score is
+// T_{>j}(v_j): v_j = 100 for the anchor and for r_j > 100, else r_j, and T_{>j}
+// the composition of the rescales of every later feasible node (oracle/
+// ms_oracle.c nam_closed). Compositions of such maps on 0..100 are 101-entry
+// tables that compose associatively, so a LIST-ordered row segment summarises
+// as ONE table (its rescales composed) plus "has a non-zero node":
+//   k_nam_seg   per (segment, pod): that table, forward over the segment's rows
+//               (T <- f_r o T at each rescale);
+//   k_nam_keys  per (segment, pod): the suffix table of the later segments (and
+//               of the later node shards) composed, then the segment's rows in
+//               REVERSE order keeping T_{>j} (T <- T o f_r after each rescale)
+//               and the best packed key; the anchor decided by whether an
+//               earlier segment or shard has a non-zero node. atomicMax over the
+//               segments; node shards combine by uint64 MAX like NU+NN.
+// Lane = pod, rows streamed through LDS. A lane's table lives in LDS (a 108-B
+// row per lane); a rescale updates one table with all 64 lanes of the wave
+// (one lane per table entry, 2 passes), the lanes with a rescale on the same row
+// taken in turn by a ballot loop. Every f_r maps 1..100 below itself, so a table
+// is all 0 after at most 100 rescales; a lane whose T(100) is 0 stops updating.
+#include <algorithm>
+
+#include "ms_device.h"
+
+namespace msgpu {
+
+namespace {
+
+constexpr uint32_t kNamThreads = 256;  // pods per workgroup (one per lane)
+constexpr uint32_t kNamTile = 1024;    // rows staged in LDS per pass
+constexpr uint32_t kNamSegRows = 2048, kNamMaxSegs = 16;
+constexpr uint32_t kNamStride = 108;   // bytes per lane table in LDS: 27 words (odd: per-lane gathers spread banks)
+
+constexpr uint32_t kNamComposeThreads = 128;
+
+struct NamSeg {
+    uint8_t T[101];  // the composed rescale map on 0..100
+    uint8_t any;     // a feasible node of the segment has a non-zero raw score
+    uint8_t _pad[2];
+};
+static_assert(sizeof(NamSeg) == MS_NAM_SEG_BYTES, "NamSeg layout");
+
+// Row word staged in LDS: bit 0 absent, bit 1 unschedulable, zone << 8,
+// label2 << 16, digit << 24 (15 = none).
+__device__ __forceinline__ uint32_t nam_row_word(const NodeTable &t, uint32_t r) {
+    const uint8_t f = t.flags[r];
+    const uint32_t d = t.digit[r];
+    return ((f & kNodeAbsent) ? 1u : 0u) | ((f & kNodeUnschedulable) ? 2u : 0u) | ((uint32_t)t.zone[r] << 8) |
+           ((uint32_t)t.label2[r] << 16) | ((d <= 9u ? d : 15u) << 24);
+}
+
+// A pod's terms, one word each: the label's bit offset in the row word
+// (8 zone, 16 label2), the matching label window [lo, lo + span] (In: value,
+// span 0; Exists: 1..254), weight (0: unused).
+struct NamTerms {
+    uint32_t sh[MS_NAM_TERMS], lo[MS_NAM_TERMS], span[MS_NAM_TERMS], w[MS_NAM_TERMS];
+};
+
+__device__ __forceinline__ NamTerms load_terms(const ms_pod_rec &pod, const ms_nam_term_set *sets, uint32_t n_sets) {
+    NamTerms m;
+    const uint32_t sid = (uint32_t)pod.pref_zone | (uint32_t)pod.pref_weight << 8;
+    ms_nam_term_set st = {};
+    if (sid != 0u && sid <= n_sets) st = sets[sid - 1u];
+#pragma unroll
+    for (int k = 0; k < MS_NAM_TERMS; ++k) {
+        const ms_pref_term x = st.term[k];
+        m.sh[k] = x.key ? 16u : 8u;
+        m.lo[k] = x.value == 0xFFu ? 1u : x.value;
+        m.span[k] = x.value == 0xFFu ? 253u : 0u;
+        m.w[k] = x.value == 0u ? 0u : x.weight;  // (value 0 = "unlabelled" never matches)
+    }
+    return m;
+}
+
+// NodeAffinity.Score: the sum of the weights of the matching terms.
+__device__ __forceinline__ uint32_t nam_raw(uint32_t w, const NamTerms &m) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < MS_NAM_TERMS; ++k) {
+        const uint32_t lab = (w >> m.sh[k]) & 0xFFu;
+        r += (lab - m.lo[k] <= m.span[k]) ? m.w[k] : 0u;
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool nam_feasible(uint32_t w, uint32_t tol) { return (w & (tol ? 1u : 3u)) == 0u; }
+
+// The identity map in a lane's LDS table.
+__device__ __forceinline__ void table_identity(uint8_t *row) {
+    for (uint32_t v = 0; v <= 100u; v += 4u) {
+        const uint32_t x = v | (v + 1u) << 8 | (v + 2u) << 16 | (v + 3u) << 24;
+        *reinterpret_cast<uint32_t *>(row + v) = x;
+    }
+}
+
+// f_r o T on table `row` (every lane of the wave: entries lane, lane + 64).
+__device__ __forceinline__ void table_post(uint8_t *row, uint32_t r, uint32_t lane) {
+    for (uint32_t v = lane; v <= 100u; v += 64u) row[v] = (uint8_t)((100u * row[v]) / r);
+}
+
+// T o f_r on table `row` (reads of both passes before the writes).
+__device__ __forceinline__ void table_pre(uint8_t *row, uint32_t r, uint32_t lane) {
+    const uint32_t v0 = lane, v1 = lane + 64u;
+    const uint8_t a = row[(100u * v0) / r];
+    const uint8_t b = v1 <= 100u ? row[(100u * v1) / r] : 0;
+    __builtin_amdgcn_wave_barrier();
+    row[v0] = a;
+    if (v1 <= 100u) row[v1] = b;
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void seg_bounds(uint32_t n_rows, uint32_t seg_rows, uint32_t seg, uint32_t &r0,
+                                           uint32_t &r1) {
+    r0 = seg * seg_rows;
+    r1 = min(n_rows, r0 + seg_rows);
+}
+
+// grid (pod blocks, segments): the segment's composed rescale table per pod.
+__global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
+                                                         const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                                                         const ms_nam_term_set *__restrict__ sets, uint32_t n_sets,
+                                                         NamSeg *__restrict__ out) {
+    __shared__ uint32_t tile[kNamTile];
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
+    const uint32_t p = blockIdx.x * kNamThreads + tid;
+    uint32_t r0, r1;
+    seg_bounds(n_rows, seg_rows, blockIdx.y, r0, r1);
+    ms_pod_rec pod = {};
+    if (p < n_pods) pod = pods[p];
+    const NamTerms m = load_terms(pod, sets, n_sets);
+    const uint32_t tol = pod.tolerates_unschedulable ? 1u : 0u;
+    uint8_t *mine = tabs + tid * kNamStride;
+    table_identity(mine);
+    uint32_t any = 0, top = 100;  // top = T(100): 0 once the table is all 0
+    for (uint32_t base = r0; base < r1; base += kNamTile) {
+        const uint32_t nt = min(kNamTile, r1 - base);
+        __syncthreads();
+        for (uint32_t i = tid; i < nt; i += kNamThreads) tile[i] = nam_row_word(t, base + i);
+        __syncthreads();
+        for (uint32_t i = 0; i < nt; ++i) {
+            const uint32_t w = tile[i];  // (LDS broadcast)
+            const bool f = nam_feasible(w, tol);
+            const uint32_t r = nam_raw(w, m);
+            any |= (f && r > 0u) ? 1u : 0u;
+            uint64_t b = __ballot(f && r > 100u && top != 0u);
+            while (b) {  // (wave-uniform) the lanes with a rescale here, one table at a time
+                const uint32_t L = (uint32_t)__builtin_ctzll(b);
+                b &= b - 1u;
+                const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
+                table_post(tabs + (wbase + L) * kNamStride, rl, lane);
+                __builtin_amdgcn_wave_barrier();
+                if (lane == L) top = mine[100];
+            }
+        }
+    }
+    if (p >= n_pods) return;
+    mine[101] = (uint8_t)any;
+    mine[102] = mine[103] = 0;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(mine);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(out + (size_t)blockIdx.y * n_pods + p);
+#pragma unroll
+    for (int k = 0; k < (int)(MS_NAM_SEG_BYTES / 4); ++k) dst[k] = src[k];
+}
+
+// Per pod: out = the composition of n segment records in order (in[s * stride + p], s
+// ascending: out.T = T_{n-1} o .. o T_0) and the OR of their "any". With skip_to:
+// only the records s > skip_to (a shard's suffix), and m_in gets the OR of the
+// records s < skip_to.
+__global__ void k_nam_compose(const NamSeg *__restrict__ in, uint32_t stride, uint32_t n, uint32_t n_pods,
+                              int32_t skip_to, NamSeg *__restrict__ out, uint8_t *__restrict__ m_in) {
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamComposeThreads * kNamStride];
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pods) return;
+    uint8_t *U = tabs + threadIdx.x * kNamStride;  // (LDS, not a dynamically indexed private array)
+    table_identity(U);
+    uint32_t any = 0, before = 0;
+    for (uint32_t s = 0; s < n; ++s) {
+        const NamSeg *x = in + (size_t)s * stride + p;
+        if (skip_to >= 0 && (int32_t)s < skip_to) {
+            before |= x->any;
+            continue;
+        }
+        if (skip_to >= 0 && (int32_t)s == skip_to) continue;
+        any |= x->any;
+        if (U[100] == 0) continue;  // (all 0 stays all 0)
+        for (uint32_t v = 0; v <= 100u; ++v) U[v] = x->T[U[v]];
+    }
+    U[101] = (uint8_t)any;
+    U[102] = U[103] = 0;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(U);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(out + p);
+#pragma unroll
+    for (int k = 0; k < (int)(MS_NAM_SEG_BYTES / 4); ++k) dst[k] = src[k];
+    if (m_in) m_in[p] = (uint8_t)before;
+}
+
+// grid (pod blocks, segments): the segment's best packed key per pod (atomicMax
+// into keys). local: this context's segment records [n_segs][n_pods]; after /
+// m_in (node shards): the later shards' composed table and "an earlier shard has
+// a non-zero node" per pod, or null (single shard).
+__global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
+                                                          const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
+                                                          const ms_nam_term_set *__restrict__ sets, uint32_t n_sets,
+                                                          uint32_t seed32, uint32_t w_nn, uint32_t w_na,
+                                                          const NamSeg *__restrict__ local, uint32_t n_segs,
+                                                          const NamSeg *__restrict__ after,
+                                                          const uint8_t *__restrict__ m_in, u64 *__restrict__ keys) {
+    __shared__ uint32_t tile[kNamTile];
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
+    const uint32_t p = blockIdx.x * kNamThreads + tid;
+    const uint32_t seg = blockIdx.y;
+    uint32_t r0, r1;
+    seg_bounds(n_rows, seg_rows, seg, r0, r1);
+    const bool live = p < n_pods;
+    ms_pod_rec pod = {};
+    if (live) pod = pods[p];
+    const NamTerms m = load_terms(pod, sets, n_sets);
+    const uint32_t tol = pod.tolerates_unschedulable ? 1u : 0u;
+    const uint32_t pd = pod.name_digit >= 0 && pod.name_digit <= 9 ? (uint32_t)pod.name_digit : 14u;
+    const uint32_t A = tb_pod(seed32, pod.ordinal);
+    // T_{>segment}: the later segments' tables, then the later shards'
+    uint8_t *mine = tabs + tid * kNamStride;
+    table_identity(mine);
+    uint32_t before = (live && m_in) ? m_in[p] : 0u;
+    if (live) {
+        for (uint32_t s = 0; s < seg; ++s) before |= local[(size_t)s * n_pods + p].any;
+        for (uint32_t s = seg + 1; s < n_segs && mine[100] != 0; ++s) {
+            const uint8_t *T = local[(size_t)s * n_pods + p].T;
+            for (uint32_t v = 0; v <= 100u; ++v) mine[v] = T[mine[v]];
+        }
+        if (after && mine[100] != 0) {
+            const uint8_t *T = after[p].T;
+            for (uint32_t v = 0; v <= 100u; ++v) mine[v] = T[mine[v]];
+        }
+    }
+    uint32_t top = mine[100];
+    u64 best = 0, cand_reg = 0, cand_anc = 0;
+    bool cand = false;
+    const uint32_t n_tiles = r1 > r0 ? (r1 - r0 + kNamTile - 1u) / kNamTile : 0u;
+    for (uint32_t ti = n_tiles; ti-- > 0;) {  // tiles and rows in reverse LIST order
+        const uint32_t base = r0 + ti * kNamTile, nt = min(kNamTile, r1 - base);
+        __syncthreads();
+        for (uint32_t i = tid; i < nt; i += kNamThreads) tile[i] = nam_row_word(t, base + i);
+        __syncthreads();
+        for (uint32_t i = nt; i-- > 0;) {
+            const uint32_t w = tile[i];
+            const bool f = nam_feasible(w, tol);
+            const uint32_t r = nam_raw(w, m);
+            if (f) {
+                const uint32_t ord = t.base + base + i;
+                const uint32_t h = tb_hash(A, ord);
+                const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
+                if (r == 0u) {
+                    best = umax64(best, make_key(sn, h, ord));  // (T(0) = 0)
+                } else {
+                    // a later non-zero node is not the anchor: its regular key counts
+                    if (cand) best = umax64(best, cand_reg);
+                    cand = true;
+                    cand_reg = make_key(sn + w_na * mine[min(r, 100u)], h, ord);
+                    cand_anc = make_key(sn + w_na * top, h, ord);
+                }
+            }
+            uint64_t b = __ballot(f && r > 100u && top != 0u);
+            while (b) {  // (wave-uniform) this row's rescale applies to the earlier rows
+                const uint32_t L = (uint32_t)__builtin_ctzll(b);
+                b &= b - 1u;
+                const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
+                table_pre(tabs + (wbase + L) * kNamStride, rl, lane);
+                if (lane == L) top = mine[100];
+            }
+        }
+    }
+    if (!live) return;
+    // the segment's first non-zero node is the anchor unless an earlier segment or shard has one
+    if (cand) best = umax64(best, before ? cand_reg : cand_anc);
+    if (best) atomicMax(keys + p, best);
+}
+
+inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+uint32_t nam_segments(uint32_t n_rows, uint32_t *seg_rows) {
+    uint32_t sr = std::max(kNamSegRows, cdiv(std::max(n_rows, 1u), kNamMaxSegs));
+    sr = cdiv(sr, kNamTile) * kNamTile;
+    if (seg_rows) *seg_rows = sr;
+    return std::max(1u, cdiv(n_rows, sr));
+}
+
+hipError_t launch_nam_seg(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                          const void *sets, uint32_t n_sets, void *segs, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    uint32_t sr = 0;
+    const uint32_t ns = nam_segments(n_rows, &sr);
+    hipLaunchKernelGGL(k_nam_seg, dim3(cdiv(n_pods, kNamThreads), ns), dim3(kNamThreads), 0, s, t, n_rows, sr, pods,
+                       n_pods, static_cast<const ms_nam_term_set *>(sets), n_sets, static_cast<NamSeg *>(segs));
+    return hipGetLastError();
+}
+
+hipError_t launch_nam_compose(const void *in, uint32_t stride, uint32_t n, uint32_t n_pods, int32_t skip_to,
+                              void *out, uint8_t *m_in, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nam_compose, dim3(cdiv(n_pods, kNamComposeThreads)), dim3(kNamComposeThreads), 0, s, static_cast<const NamSeg *>(in),
+                       stride, n, n_pods, skip_to, static_cast<NamSeg *>(out), m_in);
+    return hipGetLastError();
+}
+
+hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           const void *sets, uint32_t n_sets, uint32_t seed32, uint32_t w_nn, uint32_t w_na,
+                           const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys,
+                           hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    uint32_t sr = 0;
+    const uint32_t ns = nam_segments(n_rows, &sr);
+    hipLaunchKernelGGL(k_nam_keys, dim3(cdiv(n_pods, kNamThreads), ns), dim3(kNamThreads), 0, s, t, n_rows, sr, pods,
+                       n_pods, static_cast<const ms_nam_term_set *>(sets), n_sets, seed32, w_nn, w_na,
+                       static_cast<const NamSeg *>(local), ns, static_cast<const NamSeg *>(after), m_in, keys);
+    return hipGetLastError();
+}
+
+}  // namespace msgpu

@@ -46,7 +46,7 @@ void free_all(ms_ctx *c) {
     (void)hipSetDevice(c->cfg.device);
     comm_free(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *dev[] = {c->t.planes, c->t.zone, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
+    void *dev[] = {c->t.planes, c->t.zone, c->t.label2, c->d_terms, c->d_nam, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
@@ -520,12 +520,59 @@ int tt_summaries_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, vo
     return tt_cycle_locked(c, n_pods, d_pods, out, nullptr, 0, s);
 }
 
+// MS_PLUGINS_NU_NN_NAM scratch for chunks of n pods: the per-(segment, pod)
+// rescale tables, then one record (the later shards' table) and one byte (an
+// earlier shard has a non-zero node) per pod. Every NAM call runs on the
+// context stream or chains back into it, so one scratch serves them in order.
+int ensure_nam(ms_ctx *c, uint32_t n) {
+    const size_t need = ((size_t)nam_segments(c->rows_dev) + 1u) * n * MS_NAM_SEG_BYTES + n;
+    if (need <= c->nam_bytes) return MS_OK;
+    if (c->d_nam) (void)hipFree(c->d_nam);
+    c->d_nam = nullptr;
+    c->nam_bytes = 0;
+    if (hipMalloc(&c->d_nam, need) != hipSuccess) return fail(c, MS_E_OOM, "NodeAffinity rescale tables");
+    c->nam_bytes = need;
+    return MS_OK;
+}
+
+// This shard's packed keys of nb pods into keys (chunk already sized): its row
+// segments' tables, then per segment the best key under the later segments' and
+// (after / m_in, node shards) the later shards' rescales.
+int nam_keys_locked(ms_ctx *c, uint32_t nb, const ms_pod_rec *d_pods, const void *after, const uint8_t *m_in,
+                    unsigned long long *keys, hipStream_t s) {
+    MS_HIP(c, launch_fill_keys(keys, nb, c->present_dev ? kKeyListed : 0ull, s));
+    MS_HIP(c, launch_nam_seg(c->t, c->rows_dev, d_pods, nb, c->d_terms, c->n_terms, c->d_nam, s));
+    MS_HIP(c, launch_nam_keys(c->t, c->rows_dev, d_pods, nb, c->d_terms, c->n_terms, seed32_of(c->cfg.seed), c->w_nn,
+                              c->w_na, c->d_nam, after, m_in, keys, s));
+    return MS_OK;
+}
+
+// The single-shard NAM cycle: keys per chunk, decode, and with commit each
+// winner's NodeInfo.AddPod (stateless: no later pod reads it).
+int nam_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, int commit,
+                     hipStream_t s) {
+    const uint32_t B = c->batch_cap;
+    int rc = ensure_nam(c, std::min(B, n_pods));
+    if (rc) return rc;
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        rc = nam_keys_locked(c, nb, d_pods + s0, nullptr, nullptr, c->d_keys, s);
+        if (rc) return rc;
+        MS_HIP(c, launch_decode(d_pods + s0, nb, c->d_keys, nullptr, c->present_dev, d_res + s0, s));
+        if (commit) MS_HIP(c, launch_apply_binds(c->t, d_pods + s0, nb, d_res + s0, s));
+    }
+    return MS_OK;
+}
+
 // This shard's keys (and filter flags for the resource-aware set) for a batch.
 int sweep_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, unsigned long long *keys, uint32_t *flags,
                  hipStream_t s, hipEvent_t done) {
     const uint32_t seed32 = seed32_of(c->cfg.seed);
     if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN)
         return fail(c, MS_E_INVAL, "TaintToleration shards combine by summaries (ms_tt_summaries_device), not keys");
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NAM)
+        return fail(c, MS_E_INVAL, "multi-term NodeAffinity shards exchange rescale tables first "
+                                   "(ms_nam_segment_device, ms_nam_keys_device)");
     if (c->cfg.plugin_set == MS_PLUGINS_NU_NN) {
         MS_HIP(c, launch_sweep_pp(c->t, c->rows_dev, d_pods, n_pods, seed32, keys, nullptr, c->present_dev,
                                   c->num_cus, s, 0, done));
@@ -564,6 +611,12 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
                   int commit = 0, hipEvent_t done = nullptr) {
     const uint32_t B = c->batch_cap;
     const bool fused = c->cfg.plugin_set == MS_PLUGINS_NU_NN;
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NAM) {
+        int rc = nam_cycle_locked(c, n_pods, d_pods, d_res, commit, s);
+        if (rc) return rc;
+        if (done) MS_HIP(c, hipEventRecord(done, s));
+        return MS_OK;
+    }
     if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // (stateless: binds in the combine launch)
         int rc = tt_cycle_locked(c, n_pods, d_pods, nullptr, d_res, commit, s);
         if (rc) return rc;
@@ -804,12 +857,13 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     if (!cfg || !out) return fail(nullptr, MS_E_INVAL, "ms_create: null argument");
     *out = nullptr;
     if (cfg->plugin_set != MS_PLUGINS_NU_NN && cfg->plugin_set != MS_PLUGINS_NU_NRF_NN_LA &&
-        cfg->plugin_set != MS_PLUGINS_NU_NN_NA && cfg->plugin_set != MS_PLUGINS_NU_TT_NN)
+        cfg->plugin_set != MS_PLUGINS_NU_NN_NA && cfg->plugin_set != MS_PLUGINS_NU_TT_NN &&
+        cfg->plugin_set != MS_PLUGINS_NU_NN_NAM)
         return fail(nullptr, MS_E_INVAL, "ms_create: unknown plugin_set");
     const uint32_t w0 = cfg->score_weight[0] ? cfg->score_weight[0] : 1u;
     const uint32_t w1 = cfg->score_weight[1] ? cfg->score_weight[1] : 1u;
-    if (cfg->plugin_set != MS_PLUGINS_NU_NN_NA && (w0 != 1 || w1 != 1))
-        return fail(nullptr, MS_E_INVAL, "ms_create: score weights apply to MS_PLUGINS_NU_NN_NA only");
+    if (cfg->plugin_set != MS_PLUGINS_NU_NN_NA && cfg->plugin_set != MS_PLUGINS_NU_NN_NAM && (w0 != 1 || w1 != 1))
+        return fail(nullptr, MS_E_INVAL, "ms_create: score weights apply to MS_PLUGINS_NU_NN_NA / _NAM only");
     if (w0 * 10u + w1 * 100u >= 2048u)
         return fail(nullptr, MS_E_INVAL, "ms_create: weighted score must stay below 2048 (packed key)");
     if (cfg->max_nodes == 0 || (uint64_t)cfg->node_base + cfg->max_nodes > (uint64_t)MS_MAX_ORDINAL + 1)
@@ -850,6 +904,7 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     bool ok = hipMalloc((void **)&t.flags, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.digit, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.zone, n + kColumnPad) == hipSuccess &&
+              hipMalloc((void **)&t.label2, n + kColumnPad) == hipSuccess &&
               hipMalloc((void **)&t.taints, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
               hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
@@ -1191,7 +1246,8 @@ int ms_uncommit_bind(ms_ctx *c, uint32_t ordinal, const ms_pod_rec *pod) { retur
 int ms_sweep_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint64_t *keys_dev, uint32_t *flags_dev,
                     void *stream) {
     if (!valid_ctx(c) || (n_pods && (!pods_dev || !keys_dev))) return MS_E_INVAL;
-    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN && n_pods && !flags_dev)
+    if ((c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA || c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) && n_pods &&
+        !flags_dev)
         return fail(c, MS_E_INVAL, "ms_sweep_device: flags required for the resource-aware / NodeAffinity plugin sets");
     if (n_pods == 0) return MS_OK;
     std::lock_guard<std::mutex> g(c->sched_mu);
@@ -1393,6 +1449,88 @@ int ms_tt_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, 
     MS_HIP(c, launch_tt_combine(summaries_all_dev, n_pods, n_shards, pods_dev, n_pods, seed32_of(c->cfg.seed), nullptr,
                                 results_dev, c->t, 0, pick_stream(c, stream)));
     return MS_OK;
+}
+
+int ms_nam_term_sets(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set *sets) {
+    if (!valid_ctx(c) || (n_sets && !sets) || n_sets > 0xFFFFu) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)
+        return fail(c, MS_E_INVAL, "ms_nam_term_sets: the multi-term NodeAffinity plugin set only");
+    for (uint32_t i = 0; i < n_sets; ++i)
+        for (int k = 0; k < MS_NAM_TERMS; ++k) {
+            const ms_pref_term &x = sets[i].term[k];
+            if (x.key > 1 || x.weight > 100)
+                return fail(c, MS_E_INVAL, "ms_nam_term_sets: term key must be 0 or 1 and weight 0..100");
+        }
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    MS_HIP(c, hipDeviceSynchronize());  // (no cycle still reads the previous table; a configuration call)
+    if (n_sets > c->terms_cap) {
+        if (c->d_terms) (void)hipFree(c->d_terms);
+        c->d_terms = nullptr;
+        c->terms_cap = 0;
+        if (hipMalloc(&c->d_terms, (size_t)n_sets * sizeof(ms_nam_term_set)) != hipSuccess)
+            return fail(c, MS_E_OOM, "ms_nam_term_sets: term table");
+        c->terms_cap = n_sets;
+    }
+    if (n_sets) MS_HIP(c, hipMemcpy(c->d_terms, sets, (size_t)n_sets * sizeof(ms_nam_term_set), hipMemcpyHostToDevice));
+    c->n_terms = n_sets;
+    return MS_OK;
+}
+
+int ms_nam_segment_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, void *seg_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !seg_dev))) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)
+        return fail(c, MS_E_INVAL, "ms_nam_segment_device: the multi-term NodeAffinity plugin set only");
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);
+    if (rc) return rc;
+    const uint32_t B = c->batch_cap, ns = nam_segments(c->rows_dev);
+    rc = ensure_nam(c, std::min(B, n_pods));
+    if (rc) return rc;
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, launch_nam_seg(c->t, c->rows_dev, pods_dev + s0, nb, c->d_terms, c->n_terms, c->d_nam, s));
+        MS_HIP(c, launch_nam_compose(c->d_nam, nb, ns, nb, -1, static_cast<char *>(seg_dev) + (size_t)s0 * MS_NAM_SEG_BYTES,
+                                     nullptr, s));
+    }
+    return chain_back(c, s);
+}
+
+int ms_nam_keys_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards, uint32_t shard_index,
+                       const void *segs_all_dev, unsigned long long *keys_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !segs_all_dev || !keys_dev))) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)
+        return fail(c, MS_E_INVAL, "ms_nam_keys_device: the multi-term NodeAffinity plugin set only");
+    if (n_shards == 0 || shard_index >= n_shards)
+        return fail(c, MS_E_INVAL, "ms_nam_keys_device: shard_index must be below n_shards");
+    if (n_pods == 0) return MS_OK;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    hipStream_t s = pick_stream(c, stream);
+    rc = order_after_ctx_stream(c, s);
+    if (rc) return rc;
+    const uint32_t B = c->batch_cap, ns = nam_segments(c->rows_dev);
+    rc = ensure_nam(c, std::min(B, n_pods));
+    if (rc) return rc;
+    const uint32_t nb_max = std::min(B, n_pods);
+    char *after = static_cast<char *>(c->d_nam) + (size_t)ns * nb_max * MS_NAM_SEG_BYTES;
+    uint8_t *m_in = reinterpret_cast<uint8_t *>(after + (size_t)nb_max * MS_NAM_SEG_BYTES);
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        // the later shards' tables composed, and whether an earlier shard has a non-zero node
+        MS_HIP(c, launch_nam_compose(static_cast<const char *>(segs_all_dev) + (size_t)s0 * MS_NAM_SEG_BYTES, n_pods,
+                                     n_shards, nb, (int32_t)shard_index, after, m_in, s));
+        rc = nam_keys_locked(c, nb, pods_dev + s0, after, m_in, keys_dev + s0, s);
+        if (rc) return rc;
+    }
+    return chain_back(c, s);
 }
 
 }  // extern "C"

@@ -35,6 +35,7 @@ struct NodeTable {
     uint8_t *flags;
     uint8_t *digit;
     uint8_t *zone;  // zone label value id (MS_PLUGINS_NU_NN_NA), 0 = none
+    uint8_t *label2;  // second label value id (MS_PLUGINS_NU_NN_NAM term key 1), 0 = none
     uint32_t *taints;  // taint ids (MS_PLUGINS_NU_TT_NN): bits 0-7 NoSchedule/NoExecute, 8-15 PreferNoSchedule
     int32_t *allowed_pods;
     int32_t *pod_count;
@@ -149,6 +150,23 @@ __host__ __device__ inline uint32_t tb_hash(uint32_t A, uint32_t node_ordinal) {
 }
 // The node ordinal whose tb_hash under pod half A is h.
 __host__ __device__ inline uint32_t tb_unhash(uint32_t A, uint32_t h) { return (unmix32(h) - A) * kG24Inv; }
+
+// ---- MS_PLUGINS_NU_NN_NAM launchers (ms_affinity.hip) ----------------------
+// Row segments of a context (<= 16, >= 2048 rows each) and their rows per segment.
+uint32_t nam_segments(uint32_t n_rows, uint32_t *seg_rows = nullptr);
+// Per (segment, pod) composed rescale tables (MS_NAM_SEG_BYTES each, [seg][n_pods]).
+hipError_t launch_nam_seg(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                          const void *sets, uint32_t n_sets, void *segs, hipStream_t s);
+// Per pod the composition of n records in[s * stride + p] (s ascending); skip_to >= 0:
+// only the records after skip_to, and m_in[p] = the OR of "any" of those before it.
+hipError_t launch_nam_compose(const void *in, uint32_t stride, uint32_t n, uint32_t n_pods, int32_t skip_to,
+                              void *out, uint8_t *m_in, hipStream_t s);
+// Per pod the best packed key of this context's rows (atomicMax into keys): local =
+// launch_nam_seg's records; after / m_in as launch_nam_compose's outputs, or null.
+hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                           const void *sets, uint32_t n_sets, uint32_t seed32, uint32_t w_nn, uint32_t w_na,
+                           const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys,
+                           hipStream_t s);
 
 // ---- launchers (ms_kernels.hip) -------------------------------------------
 // All return hipError_t of the launch; none synchronises.

@@ -2516,6 +2516,7 @@ __global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uin
         t.flags[r] = kNodeAbsent;
         t.digit[r] = 0xFF;
         t.zone[r] = 0;
+        t.label2[r] = 0;
         t.taints[r] = 0;
         t.allowed_pods[r] = 0;
         t.pod_count[r] = 0;
@@ -2527,6 +2528,7 @@ __global__ void k_apply_deltas(NodeTable t, const NodeDelta *__restrict__ d, uin
     t.flags[r] = x.rec.unschedulable ? kNodeUnschedulable : 0;
     t.digit[r] = x.rec.name_digit <= 9 ? x.rec.name_digit : 0xFF;
     t.zone[r] = x.rec.zone;
+    t.label2[r] = x.rec.label2;
     t.taints[r] = x.rec.taints & 0xFFFFu;
     t.allowed_pods[r] = x.rec.allowed_pods;
     t.pod_count[r] = x.rec.pod_count;
@@ -2544,6 +2546,7 @@ __global__ void k_init_table(NodeTable t) {
     t.flags[r] = kNodeAbsent;
     t.digit[r] = 0xFF;
     t.zone[r] = 0;
+    t.label2[r] = 0;
     t.taints[r] = 0;
     t.allowed_pods[r] = 0;
     t.pod_count[r] = 0;
@@ -2561,6 +2564,7 @@ __global__ void k_read_rows(NodeTable t, uint32_t first, uint32_t n, ms_node_rec
     x.unschedulable = (f & kNodeUnschedulable) ? 1 : 0;
     x.name_digit = t.digit[r];
     x.zone = t.zone[r];
+    x.label2 = t.label2[r];
     x.taints = t.taints[r];
     x.allowed_pods = (f & kNodeAbsent) ? -1 : t.allowed_pods[r];
     x.pod_count = t.pod_count[r];

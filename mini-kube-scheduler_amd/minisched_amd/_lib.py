@@ -29,6 +29,7 @@ PLUGINS_NU_NN = 0
 PLUGINS_NU_NRF_NN_LA = 1
 PLUGINS_NU_NN_NA = 2
 PLUGINS_NU_TT_NN = 3
+PLUGINS_NU_NN_NAM = 4
 MODE_BATCHED = 0
 MODE_SEQUENTIAL = 1
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE = 0, 1, 2
@@ -52,7 +53,7 @@ NODE_REC = np.dtype(
         ("unschedulable", "u1"),
         ("name_digit", "u1"),
         ("zone", "u1"),
-        ("_pad0", "u1"),
+        ("label2", "u1"),  # second node label value id (MS_PLUGINS_NU_NN_NAM term key 1)
         ("allowed_pods", "<i4"),
         ("pod_count", "<i4"),
         ("taints", "<u4"),  # MS_PLUGINS_NU_TT_NN: bits 0-7 NoSchedule/NoExecute ids, 8-15 PreferNoSchedule
@@ -102,6 +103,23 @@ SEQ_CAND = np.dtype(
 )
 SEQ_TOPK = 4
 TT_SUMMARY_BYTES = 192  # MS_TT_SUMMARY_BYTES
+NAM_SEG_BYTES = 104  # MS_NAM_SEG_BYTES
+NAM_TERMS = 4  # MS_NAM_TERMS
+
+
+def nam_term_sets_array(sets):
+    """ms_nam_term_set records (uint8 (n, 16)) from a list of term lists
+    [(label key 0|1, value id 1..254 or 0xFF for Exists, weight 1..100), ...]
+    (at most MS_NAM_TERMS each). Set i of the list is term set id i + 1."""
+    out = np.zeros((len(sets), 16), dtype=np.uint8)
+    for i, terms in enumerate(sets):
+        if len(terms) > NAM_TERMS:
+            raise ValueError(f"at most {NAM_TERMS} preferred terms per set")
+        for k, (key, value, weight) in enumerate(terms):
+            if key not in (0, 1) or not 1 <= value <= 255 or value == 0 or not 0 <= weight <= 100:
+                raise ValueError("term: key 0/1, value 1..254 or 0xFF, weight 0..100")
+            out[i, 4 * k:4 * k + 3] = (key, value, weight)
+    return out
 SEQ_SHARD_BATCH_MAX = 256
 SEQ_MAX_SHARDS = 16
 assert NODE_REC.itemsize == 64 and POD_REC.itemsize == 40 and RESULT.itemsize == 24 and SEQ_CAND.itemsize == 72
@@ -189,6 +207,9 @@ SIGNATURES = {
     "ms_seq_validate_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "ms_tt_summaries_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_tt_decode_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp]),
+    "ms_nam_term_sets": (ctypes.c_int, [_vp, _u32, _vp]),
+    "ms_nam_segment_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_nam_keys_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _u32, _vp, _vp, _vp]),
     "ms_comm_id_create": (ctypes.c_int, [ctypes.POINTER(ms_comm_id)]),
     "ms_comm_init": (ctypes.c_int, [_vp, ctypes.POINTER(ms_comm_id), _i32, _i32]),
     "ms_sharded_slice": (ctypes.c_int, [_vp, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
@@ -435,6 +456,25 @@ class Engine:
         self._check("ms_tt_decode_device",
                     self.lib.ms_tt_decode_device(self.h, n_pods, pods_dev, n_shards, summaries_all_dev, results_dev,
                                                  stream or None))
+
+    def nam_term_sets(self, sets):
+        """MS_PLUGINS_NU_NN_NAM: registers the term sets (uint8 array (n, 4, 4) of
+        {key, value, weight, 0} per term, or a NAM_TERM_SET-compatible (n, 16)
+        array); pod term set id s is row s - 1."""
+        raw = np.ascontiguousarray(np.asarray(sets, dtype=np.uint8).reshape(-1, 16))
+        self._check("ms_nam_term_sets", self.lib.ms_nam_term_sets(self.h, len(raw), raw.ctypes.data if len(raw) else None))
+
+    def nam_segment_device(self, n_pods, pods_dev, seg_dev, stream=0):
+        """Node-sharded multi-term NodeAffinity, step 1: this shard's rescale record per pod."""
+        self._check("ms_nam_segment_device",
+                    self.lib.ms_nam_segment_device(self.h, n_pods, pods_dev, seg_dev, stream or None))
+
+    def nam_keys_device(self, n_pods, pods_dev, n_shards, shard_index, segs_all_dev, keys_dev, stream=0):
+        """Step 3: this shard's packed keys under every shard's records (shard-major);
+        the uint64 MAX over the shards decodes with decode_device (flags 0)."""
+        self._check("ms_nam_keys_device",
+                    self.lib.ms_nam_keys_device(self.h, n_pods, pods_dev, n_shards, shard_index, segs_all_dev, keys_dev,
+                                                stream or None))
 
     # ---- in-library multi-GPU (a communicator per job) -------------------------
     def comm_init(self, comm_id: bytes, rank: int, world: int):

@@ -27,7 +27,9 @@ GiB = 1 << 30
 S_NODE_UNSCHED, S_POD_TOL, S_NODE_CPU, S_NODE_MEM, S_POD_NOREQ, S_POD_CPU, S_POD_MEM = 1, 2, 3, 4, 5, 6, 7
 S_NODE_ZONE, S_POD_ZONE, S_POD_ZWEIGHT = 8, 9, 10
 S_NODE_HARD, S_NODE_SOFT, S_POD_TOLH, S_POD_TOLS = 11, 12, 13, 14
+S_NODE_LABEL2, S_POD_TERMSET, S_TERMSETS = 15, 16, 17
 N_ZONES = 8
+N_LABEL2 = 4  # second-label value ids 1..4 (MS_PLUGINS_NU_NN_NAM)
 # MS_PLUGINS_NU_TT_NN taint universe of the synthetic clusters: 3 NoSchedule /
 # NoExecute taint ids (bits 0-2 of ms_node_rec.taints) and 6 PreferNoSchedule
 # ids (bits 8-13)
@@ -61,11 +63,12 @@ def stream_u64(seed: int, stream: int, start: int, n: int) -> np.ndarray:
 
 
 def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False,
-          taints: bool = False) -> np.ndarray:
+          taints: bool = False, labels: bool = False) -> np.ndarray:
     """Node records for ordinals [start, start+n). zones: topology zone labels
     for MS_PLUGINS_NU_NN_NA (value ids 1..8, 5 % of nodes unlabelled). taints:
     for MS_PLUGINS_NU_TT_NN, each NoSchedule taint id on 4 % of nodes and each
-    PreferNoSchedule id on 30 %."""
+    PreferNoSchedule id on 30 %. labels (MS_PLUGINS_NU_NN_NAM): the zone labels
+    and a second label (value ids 1..4, 10 % unlabelled)."""
     rec = np.zeros(n, dtype=NODE_REC)
     i = np.arange(start, start + n, dtype=np.int64)
     rec["name_digit"] = (i % 10).astype(np.uint8)
@@ -78,9 +81,12 @@ def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones:
         mem = np.array([2, 4, 8, 16], dtype=np.int64) * GiB
         rec["alloc_milli_cpu"] = cpu[(stream_u64(seed, S_NODE_CPU, start, n) % np.uint64(4)).astype(np.int64)]
         rec["alloc_memory"] = mem[(stream_u64(seed, S_NODE_MEM, start, n) % np.uint64(4)).astype(np.int64)]
-    if zones:
+    if zones or labels:
         u = stream_u64(seed, S_NODE_ZONE, start, n)
         rec["zone"] = np.where(u % np.uint64(100) < np.uint64(5), 0, 1 + (u >> np.uint64(8)) % np.uint64(N_ZONES))
+    if labels:
+        u = stream_u64(seed, S_NODE_LABEL2, start, n)
+        rec["label2"] = np.where(u % np.uint64(100) < np.uint64(10), 0, 1 + (u >> np.uint64(8)) % np.uint64(N_LABEL2))
     if taints:
         rec["taints"] = _bits(seed, S_NODE_HARD, start, n, N_HARD_TAINTS, 40) | (
             _bits(seed, S_NODE_SOFT, start, n, N_SOFT_TAINTS, 300) << np.uint32(8))
@@ -88,12 +94,14 @@ def nodes(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones:
 
 
 def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: bool = False,
-         taints: bool = False) -> np.ndarray:
+         taints: bool = False, term_sets: int = 0) -> np.ndarray:
     """Pod records for ordinals [start, start+n). zones: 70 % of pods carry one
     preferred zone term (zone 1..8, weight 1..100) for MS_PLUGINS_NU_NN_NA.
     taints: MS_PLUGINS_NU_TT_NN tolerated taint ids (each with probability
     0.3), in the bytes that set shares with the NodeAffinity term
-    (tol_hard = pref_zone, tol_soft = pref_weight, minisched_gpu.h)."""
+    (tol_hard = pref_zone, tol_soft = pref_weight, minisched_gpu.h).
+    term_sets = K > 0 (MS_PLUGINS_NU_NN_NAM): 85 % of pods name one of K term
+    sets (id 1..K, synth.nam_term_sets) in pref_zone | pref_weight << 8."""
     rec = np.zeros(n, dtype=POD_REC)
     j = np.arange(start, start + n, dtype=np.int64)
     rec["ordinal"] = j.astype(np.uint32)
@@ -117,7 +125,33 @@ def pods(n: int, seed: int = 1, start: int = 0, resources: bool = False, zones: 
     if taints:
         set_tolerations(rec, _bits(seed, S_POD_TOLH, start, n, N_HARD_TAINTS, 300),
                         _bits(seed, S_POD_TOLS, start, n, N_SOFT_TAINTS, 300))
+    if term_sets:
+        u = stream_u64(seed, S_POD_TERMSET, start, n)
+        sid = np.where(u % np.uint64(100) < np.uint64(85), 1 + (u >> np.uint64(8)) % np.uint64(term_sets), 0)
+        rec["pref_zone"] = (sid & np.uint64(0xFF)).astype(np.uint8)
+        rec["pref_weight"] = (sid >> np.uint64(8)).astype(np.uint8)
     return rec
+
+
+def nam_term_sets(k: int, seed: int = 1) -> np.ndarray:
+    """K random MS_PLUGINS_NU_NN_NAM term sets (uint8 (K, 16), ms_nam_term_set):
+    1..4 terms each on the zone label (key 0, values 1..8) or the second label
+    (key 1, values 1..4), 1 in 8 of them Exists (0xFF), weights 1..100 — so a
+    node matching several terms scores above 100 and the in-loop hook rescales."""
+    from ._lib import nam_term_sets_array
+
+    u = stream_u64(seed, S_TERMSETS, 0, 16 * k).reshape(k, 16)
+    sets = []
+    for i in range(k):
+        nt = 1 + int(u[i, 0] % np.uint64(4))
+        terms = []
+        for t in range(nt):
+            x = int(u[i, 1 + t])
+            key = x & 1
+            value = 0xFF if (x >> 1) % 8 == 0 else 1 + (x >> 4) % (N_ZONES if key == 0 else N_LABEL2)
+            terms.append((key, value, 1 + (x >> 12) % 100))
+        sets.append(terms)
+    return nam_term_sets_array(sets)
 
 
 def set_tolerations(rec: np.ndarray, tol_hard, tol_soft) -> None:

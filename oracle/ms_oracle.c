@@ -403,6 +403,125 @@ int msor_schedule_na(const msor_nodes *nd, const msor_pods *pd, int64_t w_nn, in
     return 0;
 }
 
+/* ---- NodeAffinity with several preferred terms (plugin set 4) ------------- */
+
+/* k8s@v1.22.0:pkg/scheduler/framework/plugins/nodeaffinity/node_affinity.go
+ * Score: for each PreferredSchedulingTerm with a non-zero weight whose
+ * NodeSelectorTerm matches the node, count += weight. Terms here test one
+ * label key (0: topology.kubernetes.io/zone, 1: the second label) with
+ * operator In [one value] or Exists (value 0xFF). */
+static int64_t nam_raw(const msor_nodes *nd, uint32_t i, const uint8_t *set) {
+    int64_t r = 0;
+    for (int t = 0; t < MSOR_NAM_TERMS; ++t) {
+        const uint8_t key = set[4 * t], val = set[4 * t + 1], w = set[4 * t + 2];
+        if (w == 0) continue;
+        const uint8_t lab = key == 0 ? nd->zone[i] : nd->label2[i];
+        if (lab != 0 && (val == 0xFF || lab == val)) r += w;
+    }
+    return r;
+}
+
+/* Closed form of the in-loop hook for reverse=false: once an
+ * entry is non-zero the list maximum is 100 after every step, so step i is the
+ * identity when r_i <= 100 and the rescale f_{r_i}(v) = floor(100 v / r_i) of
+ * every earlier entry when r_i > 100 (entry i itself ends at 100); the first
+ * non-zero entry (the anchor) starts at 100 whatever its raw score. Entry k
+ * therefore ends at T_{>k}(v_k), T_{>k} = the composition of the later
+ * rescales: computed by one reverse scan keeping T as a 101-entry table
+ * (T <- T o f_r at each rescale; every f_r maps 1..100 below itself, so T
+ * reaches 0 everywhere after at most 100 rescales and stays there). */
+static void nam_closed(const int64_t *r, uint32_t F, int64_t *out) {
+    int64_t T[101], U[101];
+    for (int v = 0; v <= 100; ++v) T[v] = v;
+    int64_t anchor = -1;
+    for (uint32_t k = 0; k < F; ++k)
+        if (r[k] > 0) { anchor = k; break; }
+    for (int64_t k = (int64_t)F - 1; k >= 0; --k) {
+        const int64_t v = (k == anchor || r[k] > 100) ? 100 : r[k];
+        out[k] = T[v];
+        if (r[k] > 100 && T[100] != 0) {
+            for (int v2 = 0; v2 <= 100; ++v2) U[v2] = T[(100 * v2) / r[k]];
+            memcpy(T, U, sizeof(T));
+        }
+    }
+}
+
+int msor_nam_inloop(const int64_t *r, uint32_t F, int literal, int64_t *out) {
+    for (uint32_t k = 0; k < F; ++k)
+        if (r[k] < 0) return -1;
+    if (literal) {
+        for (uint32_t k = 0; k < F; ++k) out[k] = 0; /* createPluginToNodeScores (:327-334) */
+        for (uint32_t k = 0; k < F; ++k) {
+            out[k] = r[k];
+            msor_default_normalize(100, 0, out, F); /* the WHOLE list, later entries still 0 */
+        }
+        return 0;
+    }
+    nam_closed(r, F, out);
+    return 0;
+}
+
+int msor_schedule_nam(const msor_nodes *nd, const msor_pods *pd, const uint8_t *term_sets, uint32_t n_sets,
+                      int64_t w_nn, int64_t w_na, int literal, uint64_t seed, uint32_t node_base, int32_t *out_node,
+                      int64_t *out_score, int32_t *out_code, uint32_t *out_mask, uint64_t *out_key) {
+    if (!nd || !pd || !nd->flags || !nd->digit || !nd->zone || !nd->label2 || !pd->ordinal || !pd->digit || !pd->tol ||
+        !pd->pref_zone || !pd->pref_weight || (n_sets && !term_sets))
+        return -1;
+    if ((uint64_t)node_base + nd->n >= 0xFFFFFu) return -1;
+    static const uint8_t none[4 * MSOR_NAM_TERMS] = {0};
+    uint32_t *feas = (uint32_t *)malloc(sizeof(uint32_t) * (nd->n ? nd->n : 1));
+    int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * (nd->n ? nd->n : 1));
+    int64_t *na = (int64_t *)malloc(sizeof(int64_t) * (nd->n ? nd->n : 1));
+    if (!feas || !raw || !na) { free(feas); free(raw); free(na); return -1; }
+    int rc = 0;
+    for (uint32_t j = 0; j < pd->n; ++j) {
+        const uint32_t sid = (uint32_t)pd->pref_zone[j] | (uint32_t)pd->pref_weight[j] << 8;
+        if (sid > n_sets) { rc = -1; break; }
+        const uint8_t *set = sid ? term_sets + 16u * (sid - 1u) : none;
+        /* RunFilterPlugins (minisched.go:115-151): NodeUnschedulable only */
+        uint32_t F = 0, mask = 0;
+        for (uint32_t i = 0; i < nd->n; ++i) {
+            if (nd->flags[i] & MSOR_NODE_ABSENT) continue;
+            if (nu_rejects(nd->flags[i], pd->tol[j])) { mask |= MSOR_MASK_NU; continue; }
+            feas[F++] = i;
+        }
+        int32_t node = -1, code;
+        int64_t score = 0;
+        uint64_t best = 0;
+        if (F == 0) {
+            code = MSOR_CODE_UNSCHEDULABLE;
+        } else if (pd->digit[j] < 0) { /* NodeNumber.Score fails at the first node (:170-172) */
+            code = MSOR_CODE_ERROR;
+            mask = 0;
+        } else {
+            /* RunScorePlugins (minisched.go:164-185): NodeNumber then NodeAffinity per
+             * feasible node; NodeAffinity's NormalizeScore on its whole list each time */
+            for (uint32_t k = 0; k < F; ++k) raw[k] = nam_raw(nd, feas[k], set);
+            msor_nam_inloop(raw, F, literal, na);
+            const uint32_t ph = msor_pod_hash(seed, pd->ordinal[j]);
+            for (uint32_t k = 0; k < F; ++k) { /* sum (:187-196), weights applied; selectHost (:304-325) */
+                const uint32_t ord = node_base + feas[k];
+                const uint64_t key = msor_key(w_nn * nn_score(pd->digit[j], nd->digit[feas[k]]) + w_na * na[k],
+                                              msor_tb_hash(ph, ord), ord);
+                if (key > best) best = key;
+            }
+            code = MSOR_CODE_SUCCESS;
+            mask = 0;
+            node = (int32_t)(0xFFFFFu - (uint32_t)(best & 0xFFFFFu));
+            score = (int64_t)(best >> 52);
+        }
+        if (out_node) out_node[j] = node;
+        if (out_score) out_score[j] = score;
+        if (out_code) out_code[j] = code;
+        if (out_mask) out_mask[j] = code == MSOR_CODE_UNSCHEDULABLE ? mask : 0;
+        if (out_key) out_key[j] = best;
+    }
+    free(feas);
+    free(raw);
+    free(na);
+    return rc;
+}
+
 /* ---- TaintToleration + the in-loop reverse normalise hook ------------------ */
 
 /* k8s@v1.22.0:pkg/scheduler/framework/plugins/tainttoleration/taint_toleration.go

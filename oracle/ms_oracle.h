@@ -57,6 +57,8 @@ typedef struct {
     /* taint ids of the cluster's taint universe (NU_TT_NN): bits 0-7 taints with
      * effect NoSchedule or NoExecute, bits 8-15 taints with effect PreferNoSchedule */
     const uint32_t *taints;
+    /* second node label value id, 0 = none (NU_NN_NAM: label key 1 of the terms) */
+    const uint8_t *label2;
 } msor_nodes;
 
 typedef struct {
@@ -124,6 +126,27 @@ int msor_schedule_nunn_names(const char *const *node_names, const uint8_t *node_
 int msor_schedule_na(const msor_nodes *nodes, const msor_pods *pods, int64_t w_nn, int64_t w_na, int literal,
                      uint64_t seed, uint32_t node_base, int32_t *out_node, int64_t *out_score,
                      int32_t *out_code, uint32_t *out_mask, uint64_t *out_key);
+
+/* MSOR_PLUGINS_NU_NN_NAM (4), batched: NodeAffinity with SEVERAL preferred
+ * terms. A pod's term set id is pref_zone | pref_weight << 8 (0 = no terms);
+ * set s (1-based) is term_sets[16 (s-1) .. 16 s): four terms of 4 bytes
+ * {label key (0: the zone label, 1: label2), value id (0xFF: Exists), weight
+ * (1..100; 0 = unused slot), 0}. NodeAffinity.Score = the sum of the weights of
+ * the matching terms (so raw scores reach 400), normalised by
+ * DefaultNormalizeScore(100, reverse=false) on the whole list after every node
+ * (minisched.go:164-185). literal=1 runs that loop (O(F^2) per pod);
+ * literal=0 its closed form (msor_nam_inloop). Weights as msor_schedule_na. */
+#define MSOR_PLUGINS_NU_NN_NAM 4
+#define MSOR_NAM_TERMS 4
+int msor_schedule_nam(const msor_nodes *nodes, const msor_pods *pods, const uint8_t *term_sets, uint32_t n_sets,
+                      int64_t w_nn, int64_t w_na, int literal, uint64_t seed, uint32_t node_base, int32_t *out_node,
+                      int64_t *out_score, int32_t *out_code, uint32_t *out_mask, uint64_t *out_key);
+/* The in-loop reverse=false hook on one list of raw scores r[0..F) (any
+ * non-negative values): literal=1 the loop as written, 0 the closed form
+ * (out[k] = T_{>k}(v_k), T_{>k} the composition of v -> floor(100 v / r_i) over
+ * the later entries with r_i > 100, v_k = 100 for the first non-zero entry
+ * and for r_k > 100, else r_k). Returns -1 on a negative raw score. */
+int msor_nam_inloop(const int64_t *r, uint32_t F, int literal, int64_t *out);
 
 /* upstream k8s@v1.22.0 pkg/scheduler/framework/plugins/helper/normalize_score.go */
 void msor_default_normalize(int64_t max_priority, int reverse, int64_t *scores, uint32_t n);

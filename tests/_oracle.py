@@ -35,6 +35,7 @@ class msor_nodes(ctypes.Structure):
             "nz_mem",
             "zone",
             "taints",
+            "label2",
         )
     ]
 
@@ -103,6 +104,14 @@ def lib():
             ctypes.c_uint64,
             ctypes.c_uint32,
         ] + [ctypes.c_void_p] * 5
+        L.msor_schedule_nam.restype = ctypes.c_int
+        L.msor_schedule_nam.argtypes = [
+            ctypes.POINTER(msor_nodes), ctypes.POINTER(msor_pods), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ]
+        L.msor_nam_inloop.restype = ctypes.c_int
+        L.msor_nam_inloop.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
         L.msor_tt_inloop.restype = ctypes.c_int
         L.msor_tt_inloop.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
         L.msor_default_normalize.restype = None
@@ -160,6 +169,7 @@ class NodeCols:
         self.nz_mem = _col(recs["nonzero_memory"], np.int64)
         self.zone = _col(recs["zone"], np.uint8)
         self.taints = _col(recs["taints"], np.uint32)
+        self.label2 = _col(recs["label2"], np.uint8)
 
     def struct(self):
         return msor_nodes(
@@ -179,6 +189,7 @@ class NodeCols:
                     "nz_mem",
                     "zone",
                     "taints",
+                    "label2",
                 )
             ],
         )
@@ -244,6 +255,33 @@ def schedule_na(node_recs, pods, weights=(1, 1), literal=True, seed=1, node_base
     )
     assert rc == 0, "oracle rejected its arguments"
     return o
+
+
+def schedule_nam(node_recs, pods, term_sets, weights=(1, 1), literal=True, seed=1, node_base=0):
+    """MSOR_PLUGINS_NU_NN_NAM (batched): several preferred terms per pod (term set
+    id = pref_zone | pref_weight << 8, term_sets uint8 (n, 16)); literal=True runs
+    RunScorePlugins' in-loop NormalizeScore as written (O(F^2) per pod)."""
+    L = lib()
+    cols = NodeCols(node_recs)
+    nst = cols.struct()
+    pc, pst = _pod_cols(pods)
+    ts = np.ascontiguousarray(np.asarray(term_sets, dtype=np.uint8).reshape(-1, 16))
+    o = _outs(len(pods))
+    rc = L.msor_schedule_nam(
+        ctypes.byref(nst), ctypes.byref(pst), ts.ctypes.data if len(ts) else None, len(ts), int(weights[0]),
+        int(weights[1]), 1 if literal else 0, seed, node_base,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),
+    )
+    assert rc == 0, "oracle rejected its arguments"
+    return o
+
+
+def nam_inloop(raw, literal=True):
+    """msor_nam_inloop: the reverse=false in-loop hook on one raw-score list."""
+    r = np.ascontiguousarray(raw, dtype=np.int64)
+    out = np.zeros(len(r), dtype=np.int64)
+    assert lib().msor_nam_inloop(_p(r), len(r), 1 if literal else 0, _p(out)) == 0
+    return out
 
 
 def schedule_tt(node_recs, pods, literal=True, seed=1, node_base=0):

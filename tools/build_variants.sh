@@ -15,5 +15,5 @@ else
   $H $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
   CAPI=build/ms_capi.o
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o minisched_amd/libminisched_gpu_$NAME.so build/ms_kernels_$NAME.o build/ms_sweep_pp.o build/ms_taint.o $CAPI build/ms_comm.o -L/opt/rocm/lib -lrccl
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o minisched_amd/libminisched_gpu_$NAME.so build/ms_kernels_$NAME.o build/ms_sweep_pp.o build/ms_taint.o build/ms_affinity.o $CAPI build/ms_comm.o -L/opt/rocm/lib -lrccl
 echo built minisched_amd/libminisched_gpu_$NAME.so
