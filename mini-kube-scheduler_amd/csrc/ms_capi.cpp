@@ -186,8 +186,9 @@ hipError_t ctr_alloc(uint32_t **p) {
         const char *e = getenv("MINISCHED_CTR_FINE");
         return e && e[0] == '1';
     }();
-    if (fine) return hipExtMallocWithFlags((void **)p, 64, hipDeviceMallocFinegrained);
-    return hipMalloc((void **)p, 64);
+    // (a counter, or one slot per sweep workgroup: at most 255)
+    if (fine) return hipExtMallocWithFlags((void **)p, 1024, hipDeviceMallocFinegrained);
+    return hipMalloc((void **)p, 1024);
 }
 
 // Sequential-engine scratch for n_tiles tiles, kSeqBufs batches deep (pipelining).
@@ -352,7 +353,22 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         // No cross-stream hand-off (each cost ~12 us per batch, and a
         // validation launched beside a sweep waited for a SIMD to drain);
         // batch k+1 treats batch k's binds as stale.
-        const uint32_t nb0 = std::min(B, n_pods);
+        // Warm-up batches: the first 8,192 pods of the queue in batches of 64. On an
+        // empty cluster every pod prefers the same emptiest nodes, so early batches
+        // touch each other's speculative winners most (the slow-path burst of
+        // batches 20-30); half-size batches there cut the re-sweeps to 0 and the
+        // recomputes by 10 %: config E 39.7 -> 38.5 ms (profiles/r05l_e_ab.txt;
+        // 4096:32 / 8192:32 / 16384:32 / 16384:64 / 32768:64 measured slower,
+        // r05k_e_warm.txt). MINISCHED_SEQ_WARM=<pods>:<batch> overrides (0:0 off).
+        static const std::pair<uint32_t, uint32_t> warm = [] {
+            uint32_t wp = 8192, wb = 64;
+            if (const char *e = getenv("MINISCHED_SEQ_WARM")) (void)std::sscanf(e, "%u:%u", &wp, &wb);
+            return std::make_pair(wp, wb);
+        }();
+        auto batch_at = [&](uint32_t s0) {
+            return (s0 < warm.first && warm.second) ? std::min(warm.second, B) : B;
+        };
+        const uint32_t nb0 = std::min(batch_at(0), n_pods);
         MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
         MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, nb0, n_tiles, c->d_top4, c->d_spec,
                                     c->d_spec_flags, tq, c->d_top4_rec, s, top_ext));
@@ -369,11 +385,19 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         const char *merge_env = getenv("MINISCHED_SEQ_MERGE");
         const std::string merge_mode = merge_env ? merge_env : "instep";
         const bool want_instep = merge_mode == "instep" || merge_mode == "fallback";
-        if (want_instep) MS_HIP(c, hipMemsetAsync(c->d_merge_ctr, 0, sizeof(uint32_t), s));
+        if (want_instep) {
+            MS_HIP(c, hipMemsetAsync(c->d_merge_ctr, 0, 1024, s));
+            // (tagged lists: no set may hold a tag from an earlier run)
+            MS_HIP(c, hipMemsetAsync(c->d_tile_keys + cells_per_set * seq_topk(), 0,
+                                     (size_t)(kSeqBufs - 1) * cells_per_set * seq_topk() * sizeof(unsigned long long), s));
+            MS_HIP(c, hipMemsetAsync(c->d_tile_flags + cells_per_set, 0,
+                                     (size_t)(kSeqBufs - 1) * cells_per_set * sizeof(uint32_t), s));
+        }
         uint32_t k = 0, in_tag = 0, target = 0;
-        for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
-            const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
-            const uint32_t s1 = s0 + B, nn = s1 < n_pods ? std::min(B, n_pods - s1) : 0u;
+        for (uint32_t s0 = 0, nb = 0; s0 < n_pods; s0 += nb, ++k) {
+            nb = std::min(batch_at(s0), n_pods - s0);
+            const uint32_t cur = k & 1u, nxt = cur ^ 1u;
+            const uint32_t s1 = s0 + nb, nn = s1 < n_pods ? std::min(batch_at(s1), n_pods - s1) : 0u;
             unsigned long long *tk = c->d_tile_keys + cells_per_set * seq_topk() * cur;
             unsigned long long *tk1 = c->d_tile_keys + cells_per_set * seq_topk() * nxt;
             uint32_t *tf = c->d_tile_flags + cells_per_set * cur, *tf1 = c->d_tile_flags + cells_per_set * nxt;

@@ -431,26 +431,30 @@ __device__ __forceinline__ void cswap_desc(u64 &a, u64 &b) {
 // (agent-scope relaxed atomics: the store writes through, the load bypasses a
 // possibly stale L2 line). The in-step merge (k_seq_step, SeqMergeIO) reads the
 // lists of sweep workgroups that ran on other XCDs in the same launch.
-// A/B switches of the in-step merge's synchronisation (round 5):
-//   MS_CTR_SCOPE 0: counter add and polls at agent scope (relaxed); 1: system scope
-//   MS_CTR_SLEEP: s_sleep argument between polls (0: spin)
-//   MS_LIST_FENCE 0: tile lists stored / loaded write-through (st_coh / ld_coh);
-//                 1: plain stores, an agent release fence before the count, an
-//                 acquire fence after the wait, plain loads
-#ifndef MS_CTR_SCOPE
-#define MS_CTR_SCOPE 0
+// In-step merge synchronisation (round 5). MS_MERGE_TAGS 1 (default): the
+// sweep stamps every list of the step with a 2-bit tag (bits 61-62 of each key,
+// bits 16-17 of the flags word; 1..3, cycling over the steps; a buffer set is
+// rewritten every second step and zeroed at the start of each run) and a merge
+// worker polls the lists themselves until every one it reads carries the tag:
+// no counter, no barrier, and the lists arrive with the check. MS_MERGE_TAGS 0:
+// the sweep workgroups count themselves done on one counter after their stores
+// landed and the workers poll it, then load the lists (A/B). Measured and
+// dropped: system-scope counter, spin without s_sleep, fine-grained counter
+// memory (all 40.5-40.6 ms), per-workgroup slots instead of the counter (41.7),
+// release/acquire fences with plain list stores (85 ms: the fences write back
+// and invalidate whole L2s) (profiles/r05f_e_sync_ab.txt, r05j_e_slots_ab.txt).
+#ifndef MS_MERGE_TAGS
+#define MS_MERGE_TAGS 1
 #endif
-#ifndef MS_CTR_SLEEP
-#define MS_CTR_SLEEP 1
-#endif
-#ifndef MS_LIST_FENCE
-#define MS_LIST_FENCE 0
-#endif
-#if MS_CTR_SCOPE
-#define MS_CTR_SCOPE_ID __HIP_MEMORY_SCOPE_SYSTEM
-#else
-#define MS_CTR_SCOPE_ID __HIP_MEMORY_SCOPE_AGENT
-#endif
+constexpr int kListTagShift = 61;  // (config E scores stay below 512: bits 61-62 of a key are 0)
+constexpr u64 kListTagMask = 3ull << kListTagShift;
+__device__ __forceinline__ u64 untag_key(u64 k) { return k & ~kListTagMask; }
+__device__ __forceinline__ uint32_t untag_flags(uint32_t f) { return f & 0xFFFFu; }
+// Diagnostic timeline fields per workgroup (MS_VSTAMPS / MS_TIMELINE_ONLY builds,
+// s_memrealtime): 0 start, 1 swept (counted), 2 worker's wait done, 3 worker's
+// merges done, 4 validator done (workgroup 0), 5 first tile staged in LDS,
+// 6 wave 0's sweep tasks done, 7 every wave's tasks done (barrier)
+enum { kTlBegin = 0, kTlSwept, kTlWaited, kTlMerged, kTlValidated, kTlStaged, kTlWave0, kTlTasks };
 typedef __attribute__((address_space(1))) u64 gu64_t;
 typedef __attribute__((address_space(1))) uint32_t gu32_t;
 __device__ __forceinline__ void st_coh(u64 *p, u64 v) {
@@ -470,6 +474,9 @@ constexpr int kTopK = 4;
 constexpr int kTopExt = 8;  // ranks the merge lists for the validator's slow pods (4 beyond the top-4)
 static_assert(kFullSlots == kTopK, "one key per row slot feeds the per-lane sort");
 
+#ifndef MS_MERGE_WMAX
+#define MS_MERGE_WMAX wave_max_u64_dpp
+#endif
 #ifndef MS_SWEEP_WMAX
 #define MS_SWEEP_WMAX wave_max_u64_unique
 #endif
@@ -494,7 +501,8 @@ __device__ __forceinline__ PodFast lane_pod(const PodFast &m, uint32_t i) { retu
 template <int F, int NP, typename Row, typename Lanes>
 __device__ __forceinline__ void sweep_topk_group(const Row *x, uint32_t ord0, const Lanes &m, uint32_t pbeg,
                                                  uint32_t i, uint32_t lane, uint32_t tile, uint32_t n_tiles,
-                                                 u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
+                                                 u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags,
+                                                 uint32_t tag) {
     u64 k[NP][kFullSlots], out[NP];
     uint32_t nu_any[NP], nrf_any[NP];
 #pragma unroll
@@ -534,20 +542,27 @@ __device__ __forceinline__ void sweep_topk_group(const Row *x, uint32_t ord0, co
     for (int n = 0; n < NP; ++n) {
         const uint32_t f = (__ballot(nu_any[n] != 0) ? 1u : 0u) | (__ballot(nrf_any[n] != 0) ? 0x100u : 0u);
         const size_t cell = (size_t)(pbeg + i + n) * n_tiles + tile;
-        if (lane < (uint32_t)kTopK) st_coh(tile_keys + cell * kTopK + lane, out[n]);
-        if (lane == 0) st_coh(tile_flags + cell, f);
+        if (tag) {  // (launch-uniform) an in-step merge reads these lists in this launch
+            if (lane < (uint32_t)kTopK) st_coh(tile_keys + cell * kTopK + lane, out[n] | (u64)tag << kListTagShift);
+            if (lane == 0) st_coh(tile_flags + cell, f | tag << 16);
+        } else {
+            if (lane < (uint32_t)kTopK) tile_keys[cell * kTopK + lane] = out[n];
+            if (lane == 0) tile_flags[cell] = f;
+        }
     }
 }
 
 template <int F, typename Row, typename Lanes, int NPMAX = 2>
 __device__ __forceinline__ void sweep_topk_pods(const Row *x, uint32_t ord0, const Lanes &m, uint32_t pbeg,
                                                 uint32_t cnt, uint32_t lane, uint32_t tile, uint32_t n_tiles,
-                                                u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags) {
+                                                u64 *__restrict__ tile_keys, uint32_t *__restrict__ tile_flags,
+                                                uint32_t tag) {
     uint32_t i = 0;
     if (NPMAX >= 2)
         for (; i + 2 <= cnt; i += 2)
-            sweep_topk_group<F, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
-    for (; i < cnt; ++i) sweep_topk_group<F, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags);
+            sweep_topk_group<F, 2>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags, tag);
+    for (; i < cnt; ++i)
+        sweep_topk_group<F, 1>(x, ord0, m, pbeg, i, lane, tile, n_tiles, tile_keys, tile_flags, tag);
 }
 
 struct SweepArgs {
@@ -561,7 +576,8 @@ struct SweepArgs {
     uint32_t *tile_flags;
     uint32_t n_tiles;
     uint32_t fast;  // binary64 LeastAllocated where exact (default 1)
-    uint32_t coh;   // an in-step merge reads the lists in the same launch: stores write through (st_coh)
+    uint32_t coh;   // 1..3: an in-step merge reads the lists in this launch: stores write through (st_coh),
+                    // tagged with this value (MS_MERGE_TAGS); 0: plain stores
 };
 
 // One wave, lane = row: tile `tile`'s top-4 lists and filter flags for pods
@@ -583,7 +599,7 @@ __device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t til
         const PodFast m = load_pod_fast(lane < cnt ? a.pods[pbeg + lane] : z, a.seed32);
         ok = ok && (lane >= cnt || (m.bits & kPfOk));
         if (__ballot(!ok) == 0) {
-            sweep_topk_pods<2>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+            sweep_topk_pods<2>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags, a.coh);
             return;
         }
     }
@@ -591,8 +607,8 @@ __device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t til
 #pragma unroll
     for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
     const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
-    if (rows_huge(x)) sweep_topk_pods<1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
-    else sweep_topk_pods<0>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags);
+    if (rows_huge(x)) sweep_topk_pods<1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags, a.coh);
+    else sweep_topk_pods<0>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags, a.coh);
 }
 
 // The transposed form's fallback (a row or pod outside the binary64 range,
@@ -607,10 +623,10 @@ __device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_
     const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
     if (rows_huge(x))
         sweep_topk_pods<1, FullRow, PodLanes, 1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys,
-                                                 a.tile_flags);
+                                                 a.tile_flags, a.coh);
     else
         sweep_topk_pods<0, FullRow, PodLanes, 1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys,
-                                                 a.tile_flags);
+                                                 a.tile_flags, a.coh);
 }
 
 // ---- transposed sweep: lane = (pod, row part) ------------------------------
@@ -630,8 +646,10 @@ constexpr uint32_t kTpPods = 16;
 #define MS_PRAGMA(x) _Pragma(#x)
 #define MS_UNROLL(n) MS_PRAGMA(unroll n)
 
-__device__ __forceinline__ void tile_keys_store(u64 *dst, uint32_t j, const u64 (&k)[4]) {
-    st_coh(dst, j == 0 ? k[0] : j == 1 ? k[1] : j == 2 ? k[2] : k[3]);
+__device__ __forceinline__ void tile_keys_store(u64 *dst, uint32_t j, const u64 (&k)[4], uint32_t tag) {
+    const u64 v = j == 0 ? k[0] : j == 1 ? k[1] : j == 2 ? k[2] : k[3];
+    if (tag) st_coh(dst, v | (u64)tag << kListTagShift);
+    else *dst = v;
 }
 
 __device__ __forceinline__ void sort4_desc(u64 (&x)[4]) {
@@ -824,9 +842,9 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
         const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
         const double mine = part == 0 ? k[0] : part == 1 ? k[1] : part == 2 ? k[2] : k[3];
         const u64 g = global_key(mine, a.t.base + tile * kFullWaveTile);
-        if (a.coh && !MS_LIST_FENCE) {  // (launch-uniform)
-            st_coh(a.tile_keys + cell * kTopK + part, g);
-            if (part == 0) st_coh(a.tile_flags + cell, f);
+        if (a.coh) {  // (launch-uniform)
+            st_coh(a.tile_keys + cell * kTopK + part, g | (u64)a.coh << kListTagShift);
+            if (part == 0) st_coh(a.tile_flags + cell, f | a.coh << 16);
         } else {
             a.tile_keys[cell * kTopK + part] = g;
             if (part == 0) a.tile_flags[cell] = f;
@@ -850,8 +868,11 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     quad_merge4<0x4E>(k, f);  // quad_perm [2,3,0,1]
     if (pi < cnt) {
         const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
-        tile_keys_store(a.tile_keys + cell * kTopK + part, part, k);
-        if (part == 0) st_coh(a.tile_flags + cell, f);
+        tile_keys_store(a.tile_keys + cell * kTopK + part, part, k, a.coh);
+        if (part == 0) {
+            if (a.coh) st_coh(a.tile_flags + cell, f | a.coh << 16);
+            else a.tile_flags[cell] = f;
+        }
     }
     return true;
 #endif
@@ -871,13 +892,14 @@ __device__ __forceinline__ void sweep_topk_task(const SweepArgs &a, uint32_t til
 // which sweep_tp_redo then takes in the lane = row form.
 template <int W>
 __device__ __forceinline__ uint32_t sweep_tp_tile(const SweepArgs &a, uint32_t tile, DRow *rows, uint32_t wave,
-                                                  uint32_t lane) {
+                                                  uint32_t lane, u64 *tl = nullptr) {
     __syncthreads();  // the previous tile's readers are done
     const uint4 *src = reinterpret_cast<const uint4 *>(a.t.drow + (size_t)tile * kFullWaveTile);
     uint4 *dst = reinterpret_cast<uint4 *>(rows);
     constexpr uint32_t kVec = kFullWaveTile * sizeof(DRow) / sizeof(uint4);
     for (uint32_t i = threadIdx.x; i < kVec; i += 64u * W) dst[i] = src[i];
     __syncthreads();
+    if (tl && threadIdx.x == 0) tl[kTlStaged] = __builtin_amdgcn_s_memrealtime();  // (diagnostic builds)
     const TileBits tb = tile_bits(rows, lane);
     // (a batch holds at most kSeqBatch <= 256 pods, i.e. 16 groups)
     uint32_t redo = 0;
@@ -970,35 +992,70 @@ __device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int6
 // cert: how many ranks are exact. A rank past 3 may miss a row when a tile's
 // full list of four was used up before it (its fifth row is not listed), so
 // the ranks after the one that exhausts a full list are not certified.
-// COH: the lists were written in the same launch (ld_coh).
+// COH: the lists are written in the same launch (ld_coh); with tag != 0 the
+// lists carry it (MS_MERGE_TAGS) and the loads repeat until every list read
+// has it, or until `deadline` (s_memrealtime) passes: then false, nothing out.
 template <int J, int R = kTopK, bool COH = false>
-__device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_keys,
+__device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_keys,
                                                 const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
-                                                uint32_t lane, u64 &out, uint32_t &f, uint32_t *cert_out = nullptr) {
+                                                uint32_t lane, u64 &out, uint32_t &f, uint32_t *cert_out = nullptr,
+                                                uint32_t tag = 0, uint64_t deadline = 0) {
     u64 e[J][kTopK];
     uint32_t pos[J];
+    uint32_t tfs[J];
     uint32_t fl = 0;  // filters of this lane's tiles that have no feasible row
     uint32_t fa = 0;  // filters of all its tiles, + NRF for a tile with feasible rows
+    if constexpr (COH) {
+        if (tag) {  // the flag words first (4 B per list), then the keys, each until tagged
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const uint32_t tt = lane + 64u * j;
+                    tfs[j] = ld_coh(tile_flags + (size_t)p * n_tiles + min(tt, n_tiles - 1));
+                    ok = ok && (tt >= n_tiles || (tfs[j] >> 16 & 3u) == tag);
+                }
+                if (__ballot(!ok) == 0) break;
+                if (__builtin_amdgcn_s_memrealtime() > deadline) return false;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
+    for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const uint32_t tt = lane + 64u * j;
+            const uint32_t tc = min(tt, n_tiles - 1);
+            const size_t cell = (size_t)p * n_tiles + tc;
+            if constexpr (COH) {
+                if (!tag) tfs[j] = ld_coh(tile_flags + cell);
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) {
+                    e[j][k] = ld_coh(tile_keys + cell * kTopK + k);
+                    ok = ok && (!tag || tt >= n_tiles || (uint32_t)(e[j][k] >> kListTagShift) == tag);
+                }
+            } else {
+                tfs[j] = tile_flags[cell];
+                const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
+                const uint4 a = q[0], b = q[1];
+                e[j][0] = ((u64)a.y << 32) | a.x;
+                e[j][1] = ((u64)a.w << 32) | a.z;
+                e[j][2] = ((u64)b.y << 32) | b.x;
+                e[j][3] = ((u64)b.w << 32) | b.z;
+            }
+        }
+        if (!COH || !tag || __ballot(!ok) == 0) break;
+        if (__builtin_amdgcn_s_memrealtime() > deadline) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const uint32_t tt = lane + 64u * j;
         pos[j] = tt < n_tiles ? 0u : (uint32_t)kTopK;
-        const uint32_t tc = min(tt, n_tiles - 1);
-        const size_t cell = (size_t)p * n_tiles + tc;
-        uint32_t tf;
-        if constexpr (COH) {
-            tf = ld_coh(tile_flags + cell);
 #pragma unroll
-            for (int k = 0; k < kTopK; ++k) e[j][k] = ld_coh(tile_keys + cell * kTopK + k);
-        } else {
-            tf = tile_flags[cell];
-            const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
-            const uint4 a = q[0], b = q[1];
-            e[j][0] = ((u64)a.y << 32) | a.x;
-            e[j][1] = ((u64)a.w << 32) | a.z;
-            e[j][2] = ((u64)b.y << 32) | b.x;
-            e[j][3] = ((u64)b.w << 32) | b.z;
-        }
+        for (int k = 0; k < kTopK; ++k) e[j][k] = untag_key(e[j][k]);
+        const uint32_t tf = untag_flags(tfs[j]);
         if (tt < n_tiles && e[j][0] == 0) fl |= tf;
         if (tt < n_tiles) fa |= tf | (e[j][0] != 0 ? 0x100u : 0u);
     }
@@ -1018,7 +1075,7 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
                 hj = j;
             }
         }
-        const u64 m = wave_max_u64_dpp(head);
+        const u64 m = MS_MERGE_WMAX(head);
         if (lane == (uint32_t)r) out = m;
         bool used_up = false;
         if (m != 0 && head == m) {  // keys are unique: exactly one lane pops
@@ -1034,6 +1091,7 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
     if (cert_out) *cert_out = cert;
     f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u) |
         (__ballot((fa & 0xFFu) != 0) ? 0x10000u : 0u) | (__ballot((fa & 0xFF00u) != 0) ? 0x1000000u : 0u);
+    return true;
 }
 
 // Per pod (one wave): merge the tiles' top-4 lists into the global top-4, the
@@ -1042,18 +1100,23 @@ __device__ __forceinline__ void merge_pod_lists(const u64 *__restrict__ tile_key
 // ext (optional): ranks 4..7 at ext[p * 4 + r - 4] and the number of certified
 // ranks (4..8) in bits 28-31 of spec_flags (merge_pod_lists).
 // One pod's merge by one wave (k_topk_merge, and k_seq_step's merge workgroups).
+// tag / deadline: merge_pod_lists (COH, an in-step worker); false: the lists did
+// not all arrive before the deadline and nothing was written.
 template <int J, bool COH = false>
-__device__ __forceinline__ void merge_pod(const u64 *__restrict__ tile_keys, const uint32_t *__restrict__ tile_flags,
+__device__ __forceinline__ bool merge_pod(const u64 *__restrict__ tile_keys, const uint32_t *__restrict__ tile_flags,
                                           uint32_t p, uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
                                           uint32_t *__restrict__ spec_flags, const NodeTable &t,
-                                          int64_t *__restrict__ recs, u64 *__restrict__ ext, uint32_t lane) {
+                                          int64_t *__restrict__ recs, u64 *__restrict__ ext, uint32_t lane,
+                                          uint32_t tag = 0, uint64_t deadline = 0) {
     u64 out;
     uint32_t f, cert = 0;
     if (ext) {
-        merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert);
+        if (!merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert, tag, deadline))
+            return false;
         if (lane >= (uint32_t)kTopK && lane < (uint32_t)kTopExt) ext[(size_t)p * kTopK + lane - kTopK] = out;
     } else {
-        merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f);
+        if (!merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, nullptr, tag, deadline))
+            return false;
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
     if (recs && lane < (uint32_t)kTopK) store_merged_rec(t, out, recs + ((size_t)p * kTopK + lane) * kRecF);
@@ -1062,6 +1125,7 @@ __device__ __forceinline__ void merge_pod(const u64 *__restrict__ tile_keys, con
         spec[p] = out;
         spec_flags[p] = f | (cert << 28);
     }
+    return true;
 }
 
 template <int J>
@@ -1266,11 +1330,12 @@ __device__ __forceinline__ void load_lists(TileLists<J> &B, const u64 *__restric
         const size_t cell = (size_t)pc * n_tiles + tt;
         const uint4 *q = reinterpret_cast<const uint4 *>(tile_keys + cell * kTopK);
         const uint4 a = q[0], b = q[1];
-        B.e[j][0] = ((u64)a.y << 32) | a.x;
-        B.e[j][1] = ((u64)a.w << 32) | a.z;
-        B.e[j][2] = ((u64)b.y << 32) | b.x;
-        B.e[j][3] = ((u64)b.w << 32) | b.z;
-        B.f[j] = tile_flags[cell];
+        // (lists of an in-step merged batch carry the step's tag, MS_MERGE_TAGS)
+        B.e[j][0] = untag_key(((u64)a.y << 32) | a.x);
+        B.e[j][1] = untag_key(((u64)a.w << 32) | a.z);
+        B.e[j][2] = untag_key(((u64)b.y << 32) | b.x);
+        B.e[j][3] = untag_key(((u64)b.w << 32) | b.z);
+        B.f[j] = untag_flags(tile_flags[cell]);
     }
 }
 
@@ -2004,22 +2069,23 @@ struct StepMerge {
     const uint32_t *in_tags;  // batch k's tags (in_tag 0: merged by a launch, nothing to check)
     uint32_t in_tag;
     u64 *tl;                  // MS_VSTAMPS timeline (SeqMergeIO::tl): this step's row, or null
+    uint32_t list_tag;        // MS_MERGE_TAGS: the 2-bit tag of this step's lists (SweepArgs::coh)
 };
-// MS_VSTAMPS timeline fields per workgroup: 0 start, 1 swept (counted), 2 worker's
-// wait done, 3 worker's merges done, 4 validator done (workgroup 0), 5 tiles swept
-enum { kTlBegin = 0, kTlSwept, kTlWaited, kTlMerged, kTlValidated, kTlTiles };
+
 constexpr uint64_t kMergeSpinTicks = 10000;  // a worker's wait for the sweep, s_memrealtime (100 MHz): 100 us
 
-// After its sweep a workgroup counts itself done on sm.ctr (its waves' list
-// stores have landed: write-through, so other XCDs read them with ld_coh).
-// Worker wid (wave W-1 of every sweep workgroup first) then waits for all of
-// them and merges pods wid, wid + W * nsw, .. of the next batch, tagging each.
-// The wait is bounded; a worker that gives up leaves its pods untagged and the
-// next step's validation merges them (step_merge_fallback).
+// Worker wid (wave W-1 of every sweep workgroup first: idle in the transposed
+// sweep, which keeps 8 of the 12 waves busy) merges pods wid, wid + W * nsw, ..
+// of the next batch and tags each. MS_MERGE_TAGS: it polls the tagged lists
+// themselves from the start of the step (merge_pod_lists); otherwise every
+// sweep workgroup counts itself done on sm.ctr once its stores landed and the
+// worker polls the counter first. Either wait is bounded (kMergeSpinTicks); a
+// worker that gives up leaves its pods untagged and the next step's validation
+// merges them (step_merge_fallback).
 // MS_VSTAMPS (diagnostic build): the merge path's timeline relative to the
 // workgroup's start (s_memrealtime, 10 ns), summed over worker waves at stats
-// u64 [8+15] sweep done, [8+16] counter wait done, [8+17] merges done, [8+18]
-// their count, [8+19] the workgroups' counter add (summed over workgroups).
+// u64 [8+15] sweep done, [8+16] wait done, [8+17] merges done, [8+18] their
+// count, [8+19] the workgroups' count (summed over workgroups).
 template <int J, int W>
 __device__ __forceinline__ void step_merge(const SweepArgs &sw, const StepMerge &sm, uint32_t sb, uint32_t nsw,
                                            uint32_t wave, uint32_t lane, uint32_t *stats, uint64_t t_begin) {
@@ -2027,13 +2093,11 @@ __device__ __forceinline__ void step_merge(const SweepArgs &sw, const StepMerge 
     const uint64_t t_swept = __builtin_amdgcn_s_memrealtime();
     (void)t_swept;
 #endif
+#if !MS_MERGE_TAGS
     __builtin_amdgcn_s_waitcnt(0);  // (gfx9: vmcnt covers stores) this wave's lists have landed
-#if MS_LIST_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the lists reach the agent-coherent level
-#endif
     __syncthreads();
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(((gu32_t *)(sm.ctr)), 1u, __ATOMIC_RELAXED, MS_CTR_SCOPE_ID);
+        __hip_atomic_fetch_add(((gu32_t *)(sm.ctr)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
 #ifdef MS_VSTAMPS
@@ -2042,25 +2106,29 @@ __device__ __forceinline__ void step_merge(const SweepArgs &sw, const StepMerge 
         if (sm.tl) sm.tl[blockIdx.x * 8 + kTlSwept] = now;
 #endif
     }
+#endif
     const uint32_t wid = (W - 1 - wave) * nsw + sb;
     if (wid >= sm.n || sm.skip) return;  // wave-uniform
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t deadline = __builtin_amdgcn_s_memrealtime() + kMergeSpinTicks;
+#if !MS_MERGE_TAGS
     for (;;) {
         const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)__hip_atomic_load(((const gu32_t *)(sm.ctr)), __ATOMIC_RELAXED, MS_CTR_SCOPE_ID));
+            (int)__hip_atomic_load(((const gu32_t *)(sm.ctr)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if ((int32_t)(v - sm.target) >= 0) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kMergeSpinTicks) return;
-        if (MS_CTR_SLEEP) __builtin_amdgcn_s_sleep(MS_CTR_SLEEP);
+        if (__builtin_amdgcn_s_memrealtime() > deadline) return;
+        __builtin_amdgcn_s_sleep(1);
     }
-#if MS_LIST_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale lines of the other workgroups' lists
+    const uint32_t tag = 0;
+#else
+    const uint32_t tag = sm.list_tag;
 #endif
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
     const uint64_t t_waited = __builtin_amdgcn_s_memrealtime();
 #endif
     for (uint32_t p = wid; p < sm.n; p += W * nsw) {
-        merge_pod<J, !MS_LIST_FENCE>(sw.tile_keys, sw.tile_flags, p, sw.n_tiles, sm.top, sm.spec, sm.spec_flags, sw.t,
-                                     sm.recs, sm.ext, lane);
+        if (!merge_pod<J, true>(sw.tile_keys, sw.tile_flags, p, sw.n_tiles, sm.top, sm.spec, sm.spec_flags, sw.t,
+                                sm.recs, sm.ext, lane, tag, deadline))
+            return;  // (untagged: the next validation merges it)
         if (lane == 0) sm.tags[p] = sm.tag;
     }
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
@@ -2162,18 +2230,28 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         uint32_t *defer = reinterpret_cast<uint32_t *>(rows + kFullWaveTile) + wave * kTpDeferCap;
         uint32_t nd = 0;
         bool over = false;
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+        u64 *const tlw = (sm.tl && blockIdx.x < kTimelineWgs) ? sm.tl + blockIdx.x * 8 : nullptr;
+#else
+        u64 *const tlw = nullptr;
+#endif
         for (uint32_t tile = sb; tile < sw.n_tiles; tile += sg) {
-            const uint32_t r = sweep_tp_tile<W>(sw, tile, rows, wave, lane);  // (wave-uniform)
+            const uint32_t r = sweep_tp_tile<W>(sw, tile, rows, wave, lane, tile == sb ? tlw : nullptr);  // (wave-uniform)
             if (r) {
                 if (nd < kTpDeferCap) defer[nd++] = tile << 16 | r;
                 else over = true;
             }
         }
+        if (tlw && threadIdx.x == 0) tlw[kTlWave0] = __builtin_amdgcn_s_memrealtime();
         for (uint32_t i = 0; i < nd; ++i) sweep_tp_redo<W>(sw, defer[i] >> 16, defer[i] & 0xFFFFu, wave, lane);
         if (over) {  // (more deferred tiles than the list holds: every group of every tile, exactly)
             uint32_t all = 0;
             for (uint32_t grp = wave, i = 0; grp * kTpPods < sw.n_pods; grp += W, ++i) all |= 1u << i;
             for (uint32_t tile = sb; tile < sw.n_tiles; tile += sg) sweep_tp_redo<W>(sw, tile, all, wave, lane);
+        }
+        if (tlw) {  // (launch-uniform: diagnostic builds only)
+            __syncthreads();
+            if (threadIdx.x == 0) tlw[kTlTasks] = __builtin_amdgcn_s_memrealtime();
         }
     } else {
         for (uint32_t task = sb * W + wave; task < n_tasks; task += sg * W)
@@ -2211,7 +2289,7 @@ __global__ __launch_bounds__(64) void k_seq_pack_cands(NodeTable t, const u64 *_
     const uint32_t p = blockIdx.x, lane = threadIdx.x;
     if (p >= n_pods) return;
     uint32_t fl = 0;
-    for (uint32_t tt = lane; tt < n_tiles; tt += 64) fl |= tile_flags[(size_t)p * n_tiles + tt];
+    for (uint32_t tt = lane; tt < n_tiles; tt += 64) fl |= untag_flags(tile_flags[(size_t)p * n_tiles + tt]);
     const uint32_t f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u);
     if (lane == 0) flags[p] = f;
     if (lane < (uint32_t)kTopK) {
@@ -2808,7 +2886,10 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
             sm.target = mio->target;
             sm.n = n_next;
             sm.skip = mio->skip ? 1u : 0u;
-            sw.coh = 1u;
+            // the lists' tag: 1..3 over consecutive steps, so a list set (rewritten every
+            // second step, zeroed at the start of a run) never holds the tag it waits for
+            sm.list_tag = 1u + mio->tag % 3u;
+            sw.coh = sm.list_tag;
         } else if (mio->top) {
             return hipErrorInvalidValue;  // (the caller asked for an in-step merge seq_step_merges rules out)
         }

@@ -37,8 +37,15 @@ def main(path, out=None):
             r.update(merged_median=float(us(np.median(m))), merged_max=float(us(m.max())))
         if tl[s, 0, 4] > 0:
             r["validator_done"] = float(us(tl[s, 0, 4]))
+        for f, name in ((5, "staged"), (6, "wave0_tasks"), (7, "all_tasks")):
+            x = tl[s, live, f]
+            x = x[x > 0]
+            if len(x):
+                r[name + "_median"] = float(us(np.median(x)))
+                r[name + "_max"] = float(us(x.max()))
         rows.append(r)
-    keys = ["start_spread_us", "swept_min", "swept_median", "swept_max", "waited_median", "waited_max",
+    keys = ["start_spread_us", "staged_median", "staged_max", "wave0_tasks_median", "all_tasks_median",
+            "all_tasks_max", "swept_min", "swept_median", "swept_max", "waited_median", "waited_max",
             "merged_median", "merged_max", "validator_done"]
     med = {k: float(np.median([r[k] for r in rows if k in r])) for k in keys if any(k in r for r in rows)}
     for r in rows:
