@@ -369,6 +369,21 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
             return (s0 < warm.first && warm.second) ? std::min(warm.second, B) : B;
         };
         const uint32_t nb0 = std::min(batch_at(0), n_pods);
+        const char *merge_env = getenv("MINISCHED_SEQ_MERGE");
+        const std::string merge_mode = merge_env ? merge_env : "instep";
+        const bool want_instep = merge_mode == "instep" || merge_mode == "fallback";
+        if (want_instep) {
+            // Tagged lists: no cell of either set may hold a tag from an earlier run
+            // (or an earlier chunk of this call). Both sets, every pod slot: a
+            // warm-up batch rewrites only its first pods, and a cell left from a
+            // previous run whose 2-bit tag happened to match was taken as swept
+            // (config E's second 65,536-pod chunk, pods 64..127 of its first
+            // full-size batch: tests/test_gpu_fullsize.py, profiles/r05n_e_probe.txt).
+            MS_HIP(c, hipMemsetAsync(c->d_merge_ctr, 0, 1024, s));
+            MS_HIP(c, hipMemsetAsync(c->d_tile_keys, 0,
+                                     (size_t)kSeqBufs * cells_per_set * seq_topk() * sizeof(unsigned long long), s));
+            MS_HIP(c, hipMemsetAsync(c->d_tile_flags, 0, (size_t)kSeqBufs * cells_per_set * sizeof(uint32_t), s));
+        }
         MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, c->d_tile_keys, c->d_tile_flags, n_tiles, s));
         MS_HIP(c, launch_topk_merge(c->d_tile_keys, c->d_tile_flags, nb0, n_tiles, c->d_top4, c->d_spec,
                                     c->d_spec_flags, tq, c->d_top4_rec, s, top_ext));
@@ -381,18 +396,8 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         // validator: config E 44.4 -> 40.5 ms against the merge launch
         // (profiles/r05c_e_ab.txt, r05f_e_sync_ab.txt). MINISCHED_SEQ_MERGE=launch:
         // a k_topk_merge launch after each step (A/B); "fallback": the in-step
-        // workers skip (a test hook). Read per call (tests switch it).
-        const char *merge_env = getenv("MINISCHED_SEQ_MERGE");
-        const std::string merge_mode = merge_env ? merge_env : "instep";
-        const bool want_instep = merge_mode == "instep" || merge_mode == "fallback";
-        if (want_instep) {
-            MS_HIP(c, hipMemsetAsync(c->d_merge_ctr, 0, 1024, s));
-            // (tagged lists: no set may hold a tag from an earlier run)
-            MS_HIP(c, hipMemsetAsync(c->d_tile_keys + cells_per_set * seq_topk(), 0,
-                                     (size_t)(kSeqBufs - 1) * cells_per_set * seq_topk() * sizeof(unsigned long long), s));
-            MS_HIP(c, hipMemsetAsync(c->d_tile_flags + cells_per_set, 0,
-                                     (size_t)(kSeqBufs - 1) * cells_per_set * sizeof(uint32_t), s));
-        }
+        // workers skip (a test hook). Read per call (tests switch it); the lists
+        // were cleared above.
         uint32_t k = 0, in_tag = 0, target = 0;
         for (uint32_t s0 = 0, nb = 0; s0 < n_pods; s0 += nb, ++k) {
             nb = std::min(batch_at(s0), n_pods - s0);

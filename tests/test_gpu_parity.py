@@ -393,6 +393,25 @@ def test_chunked_batches(oracle):
         assert_same(e.schedule(pr, MODE_SEQUENTIAL), o)
 
 
+@pytest.mark.parametrize("max_batch", [8300, 8320, 8384])
+def test_chunked_warm_runs(oracle, max_batch):
+    # every chunk of a call is a sequential run that opens with warm-up batches of
+    # 64 (its first 8,192 pods), so only pods 0..63 of a list set are rewritten
+    # until its first full-size batch; cells left over from the previous chunk
+    # must never pass for swept ones (the 2-bit list tag repeats every third
+    # step: three chunk sizes, three tag phases), nor across two calls
+    seed = max_batch
+    nr = synth.nodes(3000, seed=seed, resources=True)
+    pr = synth.pods(3 * max_batch + 77, seed=seed, resources=True)
+    o = oracle.schedule(nr, pr, plugin_set=1, mode=1, seed=seed)
+    half = len(pr) // 2
+    with engine_with(nr, plugin_set=PLUGINS_NU_NRF_NN_LA, seed=seed, max_batch=max_batch) as e:
+        a = e.schedule(pr[:half], MODE_SEQUENTIAL)
+        b = e.schedule(pr[half:], MODE_SEQUENTIAL)
+        assert_same(np.concatenate([a, b]), o)
+        assert_table_equal(e, o["cols"], 3000)
+
+
 @pytest.mark.parametrize("pipe", ["fused2", "fused", "2", "1", "0"])
 @pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
 def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch, pipe):
