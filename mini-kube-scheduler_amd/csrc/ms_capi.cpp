@@ -509,14 +509,13 @@ int ensure_stage(ms_ctx *c, uint32_t n) {
     return MS_OK;
 }
 
-// MS_PLUGINS_NU_TT_NN: summary scratch for n pods' row segments.
-int ensure_tt(ms_ctx *c, uint32_t n) {
-    const size_t need = (size_t)tt_segments(c->rows_dev) * n * MS_TT_SUMMARY_BYTES;
+// MS_PLUGINS_NU_TT_NN scratch: `need` bytes (summaries or the two-pass cycle's).
+int ensure_tt(ms_ctx *c, size_t need) {
     if (need <= c->tt_bytes) return MS_OK;
     if (c->d_tt) (void)hipFree(c->d_tt);
     c->d_tt = nullptr;
     c->tt_bytes = 0;
-    if (hipMalloc(&c->d_tt, need) != hipSuccess) return fail(c, MS_E_OOM, "TaintToleration summaries");
+    if (hipMalloc(&c->d_tt, need) != hipSuccess) return fail(c, MS_E_OOM, "TaintToleration scratch");
     c->tt_bytes = need;
     return MS_OK;
 }
@@ -524,17 +523,32 @@ int ensure_tt(ms_ctx *c, uint32_t n) {
 // The batch's per-pod summaries of every row segment, merged in LIST order into
 // out (this shard's summary), or finalised into results (the single-shard
 // cycle; commit: the winners' NodeInfo.AddPod). Chunks of batch_cap pods.
+// A single-shard cycle (results) runs the two-pass bit-sliced form (round 5,
+// launch_tt2_cycle); MINISCHED_TT=v1: the per-pair summary sweep (A/B), which
+// the shard summaries (out) always use.
 int tt_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *out, ms_result *results, int commit,
                     hipStream_t s) {
-    const uint32_t B = c->batch_cap, segs = tt_segments(c->rows_dev);
-    int rc = ensure_tt(c, std::min(B, n_pods));
+    static const bool v1 = [] {
+        const char *e = getenv("MINISCHED_TT");
+        return e && std::string(e) == "v1";
+    }();
+    const bool two_pass = !out && !v1;
+    const uint32_t B = c->batch_cap, segs = tt_segments(c->rows_dev), cap = std::min(B, n_pods);
+    int rc = ensure_tt(c, two_pass ? tt2_scratch_bytes(c->rows_dev, cap)
+                                   : (size_t)segs * cap * MS_TT_SUMMARY_BYTES);
     if (rc) return rc;
     if (!c->ev_tt) MS_HIP(c, hipEventCreateWithFlags(&c->ev_tt, hipEventDisableTiming));
     // the previous cycle's sweep/combine on another stream still owns d_tt
     if (c->tt_stream && c->tt_stream != s) MS_HIP(c, hipStreamWaitEvent(s, c->ev_tt, 0));
     const uint32_t seed32 = seed32_of(c->cfg.seed);
+    if (two_pass) MS_HIP(c, launch_tt2_planes(c->t, c->rows_dev, c->d_tt, s));
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
+        if (two_pass) {
+            MS_HIP(c, launch_tt2_cycle(c->t, c->rows_dev, d_pods + s0, nb, seed32, c->d_tt, cap, results + s0, commit,
+                                       s));
+            continue;
+        }
         MS_HIP(c, launch_tt_sweep(c->t, c->rows_dev, d_pods + s0, nb, seed32, c->d_tt, s));
         MS_HIP(c, launch_tt_combine(c->d_tt, nb, segs, d_pods + s0, nb, seed32,
                                     out ? static_cast<char *>(out) + (size_t)s0 * MS_TT_SUMMARY_BYTES : nullptr,

@@ -338,6 +338,15 @@ hipError_t launch_decode(const ms_pod_rec *pods, uint32_t n_pods, const unsigned
 uint32_t tt_segments(uint32_t n_rows, uint32_t *seg_rows = nullptr);
 hipError_t launch_tt_sweep(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            uint32_t seed32, void *summaries, hipStream_t s);
+// The two-pass bit-sliced TaintToleration cycle of one context (ms_taint.hip
+// k_tt2_*): row planes once per cycle (launch_tt2_planes), then per chunk of up
+// to max_pods pods census -> plan -> pick -> final into results (commit: binds).
+uint32_t tt2_words(uint32_t n_rows);
+size_t tt2_scratch_bytes(uint32_t n_rows, uint32_t max_pods);
+hipError_t launch_tt2_planes(const NodeTable &t, uint32_t n_rows, void *scratch, hipStream_t s);
+hipError_t launch_tt2_cycle(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                            uint32_t seed32, void *scratch, uint32_t max_pods, ms_result *results, int commit,
+                            hipStream_t s);
 hipError_t launch_tt_combine(const void *in, uint32_t stride, uint32_t n_segs, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, void *out, ms_result *results, const NodeTable &t, int commit,
                              hipStream_t s);

@@ -157,3 +157,47 @@ def test_tt_node_shards(oracle, cuts):
         for e in engines:
             e.close()
     assert sharded.shard_bounds(n, 0, 1) == (0, n)
+
+
+def _dense_cluster(n_nodes, n_pods, seed, hard_p=0.03, soft_p=0.35, tol_p=0.3):
+    # every one of the 8 NoSchedule and 8 PreferNoSchedule ids in use, so raw
+    # counts reach 8 (the bit-sliced census' c3 plane) and classes are sparse
+    rng = np.random.default_rng(seed)
+    nr = synth.nodes(n_nodes, seed=seed, taints=True)
+    hard = (rng.random((n_nodes, 8)) < hard_p) @ (1 << np.arange(8))
+    soft = (rng.random((n_nodes, 8)) < soft_p) @ (1 << np.arange(8))
+    nr["taints"] = (hard | (soft << 8)).astype(np.uint32)
+    nr["taints"][rng.random(n_nodes) < 0.01] |= 0xFF00  # some rows with all 8 soft ids
+    pr = synth.pods(n_pods, seed=seed, taints=True)
+    synth.set_tolerations(pr, (rng.random((n_pods, 8)) < tol_p) @ (1 << np.arange(8)),
+                          (rng.random((n_pods, 8)) < tol_p) @ (1 << np.arange(8)))
+    pr["name_digit"][::23] = -1
+    pr["tolerates_unschedulable"][::5] = 1
+    return nr, pr
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,seed", [(3, 300, 21), (7, 400, 22), (40, 600, 23), (700, 800, 24),
+                                                 (2050, 500, 25)])
+def test_tt_dense_taints_literal(oracle, n_nodes, n_pods, seed):
+    # the two-pass census / pick: F <= 4, the first-three and last rows inside one
+    # word and across words, classes present only without a NodeNumber match (W0)
+    nr, pr = _dense_cluster(n_nodes, n_pods, seed)
+    dead = np.arange(0, n_nodes, 9)
+    o = _oracle(oracle, nr, pr, seed, dead, literal=True)
+    with _engine(nr, seed, dead=dead) as e:
+        _same(_device_cycle(e, pr), o, "device")
+        _same(e.schedule(pr, _lib.MODE_BATCHED), o, "host")
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,seed", [(9000, 2000, 26), (33_000, 1200, 27)])
+def test_tt_dense_taints_segments(oracle, n_nodes, n_pods, seed):
+    # several row segments (census merge, global rank parity in the pick) against the
+    # closed form; sparse digits make W0 (no matching row in the winning class) common
+    nr, pr = _dense_cluster(n_nodes, n_pods, seed, hard_p=0.05, soft_p=0.45)
+    rng = np.random.default_rng(seed)
+    nr["name_digit"][rng.random(n_nodes) < 0.7] = 255  # most nodes without a digit name
+    dead = np.arange(0, n_nodes, 31)
+    o = _oracle(oracle, nr, pr, seed, dead)
+    with _engine(nr, seed, dead=dead) as e:
+        _same(_device_cycle(e, pr), o, "device")
+    assert (o["code"] == 0).sum() > 0.5 * n_pods
