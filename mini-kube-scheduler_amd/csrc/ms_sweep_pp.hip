@@ -377,18 +377,20 @@ __global__ __launch_bounds__(64 * kPpMaxWaves) void k_sweep_nunn_pp(
     const uint32_t *__restrict__ planes, uint32_t gstride, uint32_t n_groups, uint32_t node_base,
     const ms_pod_rec *__restrict__ pods1, uint32_t n_pods1, uint32_t chunk, uint32_t seed32, u64 *__restrict__ keys1,
     int atomic_keys, ms_result *__restrict__ results, uint32_t present, NodeTable tab, int commit,
-    uint32_t pstride, ms_result_compact *__restrict__ resc, PpJob2 j2, int fix_ok) {
+    uint32_t pstride, ms_result_compact *__restrict__ resc, PpJob2 j2, int fix_ok, uint32_t xtra) {
     // LDS: one combine slot per pod of the chunk, then the chunk's pod entries
+    // (xtra: workgroups 0 .. xtra-1 take chunk + 8 pods, the balanced split)
     extern __shared__ u64 lds[];
-    uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk);
+    uint2 *pinfo = reinterpret_cast<uint2 *>(lds + chunk + (xtra ? 8u : 0u));
     const uint32_t lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const bool second = j2.pods && blockIdx.x >= j2.nblk1;  // (workgroup-uniform)
     const ms_pod_rec *__restrict__ pods = second ? j2.pods : pods1;
     const uint32_t n_pods = second ? j2.n_pods : n_pods1;
     u64 *__restrict__ keys = second ? j2.keys : keys1;
-    const uint32_t pbeg = (second ? blockIdx.x - j2.nblk1 : blockIdx.x) * chunk;
-    const uint32_t pend = min(n_pods, pbeg + chunk);
+    const uint32_t bi = second ? blockIdx.x - j2.nblk1 : blockIdx.x;
+    const uint32_t pbeg = bi * chunk + min(bi, xtra) * 8u;
+    const uint32_t pend = min(n_pods, pbeg + chunk + (bi < xtra ? 8u : 0u));
     const uint32_t np = pend > pbeg ? pend - pbeg : 0u;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
         lds[i] = 0;
@@ -647,8 +649,33 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // profiles/r04n_shard_shapes.txt, r04p_chunk56_probe.json. Not kept.)
     if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
-    const uint32_t nblk1 = cdiv(n_pods, chunk);
-    const dim3 grid(nblk1 + (pods2 ? cdiv(n_pods2, chunk) : 0u), gy);
+    uint32_t nblk1 = cdiv(n_pods, chunk), xtra = 0;
+    // Balanced split of a one-batch shard sweep (2- and 4-wave workgroups, one
+    // round of 16 waves per CU): chunks rounded up to 8 leave some SIMDs a wave
+    // short of others (12.5k rows x 100k pods: 1,786 workgroups of 56 pods over
+    // 2,048 slots, 3.5 waves per SIMD, the busiest 4 x 56 pods). Instead every
+    // slot gets a workgroup: `chunk` pods each, 8 more for the first `xtra`
+    // (4 x 48.8 pods on the busiest SIMD): the shard sweep alone 42.0 -> 38.7 us
+    // at G = 8, 71.5 -> 67.5 at G = 4 (profiles/r05r_balance_ab.txt).
+    // MINISCHED_PP_BALANCE=0: off (A/B).
+    static const bool balance = [] {
+        const char *e = getenv("MINISCHED_PP_BALANCE");
+        return !e || atoi(e) != 0;
+    }();
+    // A coalesced pair of equal batches splits the slots in halves, each balanced alike.
+    if (balance && (!pods2 || n_pods2 == n_pods) && gy == 1 && W <= 4u && !getenv("MINISCHED_PP_CHUNK")) {
+        const uint32_t slots = (16u / W) * cus / (pods2 ? 2u : 1u);
+        const uint32_t cb = (n_pods / slots) / 8u * 8u;
+        if (cb >= 8u && cb + 8u <= kPpMaxChunk && n_pods > cb * slots) {
+            const uint32_t nx = cdiv(n_pods - cb * slots, 8u);
+            if (nx <= slots) {
+                chunk = cb;
+                xtra = nx;
+                nblk1 = slots;
+            }
+        }
+    }
+    const dim3 grid(nblk1 + (pods2 ? (xtra ? nblk1 : cdiv(n_pods2, chunk)) : 0u), gy);
     // the fixed-slot form for digit-aligned waves (MINISCHED_PP_FIX=0: off, A/B)
     static const int fix_ok = [] {
         const char *e = getenv("MINISCHED_PP_FIX");
@@ -664,7 +691,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((k_sweep_nunn_pp<kPpWords, false>), grid, dim3(64 * W), chunk * (sizeof(u64) + sizeof(uint2)), s, t.planes,
                            t.gcap, n_groups, t.base, pods, n_pods, chunk, seed32, keys, 1, (ms_result *)nullptr, present,
-                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr, PpJob2{}, fix_ok);
+                           t, 0, (uint32_t)sizeof(ms_pod_rec), (ms_result_compact *)nullptr, PpJob2{}, fix_ok, 0u);
         e = hipGetLastError();
         if (e == hipSuccess && results) e = launch_decode(pods, n_pods, keys, nullptr, present, results, s);
         if (e == hipSuccess && results && commit) e = launch_apply_binds(t, pods, n_pods, results, s);
@@ -673,7 +700,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     }
     // done: recorded by the dispatch itself (hipExtLaunchKernel's stop event: no
     // separate event packet between this sweep and the next launch on s)
-    const uint32_t lds = chunk * (sizeof(u64) + sizeof(uint2));
+    const uint32_t lds = (chunk + (xtra ? 8u : 0u)) * (sizeof(u64) + sizeof(uint2));
     unsigned long long *kk = (results || resc) ? nullptr : keys;
     const int cm = (results || resc) ? commit : 0;
     // (gy == 1: the workgroup holds every group; the 8-word form stays unpacked: its
@@ -682,7 +709,7 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
 #define MS_PP_LAUNCH(KWV, TPV)                                                                                     \
     hipExtLaunchKernelGGL((k_sweep_nunn_pp<KWV, TPV>), grid, dim3(64 * W), lds, s, nullptr, done, 0, t.planes, t.gcap, \
                           n_groups, t.base, pods, n_pods, chunk, seed32, kk, 0, results, present, t, cm, pstride, resc, j2, \
-                          fix_ok)
+                          fix_ok, xtra)
     if (KW == (uint32_t)kPpWordsSmall) {
         MS_PP_LAUNCH(kPpWordsSmall, false);
     } else {
