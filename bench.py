@@ -62,12 +62,16 @@ BYTES_PER_EVAL = {"NU+NN": 2, "NU+NRF+NN+LA": 58}
 VALU_PEAK_NOMINAL = 256 * 4 * 2.4e9 / 4
 VALU_PEAK_MEASURED = 256 * 4 / 1.75e-9
 # MI355X_MICROARCH.md (lines 54, 473): a wave64 VALU op issues over 2 cycles on a
-# SIMD-32, i.e. 1.229e12 wave-instructions/s chip-wide. No instruction this
-# kernel uses reached it in our microbenchmark (~4.2 cycles each at 8 waves per
-# SIMD, profiles/r02c_valu_rates.txt), so `frac` stays against the 4-cycle
-# rate and `frac_vs_guide_peak` reports the guide's figure beside it.
+# SIMD-32, i.e. 1.229e12 wave-instructions/s chip-wide. No instruction reached it
+# in our microbenchmark, packed controls included: at 1 / 2 / 4 / 8 / 16 waves per
+# SIMD every one of 20 ops (v_bitop3, v_pk_fma_f32, v_pk_add_u16, v_max_f64, ...)
+# converges to 4.1-4.2 cycles per wave-instruction per SIMD, and the counters say
+# SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU with 4.0 active cycles each
+# (profiles/r05b_valu_issue.json), so `frac` stays against the 4-cycle rate and
+# `frac_vs_guide_peak` reports the guide's figure beside it.
 VALU_PEAK_GUIDE = 256 * 4 * 2.4e9 / 2
-VALU_RATES_UBENCH = "tools/ubench/valu_rates.hip -> profiles/r02c_valu_rates.txt"
+VALU_RATES_UBENCH = ("tools/ubench/valu_rates.hip + valu_pmc.sh -> profiles/r05b_valu_issue.json: 4.0 active "
+                     "cycles per wave64 VALU instruction, 1-16 waves per SIMD, packed ops included")
 PP_KERNEL = "k_sweep_nunn_pp"
 
 
@@ -87,11 +91,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the e2e measurements and configs B, D, E")
     ap.add_argument("--no-configs", action="store_true", help="skip configs B, D, E (device + CPU baselines)")
-    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r04z_pmc_C.json"),
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "r05t_pmc_C.json"),
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
     ap.add_argument("--profile-shard-prefix", default=os.path.join(ROOT, "profiles", "r04zh_pmc_shard"),
                     help="N > 1: per-shard K1 counters <prefix><rows>.json (tools/profile_shards.sh)")
-    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r04z_pmc_E.json"),
+    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r05t_pmc_E.json"),
                     help="rocprofv3 counter summary of config E's step kernel (tools/profile_e.sh)")
     return ap.parse_args()
 
