@@ -1005,8 +1005,14 @@ __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_key
     uint32_t tfs[J];
     uint32_t fl = 0;  // filters of this lane's tiles that have no feasible row
     uint32_t fa = 0;  // filters of all its tiles, + NRF for a tile with feasible rows
+#ifndef MS_MERGE_FUSEDPOLL
+// 1 (default): one poll loop loads flags and keys together, so the last poll is
+// one memory round trip instead of two (E 38.52 -> 38.24 ms, profiles/r05u_e_ab.txt;
+// 0: flags until tagged, then keys)
+#define MS_MERGE_FUSEDPOLL 1
+#endif
     if constexpr (COH) {
-        if (tag) {  // the flag words first (4 B per list), then the keys, each until tagged
+        if (tag && !MS_MERGE_FUSEDPOLL) {  // the flag words first (4 B per list), then the keys, each until tagged
             for (;;) {
                 bool ok = true;
 #pragma unroll
@@ -1029,7 +1035,10 @@ __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_key
             const uint32_t tc = min(tt, n_tiles - 1);
             const size_t cell = (size_t)p * n_tiles + tc;
             if constexpr (COH) {
-                if (!tag) tfs[j] = ld_coh(tile_flags + cell);
+                if (!tag || MS_MERGE_FUSEDPOLL) {
+                    tfs[j] = ld_coh(tile_flags + cell);
+                    ok = ok && (!tag || tt >= n_tiles || (tfs[j] >> 16 & 3u) == tag);
+                }
 #pragma unroll
                 for (int k = 0; k < kTopK; ++k) {
                     e[j][k] = ld_coh(tile_keys + cell * kTopK + k);
