@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <string>
@@ -798,6 +799,7 @@ int ensure_zc(ms_ctx *c, uint32_t n) {
 // round 3, slot-search K1: 4 chunks of 25k cost as much kernel time as their
 // overlap saved). MINISCHED_ZC_PARTS overrides the chunk count (1..4).
 constexpr uint32_t kZcMinChunk = 50000;
+constexpr uint32_t kZcParMin = 16384;  // pods per chunk from which the copies use the pool
 template <typename PodIn, typename ResOut>
 int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock &ck) {
     static_assert(sizeof(ms_pod_compact) <= sizeof(PodIn), "compact pod = the first 8 B of a pod record");
@@ -816,26 +818,48 @@ int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock
     const uint32_t parts = parts_env ? std::min(parts_env, std::max(1u, n)) : std::max(1u, std::min(4u, n / kZcMinChunk));
     const uint32_t per = cdiv(n, parts);
     auto beg = [&](uint32_t i) { return std::min(n, i * per); };
+    // Host copies split over the caller and the copy pool's helpers
+    // (MINISCHED_COPY_THREADS helpers, default 3; 0 = the caller alone): the first
+    // chunk's copy-in and the last one's copy-out are on the call's critical path.
+    static const unsigned helpers = [] {
+        const char *e = getenv("MINISCHED_COPY_THREADS");
+        return e ? (unsigned)std::min(15, std::max(0, atoi(e))) : 3u;
+    }();
+    if (helpers && per >= kZcParMin && !c->copy_pool) c->copy_pool.reset(new (std::nothrow) CopyPool(helpers));
+    CopyPool *pool = per >= kZcParMin ? c->copy_pool.get() : nullptr;
+    auto par = [&](uint32_t lo, uint32_t hi, const std::function<void(uint32_t, uint32_t)> &fn) {
+        if (!pool) {
+            fn(lo, hi);
+            return;
+        }
+        pool->run_parts([&](unsigned p, unsigned P) {
+            fn(lo + (uint32_t)((uint64_t)(hi - lo) * p / P), lo + (uint32_t)((uint64_t)(hi - lo) * (p + 1) / P));
+        });
+    };
     auto move_out = [&](uint32_t i) {
         const ms_result_compact *r = c->h_resz;
-        if constexpr (std::is_same<ResOut, ms_result_compact>::value) {
-            std::memcpy(out + beg(i), r + beg(i), sizeof(ms_result_compact) * (beg(i + 1) - beg(i)));
-        } else {
-            for (uint32_t j = beg(i); j < beg(i + 1); ++j) {
-                const ms_result_compact x = r[j];
-                out[j] = ms_result{x.node, (int32_t)x.code, (int64_t)x.score, (uint32_t)x.plugin_mask, 0u};
+        par(beg(i), beg(i + 1), [&](uint32_t a, uint32_t b) {
+            if constexpr (std::is_same<ResOut, ms_result_compact>::value) {
+                std::memcpy(out + a, r + a, sizeof(ms_result_compact) * (b - a));
+            } else {
+                for (uint32_t j = a; j < b; ++j) {
+                    const ms_result_compact x = r[j];
+                    out[j] = ms_result{x.node, (int32_t)x.code, (int64_t)x.score, (uint32_t)x.plugin_mask, 0u};
+                }
             }
-        }
+        });
     };
     ++c->ctx_seq;  // binds write the table on the context stream
     ck.count(MS_PH_CHUNKS, parts);
     for (uint32_t i = 0; i < parts; ++i) {
         ms_pod_compact *z = c->h_podz;
-        if constexpr (std::is_same<PodIn, ms_pod_compact>::value) {
-            std::memcpy(z + beg(i), pods + beg(i), sizeof(ms_pod_compact) * (beg(i + 1) - beg(i)));
-        } else {
-            for (uint32_t j = beg(i); j < beg(i + 1); ++j) std::memcpy(&z[j], &pods[j], sizeof(ms_pod_compact));
-        }
+        par(beg(i), beg(i + 1), [&](uint32_t a, uint32_t b) {
+            if constexpr (std::is_same<PodIn, ms_pod_compact>::value) {
+                std::memcpy(z + a, pods + a, sizeof(ms_pod_compact) * (b - a));
+            } else {
+                for (uint32_t j = a; j < b; ++j) std::memcpy(&z[j], &pods[j], sizeof(ms_pod_compact));
+            }
+        });
         ck.lap(MS_PH_STAGE_IN);
         MS_HIP(c, launch_sweep_pp_compact(c->t, c->rows_dev, c->h_podz + beg(i), beg(i + 1) - beg(i),
                                           seed32_of(c->cfg.seed), c->h_resz + beg(i), c->present_dev, c->num_cus, s));

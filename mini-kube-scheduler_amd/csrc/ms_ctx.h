@@ -7,10 +7,12 @@
 
 #include <chrono>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
 
+#include "ms_copy_pool.h"
 #include "ms_internal.h"
 
 namespace msgpu {
@@ -26,6 +28,9 @@ struct ms_ctx {
     hipStream_t stream = nullptr;
     int num_cus = 0;
     NodeTable t{};
+    // helper threads for the host copies of single-shard host-array calls
+    // (ms_copy_pool.h; created on the first large call, joined when the context is deleted)
+    std::unique_ptr<msgpu::CopyPool> copy_pool;
 
     // node deltas (informer goroutines) — guarded by delta_mu
     std::mutex delta_mu;

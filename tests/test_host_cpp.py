@@ -111,3 +111,13 @@ def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes
     assert np.array_equal(mask, o["mask"])
     if plugin_set == 1:
         assert (o["code"] == 2).sum() > 0 and (o["code"] == 1).sum() > 0
+
+
+def test_copy_pool_tsan(tmp_path):
+    # the host-copy helper threads of ms_schedule_batch(_compact) (csrc/ms_copy_pool.h)
+    exe = str(tmp_path / "test_copy_pool")
+    src = os.path.join(ROOT, "tests", "cpp", "test_copy_pool.cpp")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-pthread",
+                    "-I", os.path.join(PKG, "csrc"), src, "-o", exe], check=True)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    assert "0 failed" in _run([exe], env=env)
