@@ -660,16 +660,6 @@ __global__ void k_tt2_plan(const TtCensus *__restrict__ census, uint32_t n_segs,
     tt2_store(results, p, out, t, pod, commit);
 }
 
-// The rows of class bit k (c = k >> 1, parity k & 1) among those of the word.
-__device__ __forceinline__ uint32_t tt_class_rows(const TtWord &x, uint32_t Q, uint32_t k) {
-    const uint32_t c = k >> 1;
-    uint32_t m = (k & 1u) ? Q : ~Q;
-    m = TT_BITOP3(x.c0, (c & 1u) ? ~0u : 0u, m, kXnorAnd3);
-    m = TT_BITOP3(x.c1, (c & 2u) ? ~0u : 0u, m, kXnorAnd3);
-    m = TT_BITOP3(x.c2, (c & 4u) ? ~0u : 0u, m, kXnorAnd3);
-    return TT_BITOP3(x.c3, (c & 8u) ? ~0u : 0u, m, kXnorAnd3);
-}
-
 // grid (pod blocks, segments): per (pod, segment) the best key at S* among the
 // middle rows of the winning classes (0: none), ranks global.
 __global__ __launch_bounds__(kTt2Threads) void k_tt2_pick(const uint32_t *__restrict__ planes, uint32_t n_words,
@@ -694,7 +684,19 @@ __global__ __launch_bounds__(kTt2Threads) void k_tt2_pick(const uint32_t *__rest
     uint32_t n = 0;  // feasible rows before this segment (global ranks)
     if (active)
         for (uint32_t s = 0; s < seg; ++s) n += census[(size_t)s * n_pods + p].n;
-    const uint32_t F = plan.F, w1s = plan.w1, w0s = plan.w0;
+    const uint32_t F = plan.F;
+    // the (at most one) winning class with a matching row and the (at most one)
+    // without (k_tt2_plan: the 18 class scores are distinct), as per-lane masks:
+    // c's bits 0 / ~0, the parity as an XOR on the odd-rank mask, validity
+    const uint32_t k1 = plan.w1 ? first_slot(plan.w1) : 0u, k0 = plan.w0 ? first_slot(plan.w0) : 0u;
+    const uint32_t v1 = plan.w1 ? ~0u : 0u, v0 = plan.w0 ? ~0u : 0u;
+    const uint32_t q1x = (k1 & 1u) ? 0u : ~0u, q0x = (k0 & 1u) ? 0u : ~0u;
+    uint32_t c1b[4], c0b[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        c1b[b] = ((k1 >> (1 + b)) & 1u) ? ~0u : 0u;
+        c0b[b] = ((k0 >> (1 + b)) & 1u) ? ~0u : 0u;
+    }
     u64 best = 0;
     uint32_t fnu = 0, ftt = 0;
     for (uint32_t w = w0; w < w1; ++w) {
@@ -705,10 +707,17 @@ __global__ __launch_bounds__(kTt2Threads) void k_tt2_pick(const uint32_t *__rest
         if (!x.feas) continue;
         const uint32_t Q = tt_odd_rows(x.feas, n);
         const uint32_t cnt = (uint32_t)__popc(x.feas);
-        uint32_t sel = 0;
-        for (uint32_t m = w1s; m; m &= m - 1u) sel |= tt_class_rows(x, Q, first_slot(m)) & x.N;
-        for (uint32_t m = w0s; m; m &= m - 1u) sel |= tt_class_rows(x, Q, first_slot(m));
-        uint32_t cand = x.feas & sel;
+        // rows of the winning classes: count bits equal to c, parity, (W1) a NodeNumber match
+        uint32_t m1 = (Q ^ q1x) & x.N & v1, m0 = (Q ^ q0x) & v0;
+        m1 = TT_BITOP3(x.c0, c1b[0], m1, kXnorAnd3);
+        m0 = TT_BITOP3(x.c0, c0b[0], m0, kXnorAnd3);
+        m1 = TT_BITOP3(x.c1, c1b[1], m1, kXnorAnd3);
+        m0 = TT_BITOP3(x.c1, c0b[1], m0, kXnorAnd3);
+        m1 = TT_BITOP3(x.c2, c1b[2], m1, kXnorAnd3);
+        m0 = TT_BITOP3(x.c2, c0b[2], m0, kXnorAnd3);
+        m1 = TT_BITOP3(x.c3, c1b[3], m1, kXnorAnd3);
+        m0 = TT_BITOP3(x.c3, c0b[3], m0, kXnorAnd3);
+        uint32_t cand = x.feas & (m1 | m0);
         if (n < 3u) {  // global ranks 0..2 are explicit entries
             uint32_t m = x.feas;
             for (uint32_t k = n; k < 3u && m; ++k) {
