@@ -145,9 +145,14 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n
     uint32_t any = 0, top = 100;  // top = T(100): 0 once the table is all 0
     for (uint32_t base = r0; base < r1; base += kNamTile) {
         const uint32_t nt = min(kNamTile, r1 - base);
-        __syncthreads();
+        // a lane is done once its table is all 0 and it has seen a non-zero node:
+        // nothing later in the segment changes its record (the workgroup stops
+        // when all its lanes are, a wave skips the tile's rows)
+        const bool done = p >= n_pods || (top == 0u && any);
+        if (__syncthreads_and(done)) break;
         for (uint32_t i = tid; i < nt; i += kNamThreads) tile[i] = nam_row_word(t, base + i);
         __syncthreads();
+        if (__ballot(!done) == 0) continue;  // (wave-uniform)
         for (uint32_t i = 0; i < nt; ++i) {
             const uint32_t w = tile[i];  // (LDS broadcast)
             const bool f = nam_feasible(w, tol);
@@ -215,15 +220,19 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
                                                           uint32_t seed32, uint32_t w_nn, uint32_t w_na,
                                                           const NamSeg *__restrict__ local, uint32_t n_segs,
                                                           const NamSeg *__restrict__ after,
-                                                          const uint8_t *__restrict__ m_in, u64 *__restrict__ keys) {
+                                                          const uint8_t *__restrict__ m_in, u64 *__restrict__ keys,
+                                                          const uint32_t *__restrict__ perm) {
     __shared__ uint32_t tile[kNamTile];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
-    const uint32_t p = blockIdx.x * kNamThreads + tid;
+    const uint32_t pi = blockIdx.x * kNamThreads + tid;
+    const bool live = pi < n_pods;
+    // lanes take the pods in name-digit order (perm, k_nam_perm): a wave's pods then
+    // mostly share the rows that can score NodeNumber's 10
+    const uint32_t p = live ? (perm ? perm[pi] : pi) : pi;
     const uint32_t seg = blockIdx.y;
     uint32_t r0, r1;
     seg_bounds(n_rows, seg_rows, seg, r0, r1);
-    const bool live = p < n_pods;
     ms_pod_rec pod = {};
     if (live) pod = pods[p];
     const NamTerms m = load_terms(pod, sets, n_sets);
@@ -246,7 +255,12 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
         }
     }
     uint32_t top = mine[100];
-    u64 best = 0, cand_reg = 0, cand_anc = 0;
+    // A row's key is hashed only when its score can reach the best so far (a lower
+    // score cannot win; an equal one needs its hash). The latest non-zero row
+    // (the anchor candidate) keeps its two scores and ordinal; it is hashed when
+    // committed.
+    u64 best = 0;
+    uint32_t cand_sreg = 0, cand_sanc = 0, cand_ord = 0;
     bool cand = false;
     const uint32_t n_tiles = r1 > r0 ? (r1 - r0 + kNamTile - 1u) / kNamTile : 0u;
     for (uint32_t ti = n_tiles; ti-- > 0;) {  // tiles and rows in reverse LIST order
@@ -260,16 +274,17 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
             const uint32_t r = nam_raw(w, m);
             if (f) {
                 const uint32_t ord = t.base + base + i;
-                const uint32_t h = tb_hash(A, ord);
                 const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
+                const uint32_t bs = (uint32_t)(best >> 52);
                 if (r == 0u) {
-                    best = umax64(best, make_key(sn, h, ord));  // (T(0) = 0)
+                    if (sn >= bs) best = umax64(best, make_key(sn, tb_hash(A, ord), ord));  // (T(0) = 0)
                 } else {
                     // a later non-zero node is not the anchor: its regular key counts
-                    if (cand) best = umax64(best, cand_reg);
+                    if (cand && cand_sreg >= bs) best = umax64(best, make_key(cand_sreg, tb_hash(A, cand_ord), cand_ord));
                     cand = true;
-                    cand_reg = make_key(sn + w_na * mine[min(r, 100u)], h, ord);
-                    cand_anc = make_key(sn + w_na * top, h, ord);
+                    cand_sreg = sn + w_na * mine[min(r, 100u)];
+                    cand_sanc = sn + w_na * top;
+                    cand_ord = ord;
                 }
             }
             uint64_t b = __ballot(f && r > 100u && top != 0u);
@@ -284,8 +299,36 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
     }
     if (!live) return;
     // the segment's first non-zero node is the anchor unless an earlier segment or shard has one
-    if (cand) best = umax64(best, before ? cand_reg : cand_anc);
+    if (cand) {
+        const uint32_t sc = before ? cand_sreg : cand_sanc;
+        best = umax64(best, make_key(sc, tb_hash(A, cand_ord), cand_ord));
+    }
     if (best) atomicMax(keys + p, best);
+}
+
+// The pods of a chunk in name-digit order (digits 0..9, then the rest): perm[i]
+// = the pod index lane i of k_nam_keys takes. One workgroup, LDS counting sort.
+__global__ __launch_bounds__(1024) void k_nam_perm(const ms_pod_rec *__restrict__ pods, uint32_t n,
+                                                   uint32_t *__restrict__ perm) {
+    __shared__ uint32_t cnt[11], off[11];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 11u) cnt[tid] = 0u;
+    __syncthreads();
+    auto cls = [&](uint32_t i) {
+        const int d = pods[i].name_digit;
+        return d >= 0 && d <= 9 ? (uint32_t)d : 10u;
+    };
+    for (uint32_t i = tid; i < n; i += 1024u) atomicAdd(&cnt[cls(i)], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t a = 0;
+        for (int k = 0; k < 11; ++k) {
+            off[k] = a;
+            a += cnt[k];
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += 1024u) perm[atomicAdd(&off[cls(i)], 1u)] = i;
 }
 
 inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -320,13 +363,15 @@ hipError_t launch_nam_compose(const void *in, uint32_t stride, uint32_t n, uint3
 hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            const void *sets, uint32_t n_sets, uint32_t seed32, uint32_t w_nn, uint32_t w_na,
                            const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys,
-                           hipStream_t s) {
+                           uint32_t *perm, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
     uint32_t sr = 0;
     const uint32_t ns = nam_segments(n_rows, &sr);
+    if (perm) hipLaunchKernelGGL(k_nam_perm, dim3(1), dim3(1024), 0, s, pods, n_pods, perm);
     hipLaunchKernelGGL(k_nam_keys, dim3(cdiv(n_pods, kNamThreads), ns), dim3(kNamThreads), 0, s, t, n_rows, sr, pods,
                        n_pods, static_cast<const ms_nam_term_set *>(sets), n_sets, seed32, w_nn, w_na,
-                       static_cast<const NamSeg *>(local), ns, static_cast<const NamSeg *>(after), m_in, keys);
+                       static_cast<const NamSeg *>(local), ns, static_cast<const NamSeg *>(after), m_in, keys,
+                       static_cast<const uint32_t *>(perm));
     return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ void free_all(ms_ctx *c) {
     (void)hipSetDevice(c->cfg.device);
     comm_free(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *dev[] = {c->t.planes, c->t.zone, c->t.label2, c->d_terms, c->d_nam, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
+    void *dev[] = {c->t.planes, c->t.zone, c->t.label2, c->d_terms, c->d_nam, c->d_nam_perm, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
@@ -574,7 +574,11 @@ int ensure_nam(ms_ctx *c, uint32_t n) {
     if (c->d_nam) (void)hipFree(c->d_nam);
     c->d_nam = nullptr;
     c->nam_bytes = 0;
-    if (hipMalloc(&c->d_nam, need) != hipSuccess) return fail(c, MS_E_OOM, "NodeAffinity rescale tables");
+    if (c->d_nam_perm) (void)hipFree(c->d_nam_perm);
+    c->d_nam_perm = nullptr;
+    if (hipMalloc(&c->d_nam, need) != hipSuccess ||
+        hipMalloc((void **)&c->d_nam_perm, sizeof(uint32_t) * std::max(1u, n)) != hipSuccess)
+        return fail(c, MS_E_OOM, "NodeAffinity rescale tables");
     c->nam_bytes = need;
     return MS_OK;
 }
@@ -587,7 +591,7 @@ int nam_keys_locked(ms_ctx *c, uint32_t nb, const ms_pod_rec *d_pods, const void
     MS_HIP(c, launch_fill_keys(keys, nb, c->present_dev ? kKeyListed : 0ull, s));
     MS_HIP(c, launch_nam_seg(c->t, c->rows_dev, d_pods, nb, c->d_terms, c->n_terms, c->d_nam, s));
     MS_HIP(c, launch_nam_keys(c->t, c->rows_dev, d_pods, nb, c->d_terms, c->n_terms, seed32_of(c->cfg.seed), c->w_nn,
-                              c->w_na, c->d_nam, after, m_in, keys, s));
+                              c->w_na, c->d_nam, after, m_in, keys, c->d_nam_perm, s));
     return MS_OK;
 }
 

@@ -106,6 +106,7 @@ struct ms_ctx {
     void *d_terms = nullptr;
     uint32_t n_terms = 0, terms_cap = 0;
     void *d_nam = nullptr;
+    uint32_t *d_nam_perm = nullptr;  // pods in name-digit order per chunk (k_nam_perm)
     size_t nam_bytes = 0;
     // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
     ms_seq_cand *d_merged = nullptr;

@@ -165,7 +165,7 @@ hipError_t launch_nam_compose(const void *in, uint32_t stride, uint32_t n, uint3
 // launch_nam_seg's records; after / m_in as launch_nam_compose's outputs, or null.
 hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            const void *sets, uint32_t n_sets, uint32_t seed32, uint32_t w_nn, uint32_t w_na,
-                           const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys,
+                           const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys, uint32_t *perm,
                            hipStream_t s);
 
 // ---- launchers (ms_kernels.hip) -------------------------------------------
