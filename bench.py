@@ -435,6 +435,38 @@ def other_configs(args, dev, stream):
                              sample=f"oracle msor_schedule_tt closed form (1 thread), first {n_pre} pods "
                                     f"({cpu_tt:.2f} s)", pods_per_s=n_pre / cpu_tt, **_cpu_info(1)),
     }
+    del pods, res
+
+    # ---- NAM (not a BASELINE config): NodeAffinity with up to four preferred
+    # terms per pod (raw scores to 400) through the in-loop DefaultNormalizeScore, 50k x 100k
+    n_sets = 64
+    nr = synth.nodes(N, seed=args.seed, labels=True)
+    pr = synth.pods(P, seed=args.seed, term_sets=n_sets)
+    ts = synth.nam_term_sets(n_sets, seed=args.seed)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    with _lib.Engine(max_nodes=N, plugin_set=_lib.PLUGINS_NU_NN_NAM, seed=args.seed, device=dev.index) as e:
+        e.nam_term_sets(ts)
+        e.upsert(np.arange(N), nr)
+        e.flush()
+        med, ts_run = _median_time(lambda: e.select_batch_device(P, pods.data_ptr(), res.data_ptr()), sync=sync)
+        got = res.cpu().numpy().view(_lib.RESULT)
+    t0 = time.perf_counter()
+    o = _oracle.schedule_nam(nr, pr[:n_pre], ts, literal=False, seed=args.seed)
+    cpu_nam = time.perf_counter() - t0
+    out["NAM"] = {
+        "workload": "NAM (extension, not a BASELINE config): 50000 nodes x 100000 pods, NU filter, NN + NodeAffinity "
+                    f"with up to 4 preferred terms per pod ({n_sets} term sets, raw scores to 400) and the in-loop "
+                    "DefaultNormalizeScore, batched",
+        "ms": med * 1e3, "runs_ms": [t * 1e3 for t in ts_run], "evals_per_s": N * P / med, "pods_per_s": P / med,
+        "parity_vs_oracle_prefix": bool(np.array_equal(got["node"][:n_pre], o["node"])
+                                        and np.array_equal(got["code"][:n_pre], o["code"])
+                                        and np.array_equal(got["score"][:n_pre].astype(np.int64),
+                                                           o["score"].astype(np.int64))),
+        "cpu_baseline": dict(value=N * n_pre / cpu_nam, unit="pod×node evals/s", kind="port",
+                             sample=f"oracle msor_schedule_nam closed form (1 thread), first {n_pre} pods "
+                                    f"({cpu_nam:.2f} s)", pods_per_s=n_pre / cpu_nam, **_cpu_info(1)),
+    }
     return out
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 5
+#define MS_ABI_VERSION 6
 
 /* ---- return codes -------------------------------------------------------- */
 #define MS_OK 0
@@ -361,6 +361,26 @@ int ms_tt_summaries_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_
                            void *stream);
 int ms_tt_decode_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
                         const void *summaries_all_dev, ms_result *results_dev, void *stream);
+/* The same cycle in the two-pass bit-sliced form (ABI 6): per
+ * pod a 32-byte census of the shard's nodes (feasible count, filter flags, the
+ * first three and the last feasible node, which (raw count, rank parity)
+ * classes occur, with and without a NodeNumber match), then a key per pod from
+ * every shard's census and its own rows, combined by uint64 MAX like NU+NN:
+ *   1. ms_tt_census_device: this shard's census (census_dev: n_pods x
+ *      MS_TT_CENSUS_BYTES);
+ *   2. the caller gathers them shard-major (census_all[s][p], shards in
+ *      ordinal order = LIST order);
+ *   3. ms_tt_pick_device: this shard's keys (keys_dev, n_pods x u64) under the
+ *      plan every shard's census implies;
+ *   4. the element-wise uint64 MAX of the shards' keys;
+ *   5. ms_tt_final_device (any shard): each pod's result (no bind commit). */
+#define MS_TT_CENSUS_BYTES 32u
+int ms_tt_census_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, void *census_dev, void *stream);
+int ms_tt_pick_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                      uint32_t shard_index, const void *census_all_dev, unsigned long long *keys_dev, void *stream);
+int ms_tt_final_device(ms_ctx *ctx, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                       const void *census_all_dev, const unsigned long long *keys_max_dev, ms_result *results_dev,
+                       void *stream);
 
 /* ---- MS_PLUGINS_NU_NN_NAM: several preferred NodeAffinity terms ----------- */
 /* One PreferredSchedulingTerm: its NodeSelectorTerm tests one node label

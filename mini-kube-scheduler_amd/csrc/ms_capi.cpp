@@ -1522,6 +1522,87 @@ int ms_tt_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, 
     return MS_OK;
 }
 
+// The two-pass TaintToleration cycle over node shards (ms_taint.hip launch_tt2_*):
+// chunks of batch_cap pods; each call rebuilds the row planes on its stream.
+static int tt2_shard_prologue(ms_ctx *c, uint32_t n_pods, const char *who, hipStream_t &s) {
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_TT_NN)
+        return fail(c, MS_E_INVAL, std::string(who) + ": the TaintToleration plugin set only");
+    MS_HIP(c, hipSetDevice(c->cfg.device));
+    int rc = flush_locked(c);
+    if (rc) return rc;
+    rc = order_after_ctx_stream(c, s);
+    if (rc) return rc;
+    rc = ensure_tt(c, tt2_scratch_bytes(c->rows_dev, std::min(c->batch_cap, n_pods)));
+    if (rc) return rc;
+    if (!c->ev_tt) MS_HIP(c, hipEventCreateWithFlags(&c->ev_tt, hipEventDisableTiming));
+    if (c->tt_stream && c->tt_stream != s) MS_HIP(c, hipStreamWaitEvent(s, c->ev_tt, 0));
+    MS_HIP(c, launch_tt2_planes(c->t, c->rows_dev, c->d_tt, s));
+    return MS_OK;
+}
+
+static int tt2_shard_epilogue(ms_ctx *c, hipStream_t s) {
+    MS_HIP(c, hipEventRecord(c->ev_tt, s));
+    c->tt_stream = s;
+    return chain_back(c, s);
+}
+
+int ms_tt_census_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, void *census_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !census_dev))) return MS_E_INVAL;
+    if (n_pods == 0) return c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN ? MS_OK : MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    hipStream_t s = pick_stream(c, stream);
+    int rc = tt2_shard_prologue(c, n_pods, "ms_tt_census_device", s);
+    if (rc) return rc;
+    const uint32_t B = c->batch_cap, cap = std::min(B, n_pods), seed32 = seed32_of(c->cfg.seed);
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, launch_tt2_census_shard(c->t, c->rows_dev, pods_dev + s0, nb, seed32, c->d_tt, cap,
+                                          static_cast<char *>(census_dev) + (size_t)s0 * MS_TT_CENSUS_BYTES, s));
+    }
+    return tt2_shard_epilogue(c, s);
+}
+
+int ms_tt_pick_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards, uint32_t shard_index,
+                      const void *census_all_dev, unsigned long long *keys_dev, void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !census_all_dev || !keys_dev))) return MS_E_INVAL;
+    if (n_shards == 0 || shard_index >= n_shards)
+        return fail(c, MS_E_INVAL, "ms_tt_pick_device: shard_index must be below n_shards");
+    if (n_pods == 0) return c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN ? MS_OK : MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    hipStream_t s = pick_stream(c, stream);
+    int rc = tt2_shard_prologue(c, n_pods, "ms_tt_pick_device", s);
+    if (rc) return rc;
+    const uint32_t B = c->batch_cap, cap = std::min(B, n_pods), seed32 = seed32_of(c->cfg.seed);
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, launch_tt2_pick_shard(c->t, c->rows_dev, pods_dev + s0, nb, seed32, c->d_tt, cap,
+                                        static_cast<const char *>(census_all_dev) + (size_t)s0 * MS_TT_CENSUS_BYTES,
+                                        n_pods, n_shards, shard_index, keys_dev + s0, s));
+    }
+    return tt2_shard_epilogue(c, s);
+}
+
+int ms_tt_final_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, uint32_t n_shards,
+                       const void *census_all_dev, const unsigned long long *keys_max_dev, ms_result *results_dev,
+                       void *stream) {
+    if (!valid_ctx(c) || (n_pods && (!pods_dev || !census_all_dev || !keys_max_dev || !results_dev)))
+        return MS_E_INVAL;
+    if (n_shards == 0) return fail(c, MS_E_INVAL, "ms_tt_final_device: no shards");
+    if (n_pods == 0) return c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN ? MS_OK : MS_E_INVAL;
+    std::lock_guard<std::mutex> g(c->sched_mu);
+    hipStream_t s = pick_stream(c, stream);
+    int rc = tt2_shard_prologue(c, n_pods, "ms_tt_final_device", s);
+    if (rc) return rc;
+    const uint32_t B = c->batch_cap, cap = std::min(B, n_pods), seed32 = seed32_of(c->cfg.seed);
+    for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
+        const uint32_t nb = std::min(B, n_pods - s0);
+        MS_HIP(c, launch_tt2_final_shard(c->t, c->rows_dev, pods_dev + s0, nb, seed32, c->d_tt, cap,
+                                         static_cast<const char *>(census_all_dev) + (size_t)s0 * MS_TT_CENSUS_BYTES,
+                                         n_pods, n_shards, keys_max_dev + s0, results_dev + s0, s));
+    }
+    return tt2_shard_epilogue(c, s);
+}
+
 int ms_nam_term_sets(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set *sets) {
     if (!valid_ctx(c) || (n_sets && !sets) || n_sets > 0xFFFFu) return MS_E_INVAL;
     if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)

@@ -347,6 +347,22 @@ hipError_t launch_tt2_planes(const NodeTable &t, uint32_t n_rows, void *scratch,
 hipError_t launch_tt2_cycle(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                             uint32_t seed32, void *scratch, uint32_t max_pods, ms_result *results, int commit,
                             hipStream_t s);
+// Node shards of the two-pass cycle: a shard's census (one MS_TT_CENSUS_BYTES
+// record per pod, its segments merged, ordinals global); its pick under the plan
+// of every shard's census (census_all[s * stride + p], shards in LIST order) ->
+// one key per pod for the cross-shard uint64 MAX; the results from the census of
+// every shard and the MAX of the keys.
+hipError_t launch_tt2_census_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                   uint32_t seed32, void *scratch, uint32_t max_pods, void *census_out,
+                                   hipStream_t s);
+hipError_t launch_tt2_pick_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                 uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                 uint32_t stride, uint32_t n_shards, uint32_t shard, unsigned long long *keys_out,
+                                 hipStream_t s);
+hipError_t launch_tt2_final_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                  uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                  uint32_t stride, uint32_t n_shards, const unsigned long long *keys_max,
+                                  ms_result *results, hipStream_t s);
 hipError_t launch_tt_combine(const void *in, uint32_t stride, uint32_t n_segs, const ms_pod_rec *pods, uint32_t n_pods,
                              uint32_t seed32, void *out, ms_result *results, const NodeTable &t, int commit,
                              hipStream_t s);

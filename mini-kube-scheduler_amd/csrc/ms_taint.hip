@@ -300,8 +300,9 @@ constexpr uint32_t kEntNone = 0xFFFFFFFFu;
 struct TtCensus {  // 32 B per (segment, pod)
     uint32_t n, flags;
     uint32_t occ, occ1;  // bit 2c + q: a middle row of class (c, q) / one matching NodeNumber
-    uint32_t first[3], last;  // entries: row | nn << 21 | c << 24 (kEntNone: none)
+    uint32_t first[3], last;  // entries: ordinal | nn << 21 | c << 24 (kEntNone: none)
 };
+static_assert(sizeof(TtCensus) == MS_TT_CENSUS_BYTES, "TtCensus layout (ms_tt_census_device)");
 struct TtPlan {  // 32 B per pod
     uint32_t mode;  // 0: the plan kernel wrote the result, 1: pick
     uint32_t score; // S*
@@ -433,7 +434,7 @@ __device__ __forceinline__ uint32_t swap_parity(uint32_t occ) {  // 18 class bit
 // grid (pod blocks, segments of seg_words words): lane = pod.
 __global__ __launch_bounds__(kTt2Threads) void k_tt2_census(const uint32_t *__restrict__ planes, uint32_t n_words,
                                                             uint32_t seg_words, const ms_pod_rec *__restrict__ pods,
-                                                            uint32_t n_pods, uint32_t seed32,
+                                                            uint32_t n_pods, uint32_t seed32, uint32_t node_base,
                                                             TtCensus *__restrict__ out) {
     const uint32_t p = blockIdx.x * kTt2Threads + threadIdx.x;
     const uint32_t w0 = blockIdx.y * seg_words, w1 = min(n_words, w0 + seg_words);
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(kTt2Threads) void k_tt2_census(const uint32_t *__re
             uint32_t m = x.feas, k = n;
             while (k < 3u && m) {
                 const uint32_t b = first_slot(m);
-                const uint32_t e = ent_pack(w * 32u + b, tt_c_at(x, b), (x.N >> b) & 1u);
+                const uint32_t e = ent_pack(node_base + w * 32u + b, tt_c_at(x, b), (x.N >> b) & 1u);
                 f0 = k == 0u ? e : f0;
                 f1 = k == 1u ? e : f1;
                 f2 = k == 2u ? e : f2;
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(kTt2Threads) void k_tt2_census(const uint32_t *__re
         occ |= pend;
         occ1 |= pend1;
         const uint32_t ct = tt_c_at(x, t), nt = (x.N >> t) & 1u;
-        last = ent_pack(w * 32u + t, ct, nt);
+        last = ent_pack(node_base + w * 32u + t, ct, nt);
         pend = n + cnt - 1u >= 3u ? 1u << (2u * ct + ((Q >> t) & 1u)) : 0u;
         pend1 = nt ? pend : 0u;
         n += cnt;
@@ -543,6 +544,7 @@ __device__ __forceinline__ void tt2_merge(TtCensus &r, const TtCensus &b) {
 
 __device__ __forceinline__ void tt2_store(ms_result *results, uint32_t p, const ms_result &res, const NodeTable &t,
                                           const ms_pod_rec &pod, int commit) {
+    if (!results) return;
     results[p] = res;
     if (commit && res.code == MS_CODE_SUCCESS) {
         const uint32_t node = (uint32_t)res.node;
@@ -552,13 +554,16 @@ __device__ __forceinline__ void tt2_store(ms_result *results, uint32_t p, const 
 
 // Per pod: the segments merged, then the closed form (tt_finalize's, classes by
 // occupancy): the result when no class can win, else the pick plan.
-__global__ void k_tt2_plan(const TtCensus *__restrict__ census, uint32_t n_segs, const ms_pod_rec *__restrict__ pods,
-                           uint32_t n_pods, uint32_t seed32, TtPlan *__restrict__ plans,
-                           ms_result *__restrict__ results, NodeTable t, int commit) {
+// census: n_segs records per pod in LIST order (segments of one context, or the
+// node shards' records), record s of pod p at census[s * stride + p]; results
+// null: the plan only (a shard's pick).
+__global__ void k_tt2_plan(const TtCensus *__restrict__ census, uint32_t n_segs, uint32_t stride,
+                           const ms_pod_rec *__restrict__ pods, uint32_t n_pods, uint32_t seed32,
+                           TtPlan *__restrict__ plans, ms_result *__restrict__ results, NodeTable t, int commit) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pods) return;
     TtCensus r = census[p];
-    for (uint32_t s = 1; s < n_segs; ++s) tt2_merge(r, census[(size_t)s * n_pods + p]);
+    for (uint32_t s = 1; s < n_segs; ++s) tt2_merge(r, census[(size_t)s * stride + p]);
     const ms_pod_rec pod = pods[p];
     TtPlan plan = {};
     ms_result out;
@@ -584,7 +589,7 @@ __global__ void k_tt2_plan(const TtCensus *__restrict__ census, uint32_t n_segs,
     }
     const uint32_t A = tb_pod(seed32, pod.ordinal);
     auto key_of = [&](uint32_t e, uint32_t score) {
-        const uint32_t ord = t.base + ent_row(e);
+        const uint32_t ord = ent_row(e);  // (a global ordinal)
         return make_key(score, tb_hash(A, ord), ord);
     };
     u64 best = 0;
@@ -665,7 +670,8 @@ __global__ void k_tt2_plan(const TtCensus *__restrict__ census, uint32_t n_segs,
 __global__ __launch_bounds__(kTt2Threads) void k_tt2_pick(const uint32_t *__restrict__ planes, uint32_t n_words,
                                                           uint32_t seg_words, const ms_pod_rec *__restrict__ pods,
                                                           uint32_t n_pods, uint32_t seed32,
-                                                          const TtCensus *__restrict__ census,
+                                                          const uint32_t *__restrict__ cnt, uint32_t cnt_words,
+                                                          const uint32_t *__restrict__ base_in,
                                                           const TtPlan *__restrict__ plans, uint32_t node_base,
                                                           u64 *__restrict__ keys) {
     const uint32_t p = blockIdx.x * kTt2Threads + threadIdx.x;
@@ -681,9 +687,12 @@ __global__ __launch_bounds__(kTt2Threads) void k_tt2_pick(const uint32_t *__rest
     ms_pod_rec pod = {};
     if (active) pod = pods[p];
     const TtLane q = tt_lane(pod, seed32);
-    uint32_t n = 0;  // feasible rows before this segment (global ranks)
+    // feasible rows before this segment (global ranks): the earlier node shards'
+    // (base_in) and this context's earlier segments' (cnt: word 0 of records of
+    // cnt_words words, [segment][pod])
+    uint32_t n = (active && base_in) ? base_in[p] : 0u;
     if (active)
-        for (uint32_t s = 0; s < seg; ++s) n += census[(size_t)s * n_pods + p].n;
+        for (uint32_t s = 0; s < seg; ++s) n += cnt[((size_t)s * n_pods + p) * cnt_words];
     const uint32_t F = plan.F;
     // the (at most one) winning class with a matching row and the (at most one)
     // without (k_tt2_plan: the 18 class scores are distinct), as per-lane masks:
@@ -755,6 +764,68 @@ __global__ void k_tt2_final(const TtPlan *__restrict__ plans, const u64 *__restr
     tt2_store(results, p, out, t, pods[p], commit);
 }
 
+// grid (pod blocks, segments): the feasible-row count per (segment, pod) alone
+// (a shard's pick needs its segments' rank offsets, not their census).
+__global__ __launch_bounds__(kTt2Threads) void k_tt2_count(const uint32_t *__restrict__ planes, uint32_t n_words,
+                                                           uint32_t seg_words, const ms_pod_rec *__restrict__ pods,
+                                                           uint32_t n_pods, uint32_t *__restrict__ out) {
+    const uint32_t p = blockIdx.x * kTt2Threads + threadIdx.x;
+    const uint32_t w0 = blockIdx.y * seg_words, w1 = min(n_words, w0 + seg_words);
+    ms_pod_rec pod = {};
+    if (p < n_pods) pod = pods[p];
+    const TtLane q = tt_lane(pod, 0u);
+    uint32_t n = 0;
+    for (uint32_t w = w0; w < w1; ++w) {
+        const uint32_t *pl = planes + (size_t)w * kTt2Planes;
+        const uint32_t nz = (uint32_t)__builtin_amdgcn_readfirstlane((int)pl[kPlNz]);
+        const uint32_t pres = pl[kPlPres];
+        if (!__builtin_amdgcn_readfirstlane((int)pres)) continue;
+        uint32_t hard = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (nz & (1u << (kPlHard + i))) hard = TT_BITOP3(pl[kPlHard + i], q.hm[i], hard, kAndOr);
+        n += (uint32_t)__popc(pres & ~((pl[kPlUns] & q.tolu_n) | hard));
+    }
+    if (p < n_pods) out[(size_t)blockIdx.y * n_pods + p] = n;
+}
+
+// Per pod: the feasible nodes of the shards before `shard` (census_all records,
+// [shard][pod] with stride) -- this shard's global rank offset.
+__global__ void k_tt2_shard_base(const TtCensus *__restrict__ census_all, uint32_t stride, uint32_t shard,
+                                 uint32_t n_pods, uint32_t *__restrict__ base) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pods) return;
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < shard; ++s) n += census_all[(size_t)s * stride + p].n;
+    base[p] = n;
+}
+
+// Per pod: this shard's key for the cross-shard uint64 MAX: the best of its
+// segments' picks and the plan's explicit entry (the same on every shard), 0
+// when the plan decided the pod outright (the final pass redoes that).
+__global__ void k_tt2_keymax(const TtPlan *__restrict__ plans, const u64 *__restrict__ seg_keys, uint32_t n_segs,
+                             uint32_t n_pods, u64 *__restrict__ keys) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pods) return;
+    const TtPlan plan = plans[p];
+    u64 best = 0;
+    if (plan.mode == 1u) {
+        best = plan.best;
+        for (uint32_t s = 0; s < n_segs; ++s) best = umax64(best, seg_keys[(size_t)s * n_pods + p]);
+    }
+    keys[p] = best;
+}
+
+// Per pod: the merge of a context's segment records into one (a node shard's census).
+__global__ void k_tt2_merge_segs(const TtCensus *__restrict__ census, uint32_t n_segs, uint32_t n_pods,
+                                 TtCensus *__restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pods) return;
+    TtCensus r = census[p];
+    for (uint32_t s = 1; s < n_segs; ++s) tt2_merge(r, census[(size_t)s * n_pods + p]);
+    out[p] = r;
+}
+
 // One thread per row: 64 rows of a wave -> 2 words of planes by ballot.
 __global__ __launch_bounds__(256) void k_tt2_planes(NodeTable t, uint32_t n_rows, uint32_t n_words,
                                                     uint32_t *__restrict__ planes) {
@@ -817,11 +888,39 @@ uint32_t tt2_words(uint32_t n_rows) { return cdiv(std::max(n_rows, 1u), 32u); }
 
 // Two-pass scratch (d_tt): the row planes, then per chunk of up to max_pods pods
 // the census [segs][pods], the plans [pods] and the picks [segs][pods].
-size_t tt2_scratch_bytes(uint32_t n_rows, uint32_t max_pods) {
-    const size_t segs = tt_segments(n_rows);
-    return (size_t)tt2_words(n_rows) * kTt2Planes * 4 + segs * max_pods * sizeof(TtCensus) +
-           (size_t)max_pods * sizeof(TtPlan) + segs * max_pods * sizeof(u64);
+// The two-pass scratch (d_tt): the row planes, then per chunk of up to max_pods
+// pods the census [segs][pods], the plans [pods], the picks [segs][pods], and
+// for node shards the segments' counts [segs][pods] and the shard offsets [pods].
+struct Tt2Scratch {
+    uint32_t *planes;
+    TtCensus *census;
+    TtPlan *plans;
+    u64 *keys;
+    uint32_t *counts, *base;
+    size_t bytes;
+};
+Tt2Scratch tt2_layout(void *scratch, uint32_t n_rows, uint32_t max_pods) {
+    const size_t segs = tt_segments(n_rows), m = max_pods;
+    char *b = static_cast<char *>(scratch);
+    Tt2Scratch x;
+    size_t o = 0;
+    x.planes = reinterpret_cast<uint32_t *>(b + o);
+    o += (size_t)tt2_words(n_rows) * kTt2Planes * 4;
+    x.census = reinterpret_cast<TtCensus *>(b + o);
+    o += segs * m * sizeof(TtCensus);
+    x.plans = reinterpret_cast<TtPlan *>(b + o);
+    o += m * sizeof(TtPlan);
+    x.keys = reinterpret_cast<u64 *>(b + o);
+    o += segs * m * sizeof(u64);
+    x.counts = reinterpret_cast<uint32_t *>(b + o);
+    o += segs * m * 4;
+    x.base = reinterpret_cast<uint32_t *>(b + o);
+    o += m * 4;
+    x.bytes = o;
+    return x;
 }
+
+size_t tt2_scratch_bytes(uint32_t n_rows, uint32_t max_pods) { return tt2_layout(nullptr, n_rows, max_pods).bytes; }
 
 hipError_t launch_tt2_planes(const NodeTable &t, uint32_t n_rows, void *scratch, hipStream_t s) {
     const uint32_t nw = tt2_words(n_rows);
@@ -837,22 +936,71 @@ hipError_t launch_tt2_cycle(const NodeTable &t, uint32_t n_rows, const ms_pod_re
     if (n_pods > max_pods || !results) return hipErrorInvalidValue;
     uint32_t sr = 0;
     const uint32_t segs = tt_segments(n_rows, &sr), nw = tt2_words(n_rows), sw = sr / 32u;
-    char *b = static_cast<char *>(scratch);
-    const uint32_t *planes = reinterpret_cast<const uint32_t *>(b);
-    b += (size_t)nw * kTt2Planes * 4;
-    TtCensus *census = reinterpret_cast<TtCensus *>(b);
-    b += (size_t)segs * max_pods * sizeof(TtCensus);
-    TtPlan *plans = reinterpret_cast<TtPlan *>(b);
-    b += (size_t)max_pods * sizeof(TtPlan);
-    u64 *keys = reinterpret_cast<u64 *>(b);
+    const Tt2Scratch x = tt2_layout(scratch, n_rows, max_pods);
     const dim3 grid(cdiv(n_pods, kTt2Threads), segs);
-    hipLaunchKernelGGL(k_tt2_census, grid, dim3(kTt2Threads), 0, s, planes, nw, sw, pods, n_pods, seed32, census);
-    hipLaunchKernelGGL(k_tt2_plan, dim3(cdiv(n_pods, 128u)), dim3(128), 0, s, census, segs, pods, n_pods, seed32,
-                       plans, results, t, commit);
-    hipLaunchKernelGGL(k_tt2_pick, grid, dim3(kTt2Threads), 0, s, planes, nw, sw, pods, n_pods, seed32, census, plans,
-                       t.base, keys);
-    hipLaunchKernelGGL(k_tt2_final, dim3(cdiv(n_pods, 128u)), dim3(128), 0, s, plans, keys, segs, pods, n_pods,
+    hipLaunchKernelGGL(k_tt2_census, grid, dim3(kTt2Threads), 0, s, x.planes, nw, sw, pods, n_pods, seed32, t.base,
+                       x.census);
+    hipLaunchKernelGGL(k_tt2_plan, dim3(cdiv(n_pods, 128u)), dim3(128), 0, s, x.census, segs, n_pods, pods, n_pods,
+                       seed32, x.plans, results, t, commit);
+    hipLaunchKernelGGL(k_tt2_pick, grid, dim3(kTt2Threads), 0, s, x.planes, nw, sw, pods, n_pods, seed32,
+                       reinterpret_cast<const uint32_t *>(x.census), (uint32_t)(sizeof(TtCensus) / 4),
+                       (const uint32_t *)nullptr, x.plans, t.base, x.keys);
+    hipLaunchKernelGGL(k_tt2_final, dim3(cdiv(n_pods, 128u)), dim3(128), 0, s, x.plans, x.keys, segs, pods, n_pods,
                        results, t, commit);
+    return hipGetLastError();
+}
+
+// Node shards (ms_tt_census_device / ms_tt_pick_device / ms_tt_final_device): the
+// row planes must be current (launch_tt2_planes earlier on s).
+hipError_t launch_tt2_census_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                   uint32_t seed32, void *scratch, uint32_t max_pods, void *census_out,
+                                   hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    if (n_pods > max_pods) return hipErrorInvalidValue;
+    uint32_t sr = 0;
+    const uint32_t segs = tt_segments(n_rows, &sr), nw = tt2_words(n_rows), sw = sr / 32u;
+    const Tt2Scratch x = tt2_layout(scratch, n_rows, max_pods);
+    hipLaunchKernelGGL(k_tt2_census, dim3(cdiv(n_pods, kTt2Threads), segs), dim3(kTt2Threads), 0, s, x.planes, nw, sw,
+                       pods, n_pods, seed32, t.base, x.census);
+    hipLaunchKernelGGL(k_tt2_merge_segs, dim3(cdiv(n_pods, 128u)), dim3(128), 0, s, x.census, segs, n_pods,
+                       static_cast<TtCensus *>(census_out));
+    return hipGetLastError();
+}
+
+hipError_t launch_tt2_pick_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                 uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                 uint32_t stride, uint32_t n_shards, uint32_t shard, unsigned long long *keys_out,
+                                 hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    if (n_pods > max_pods || shard >= n_shards) return hipErrorInvalidValue;
+    uint32_t sr = 0;
+    const uint32_t segs = tt_segments(n_rows, &sr), nw = tt2_words(n_rows), sw = sr / 32u;
+    const Tt2Scratch x = tt2_layout(scratch, n_rows, max_pods);
+    const TtCensus *ca = static_cast<const TtCensus *>(census_all);
+    const dim3 grid(cdiv(n_pods, kTt2Threads), segs), g1(cdiv(n_pods, 128u));
+    hipLaunchKernelGGL(k_tt2_plan, g1, dim3(128), 0, s, ca, n_shards, stride, pods, n_pods, seed32, x.plans,
+                       (ms_result *)nullptr, t, 0);
+    hipLaunchKernelGGL(k_tt2_count, grid, dim3(kTt2Threads), 0, s, x.planes, nw, sw, pods, n_pods, x.counts);
+    hipLaunchKernelGGL(k_tt2_shard_base, g1, dim3(128), 0, s, ca, stride, shard, n_pods, x.base);
+    hipLaunchKernelGGL(k_tt2_pick, grid, dim3(kTt2Threads), 0, s, x.planes, nw, sw, pods, n_pods, seed32,
+                       (const uint32_t *)x.counts, 1u, (const uint32_t *)x.base, x.plans, t.base, x.keys);
+    hipLaunchKernelGGL(k_tt2_keymax, g1, dim3(128), 0, s, x.plans, x.keys, segs, n_pods,
+                       reinterpret_cast<u64 *>(keys_out));
+    return hipGetLastError();
+}
+
+hipError_t launch_tt2_final_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                  uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                  uint32_t stride, uint32_t n_shards, const unsigned long long *keys_max,
+                                  ms_result *results, hipStream_t s) {
+    if (n_pods == 0) return hipSuccess;
+    if (n_pods > max_pods || !results) return hipErrorInvalidValue;
+    const Tt2Scratch x = tt2_layout(scratch, n_rows, max_pods);
+    const dim3 g1(cdiv(n_pods, 128u));
+    hipLaunchKernelGGL(k_tt2_plan, g1, dim3(128), 0, s, static_cast<const TtCensus *>(census_all), n_shards, stride,
+                       pods, n_pods, seed32, x.plans, results, t, 0);
+    hipLaunchKernelGGL(k_tt2_final, g1, dim3(128), 0, s, x.plans, reinterpret_cast<const u64 *>(keys_max), 1u, pods,
+                       n_pods, results, t, 0);
     return hipGetLastError();
 }
 

@@ -103,6 +103,7 @@ SEQ_CAND = np.dtype(
 )
 SEQ_TOPK = 4
 TT_SUMMARY_BYTES = 192  # MS_TT_SUMMARY_BYTES
+TT_CENSUS_BYTES = 32  # MS_TT_CENSUS_BYTES
 NAM_SEG_BYTES = 104  # MS_NAM_SEG_BYTES
 NAM_TERMS = 4  # MS_NAM_TERMS
 
@@ -207,6 +208,9 @@ SIGNATURES = {
     "ms_seq_validate_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "ms_tt_summaries_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_tt_decode_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp]),
+    "ms_tt_census_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
+    "ms_tt_pick_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _u32, _vp, _vp, _vp]),
+    "ms_tt_final_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp]),
     "ms_nam_term_sets": (ctypes.c_int, [_vp, _u32, _vp]),
     "ms_nam_segment_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_nam_keys_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _u32, _vp, _vp, _vp]),
@@ -456,6 +460,23 @@ class Engine:
         self._check("ms_tt_decode_device",
                     self.lib.ms_tt_decode_device(self.h, n_pods, pods_dev, n_shards, summaries_all_dev, results_dev,
                                                  stream or None))
+
+    def tt_census_device(self, n_pods, pods_dev, census_dev, stream=0):
+        """Node-sharded TaintToleration, two-pass form, step 1: this shard's census."""
+        self._check("ms_tt_census_device", self.lib.ms_tt_census_device(self.h, n_pods, pods_dev, census_dev,
+                                                                        stream or None))
+
+    def tt_pick_device(self, n_pods, pods_dev, n_shards, shard_index, census_all_dev, keys_dev, stream=0):
+        """Step 3: this shard's keys under the plan of every shard's census (shard-major)."""
+        self._check("ms_tt_pick_device",
+                    self.lib.ms_tt_pick_device(self.h, n_pods, pods_dev, n_shards, shard_index, census_all_dev,
+                                               keys_dev, stream or None))
+
+    def tt_final_device(self, n_pods, pods_dev, n_shards, census_all_dev, keys_max_dev, results_dev, stream=0):
+        """Step 5: results from every shard's census and the uint64 MAX of the shards' keys."""
+        self._check("ms_tt_final_device",
+                    self.lib.ms_tt_final_device(self.h, n_pods, pods_dev, n_shards, census_all_dev, keys_max_dev,
+                                                results_dev, stream or None))
 
     def nam_term_sets(self, sets):
         """MS_PLUGINS_NU_NN_NAM: registers the term sets (uint8 array (n, 4, 4) of

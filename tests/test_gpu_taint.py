@@ -201,3 +201,48 @@ def test_tt_dense_taints_segments(oracle, n_nodes, n_pods, seed):
     with _engine(nr, seed, dead=dead) as e:
         _same(_device_cycle(e, pr), o, "device")
     assert (o["code"] == 0).sum() > 0.5 * n_pods
+
+
+@pytest.mark.parametrize("cuts,dense", [((0, 5000, 10_000), False), ((0, 37, 38, 4000, 9000), False),
+                                        ((0, 3, 6000), False), ((0, 1100, 2600, 7000), True)])
+def test_tt_node_shards_two_pass(oracle, cuts, dense):
+    # the two-pass form over node shards: censuses gathered shard-major, each shard's
+    # keys under the plan of all of them, uint64 MAX, the results on any shard; incl. a
+    # one-node shard, an all-deleted shard, shards under 4 feasible nodes, and dense
+    # 8 + 8-id taints (the literal loop checks the small one)
+    import torch
+
+    seed = 70 + len(cuts) + (5 if dense else 0)
+    n = cuts[-1]
+    if dense:
+        nr, pr = _dense_cluster(n, 1500, seed, hard_p=0.05, soft_p=0.45)
+        dead = np.arange(0, n, 17)
+    else:
+        nr, pr, _ = _cluster(n, 2000, seed)
+        dead = np.arange(cuts[1], cuts[2]) if len(cuts) > 3 else np.arange(0, n, 13)
+    o = _oracle(oracle, nr, pr, seed, dead)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    G, P, CB = len(cuts) - 1, len(pr), _lib.TT_CENSUS_BYTES
+    census = torch.zeros(G * P * CB, dtype=torch.uint8, device=dev)
+    keys = torch.zeros((G, P), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()  # (the fills ran on torch's stream, not s)
+    engines = [_engine(nr, seed, lo, hi, dead) for lo, hi in zip(cuts[:-1], cuts[1:])]
+    try:
+        for g, e in enumerate(engines):
+            e.tt_census_device(P, pods.data_ptr(), census.data_ptr() + g * P * CB, s.cuda_stream)
+        for g, e in enumerate(engines):
+            e.tt_pick_device(P, pods.data_ptr(), G, g, census.data_ptr(), keys[g].data_ptr(), s.cuda_stream)
+        s.synchronize()
+        best = keys.max(dim=0).values.contiguous()  # keys < 2^63: the signed max is the unsigned one
+        torch.cuda.synchronize()
+        for g, e in enumerate(engines):  # any shard decodes
+            out = torch.full((P * 24,), 0xCD, dtype=torch.uint8, device=dev)
+            torch.cuda.synchronize()
+            e.tt_final_device(P, pods.data_ptr(), G, census.data_ptr(), best.data_ptr(), out.data_ptr(), s.cuda_stream)
+            s.synchronize()
+            _same(out.cpu().numpy().view(_lib.RESULT), o, f"two-pass shards {cuts} decoded on {g}")
+    finally:
+        for e in engines:
+            e.close()
