@@ -510,6 +510,14 @@ int ensure_stage(ms_ctx *c, uint32_t n) {
     return MS_OK;
 }
 
+bool tt_two_pass() {
+    static const bool v2 = [] {
+        const char *e = getenv("MINISCHED_TT");
+        return !(e && std::string(e) == "v1");
+    }();
+    return v2;
+}
+
 // MS_PLUGINS_NU_TT_NN scratch: `need` bytes (summaries or the two-pass cycle's).
 int ensure_tt(ms_ctx *c, size_t need) {
     if (need <= c->tt_bytes) return MS_OK;
@@ -529,11 +537,7 @@ int ensure_tt(ms_ctx *c, size_t need) {
 // the shard summaries (out) always use.
 int tt_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *out, ms_result *results, int commit,
                     hipStream_t s) {
-    static const bool v1 = [] {
-        const char *e = getenv("MINISCHED_TT");
-        return e && std::string(e) == "v1";
-    }();
-    const bool two_pass = !out && !v1;
+    const bool two_pass = !out && tt_two_pass();
     const uint32_t B = c->batch_cap, segs = tt_segments(c->rows_dev), cap = std::min(B, n_pods);
     int rc = ensure_tt(c, two_pass ? tt2_scratch_bytes(c->rows_dev, cap)
                                    : (size_t)segs * cap * MS_TT_SUMMARY_BYTES);

@@ -81,6 +81,10 @@ struct ShardSlot {
     // MS_PLUGINS_NU_TT_NN: this shard's per-pod summaries (G x cap, pod order) and
     // the slice's summaries from every shard (G x cap, shard order) after the all-to-all
     void *summ = nullptr, *summ_mine = nullptr;
+    // the two-pass form (tt_two_pass()): this shard's census (G x cap records, pod
+    // order), every shard's after the all-gather (G x G x cap, shard-major,
+    // stride = the batch), and the slice's plans for the final pass
+    void *cen_mine = nullptr, *cen_all = nullptr, *plans = nullptr;
     uint32_t cap = 0;       // pods per slice the buffers hold
     bool used = false;      // a batch went through this slot
     uint64_t dec_gen = 0;   // the drain that decoded its last batch
@@ -100,6 +104,7 @@ struct CommState {
     hipStream_t cs = nullptr;  // collective stream
     hipStream_t ss[2] = {nullptr, nullptr};  // sweep streams, alternating batch by batch
     hipEvent_t ev_swept[kPipeMax] = {}, ev_comb[kPipeMax] = {};
+    hipEvent_t ev_ag[kPipeMax] = {};  // TaintToleration two-pass: the slot's census all-gather
     hipEvent_t ev_in = nullptr, ev_ctx = nullptr;  // caller stream -> sweep stream, context stream -> sweep stream
     hipEvent_t ev_drained = nullptr;               // after the newest drain's decodes (decode stream)
     uint64_t drains = 0, cs_drain_seen = 0;        // drains enqueued / the newest the collective stream waited for
@@ -148,7 +153,7 @@ namespace {
     } while (0)
 
 void free_slot(ShardSlot &sl) {
-    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.summ, sl.summ_mine};
+    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.summ, sl.summ_mine, sl.cen_mine, sl.cen_all, sl.plans};
     for (void *q : p)
         if (q) (void)hipFree(q);
     sl = ShardSlot{};
@@ -165,9 +170,13 @@ int slot_ensure(ms_ctx *c, ShardSlot &sl, uint32_t per) {
         hipMalloc((void **)&sl.keys_mine, cap * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&sl.flags, G * cap * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess ||
-        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN &&
+        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN && !tt_two_pass() &&
          (hipMalloc(&sl.summ, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess ||
-          hipMalloc(&sl.summ_mine, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess))) {
+          hipMalloc(&sl.summ_mine, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess)) ||
+        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN && tt_two_pass() &&
+         (hipMalloc(&sl.cen_mine, G * cap * MS_TT_CENSUS_BYTES) != hipSuccess ||
+          hipMalloc(&sl.cen_all, G * G * cap * MS_TT_CENSUS_BYTES) != hipSuccess ||
+          hipMalloc(&sl.plans, cap * MS_TT_CENSUS_BYTES) != hipSuccess))) {
         free_slot(sl);
         return fail(c, MS_E_OOM, "sharded combine buffers");
     }
@@ -190,7 +199,16 @@ int drain_locked(ms_ctx *c, size_t k) {
     k = std::min(k, m.pending.size());
     if (k == 0) return MS_OK;
     MS_HIP(c, hipStreamWaitEvent(s, m.ev_comb[m.pending[k - 1].slot], 0));  // collectives run in issue order
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // the slice's G summaries merged in shard (LIST) order
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN && tt_two_pass()) {  // the slice's plans + the MAX of the picks
+        for (size_t i = 0; i < k; ++i) {
+            const Pending &p = m.pending[i];
+            const ShardSlot &sl = m.slot[p.slot];
+            MS_HIP(c, launch_tt2_final_shard(c->t, c->rows_dev, p.pods + p.first, p.count, seed32_of(c->cfg.seed),
+                                             sl.plans, p.count, static_cast<const char *>(sl.cen_all) +
+                                                                    (size_t)p.first * MS_TT_CENSUS_BYTES,
+                                             p.n, (uint32_t)m.world, sl.keys_mine, p.results, s));
+        }
+    } else if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // the slice's G summaries merged in shard (LIST) order
         for (size_t i = 0; i < k; ++i) {
             const Pending &p = m.pending[i];
             const ShardSlot &sl = m.slot[p.slot];
@@ -316,7 +334,7 @@ int collective_locked(ms_ctx *c, uint32_t si, hipEvent_t ev, uint32_t n, const m
     sl.used = true;
     host_tick(m, 2, tp);  // events to the collective stream
     ncclResult_t r = ncclSuccess;
-    if (ps == MS_PLUGINS_NU_NN) {  // the keys alone: one call, no group
+    if (ps == MS_PLUGINS_NU_NN || (ps == MS_PLUGINS_NU_TT_NN && tt_two_pass())) {  // the keys alone: one call
         r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
     } else if (ps == MS_PLUGINS_NU_TT_NN) {
         // summaries do not combine by MAX: every rank sends each rank its pod slice's
@@ -355,6 +373,39 @@ int flush_stash(ms_ctx *c) {
     if (rc) return rc;
     m.reads_outstanding = true;
     return collective_locked(c, st.si, m.ev_swept[st.si], st.n, st.pods, st.results, tp);
+}
+
+// MS_PLUGINS_NU_TT_NN, two-pass: the census of this shard on X, the all-gather of
+// every shard's on the collective stream, then the picks on X again (the table's
+// readers stay on the sweep stream, behind the delta fence ev_swept). The shared
+// two-pass scratch (d_tt) passes from sweep stream to sweep stream by ev_tt.
+int tt2_sharded_sweep(ms_ctx *c, uint32_t si, uint32_t n, const ms_pod_rec *pods, hipStream_t X) {
+    CommState &m = *c->comm;
+    ShardSlot &sl = m.slot[si];
+    const uint32_t seed32 = seed32_of(c->cfg.seed);
+    int rc = ensure_tt(c, tt2_scratch_bytes(c->rows_dev, std::max(1u, n)));
+    if (rc) return rc;
+    if (!c->ev_tt) MS_HIP(c, hipEventCreateWithFlags(&c->ev_tt, hipEventDisableTiming));
+    if (c->tt_stream && c->tt_stream != X) MS_HIP(c, hipStreamWaitEvent(X, c->ev_tt, 0));
+    MS_HIP(c, launch_tt2_planes(c->t, c->rows_dev, c->d_tt, X));
+    MS_HIP(c, launch_tt2_census_shard(c->t, c->rows_dev, pods, n, seed32, c->d_tt, std::max(1u, n), sl.cen_mine, X));
+    MS_HIP(c, hipEventRecord(m.ev_swept[si], X));
+    MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_swept[si], 0));
+    if (sl.used && sl.dec_gen > m.cs_drain_seen) {  // the slot's previous final read cen_all
+        MS_HIP(c, hipStreamWaitEvent(m.cs, m.ev_drained, 0));
+        m.cs_drain_seen = m.drains;
+    }
+    const ncclResult_t r = CCL(ncclAllGather)(sl.cen_mine, sl.cen_all, (size_t)n * MS_TT_CENSUS_BYTES, ncclUint8,
+                                              m.comm, m.cs);
+    if (r != ncclSuccess) return fail(c, MS_E_RCCL, std::string("TaintToleration census all-gather: ") +
+                                                        CCL(ncclGetErrorString)(r));
+    MS_HIP(c, hipEventRecord(m.ev_ag[si], m.cs));
+    MS_HIP(c, hipStreamWaitEvent(X, m.ev_ag[si], 0));
+    MS_HIP(c, launch_tt2_pick_shard(c->t, c->rows_dev, pods, n, seed32, c->d_tt, std::max(1u, n), sl.cen_all, n,
+                                    (uint32_t)m.world, (uint32_t)m.rank, sl.keys, X));
+    MS_HIP(c, hipEventRecord(c->ev_tt, X));
+    c->tt_stream = X;
+    return MS_OK;
 }
 
 int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *results, hipStream_t s) {
@@ -397,7 +448,12 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     const int ps = c->cfg.plugin_set;
     // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
     // packet between consecutive sweeps on X)
-    if (ps == MS_PLUGINS_NU_TT_NN) {  // per-pod summaries of this shard's nodes, no keys
+    if (ps == MS_PLUGINS_NU_TT_NN && tt_two_pass()) {
+        // the two-pass form: this shard's census, every shard's by one all-gather,
+        // then this shard's picks for every pod (keys, combined by the reduce-scatter)
+        rc = tt2_sharded_sweep(c, si, n, pods, X);
+        if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
+    } else if (ps == MS_PLUGINS_NU_TT_NN) {  // per-pod summaries of this shard's nodes, no keys
         rc = tt_summaries_locked(c, n, pods, sl.summ, X);
         if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
     } else {
@@ -542,6 +598,7 @@ void comm_free(ms_ctx *c) {
         free_slot(m->slot[i]);
         if (m->ev_swept[i]) (void)hipEventDestroy(m->ev_swept[i]);
         if (m->ev_comb[i]) (void)hipEventDestroy(m->ev_comb[i]);
+        if (m->ev_ag[i]) (void)hipEventDestroy(m->ev_ag[i]);
     }
     if (m->ev_drained) (void)hipEventDestroy(m->ev_drained);
     if (m->ev_in) (void)hipEventDestroy(m->ev_in);
@@ -637,6 +694,7 @@ int comm_setup(ms_ctx *c, CommState &m, const ms_comm_id *id, int32_t rank, int3
     for (uint32_t i = 0; i < kPipeMax; ++i) {
         MS_HIP(c, hipEventCreateWithFlags(&m.ev_swept[i], hipEventDisableTiming));
         MS_HIP(c, hipEventCreateWithFlags(&m.ev_comb[i], hipEventDisableTiming));
+        MS_HIP(c, hipEventCreateWithFlags(&m.ev_ag[i], hipEventDisableTiming));
     }
     MS_HIP(c, hipEventCreateWithFlags(&m.ev_drained, hipEventDisableTiming));
     MS_HIP(c, hipEventCreateWithFlags(&m.ev_in, hipEventDisableTiming));

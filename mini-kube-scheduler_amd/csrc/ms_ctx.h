@@ -215,5 +215,9 @@ void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world);
 // communicator's internal streams; returns 1 if it inserted waits, 0 if none
 // were outstanding (or no communicator), < 0 on failure.
 int comm_fence_reads(ms_ctx *c, hipStream_t writer);
+// MS_PLUGINS_NU_TT_NN: the two-pass bit-sliced cycle (default) or, with
+// MINISCHED_TT=v1, the per-pair summary sweep (read once per process).
+bool tt_two_pass();
+int ensure_tt(ms_ctx *c, size_t need);
 
 }  // namespace msgpu

@@ -360,7 +360,7 @@ hipError_t launch_tt2_pick_shard(const NodeTable &t, uint32_t n_rows, const ms_p
                                  uint32_t stride, uint32_t n_shards, uint32_t shard, unsigned long long *keys_out,
                                  hipStream_t s);
 hipError_t launch_tt2_final_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                                  uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                  uint32_t seed32, void *plans_buf, uint32_t max_pods, const void *census_all,
                                   uint32_t stride, uint32_t n_shards, const unsigned long long *keys_max,
                                   ms_result *results, hipStream_t s);
 hipError_t launch_tt_combine(const void *in, uint32_t stride, uint32_t n_segs, const ms_pod_rec *pods, uint32_t n_pods,

@@ -310,6 +310,7 @@ struct TtPlan {  // 32 B per pod
     uint32_t F, _pad;
     u64 best;       // best explicit entry at S* (make_key), 0: none
 };
+static_assert(sizeof(TtPlan) == MS_TT_CENSUS_BYTES, "plans buffers are sized in census records (ms_comm.cpp)");
 
 __device__ __forceinline__ uint32_t ent_pack(uint32_t row, uint32_t c, uint32_t nn) { return row | nn << 21 | c << 24; }
 __device__ __forceinline__ uint32_t ent_row(uint32_t e) { return e & 0x1FFFFFu; }
@@ -990,16 +991,17 @@ hipError_t launch_tt2_pick_shard(const NodeTable &t, uint32_t n_rows, const ms_p
 }
 
 hipError_t launch_tt2_final_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                                  uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                  uint32_t seed32, void *plans_buf, uint32_t max_pods, const void *census_all,
                                   uint32_t stride, uint32_t n_shards, const unsigned long long *keys_max,
                                   ms_result *results, hipStream_t s) {
+    (void)n_rows;
     if (n_pods == 0) return hipSuccess;
-    if (n_pods > max_pods || !results) return hipErrorInvalidValue;
-    const Tt2Scratch x = tt2_layout(scratch, n_rows, max_pods);
+    if (n_pods > max_pods || !results || !plans_buf) return hipErrorInvalidValue;
+    TtPlan *plans = static_cast<TtPlan *>(plans_buf);  // (n_pods records)
     const dim3 g1(cdiv(n_pods, 128u));
     hipLaunchKernelGGL(k_tt2_plan, g1, dim3(128), 0, s, static_cast<const TtCensus *>(census_all), n_shards, stride,
-                       pods, n_pods, seed32, x.plans, results, t, 0);
-    hipLaunchKernelGGL(k_tt2_final, g1, dim3(128), 0, s, x.plans, reinterpret_cast<const u64 *>(keys_max), 1u, pods,
+                       pods, n_pods, seed32, plans, results, t, 0);
+    hipLaunchKernelGGL(k_tt2_final, g1, dim3(128), 0, s, plans, reinterpret_cast<const u64 *>(keys_max), 1u, pods,
                        n_pods, results, t, 0);
     return hipGetLastError();
 }
