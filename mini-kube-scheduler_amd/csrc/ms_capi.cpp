@@ -833,7 +833,13 @@ int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock
         const char *e = getenv("MINISCHED_COPY_THREADS");
         return e ? (unsigned)std::min(15, std::max(0, atoi(e))) : 3u;
     }();
-    if (helpers && per >= kZcParMin && !c->copy_pool) c->copy_pool.reset(new (std::nothrow) CopyPool(helpers));
+    if (helpers && per >= kZcParMin && !c->copy_pool) {
+        try {  // (no helper threads, e.g. none can be created: the caller copies alone)
+            c->copy_pool.reset(new CopyPool(helpers));
+        } catch (...) {
+            c->copy_pool.reset();
+        }
+    }
     CopyPool *pool = per >= kZcParMin ? c->copy_pool.get() : nullptr;
     auto par = [&](uint32_t lo, uint32_t hi, const std::function<void(uint32_t, uint32_t)> &fn) {
         if (!pool) {

@@ -26,17 +26,14 @@ namespace msgpu {
 class CopyPool {
   public:
     explicit CopyPool(unsigned helpers) {
-        for (unsigned i = 0; i < helpers; ++i) th_.emplace_back([this, i] { run(i + 1); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_.store(true, std::memory_order_relaxed);
-            epoch_.fetch_add(1, std::memory_order_release);
+        try {
+            for (unsigned i = 0; i < helpers; ++i) th_.emplace_back([this, i] { run(i + 1); });
+        } catch (...) {  // a thread could not be created: join the ones that were, then report
+            shutdown();
+            throw;
         }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
     }
+    ~CopyPool() { shutdown(); }
     CopyPool(const CopyPool &) = delete;
     CopyPool &operator=(const CopyPool &) = delete;
 
@@ -58,6 +55,17 @@ class CopyPool {
     }
 
   private:
+    void shutdown() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_.store(true, std::memory_order_relaxed);
+            epoch_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        for (auto &t : th_)
+            if (t.joinable()) t.join();
+    }
+
     void run(unsigned part) {
         // (0, the epoch at construction, not a fresh load: a job posted before this
         // thread got here would otherwise be missed and its caller would wait forever)
