@@ -521,6 +521,9 @@ bool tt_two_pass() {
 // MS_PLUGINS_NU_TT_NN scratch: `need` bytes (summaries or the two-pass cycle's).
 int ensure_tt(ms_ctx *c, size_t need) {
     if (need <= c->tt_bytes) return MS_OK;
+    // (growing: the previous scratch may still be read by work on the sweep,
+    // collective or decode streams of a node-sharded cycle)
+    if (c->d_tt) MS_HIP(c, hipDeviceSynchronize());
     if (c->d_tt) (void)hipFree(c->d_tt);
     c->d_tt = nullptr;
     c->tt_bytes = 0;
