@@ -1601,6 +1601,7 @@ struct SeqArgs {
     int carry;
     ms_result *results;
     uint32_t *stats;
+    u64 *tl;  // (diagnostic timeline builds) this step's row: the validator's phase stamps
 };
 
 // The validator's LDS tables cleared by nthreads threads: touched-node map,
@@ -1769,6 +1770,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 #pragma unroll
     for (int j = 0; j < J; ++j) tiles |= (lane + 64u * j < n_tiles) ? 1u << j : 0u;
     MS_VST(0);
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (va.tl && lane == 0) va.tl[kTlWave0] = __builtin_amdgcn_s_memrealtime();  // (workgroup 0: prologue done)
+#endif
 
     // Pods go in groups of 64, lane i <-> pod g+i, decided in rounds. A round
     // takes the group's undecided pods i0.. in parallel, each with its winner
@@ -1984,6 +1988,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     // counters (one atomic instruction: lane i adds counter i + 1; the recomputes
     // are per lane, the rest wave-uniform), then every touched node's record
     // goes back to the table
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (va.tl && lane == 0) va.tl[kTlStaged] = __builtin_amdgcn_s_memrealtime();  // (workgroup 0: decisions done)
+#endif
     {
         const uint32_t rsum = wave_sum_u32_dpp(ctr.recompute);
         const uint32_t v = lane == 0 ? ctr.resweep : lane == 1 ? rsum : lane == 2 ? n_pods : lane == 3 ? ctr.miss
@@ -2032,6 +2039,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     MS_VST(11);
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (va.tl && lane == 0) va.tl[kTlTasks] = __builtin_amdgcn_s_memrealtime();  // (workgroup 0: write-back issued)
+#endif
     if (prev_out) {
         // carried: the previous batch's own binds that this batch did not bind again
         const uint32_t n_own = S.n_out;
@@ -2852,7 +2862,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
         (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
         return hipErrorInvalidValue;
-    const SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
+    SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
                         spec,     spec_flags,   top4,    top4_recs,  top_ext, n_tiles, prev_in, prev_recs_in,
                         prev_out, prev_recs_out, carry,  results,    stats};
     // tasks: (tile, chunk of next pods) pairs, sized to fit one pass of the
@@ -2905,6 +2915,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
         if (mio->tl && mio->tl_step < kTimelineSteps && grid <= kTimelineWgs)
             sm.tl = reinterpret_cast<u64 *>(mio->tl) + (size_t)mio->tl_step * kTimelineWgs * 8;
     }
+    va.tl = sm.tl;
 #define MS_STEP(JJ, WW) \
     hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, mg, merge_wgs, sm)
     if (J == 1) MS_STEP(1, 12);

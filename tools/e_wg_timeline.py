@@ -37,8 +37,12 @@ def main(path, out=None):
             r.update(merged_median=float(us(np.median(m))), merged_max=float(us(m.max())))
         if tl[s, 0, 4] > 0:
             r["validator_done"] = float(us(tl[s, 0, 4]))
+        # workgroup 0 (the validator's): 6 prologue done, 5 decisions done, 7 write-back issued
+        for f, name in ((6, "val_prologue"), (5, "val_decided"), (7, "val_written")):
+            if tl[s, 0, f] > 0:
+                r[name] = float(us(tl[s, 0, f]))
         for f, name in ((5, "staged"), (6, "wave0_tasks"), (7, "all_tasks")):
-            x = tl[s, live, f]
+            x = tl[s, 1:, f][live[1:]]
             x = x[x > 0]
             if len(x):
                 r[name + "_median"] = float(us(np.median(x)))
@@ -46,7 +50,7 @@ def main(path, out=None):
         rows.append(r)
     keys = ["start_spread_us", "staged_median", "staged_max", "wave0_tasks_median", "all_tasks_median",
             "all_tasks_max", "swept_min", "swept_median", "swept_max", "waited_median", "waited_max",
-            "merged_median", "merged_max", "validator_done"]
+            "merged_median", "merged_max", "val_prologue", "val_decided", "val_written", "validator_done"]
     med = {k: float(np.median([r[k] for r in rows if k in r])) for k in keys if any(k in r for r in rows)}
     for r in rows:
         print(" ".join(f"{k}={r[k]:.2f}" if isinstance(r[k], float) else f"{k}={r[k]}" for k in r))
