@@ -1216,10 +1216,11 @@ struct SeqShared {
     int64_t rec[kSeqSlots][kRecF];
     alignas(16) uint8_t bound[kSeqSlots];  // binds on the slot in this batch (<= 128: no wrap)
     uint32_t n_out;
+    uint32_t n_prorec;  // recomputes of the workgroup prologue (prologue_wg_finish), for the counters
     ms_pod_rec pods[kSeqBatch];
     u64 spec_key[kSeqBatch];     // speculative winner key per pod (0: no feasible row at speculation)
     uint32_t spec_flags[kSeqBatch];  // OR of the tile flags of tiles with no feasible row at speculation
-    u64 top4[kSeqBatch][kTopK];      // global speculative top-4 keys per pod (k_topk_merge)
+    alignas(16) u64 top4[kSeqBatch][kTopK];  // global speculative top-4 keys per pod (k_topk_merge)
     u64 top_ext[kSeqBatch][kTopK];   // ranks 4..7 (keys only), exact up to cert[]
     uint8_t cert[kSeqBatch];         // certified ranks, 4..8 (4 without the extension)
     alignas(16) uint32_t claim[kClaimCap];  // per round: lowest lane whose speculative winner hashes here
@@ -1633,29 +1634,153 @@ __device__ __forceinline__ void validate_prologue_wg(SeqShared &S, const SeqArgs
     }
 }
 
-template <int J>  // tile lists per lane: n_tiles <= 64 * J
-__device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, uint32_t lane, bool wg_dma = false) {
+// The validator's whole prologue on all W waves of workgroup 0 (k_seq_step,
+// MS_WG_PROLOGUE=2): validate_prologue_wave's work, its loads issued with the
+// bulk copies (one memory round trip for the workgroup) and its speculative
+// winner re-resolution spread over the waves, 16 pods per wave and pass (lane
+// 4i + r on entry r of pod i), where the single wave took up to eight passes
+// in a row. prologue_wg_issue clears the tables, issues everything and waits;
+// prologue_wg_finish (after a barrier) stores, maps the stale nodes and
+// resolves. validate_batch (pro 2) then starts at the decisions.
+template <int W>
+struct ProRegs {
+    static constexpr uint32_t kNT = 64u * W;
+    static constexpr int kPodU = (int)((kSeqBatch * sizeof(ms_pod_rec) / 8 + kNT - 1) / kNT);  // uint2 per thread
+    static constexpr int kPW = (int)((kPrevWords + kNT - 1) / kNT);                            // prev_in words
+    uint2 pod[kPodU];
+    uint32_t prow[kPW];
+    u64 sk;        // thread i < n_pods: pod i's speculative key
+    uint32_t sf;   // and flags
+    uint32_t n_prev;
+};
+
+template <int W>
+__device__ __forceinline__ void prologue_wg_issue(SeqShared &S, const SeqArgs &va, uint32_t tid, ProRegs<W> &R) {
+    constexpr uint32_t NT = ProRegs<W>::kNT;
+    const uint32_t n_pods = va.n_pods;
+    validate_prologue_wg(S, va, tid, NT);  // tables cleared, records / ranks 4..7 / stale records
+    lds_dma16_wg(&S.top4[0][0], va.top4, n_pods * kTopK / 2, kSeqBatch * kTopK / 2, tid, NT);
+    const uint2 *sp = reinterpret_cast<const uint2 *>(va.pods);
+    const uint32_t n_pod_u = n_pods * (uint32_t)sizeof(ms_pod_rec) / 8;
+#pragma unroll
+    for (int k = 0; k < ProRegs<W>::kPodU; ++k) R.pod[k] = sp[min(tid + NT * k, n_pod_u - 1)];
+    const uint32_t ts = min(tid, n_pods - 1);
+    R.sk = va.spec[ts];
+    R.sf = va.spec_flags[ts];
+    const uint32_t *prev_in = va.prev_in;
+#pragma unroll
+    for (int k = 0; k < ProRegs<W>::kPW; ++k) R.prow[k] = prev_in ? prev_in[min(tid + NT * k, (uint32_t)kPrevWords - 1)] : 0u;
+    R.n_prev = prev_in ? min(prev_in[0] + prev_in[1], (uint32_t)kPrevCap) : 0u;
+    __builtin_amdgcn_s_waitcnt(0);
+}
+
+template <int W>
+__device__ __forceinline__ void prologue_wg_finish(SeqShared &S, const SeqArgs &va, uint32_t tid, const ProRegs<W> &R) {
+    constexpr uint32_t NT = ProRegs<W>::kNT;
+    const uint32_t n_pods = va.n_pods, n_prev = R.n_prev;
+    const uint32_t n_pod_u = n_pods * (uint32_t)sizeof(ms_pod_rec) / 8;
+    uint2 *dp = reinterpret_cast<uint2 *>(S.pods);
+#pragma unroll
+    for (int k = 0; k < ProRegs<W>::kPodU; ++k)
+        if (tid + NT * k < n_pod_u) dp[tid + NT * k] = R.pod[k];
+    if (tid < n_pods) {  // (bits 28-31: the merge's certified ranks, 0 without ranks 4..7)
+        S.spec_key[tid] = R.sk;
+        S.spec_flags[tid] = R.sf & 0x0FFFFFFFu;
+        S.cert[tid] = (uint8_t)max(R.sf >> 28, (uint32_t)kTopK);
+    }
+    if (tid == 0) {
+        S.n_out = 0;
+        S.n_prorec = 0;
+    }
+    // the stale nodes are "touched" (validate_prologue_wave); word a >= 2 of prev_in is stale node a - 2
+#pragma unroll
+    for (int k = 0; k < ProRegs<W>::kPW; ++k) {
+        const uint32_t a = tid + NT * k;
+        if (a >= 2 && a < n_prev + 2) {
+            const uint32_t r = R.prow[k];
+            uint32_t h = map_hash(r);
+            while (atomicCAS(&S.map[h], 0u, ((r + 1) << kSlotBits) | (uint32_t)(kPrevSlot0 + a - 2)) != 0u)
+                h = (h + 1) & (kMapCap - 1);
+        }
+    }
+    __syncthreads();
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (va.tl && tid == 0) va.tl[kTlMerged] = __builtin_amdgcn_s_memrealtime();  // (workgroup 0: stale nodes mapped)
+#endif
+    // each pod's speculative winner slot: its own top-4 record (normally entry
+    // 0); a stale winner is re-resolved against the current state (walk_top4's
+    // rule: touched entries from their records, the first untouched one exact;
+    // all four touched, or none feasible: kForceSlow)
     const NodeTable &t = va.t;
-    const uint32_t n_rows = va.n_rows, n_pods = va.n_pods, seed32 = va.seed32, n_tiles = va.n_tiles;
+    const uint32_t lane = tid & 63u, qi = lane >> 2, r = lane & 3u;
+    uint32_t nrec = 0;
+    for (uint32_t c0 = 16u * (tid >> 6); c0 < n_pods; c0 += 16u * W) {  // (wave-uniform trip count)
+        const uint32_t p = c0 + qi;
+        const bool inb = p < n_pods;
+        const u64 sk = inb ? S.spec_key[p] : 0ull;
+        const bool stale = sk && n_prev && map_find(S, row_of_key(sk, t.base)) >= 0;  // (quad-uniform)
+        u64 v = 0;
+        uint32_t vs = 0;
+        bool unt = false, end = false;
+        if (stale) {
+            const u64 e = S.top4[p][r];
+            if (e == 0) {
+                end = true;
+            } else {
+                const uint32_t er = row_of_key(e, t.base);
+                const int es = map_find(S, er);
+                if (es < 0) {
+                    unt = true;
+                    v = e;
+                    vs = kTopK * p + r;
+                } else {
+                    uint32_t nu, nrf;
+                    v = eval_full(slot_row(S, es), er + t.base, load_pod(S.pods[p], va.seed32), nu, nrf);
+                    vs = (uint32_t)es;
+                    ++nrec;
+                }
+            }
+        }
+        const uint32_t qb = (uint32_t)(__ballot(unt || end) >> (4u * qi)) & 0xFu;
+        const uint32_t f = qb ? (uint32_t)__builtin_ctz(qb) : 4u;
+        const bool valid = stale && !end && (r < f || (r == f && unt));
+        const u64 ve = valid ? v : 0ull;
+        const u64 m = quad_max_u64(ve);
+        const uint32_t own = (uint32_t)(__ballot(valid && m != 0 && ve == m) >> (4u * qi)) & 0xFu;
+        if (inb && r == (own ? (uint32_t)__builtin_ctz(own) : 0u)) {
+            uint32_t sslot = kTopK * p;
+            if (stale) {
+                if (f != 4u && m != 0) {
+                    S.spec_key[p] = m;
+                    sslot = vs;
+                } else {
+                    sslot = kForceSlow;
+                }
+            }
+            S.spec_slot[p] = (uint16_t)sslot;
+        }
+    }
+    const uint32_t rsum = wave_sum_u32_dpp(nrec);
+    if (lane == 0 && rsum) atomicAdd(&S.n_prorec, rsum);  // (LDS: a global atomic here would hold the barrier)
+    __syncthreads();
+}
+
+// The validator's prologue on its one wave (k_validate_seq; k_seq_step with
+// MS_WG_PROLOGUE=1, whose workgroup issued the bulk copies: wg_dma): the
+// batch's pods, top-4 keys and speculative winners into LDS, the stale nodes
+// mapped, each pod's speculative winner slot resolved. Returns prev_in[0].
+__device__ __forceinline__ uint32_t validate_prologue_wave(SeqShared &S, const SeqArgs &va, uint32_t lane, bool wg_dma,
+                                                           SeqCounters &ctr) {
+    const NodeTable &t = va.t;
+    const uint32_t n_pods = va.n_pods, seed32 = va.seed32;
     const ms_pod_rec *__restrict__ pods = va.pods;
-    const u64 *__restrict__ tile_keys = va.tile_keys;
-    const uint32_t *__restrict__ tile_flags = va.tile_flags;
     const u64 *__restrict__ spec = va.spec;
     const uint32_t *__restrict__ spec_flags = va.spec_flags;
     const u64 *__restrict__ top4 = va.top4;
     const int64_t *__restrict__ top4_recs = va.top4_recs;
     const uint32_t *__restrict__ prev_in = va.prev_in;
     const int64_t *__restrict__ prev_recs_in = va.prev_recs_in;
-    uint32_t *__restrict__ prev_out = va.prev_out;
-    int64_t *__restrict__ prev_recs_out = va.prev_recs_out;
     const int carry = va.carry;
-    ms_result *__restrict__ results = va.results;
-    uint32_t *__restrict__ stats = va.stats;
-    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
-        if (lane == 0) atomicOr(&stats[0], 1u);
-        return;
-    }
-    MS_VST_DECL
     // prologue, one memory round trip: every load below is issued (from clamped,
     // always valid addresses; no branches) before the first wait. The records
     // go global -> LDS directly (no registers); stores past the batch stay
@@ -1715,7 +1840,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
         }
     }
     __builtin_amdgcn_s_waitcnt(0);  // the LDS DMA above has landed
-    MS_VST(2);
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (va.tl && lane == 0) va.tl[kTlWaited] = __builtin_amdgcn_s_memrealtime();  // (workgroup 0: wave-0 loads landed)
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     // the stale nodes are "touched" here: this batch's speculation may have read
@@ -1736,12 +1863,14 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+    if (va.tl && lane == 0) va.tl[kTlMerged] = __builtin_amdgcn_s_memrealtime();  // (workgroup 0: stale nodes mapped)
+#endif
     // each pod's speculative winner slot: its own top-4 record (normally entry 0).
     // Pipelined: a winner that is a stale node (bound by a previous batch after
     // this batch's speculation may have read it) is re-resolved against the
     // current state, nothing of this batch being bound yet (walk_top4); all
     // four entries stale, or none feasible now: resolved in order (kForceSlow).
-    SeqCounters ctr = {0, 0, 0, 0, 0, 0};
     for (uint32_t i0 = 0; i0 < (uint32_t)kSeqBatch; i0 += 64) {  // (wave-uniform trip count)
         const uint32_t i = i0 + lane;
         const u64 sk = i < n_pods ? S.spec_key[i] : 0ull;
@@ -1766,6 +1895,30 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    return n_own_in;
+}
+
+template <int J>  // tile lists per lane: n_tiles <= 64 * J
+__device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, uint32_t lane, int pro = 0) {
+    const NodeTable &t = va.t;
+    const uint32_t n_rows = va.n_rows, n_pods = va.n_pods, seed32 = va.seed32, n_tiles = va.n_tiles;
+    const u64 *__restrict__ tile_keys = va.tile_keys;
+    const uint32_t *__restrict__ tile_flags = va.tile_flags;
+    const uint32_t *__restrict__ prev_in = va.prev_in;
+    uint32_t *__restrict__ prev_out = va.prev_out;
+    int64_t *__restrict__ prev_recs_out = va.prev_recs_out;
+    const int carry = va.carry;
+    ms_result *__restrict__ results = va.results;
+    uint32_t *__restrict__ stats = va.stats;
+    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * J) {  // host guarantees this
+        if (lane == 0) atomicOr(&stats[0], 1u);
+        return;
+    }
+    MS_VST_DECL
+    SeqCounters ctr = {0, 0, 0, 0, 0, 0};
+    // (pro 2: the whole prologue ran on the workgroup: prologue_wg_issue / _finish)
+    const uint32_t n_own_in = pro == 2 ? (prev_in ? prev_in[0] : 0u) : validate_prologue_wave(S, va, lane, pro == 1, ctr);
+    if (pro == 2 && lane == 0) ctr.recompute = S.n_prorec;  // (summed over lanes at the end)
     uint32_t tiles = 0;  // tiles: bit j <=> this lane owns tile lane + 64 j
 #pragma unroll
     for (int j = 0; j < J; ++j) tiles |= (lane + 64u * j < n_tiles) ? 1u << j : 0u;
@@ -2200,15 +2353,26 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
     if (sm.tl && threadIdx.x == 0 && blockIdx.x < kTimelineWgs) sm.tl[blockIdx.x * 8 + kTlBegin] = t_begin;
 #endif
     if (blockIdx.x == 0) {
-        // the bulk prologue copies by all W waves (MS_WG_PROLOGUE=0: by the validating wave alone, A/B)
+        // the prologue by all W waves (MS_WG_PROLOGUE=2: all of it; 1: the bulk copies,
+        // the rest on the validating wave; 0: all on the validating wave, A/B)
 #ifndef MS_WG_PROLOGUE
-#define MS_WG_PROLOGUE 1
+#define MS_WG_PROLOGUE 2
 #endif
         // the tags of an in-step merged batch, loaded beside the prologue's loads
         const bool check = sm.in_tag != 0u && va.n_pods;
         uint32_t tg = sm.in_tag;
         if (check && threadIdx.x < va.n_pods) tg = sm.in_tags[threadIdx.x];
-        if (MS_WG_PROLOGUE && va.n_pods) {
+        if (MS_WG_PROLOGUE == 2 && va.n_pods) {
+            ProRegs<W> R;
+            prologue_wg_issue<W>(S, va, threadIdx.x, R);
+            if (check && step_merge_fallback<J, W>(va, sm, tg != sm.in_tag, threadIdx.x >> 6, lane_id()))
+                prologue_wg_issue<W>(S, va, threadIdx.x, R);  // again, with the merged entries
+            __syncthreads();
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+            if (sm.tl && threadIdx.x == 0) sm.tl[kTlSwept] = __builtin_amdgcn_s_memrealtime();  // (bulk copies landed)
+#endif
+            prologue_wg_finish<W>(S, va, threadIdx.x, R);
+        } else if (MS_WG_PROLOGUE && va.n_pods) {
             validate_prologue_wg(S, va, threadIdx.x, 64u * W);
             __builtin_amdgcn_s_waitcnt(0);
             if (check && step_merge_fallback<J, W>(va, sm, tg != sm.in_tag, threadIdx.x >> 6, lane_id())) {
@@ -2216,10 +2380,13 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
                 __builtin_amdgcn_s_waitcnt(0);
             }
             __syncthreads();
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+            if (sm.tl && threadIdx.x == 0) sm.tl[kTlSwept] = __builtin_amdgcn_s_memrealtime();  // (bulk copies landed)
+#endif
         } else if (check) {
             step_merge_fallback<J, W>(va, sm, tg != sm.in_tag, threadIdx.x >> 6, lane_id());
         }
-        if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x, MS_WG_PROLOGUE != 0);
+        if (threadIdx.x < 64 && va.n_pods) validate_batch<J>(S, va, threadIdx.x, MS_WG_PROLOGUE);
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
         if (threadIdx.x == 0 && va.n_pods) {
             const u64 now = __builtin_amdgcn_s_memrealtime();
