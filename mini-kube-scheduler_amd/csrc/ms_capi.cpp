@@ -408,14 +408,14 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
             unsigned long long *tk1 = c->d_tile_keys + cells_per_set * seq_topk() * nxt;
             uint32_t *tf = c->d_tile_flags + cells_per_set * cur, *tf1 = c->d_tile_flags + cells_per_set * nxt;
             SeqMergeIO mio;
-            // timeline of steps 200 .. 215 (MS_TIMELINE=<file>; recorded by the
-            // MS_VSTAMPS / MS_TIMELINE_ONLY diagnostic kernels only)
+            // timeline of steps 0 .. kTimelineSteps - 1 (MS_TIMELINE=<file>; recorded
+            // by the MS_VSTAMPS / MS_TIMELINE_ONLY diagnostic kernels only)
             static const bool want_tl = getenv("MS_TIMELINE") != nullptr;
             if (want_tl && !c->d_tl &&
                 hipMalloc((void **)&c->d_tl, (size_t)kTimelineSteps * kTimelineWgs * 8 * 8) == hipSuccess)
                 MS_HIP(c, hipMemsetAsync(c->d_tl, 0, (size_t)kTimelineSteps * kTimelineWgs * 8 * 8, s));
             mio.tl = c->d_tl;
-            mio.tl_step = k >= 200 ? k - 200 : ~0u;
+            mio.tl_step = k;
             mio.in_tags = c->d_merge_tags + SB * cur;
             mio.in_tag = in_tag;
             mio.ctr = c->d_merge_ctr;

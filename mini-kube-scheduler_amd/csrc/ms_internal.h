@@ -286,7 +286,7 @@ struct SeqMergeIO {
     unsigned long long *tl = nullptr;
     uint32_t tl_step = ~0u;
 };
-constexpr uint32_t kTimelineSteps = 16, kTimelineWgs = 256;
+constexpr uint32_t kTimelineSteps = 2048, kTimelineWgs = 256;  // (a config E run: 1627 steps)
 // Whether launch_seq_step can merge n_next pods in-step (else launch_topk_merge follows).
 bool seq_step_merges(const NodeTable &t, uint32_t n_tiles, uint32_t n_next);
 // One single-stream step: validate batch k (n_pods) while sweeping the next

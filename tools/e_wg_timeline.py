@@ -1,62 +1,93 @@
 #!/usr/bin/env python3
-"""Per-workgroup timeline of config-E steps from the MS_VSTAMPS build
-(MS_TIMELINE=<file>: u64 [16 steps][256 workgroups][8], s_memrealtime ticks of
-10 ns; fields: 0 start, 1 swept + counted, 2 worker wait done, 3 worker merges
-done, 4 validator done (workgroup 0)). Prints, per step, microseconds from the
-first workgroup's start: the start spread, swept min / median / max, the
-workers' wait done (median / max), merges done (max) and the validator's end.
+"""Per-workgroup timeline of config-E steps from the diagnostic timeline build
+(MS_TIMELINE=<file>: u64 [steps][256 workgroups][8], s_memrealtime ticks of
+10 ns, steps 0 .. 2047 of the last run; fields: 0 start, 1 swept + counted,
+2 worker wait done, 3 worker merges done, 4 validator done (workgroup 0)).
+Workgroup 0 (the validator's) also stamps 1 bulk LDS copies landed, 2 wave-0
+loads landed (single-wave prologue), 3 stale nodes mapped, 6 prologue done,
+5 decisions done, 7 write-back issued; sweep workgroups 5 tile staged, 6 wave
+0's tasks done, 7 all tasks done.
+
+Prints the per-phase medians over steps 200 .. 215 (the window earlier rounds
+recorded) and, over the whole run, each step's validator end V and merge-path
+end M (the last merge worker's), both from the step's first workgroup start,
+with the step's length to the next step's start: how often the validator is
+the critical path and what either path would save.
 usage: python tools/e_wg_timeline.py <file> [json_out]"""
 import json
+import os
 import sys
 
 import numpy as np
 
 
+def step_row(tl, s):
+    b = tl[s, :, 0]
+    live = b > 0
+    if not live.any():
+        return None
+    t0 = b[live].min()
+    us = lambda v: (v - t0) / 100.0  # noqa: E731
+    r = {"step": s, "workgroups": int(live.sum()), "start_spread_us": float(us(b[live].max())), "t0": int(t0)}
+    for f, name in ((1, "swept"), (2, "waited"), (3, "merged")):
+        x = tl[s, 1:, f][live[1:]]
+        x = x[x > 0]
+        if len(x):
+            r[name + "_median"] = float(us(np.median(x)))
+            r[name + "_max"] = float(us(x.max()))
+    if tl[s, 0, 4] > 0:
+        r["validator_done"] = float(us(tl[s, 0, 4]))
+    for f, name in ((1, "val_dma"), (2, "val_loads"), (3, "val_mapped"), (6, "val_prologue"),
+                    (5, "val_decided"), (7, "val_written")):
+        if tl[s, 0, f] > 0:
+            r[name] = float(us(tl[s, 0, f]))
+    for f, name in ((5, "staged"), (6, "wave0_tasks"), (7, "all_tasks")):
+        x = tl[s, 1:, f][live[1:]]
+        x = x[x > 0]
+        if len(x):
+            r[name + "_median"] = float(us(np.median(x)))
+            r[name + "_max"] = float(us(x.max()))
+    return r
+
+
 def main(path, out=None):
-    tl = np.fromfile(path, dtype=np.uint64).reshape(16, 256, 8).astype(np.int64)
-    rows = []
-    for s in range(16):
-        b = tl[s, :, 0]
-        live = b > 0
-        if not live.any():
-            continue
-        t0 = b[live].min()
-        us = lambda v: (v - t0) / 100.0  # noqa: E731
-        r = {"step": 200 + s, "workgroups": int(live.sum()), "start_spread_us": float(us(b[live].max()))}
-        sw = tl[s, live, 1]
-        sw = sw[sw > 0]
-        if len(sw):
-            r.update(swept_min=float(us(sw.min())), swept_median=float(us(np.median(sw))), swept_max=float(us(sw.max())))
-        w = tl[s, live, 2]
-        w = w[w > 0]
-        if len(w):
-            r.update(waited_median=float(us(np.median(w))), waited_max=float(us(w.max())))
-        m = tl[s, live, 3]
-        m = m[m > 0]
-        if len(m):
-            r.update(merged_median=float(us(np.median(m))), merged_max=float(us(m.max())))
-        if tl[s, 0, 4] > 0:
-            r["validator_done"] = float(us(tl[s, 0, 4]))
-        # workgroup 0 (the validator's): 6 prologue done, 5 decisions done, 7 write-back issued
-        for f, name in ((6, "val_prologue"), (5, "val_decided"), (7, "val_written")):
-            if tl[s, 0, f] > 0:
-                r[name] = float(us(tl[s, 0, f]))
-        for f, name in ((5, "staged"), (6, "wave0_tasks"), (7, "all_tasks")):
-            x = tl[s, 1:, f][live[1:]]
-            x = x[x > 0]
-            if len(x):
-                r[name + "_median"] = float(us(np.median(x)))
-                r[name + "_max"] = float(us(x.max()))
-        rows.append(r)
+    n_steps = os.path.getsize(path) // (256 * 8 * 8)
+    tl = np.fromfile(path, dtype=np.uint64).reshape(n_steps, 256, 8).astype(np.int64)
+    rows = [r for r in (step_row(tl, s) for s in range(n_steps)) if r]
+    window = [r for r in rows if 200 <= r["step"] < 216]
     keys = ["start_spread_us", "staged_median", "staged_max", "wave0_tasks_median", "all_tasks_median",
-            "all_tasks_max", "swept_min", "swept_median", "swept_max", "waited_median", "waited_max",
-            "merged_median", "merged_max", "val_prologue", "val_decided", "val_written", "validator_done"]
-    med = {k: float(np.median([r[k] for r in rows if k in r])) for k in keys if any(k in r for r in rows)}
-    for r in rows:
-        print(" ".join(f"{k}={r[k]:.2f}" if isinstance(r[k], float) else f"{k}={r[k]}" for k in r))
-    print("median over steps:", json.dumps(med))
+            "all_tasks_max", "swept_median", "swept_max", "waited_median", "waited_max",
+            "merged_median", "merged_max", "val_dma", "val_loads", "val_mapped", "val_prologue", "val_decided",
+            "val_written", "validator_done"]
+    med = {k: float(np.median([r[k] for r in window if k in r])) for k in keys if any(k in r for r in window)}
+    for r in window:
+        print(" ".join(f"{k}={r[k]:.2f}" if isinstance(r[k], float) else f"{k}={r[k]}" for k in r if k != "t0"))
+    print("median over steps 200-215:", json.dumps(med))
+    # whole run: V (validator end), M (merge-path end: the last merge worker, or the
+    # last sweep workgroup where no merge ran), step length D to the next start
+    run = {}
+    full = [r for r in rows if "validator_done" in r]
+    if len(full) > 1:
+        V = np.array([r["validator_done"] for r in full])
+        M = np.array([r.get("merged_max", r.get("swept_max", 0.0)) for r in full])
+        t0 = np.array([r["t0"] for r in full], dtype=np.int64)
+        D = np.diff(t0) / 100.0
+        V1, M1 = V[:-1], M[:-1]
+        run = {"steps": len(full), "run_us_first_to_last_start": float((t0[-1] - t0[0]) / 100.0),
+               "step_us_mean": float(D.mean()), "V_mean": float(V.mean()), "M_mean": float(M.mean()),
+               "V_median": float(np.median(V)), "M_median": float(np.median(M)),
+               "V_p90": float(np.percentile(V, 90)), "frac_validator_critical": float((V > M).mean()),
+               "sum_max_VM_us": float(np.maximum(V1, M1).sum()), "sum_D_us": float(D.sum()),
+               "gap_us_mean": float((D - np.maximum(V1, M1)).mean()),
+               "validator_excess_us": float(np.maximum(V1 - M1, 0).sum()),
+               "merge_excess_us": float(np.maximum(M1 - V1, 0).sum())}
+        print("whole run:", json.dumps(run))
     if out:
-        json.dump({"steps": rows, "median": med}, open(out, "w"), indent=1)
+        with open(out, "w") as f:
+            json.dump({"steps": window, "median": med, "run": run,
+                       "per_step": [{"step": r["step"], "V": r.get("validator_done"),
+                                     "M": r.get("merged_max", r.get("swept_max")),
+                                     "prologue": r.get("val_prologue")} for r in full]}, f, indent=0)
 
 
 if __name__ == "__main__":
