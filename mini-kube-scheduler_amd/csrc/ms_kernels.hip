@@ -693,6 +693,9 @@ __device__ __forceinline__ void quad_merge4(u64 (&k)[4], uint32_t &f) {
 // Issued as inline asm: in IEEE mode the compiler would quiet (canonicalise)
 // operands it cannot prove canonical before llvm.maxnum, one more v_max_f64
 // per operand; every operand here is +0.0 or a normal number.
+#ifndef MS_TP_LDROW  // staged rows read as 16-B vectors (ld_drow; 0: field by field, A/B)
+#define MS_TP_LDROW 1
+#endif
 #ifndef MS_TP_F64KEYS
 #define MS_TP_F64KEYS 1
 #endif
@@ -756,6 +759,27 @@ __device__ __forceinline__ void quad_merge4(double (&k)[4], uint32_t &f) {
     for (int j = 0; j < 4; ++j) o[j] = __longlong_as_double((long long)dpp_u64<CTRL>((u64)__double_as_longlong(k[j])));
     merge4_desc(k, o);
     f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, CTRL, 0xF, 0xF, false);
+}
+
+// The fields eval_tp64 reads of a staged row, as three 16-B and one 8-B LDS
+// reads (4 + 4 + 4 + 2 LDS cycles per wave; the compiler's own split of the
+// middle 32 B into two ds_read2_b64 took 8 + 8, MICROARCH §LDS).
+__device__ __forceinline__ DRow ld_drow(const DRow *p) {
+    const longlong2 a = reinterpret_cast<const longlong2 *>(p)[0];
+    const double2 b = reinterpret_cast<const double2 *>(p)[1], c = reinterpret_cast<const double2 *>(p)[2];
+    const uint2 e = reinterpret_cast<const uint2 *>(p)[7];
+    DRow x;
+    x.fr_cpu = a.x;
+    x.fr_mem = a.y;
+    x.r_cpu = b.x;
+    x.r_mem = b.y;
+    x.a_cpu = c.x;
+    x.a_mem = c.y;
+    x.room = 0;
+    x.fd = 0;
+    x.digit = e.x;
+    x.rbits = e.y;
+    return x;
 }
 
 // eval_tp with the tile-local binary64 key (place: the row's index in its tile).
@@ -830,7 +854,8 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
         double x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = eval_tp64(d[4 * (i + u)], ord0 + 4 * (i + u), part + 4 * (i + u), q);
+        for (int u = 0; u < 4; ++u)
+            x[u] = eval_tp64(MS_TP_LDROW ? ld_drow(d + 4 * (i + u)) : d[4 * (i + u)], ord0 + 4 * (i + u), part + 4 * (i + u), q);
         sort4_desc(x);
         merge4_desc(k, x);
     }
