@@ -389,6 +389,17 @@ def other_configs(args, dev, stream):
         pj = json.load(open(args.profile_json_e))
     except Exception:
         pass
+    # the step's two paths over a whole run (timeline build, tools/e_wg_timeline.py):
+    # validator end V and merge-path end M from the step's start, and how often V is later
+    step_split = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r05am_e_wg_timeline_run.json")) as f:
+            run = json.load(f)["run"]
+        step_split = {k: run[k] for k in ("step_us_mean", "V_mean", "M_mean", "frac_validator_critical",
+                                          "gap_us_mean")}
+        step_split["profile"] = "profiles/r05am_e_wg_timeline_run.json"
+    except Exception:
+        pass
     if pj and pj.get("nodes") == N and pj.get("pods") == P:
         step_s = pj["step_avg_ns_rocprof"] * 1e-9
         valu = pj["step_SQ_INSTS_VALU"]
@@ -398,8 +409,7 @@ def other_configs(args, dev, stream):
             "frac": valu / step_s / VALU_PEAK_NOMINAL,
             "frac_vs_guide_peak": valu / step_s / VALU_PEAK_GUIDE,
             "valu_insts_per_launch": valu, "kernel_ms_rocprof": step_s * 1e3,
-            "validator_ns_per_pod": pj.get("validator_ns_per_pod"),
-            "validator_frac_of_step": pj.get("validator_frac_of_step"),
+            "step_split": step_split,
             "traffic": pj.get("step_hbm_bytes"),
             "fetch_bytes_per_step": pj.get("step_FETCH_SIZE_KB", 0) * 1024 * 2 or None,  # (gfx950 x2 read correction)
             "write_bytes_per_step": pj.get("step_WRITE_SIZE_KB", 0) * 1024 or None,
