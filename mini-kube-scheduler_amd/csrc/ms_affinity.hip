@@ -59,12 +59,27 @@ __device__ __forceinline__ uint32_t nam_row_word(const NodeTable &t, uint32_t r)
            ((uint32_t)t.label2[r] << 16) | ((d <= 9u ? d : 15u) << 24);
 }
 
-// A pod's terms, one word each: the label's bit offset in the row word
-// (8 zone, 16 label2), the matching label window [lo, lo + span] (In: value,
-// span 0; Exists: 1..254), weight (0: unused).
+// A pod's terms: term k matches a row whose label byte (zone: byte 1 of the
+// row word, label2: byte 2) lies in [lo, lo + span] (In: value, span 0;
+// Exists: 1..254) and adds weight (0: unused slot, or value 0 = "unlabelled",
+// which never matches).
+#ifndef MS_NAM_PACKED  // terms two per register in 16-bit halves (v_perm + v_pk_*_u16; 0: one at a time, A/B)
+#define MS_NAM_PACKED 1
+#endif
+#if MS_NAM_PACKED
+typedef unsigned short nam_u16x2 __attribute__((ext_vector_type(2)));
+// Terms (0, 1) and (2, 3) in the halves of one register each: sel picks the
+// terms' label bytes out of the row word into the low byte of each half
+// (v_perm_b32, 0x0C = a zero byte), lo / span + 1 / weight per half.
+struct NamTerms {
+    uint32_t sel[2];
+    nam_u16x2 lo[2], sp1[2], w[2];
+};
+#else
 struct NamTerms {
     uint32_t sh[MS_NAM_TERMS], lo[MS_NAM_TERMS], span[MS_NAM_TERMS], w[MS_NAM_TERMS];
 };
+#endif
 
 __device__ __forceinline__ NamTerms load_terms(const ms_pod_rec &pod, const ms_nam_term_set *sets, uint32_t n_sets) {
     NamTerms m;
@@ -74,16 +89,48 @@ __device__ __forceinline__ NamTerms load_terms(const ms_pod_rec &pod, const ms_n
 #pragma unroll
     for (int k = 0; k < MS_NAM_TERMS; ++k) {
         const ms_pref_term x = st.term[k];
+        const uint32_t lo = x.value == 0xFFu ? 1u : x.value, span = x.value == 0xFFu ? 253u : 0u;
+        const uint32_t w = x.value == 0u ? 0u : x.weight;
+#if MS_NAM_PACKED
+        const int h = k >> 1, half = k & 1;
+        const uint32_t b = x.key ? 2u : 1u;
+        if (half == 0) {
+            m.sel[h] = b | 0x0C0C0C00u;  // (bytes 1-3 zero until term k+1 fills byte 2)
+            m.lo[h].x = (unsigned short)lo;
+            m.sp1[h].x = (unsigned short)(span + 1u);
+            m.w[h].x = (unsigned short)w;
+        } else {
+            m.sel[h] = (m.sel[h] & 0xFF00FFFFu) | b << 16;
+            m.lo[h].y = (unsigned short)lo;
+            m.sp1[h].y = (unsigned short)(span + 1u);
+            m.w[h].y = (unsigned short)w;
+        }
+#else
         m.sh[k] = x.key ? 16u : 8u;
-        m.lo[k] = x.value == 0xFFu ? 1u : x.value;
-        m.span[k] = x.value == 0xFFu ? 253u : 0u;
-        m.w[k] = x.value == 0u ? 0u : x.weight;  // (value 0 = "unlabelled" never matches)
+        m.lo[k] = lo;
+        m.span[k] = span;
+        m.w[k] = w;
+#endif
     }
     return m;
 }
 
 // NodeAffinity.Score: the sum of the weights of the matching terms.
 __device__ __forceinline__ uint32_t nam_raw(uint32_t w, const NamTerms &m) {
+#if MS_NAM_PACKED
+    // per half: d = label - lo (wrapping: a label below lo lands above 65280),
+    // s = sat(span + 1 - d) > 0 exactly when lo <= label <= lo + span, and
+    // min(s * weight, weight) (s * weight <= 254 * 255 < 2^16) the term's share
+    nam_u16x2 t = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t lab = __builtin_amdgcn_perm(0u, w, m.sel[h]);
+        const nam_u16x2 d = __builtin_bit_cast(nam_u16x2, lab) - m.lo[h];
+        const nam_u16x2 s = __builtin_elementwise_sub_sat(m.sp1[h], d);
+        t += __builtin_elementwise_min(s * m.w[h], m.w[h]);
+    }
+    return (uint32_t)t.x + (uint32_t)t.y;
+#else
     uint32_t r = 0;
 #pragma unroll
     for (int k = 0; k < MS_NAM_TERMS; ++k) {
@@ -91,6 +138,7 @@ __device__ __forceinline__ uint32_t nam_raw(uint32_t w, const NamTerms &m) {
         r += (lab - m.lo[k] <= m.span[k]) ? m.w[k] : 0u;
     }
     return r;
+#endif
 }
 
 __device__ __forceinline__ bool nam_feasible(uint32_t w, uint32_t tol) { return (w & (tol ? 1u : 3u)) == 0u; }
