@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n
                                                          const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
                                                          const ms_nam_term_set *__restrict__ sets, uint32_t n_sets,
                                                          NamSeg *__restrict__ out) {
-    __shared__ uint32_t tile[kNamTile];
+    __shared__ __attribute__((aligned(16))) uint32_t tile[kNamTile];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
     const uint32_t p = blockIdx.x * kNamThreads + tid;
@@ -198,22 +198,38 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n
         // when all its lanes are, a wave skips the tile's rows)
         const bool done = p >= n_pods || (top == 0u && any);
         if (__syncthreads_and(done)) break;
-        for (uint32_t i = tid; i < nt; i += kNamThreads) tile[i] = nam_row_word(t, base + i);
+        // (rows past nt up to a multiple of 4: absent, never feasible)
+        const uint32_t nt4 = (nt + 3u) & ~3u;
+        for (uint32_t i = tid; i < nt4; i += kNamThreads) tile[i] = i < nt ? nam_row_word(t, base + i) : 1u;
         __syncthreads();
         if (__ballot(!done) == 0) continue;  // (wave-uniform)
-        for (uint32_t i = 0; i < nt; ++i) {
-            const uint32_t w = tile[i];  // (LDS broadcast)
-            const bool f = nam_feasible(w, tol);
-            const uint32_t r = nam_raw(w, m);
-            any |= (f && r > 0u) ? 1u : 0u;
-            uint64_t b = __ballot(f && r > 100u && top != 0u);
-            while (b) {  // (wave-uniform) the lanes with a rescale here, one table at a time
-                const uint32_t L = (uint32_t)__builtin_ctzll(b);
-                b &= b - 1u;
-                const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
-                table_post(tabs + (wbase + L) * kNamStride, rl, lane);
-                __builtin_amdgcn_wave_barrier();
-                if (lane == L) top = mine[100];
+        // four rows per step (one 16-B LDS broadcast): when no lane rescales at any
+        // of them (one ballot), their only effect is `any`; else they go one by one
+        for (uint32_t i = 0; i < nt4; i += 4) {
+            const uint4 w4 = *reinterpret_cast<const uint4 *>(tile + i);
+            const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+            uint32_t rv[4];
+            bool fv[4], resc = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                fv[k] = nam_feasible(wv[k], tol);
+                rv[k] = nam_raw(wv[k], m);
+                any |= (fv[k] && rv[k] > 0u) ? 1u : 0u;
+                resc = resc || (fv[k] && rv[k] > 100u);
+            }
+            if (__ballot(resc && top != 0u) == 0) continue;  // (wave-uniform)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t r = rv[k];
+                uint64_t b = __ballot(fv[k] && r > 100u && top != 0u);
+                while (b) {  // (wave-uniform) the lanes with a rescale here, one table at a time
+                    const uint32_t L = (uint32_t)__builtin_ctzll(b);
+                    b &= b - 1u;
+                    const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
+                    table_post(tabs + (wbase + L) * kNamStride, rl, lane);
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == L) top = mine[100];
+                }
             }
         }
     }
