@@ -286,7 +286,7 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
                                                           const NamSeg *__restrict__ after,
                                                           const uint8_t *__restrict__ m_in, u64 *__restrict__ keys,
                                                           const uint32_t *__restrict__ perm) {
-    __shared__ uint32_t tile[kNamTile];
+    __shared__ __attribute__((aligned(16))) uint32_t tile[kNamTile];
     __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
     const uint32_t pi = blockIdx.x * kNamThreads + tid;
@@ -327,37 +327,60 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
     uint32_t cand_sreg = 0, cand_sanc = 0, cand_ord = 0;
     bool cand = false;
     const uint32_t n_tiles = r1 > r0 ? (r1 - r0 + kNamTile - 1u) / kNamTile : 0u;
+    // one row's candidate update (before its own rescale, which applies to earlier rows)
+    auto row_key = [&](uint32_t w, bool f, uint32_t r, uint32_t ord) {
+        if (f) {
+            const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
+            const uint32_t bs = (uint32_t)(best >> 52);
+            if (r == 0u) {
+                if (sn >= bs) best = umax64(best, make_key(sn, tb_hash(A, ord), ord));  // (T(0) = 0)
+            } else {
+                // a later non-zero node is not the anchor: its regular key counts
+                if (cand && cand_sreg >= bs) best = umax64(best, make_key(cand_sreg, tb_hash(A, cand_ord), cand_ord));
+                cand = true;
+                cand_sreg = sn + w_na * mine[min(r, 100u)];
+                cand_sanc = sn + w_na * top;
+                cand_ord = ord;
+            }
+        }
+    };
     for (uint32_t ti = n_tiles; ti-- > 0;) {  // tiles and rows in reverse LIST order
         const uint32_t base = r0 + ti * kNamTile, nt = min(kNamTile, r1 - base);
+        const uint32_t nt4 = (nt + 3u) & ~3u;  // (rows past nt: absent, never feasible)
         __syncthreads();
-        for (uint32_t i = tid; i < nt; i += kNamThreads) tile[i] = nam_row_word(t, base + i);
+        for (uint32_t i = tid; i < nt4; i += kNamThreads) tile[i] = i < nt ? nam_row_word(t, base + i) : 1u;
         __syncthreads();
-        for (uint32_t i = nt; i-- > 0;) {
-            const uint32_t w = tile[i];
-            const bool f = nam_feasible(w, tol);
-            const uint32_t r = nam_raw(w, m);
-            if (f) {
-                const uint32_t ord = t.base + base + i;
-                const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
-                const uint32_t bs = (uint32_t)(best >> 52);
-                if (r == 0u) {
-                    if (sn >= bs) best = umax64(best, make_key(sn, tb_hash(A, ord), ord));  // (T(0) = 0)
-                } else {
-                    // a later non-zero node is not the anchor: its regular key counts
-                    if (cand && cand_sreg >= bs) best = umax64(best, make_key(cand_sreg, tb_hash(A, cand_ord), cand_ord));
-                    cand = true;
-                    cand_sreg = sn + w_na * mine[min(r, 100u)];
-                    cand_sanc = sn + w_na * top;
-                    cand_ord = ord;
-                }
+        // four rows per step (one 16-B LDS broadcast, one ballot): while no lane
+        // rescales at any of them the table is fixed across the four
+        for (uint32_t i4 = nt4; i4 > 0; i4 -= 4) {
+            const uint4 w4 = *reinterpret_cast<const uint4 *>(tile + i4 - 4);
+            const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+            uint32_t rv[4];
+            bool fv[4], resc = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                fv[k] = nam_feasible(wv[k], tol);
+                rv[k] = nam_raw(wv[k], m);
+                resc = resc || (fv[k] && rv[k] > 100u);
             }
-            uint64_t b = __ballot(f && r > 100u && top != 0u);
-            while (b) {  // (wave-uniform) this row's rescale applies to the earlier rows
-                const uint32_t L = (uint32_t)__builtin_ctzll(b);
-                b &= b - 1u;
-                const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
-                table_pre(tabs + (wbase + L) * kNamStride, rl, lane);
-                if (lane == L) top = mine[100];
+            const uint32_t ord0 = t.base + base + i4 - 4;
+            if (__ballot(resc && top != 0u) == 0) {  // (wave-uniform)
+#pragma unroll
+                for (int k = 3; k >= 0; --k) row_key(wv[k], fv[k], rv[k], ord0 + k);
+                continue;
+            }
+#pragma unroll
+            for (int k = 3; k >= 0; --k) {
+                row_key(wv[k], fv[k], rv[k], ord0 + k);
+                const uint32_t r = rv[k];
+                uint64_t b = __ballot(fv[k] && r > 100u && top != 0u);
+                while (b) {  // (wave-uniform) this row's rescale applies to the earlier rows
+                    const uint32_t L = (uint32_t)__builtin_ctzll(b);
+                    b &= b - 1u;
+                    const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
+                    table_pre(tabs + (wbase + L) * kNamStride, rl, lane);
+                    if (lane == L) top = mine[100];
+                }
             }
         }
     }
