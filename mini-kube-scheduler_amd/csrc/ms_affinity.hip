@@ -328,21 +328,23 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
     bool cand = false;
     const uint32_t n_tiles = r1 > r0 ? (r1 - r0 + kNamTile - 1u) / kNamTile : 0u;
     // one row's candidate update (before its own rescale, which applies to earlier rows)
+    // Branch-light: at most one key is hashed per row (the row's own with a
+    // zero raw score, T(0) = 0, or -- a later non-zero node is not the anchor --
+    // the previous candidate's regular key), the candidate update is selects.
     auto row_key = [&](uint32_t w, bool f, uint32_t r, uint32_t ord) {
-        if (f) {
-            const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
-            const uint32_t bs = (uint32_t)(best >> 52);
-            if (r == 0u) {
-                if (sn >= bs) best = umax64(best, make_key(sn, tb_hash(A, ord), ord));  // (T(0) = 0)
-            } else {
-                // a later non-zero node is not the anchor: its regular key counts
-                if (cand && cand_sreg >= bs) best = umax64(best, make_key(cand_sreg, tb_hash(A, cand_ord), cand_ord));
-                cand = true;
-                cand_sreg = sn + w_na * mine[min(r, 100u)];
-                cand_sanc = sn + w_na * top;
-                cand_ord = ord;
-            }
+        const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
+        const uint32_t bs = (uint32_t)(best >> 52);
+        const bool nz = f && r != 0u;
+        const bool h0 = f && r == 0u && sn >= bs, h1 = nz && cand && cand_sreg >= bs;
+        if (h0 || h1) {
+            const uint32_t o = h0 ? ord : cand_ord, sc = h0 ? sn : cand_sreg;
+            best = umax64(best, make_key(sc, tb_hash(A, o), o));
         }
+        const uint32_t mv = mine[min(r, 100u)];
+        cand = cand || nz;
+        cand_sreg = nz ? sn + w_na * mv : cand_sreg;
+        cand_sanc = nz ? sn + w_na * top : cand_sanc;
+        cand_ord = nz ? ord : cand_ord;
     };
     for (uint32_t ti = n_tiles; ti-- > 0;) {  // tiles and rows in reverse LIST order
         const uint32_t base = r0 + ti * kNamTile, nt = min(kNamTile, r1 - base);
