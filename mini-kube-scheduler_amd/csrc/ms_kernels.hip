@@ -641,7 +641,7 @@ __device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_
 // per (pod, tile) on top of its evaluations.
 constexpr uint32_t kTpPods = 16;
 #ifndef MS_TP_UNROLL
-#define MS_TP_UNROLL 1  // row blocks unrolled in sweep_tp_task (A/B: 1 / 2 / 4 / 8 = 44.4 / 45.2 / 44.9 / 44.9 ms at config E, profiles/r04s_e_unroll.txt)
+#define MS_TP_UNROLL 2  // row blocks unrolled in sweep_tp_task (round 5, binary64 keys + ld_drow: 2 vs 1 = 33.87 vs 34.16 ms at config E, profiles/r05ay_e_unroll_ab.txt; round 4 form: 1 / 2 / 4 / 8 = 44.4 / 45.2 / 44.9 / 44.9 ms, r04s_e_unroll.txt)
 #endif
 #define MS_PRAGMA(x) _Pragma(#x)
 #define MS_UNROLL(n) MS_PRAGMA(unroll n)
