@@ -95,7 +95,7 @@ def parse():
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
     ap.add_argument("--profile-shard-prefix", default=os.path.join(ROOT, "profiles", "r04zh_pmc_shard"),
                     help="N > 1: per-shard K1 counters <prefix><rows>.json (tools/profile_shards.sh)")
-    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r05ap_pmc_E.json"),
+    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r05bc_pmc_E.json"),
                     help="rocprofv3 counter summary of config E's step kernel (tools/profile_e.sh)")
     return ap.parse_args()
 
