@@ -159,6 +159,15 @@ ms_pod_rec EncodePod(const v1::Pod &pod, uint32_t ordinal) {
     return r;
 }
 
+std::string UnsupportedRequest(const v1::Pod &pod) {
+    for (const auto &c : pod.containers)
+        if (!c.requests.other.empty()) return c.requests.other.begin()->first;
+    for (const auto &c : pod.init_containers)
+        if (!c.requests.other.empty()) return c.requests.other.begin()->first;
+    if (pod.overhead && !pod.overhead->other.empty()) return pod.overhead->other.begin()->first;
+    return "";
+}
+
 ms_node_rec EncodeNode(const v1::Node &node, const NodeUsage &u) {
     ms_node_rec r{};
     const int d = NameDigit(node.name);
@@ -398,7 +407,13 @@ ScheduleResult Scheduler::Finish(const v1::Pod &pod, const ms_pod_rec &rec, cons
 std::vector<ScheduleResult> Scheduler::ScheduleBatch(size_t k) {
     std::vector<v1::Pod> pods;
     std::vector<ms_pod_rec> recs;
-    while (pods.size() < k) {
+    std::vector<ScheduleResult> out;
+    // pods NodeResourcesFit would check on a resource the records cannot carry:
+    // a plain Error (ErrorFunc, empty plugin set), in queue order among the
+    // device results; they bind nothing, so the other pods' sequential outcomes
+    // are those of the queue without them
+    std::vector<std::pair<size_t, ScheduleResult>> refused;
+    while (pods.size() + refused.size() < k) {
         auto p = queue_->NextPod();
         if (!p) break;
         auto it = pod_ordinal_.find(p->uid.empty() ? SchedulingQueue::KeyFunc(*p) : p->uid);
@@ -409,11 +424,30 @@ std::vector<ScheduleResult> Scheduler::ScheduleBatch(size_t k) {
         } else {
             o = it->second;
         }
+        if (opt_.plugins == PluginSet::NU_NRF_NN_LA) {
+            const std::string bad = UnsupportedRequest(*p);
+            if (!bad.empty()) {
+                ScheduleResult r;
+                r.kind = ScheduleResult::Error;
+                r.pod = p->name;
+                r.error.message = "NodeResourcesFit: request for " + bad +
+                                  " cannot be evaluated on the device (cpu and memory only)";
+                ErrorFunc(*p, r.error);
+                refused.emplace_back(pods.size() + refused.size(), std::move(r));
+                continue;
+            }
+        }
         recs.push_back(EncodePod(*p, o));
         pods.push_back(std::move(*p));
     }
-    std::vector<ScheduleResult> out;
-    if (pods.empty()) return out;
+    auto merge = [&refused](std::vector<ScheduleResult> dev) {  // refused pods back at their queue places
+        std::vector<ScheduleResult> all;
+        size_t j = 0, d = 0;
+        for (size_t i = 0; i < dev.size() + refused.size(); ++i)
+            all.push_back(j < refused.size() && refused[j].first == i ? refused[j++].second : dev[d++]);
+        return all;
+    };
+    if (pods.empty()) return merge({});
     std::vector<ms_result> res(pods.size());
     const int rc = ms_schedule_batch(ctx_, (uint32_t)pods.size(), recs.data(), MS_MODE_SEQUENTIAL, res.data());
     if (rc != MS_OK) {  // device failure: every pod stays re-queueable (a plain error)
@@ -425,10 +459,10 @@ std::vector<ScheduleResult> Scheduler::ScheduleBatch(size_t k) {
             ErrorFunc(p, r.error);
             out.push_back(r);
         }
-        return out;
+        return merge(std::move(out));
     }
     for (size_t i = 0; i < pods.size(); ++i) out.push_back(Finish(pods[i], recs[i], res[i]));
-    return out;
+    return merge(std::move(out));
 }
 
 ScheduleResult Scheduler::ScheduleOne() {

@@ -50,9 +50,15 @@ struct Toleration {
 
 bool TolerationsTolerateTaint(const std::vector<Toleration> &tols, const Taint &t);
 
-// Quantities already normalised: cpu in millicores, memory in bytes.
+// Quantities already normalised: cpu in millicores, memory in bytes. `other`
+// holds every other resource name (ephemeral-storage, hugepages-*, extended
+// resources such as amd.com/gpu): upstream Fit.fitsRequest checks the ones a
+// pod requests, ms_pod_rec cannot carry them, so a pod requesting any is
+// refused under NodeResourcesFit (UnsupportedRequest); on nodes they are ignored
+// (no admitted pod requests them, so Requested stays 0 and no decision reads them).
 struct ResourceList {
     std::optional<int64_t> cpu_milli, memory, pods;
+    std::map<std::string, int64_t> other;
 };
 
 struct Container {
@@ -195,6 +201,10 @@ struct ScheduleResult {
 // Record encoders (what the cgo shim computes per object).
 int NameDigit(const std::string &name);  // strconv.Atoi(name[len-1:]) : 0..9 or -1
 ms_pod_rec EncodePod(const v1::Pod &pod, uint32_t ordinal);
+// The first request name of a container, init container or the overhead that
+// ms_pod_rec cannot carry ("" if none). Under NodeResourcesFit such a pod gets
+// a plain Error from ScheduleOne and never reaches the device.
+std::string UnsupportedRequest(const v1::Pod &pod);
 
 // Node ordinals aligned to the name digit: a node whose name ends in digit d
 // gets an ordinal with ordinal % 10 == d (the lowest free one), so every 30

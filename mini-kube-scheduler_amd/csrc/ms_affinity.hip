@@ -61,7 +61,7 @@ __device__ __forceinline__ uint32_t nam_row_word(const NodeTable &t, uint32_t r)
 
 // A pod's terms: term k matches a row whose label byte (zone: byte 1 of the
 // row word, label2: byte 2) lies in [lo, lo + span] (In: value, span 0;
-// Exists: 1..254) and adds weight (0: unused slot, or value 0 = "unlabelled",
+// Exists: 1..255, every labelled row) and adds weight (0: unused slot, or value 0 = "unlabelled",
 // which never matches).
 #ifndef MS_NAM_PACKED  // terms two per register in 16-bit halves (v_perm + v_pk_*_u16; 0: one at a time, A/B)
 #define MS_NAM_PACKED 1
@@ -89,7 +89,7 @@ __device__ __forceinline__ NamTerms load_terms(const ms_pod_rec &pod, const ms_n
 #pragma unroll
     for (int k = 0; k < MS_NAM_TERMS; ++k) {
         const ms_pref_term x = st.term[k];
-        const uint32_t lo = x.value == 0xFFu ? 1u : x.value, span = x.value == 0xFFu ? 253u : 0u;
+        const uint32_t lo = x.value == 0xFFu ? 1u : x.value, span = x.value == 0xFFu ? 254u : 0u;
         const uint32_t w = x.value == 0u ? 0u : x.weight;
 #if MS_NAM_PACKED
         const int h = k >> 1, half = k & 1;
@@ -120,7 +120,7 @@ __device__ __forceinline__ uint32_t nam_raw(uint32_t w, const NamTerms &m) {
 #if MS_NAM_PACKED
     // per half: d = label - lo (wrapping: a label below lo lands above 65280),
     // s = sat(span + 1 - d) > 0 exactly when lo <= label <= lo + span, and
-    // min(s * weight, weight) (s * weight <= 254 * 255 < 2^16) the term's share
+    // min(s * weight, weight) (s * weight <= 255 * 100 < 2^16) the term's share
     nam_u16x2 t = {0, 0};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {

@@ -578,6 +578,8 @@ int tt_summaries_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, vo
 int ensure_nam(ms_ctx *c, uint32_t n) {
     const size_t need = ((size_t)nam_segments(c->rows_dev) + 1u) * n * MS_NAM_SEG_BYTES + n;
     if (need <= c->nam_bytes) return MS_OK;
+    // (growing: a NodeAffinity call on a caller stream may still read the tables; as ensure_tt)
+    if (c->d_nam) MS_HIP(c, hipDeviceSynchronize());
     if (c->d_nam) (void)hipFree(c->d_nam);
     c->d_nam = nullptr;
     c->nam_bytes = 0;
@@ -1044,6 +1046,9 @@ int ms_destroy(ms_ctx *c) {
     {
         const char *tlf = getenv("MS_TIMELINE");
         if (tlf && c->d_tl) {
+            // (the last step kernels may still be writing the timeline)
+            if (c->stream) (void)hipStreamSynchronize(c->stream);
+            if (c->seq_stream) (void)hipStreamSynchronize(c->seq_stream);
             std::vector<unsigned long long> tl((size_t)kTimelineSteps * kTimelineWgs * 8);
             if (hipMemcpy(tl.data(), c->d_tl, tl.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
                 if (FILE *f = std::fopen(tlf, "wb")) {
@@ -1537,7 +1542,7 @@ int ms_tt_decode_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, 
 
 // The two-pass TaintToleration cycle over node shards (ms_taint.hip launch_tt2_*):
 // chunks of batch_cap pods; each call rebuilds the row planes on its stream.
-static int tt2_shard_prologue(ms_ctx *c, uint32_t n_pods, const char *who, hipStream_t &s) {
+static int tt2_shard_prologue(ms_ctx *c, uint32_t n_pods, const char *who, hipStream_t &s, bool planes = true) {
     if (c->cfg.plugin_set != MS_PLUGINS_NU_TT_NN)
         return fail(c, MS_E_INVAL, std::string(who) + ": the TaintToleration plugin set only");
     MS_HIP(c, hipSetDevice(c->cfg.device));
@@ -1549,7 +1554,7 @@ static int tt2_shard_prologue(ms_ctx *c, uint32_t n_pods, const char *who, hipSt
     if (rc) return rc;
     if (!c->ev_tt) MS_HIP(c, hipEventCreateWithFlags(&c->ev_tt, hipEventDisableTiming));
     if (c->tt_stream && c->tt_stream != s) MS_HIP(c, hipStreamWaitEvent(s, c->ev_tt, 0));
-    MS_HIP(c, launch_tt2_planes(c->t, c->rows_dev, c->d_tt, s));
+    if (planes) MS_HIP(c, launch_tt2_planes(c->t, c->rows_dev, c->d_tt, s));
     return MS_OK;
 }
 
@@ -1604,7 +1609,7 @@ int ms_tt_final_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, u
     if (n_pods == 0) return c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN ? MS_OK : MS_E_INVAL;
     std::lock_guard<std::mutex> g(c->sched_mu);
     hipStream_t s = pick_stream(c, stream);
-    int rc = tt2_shard_prologue(c, n_pods, "ms_tt_final_device", s);
+    int rc = tt2_shard_prologue(c, n_pods, "ms_tt_final_device", s, false);  // (the final pass reads no planes)
     if (rc) return rc;
     const uint32_t B = c->batch_cap, cap = std::min(B, n_pods), seed32 = seed32_of(c->cfg.seed);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
@@ -1625,6 +1630,8 @@ int ms_nam_term_sets(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set *sets) {
             const ms_pref_term &x = sets[i].term[k];
             if (x.key > 1 || x.weight > 100)
                 return fail(c, MS_E_INVAL, "ms_nam_term_sets: term key must be 0 or 1 and weight 0..100");
+            // (value 0xFF is Exists; an In term names a value id 1..254, so a node label id
+            // of 255 matches Exists only: ZoneIds hands out at most 254 ids)
         }
     std::lock_guard<std::mutex> g(c->sched_mu);
     MS_HIP(c, hipSetDevice(c->cfg.device));

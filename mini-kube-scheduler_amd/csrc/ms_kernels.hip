@@ -2372,6 +2372,8 @@ __device__ __forceinline__ bool step_merge_fallback(const SeqArgs &va, const Ste
 template <int J, int W>
 __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks, MergeArgs mg,
                                                      uint32_t merge_wgs, StepMerge sm) {
+    // (the untagged-pod check below reads one tag per thread)
+    static_assert(kSeqBatch <= 64 * W, "k_seq_step: one in-step merge tag per thread of the validating workgroup");
     __shared__ SeqShared S;
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)  // wave durations (s_memrealtime, 100 MHz): u64 stats[8+9] validator, [8+10] sweep waves, [8+11] their count
     const u64 t_begin = __builtin_amdgcn_s_memrealtime();

@@ -117,7 +117,7 @@ def nam_term_sets_array(sets):
         if len(terms) > NAM_TERMS:
             raise ValueError(f"at most {NAM_TERMS} preferred terms per set")
         for k, (key, value, weight) in enumerate(terms):
-            if key not in (0, 1) or not 1 <= value <= 255 or value == 0 or not 0 <= weight <= 100:
+            if key not in (0, 1) or not 1 <= value <= 255 or not 0 <= weight <= 100:
                 raise ValueError("term: key 0/1, value 1..254 or 0xFF, weight 0..100")
             out[i, 4 * k:4 * k + 3] = (key, value, weight)
     return out

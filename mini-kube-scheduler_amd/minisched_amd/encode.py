@@ -18,6 +18,18 @@ Only the fields the in-scope plugins read cross the boundary:
                   cluster), and per pod the ids some toleration tolerates
                   (Toleration.ToleratesTaint, restated below).
 Quantities are already integers here: cpu in millicores, memory in bytes.
+
+Resources the device cannot evaluate are refused, never dropped (VERDICT r5
+item 3). Upstream Fit.fitsRequest (k8s@v1.22.0 noderesources/fit.go) also
+compares ephemeral-storage and every scalar (extended, hugepages-*) resource a
+pod requests against Allocatable - Requested; ms_pod_rec carries cpu and memory
+only. So pod_requests raises UnsupportedResource for any other request name in
+a container, an init container or the overhead (an explicit 0 too: it makes
+upstream's "all requests are 0" early return false). Node allocatable entries
+for other names are accepted and ignored: with no admitted pod requesting them,
+Requested stays 0 <= Allocatable and fitsRequest never reads them (it loops over
+the POD's scalar names), so no decision depends on them. Plugin sets without
+NodeResourcesFit read no resources at all (pod_records(check_resources=False)).
 """
 from __future__ import annotations
 
@@ -36,6 +48,12 @@ TAINT_EFFECT_PREFER_NO_SCHEDULE = "PreferNoSchedule"
 TAINT_IDS_PER_KIND = 8  # ms_node_rec.taints: bits 0-7 hard, 8-15 PreferNoSchedule
 DEFAULT_MILLI_CPU_REQUEST = 100
 DEFAULT_MEMORY_REQUEST = 200 * 1024 * 1024
+DEVICE_RESOURCES = ("cpu", "memory")  # the request names ms_pod_rec carries
+
+
+class UnsupportedResource(ValueError):
+    """A pod requests a resource NodeResourcesFit would check but the device
+    records cannot carry (ephemeral-storage, hugepages-*, extended resources)."""
 
 
 def name_digit(name: str) -> int:
@@ -82,7 +100,8 @@ def tolerates_unschedulable(tolerations: List[Toleration]) -> bool:
 
 @dataclass
 class Container:
-    requests: Dict[str, int] = field(default_factory=dict)  # "cpu" (milli), "memory" (bytes)
+    # "cpu" (milli), "memory" (bytes); any other name is refused by pod_requests
+    requests: Dict[str, int] = field(default_factory=dict)
 
 
 @dataclass
@@ -101,7 +120,8 @@ class Pod:
 class Node:
     name: str
     unschedulable: bool = False
-    allocatable: Dict[str, int] = field(default_factory=dict)  # cpu (milli), memory (bytes), pods
+    # cpu (milli), memory (bytes), pods; other names (ephemeral-storage, ...) are ignored
+    allocatable: Dict[str, int] = field(default_factory=dict)
     labels: Dict[str, str] = field(default_factory=dict)
     taints: List[Taint] = field(default_factory=list)
 
@@ -176,7 +196,12 @@ class TaintIds:
 
 
 class ZoneIds:
-    """Label value -> id 1..255, shared by node and pod encoding (the shim's map)."""
+    """Label value -> id 1..254, shared by node and pod encoding (the shim's map).
+    Id 0xFF is not handed out: in a multi-term NodeAffinity set (ms_pref_term)
+    value 0xFF means Exists, so a label value with that id could not be named
+    by an In term."""
+
+    MAX_IDS = 254
 
     def __init__(self):
         self.ids: Dict[str, int] = {}
@@ -185,20 +210,39 @@ class ZoneIds:
         if value is None:
             return 0
         if value not in self.ids:
-            if len(self.ids) >= 255:
-                raise ValueError("more than 255 zone label values")
+            if len(self.ids) >= self.MAX_IDS:
+                raise ValueError(f"more than {self.MAX_IDS} label values")
             self.ids[value] = len(self.ids) + 1
         return self.ids[value]
 
 
-def pod_requests(p: Pod):
+def unsupported_request(p: Pod) -> Optional[str]:
+    """The first request name of p outside DEVICE_RESOURCES (containers, init
+    containers, overhead), or None."""
+    lists = [c.requests for c in p.containers] + [c.requests for c in p.init_containers]
+    if p.overhead:
+        lists.append(p.overhead)
+    for r in lists:
+        for name in r:
+            if name not in DEVICE_RESOURCES:
+                return name
+    return None
+
+
+def pod_requests(p: Pod, check_resources: bool = True):
     """(req_cpu, req_mem, nz_cpu, nz_mem).
 
     req: Fit.computePodResourceRequest — sum of containers, max with each init
     container, plus overhead. nz: NodeInfo.calculateResource's non-zero pair —
     per container GetNonzeroRequests (missing cpu -> 100 m, missing memory ->
     200 MiB, explicit 0 stays 0), max with init containers, plus overhead.
+    Raises UnsupportedResource for a request the device cannot evaluate
+    (module docstring) unless check_resources is False.
     """
+    bad = unsupported_request(p) if check_resources else None
+    if bad is not None:
+        raise UnsupportedResource(f"pod {p.name} requests {bad!r}: NodeResourcesFit would check it, but the device "
+                                  f"records carry {' and '.join(DEVICE_RESOURCES)} only")
     rc = sum(c.requests.get("cpu", 0) for c in p.containers)
     rm = sum(c.requests.get("memory", 0) for c in p.containers)
     nc = sum(c.requests.get("cpu", DEFAULT_MILLI_CPU_REQUEST) for c in p.containers)
@@ -217,9 +261,11 @@ def pod_requests(p: Pod):
 
 
 def pod_records(pods: List[Pod], zone_ids: Optional[ZoneIds] = None,
-                taint_ids: Optional[TaintIds] = None) -> np.ndarray:
+                taint_ids: Optional[TaintIds] = None, check_resources: bool = True) -> np.ndarray:
     """taint_ids (MS_PLUGINS_NU_TT_NN): pref_zone / pref_weight carry the pod's
-    tol_hard / tol_soft masks instead of a NodeAffinity term."""
+    tol_hard / tol_soft masks instead of a NodeAffinity term. check_resources:
+    refuse requests the device cannot evaluate (pod_requests); a plugin set
+    without NodeResourcesFit reads no resources and may pass False."""
     rec = np.zeros(len(pods), dtype=POD_REC)
     for i, p in enumerate(pods):
         if taint_ids is not None:
@@ -232,7 +278,7 @@ def pod_records(pods: List[Pod], zone_ids: Optional[ZoneIds] = None,
                 raise ValueError("PreferredSchedulingTerm weight must be in 1..100 (API validation)")
             rec[i]["pref_zone"] = (zone_ids or ZoneIds())(zone)
             rec[i]["pref_weight"] = weight
-        rc, rm, nc, nm = pod_requests(p)
+        rc, rm, nc, nm = pod_requests(p, check_resources)
         rec[i]["ordinal"] = p.ordinal
         rec[i]["name_digit"] = name_digit(p.name)
         rec[i]["tolerates_unschedulable"] = 1 if tolerates_unschedulable(p.tolerations) else 0

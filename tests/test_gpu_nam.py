@@ -152,3 +152,19 @@ def test_nam_node_shards(oracle, cuts):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("key", [0, 1])
+def test_nam_label_id_255_matches_exists(oracle, key):
+    # a node label id of 255 is a labelled node, so an Exists term (value 0xFF)
+    # must match it as the oracle's nam_raw does; In terms name ids 1..254 (0xFF is Exists)
+    nr, pr, _ = _cluster(600, 300, 4, 7)
+    field = "zone" if key == 0 else "label2"
+    nr[field][::3] = 255
+    nr[field][1::7] = 254
+    nr[field][2::11] = 0  # unlabelled: never matches
+    ts = _lib.nam_term_sets_array([[(key, 0xFF, 40)], [(key, 254, 90), (key, 0xFF, 15)],
+                                   [(1 - key, 0xFF, 60), (key, 0xFF, 70), (key, 1, 5)], [(key, 254, 100)]])
+    o = _oracle(oracle, nr, pr, ts, 7)
+    with _engine(nr, ts, 7) as e:
+        _same(_device_cycle(e, pr), o, f"label id 255 on key {key}")

@@ -83,11 +83,17 @@ def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes
     for i in order:
         lines.append(f"N {node_names[i]} {int(nr['unschedulable'][i])} {int(nr['alloc_milli_cpu'][i])} "
                      f"{int(nr['alloc_memory'][i])} {int(nr['allowed_pods'][i])}")
+    # some pods also request a resource the records cannot carry (a GPU-only
+    # pod among them); under NodeResourcesFit their cycle is a plain Error and they bind nothing
+    extra = {j: ("amd.com/gpu=1" if j % 2 else "ephemeral-storage=1073741824") for j in range(5, n_pods, 41)}
+    for j in extra:
+        if j % 4 == 1:
+            pr["req_milli_cpu"][j] = pr["req_memory"][j] = 0  # only the extended resource
     for j in range(n_pods):
         none = pr["req_milli_cpu"][j] == 0 and pr["req_memory"][j] == 0
         cpu = -1 if none else int(pr["req_milli_cpu"][j])
         mem = -1 if none else int(pr["req_memory"][j])
-        lines.append(f"P {names[j]} {cpu} {mem} {int(pr['tolerates_unschedulable'][j])}")
+        lines.append(f"P {names[j]} {cpu} {mem} {int(pr['tolerates_unschedulable'][j])} {extra.get(j, '-')}")
     cluster = tmp_path / "cluster.txt"
     cluster.write_text("\n".join(lines) + "\n")
     out = tmp_path / "out.txt"
@@ -104,7 +110,14 @@ def test_host_mirror_replay_matches_oracle(oracle, tmp_path, plugin_set, n_nodes
     nr["name_digit"] = [max(encode.name_digit(n), -1) & 0xFF for n in node_names]
     table = np.zeros(n_nodes, dtype=nr.dtype)  # the oracle's records at the allocated ordinals
     table[ords] = nr
-    o = oracle.schedule(table, pr, plugin_set=plugin_set, mode=1, seed=seed)
+    # NU+NN reads no resources: every pod is scheduled; NodeResourcesFit refuses the extra ones
+    # (Error, no node, no mask) and the others equal the oracle's queue without them (same ordinals)
+    keep = np.ones(n_pods, dtype=bool)
+    if plugin_set == 1:
+        keep[list(extra)] = False
+        assert (code[~keep] == 1).all() and (node[~keep] == -1).all() and (mask[~keep] == 0).all()
+    o = oracle.schedule(table, pr[keep], plugin_set=plugin_set, mode=1, seed=seed)
+    code, node, score, mask = code[keep], node[keep], score[keep], mask[keep]
     assert np.array_equal(code, o["code"])
     assert np.array_equal(node, o["node"])
     assert np.array_equal(score, o["score"])

@@ -142,6 +142,35 @@ def test_fit_and_least_allocated_kat(oracle):
     assert encode.pod_requests(ic)[0] == 750
 
 
+@pytest.mark.parametrize("where", ["containers", "init_containers", "overhead"])
+@pytest.mark.parametrize("name,qty", [("amd.com/gpu", 1), ("ephemeral-storage", 1 << 30),
+                                      ("hugepages-2Mi", 2 << 20), ("amd.com/gpu", 0)])
+def test_unsupported_requests_are_refused(where, name, qty):
+    # upstream fitsRequest also checks ephemeral-storage and every scalar resource
+    # the pod requests (k8s@v1.22.0 noderesources/fit.go); ms_pod_rec carries cpu and memory only, so
+    # a pod requesting anything else (an explicit 0 included: it defeats the "all requests are 0"
+    # early return) must be refused, never encoded as a request-less pod that passes Fit everywhere
+    GiB = 1 << 30
+    kw = {"containers": [Container({"cpu": 100})]}
+    if where == "overhead":
+        kw["overhead"] = {name: qty}
+    else:
+        kw[where] = kw.get(where, []) + [Container({name: qty})]
+    p = Pod("pod1", 1, **kw)
+    assert encode.unsupported_request(p) == name
+    with pytest.raises(encode.UnsupportedResource, match=name):
+        encode.pod_requests(p)
+    with pytest.raises(encode.UnsupportedResource):
+        encode.pod_records([Pod("pod0", 0), p])
+    # a plugin set without NodeResourcesFit reads no resources: the cpu / memory fields still encode
+    rec = encode.pod_records([p], check_resources=False)[0]
+    assert rec["req_milli_cpu"] == 100
+    # node-side allocatable of other names is accepted and ignored (no admitted pod requests them)
+    nr = encode.node_records([Node("node0", allocatable={"cpu": 4000, "memory": 8 * GiB, "pods": 110,
+                                                         "ephemeral-storage": 100 * GiB, "amd.com/gpu": 8})])
+    assert (nr[0]["alloc_milli_cpu"], nr[0]["alloc_memory"]) == (4000, 8 * GiB)
+
+
 def _random_objects(rng, n_nodes, n_pods, resources):
     GiB = 1 << 30
     nodes = []

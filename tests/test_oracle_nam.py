@@ -132,3 +132,15 @@ def test_term_set_encoder_validates():
         _lib.nam_term_sets_array([[(0, 1, 10)] * 5])
     a = _lib.nam_term_sets_array([[(1, 0xFF, 7), (0, 4, 100)]])
     assert a.shape == (1, 16) and list(a[0, :8]) == [1, 0xFF, 7, 0, 0, 4, 100, 0]
+
+
+def test_zone_ids_stop_at_254():
+    # 0xFF is the Exists marker of a multi-term set, so the shared value-id table never
+    # hands it to a label value (an In term could not name it)
+    from minisched_amd import encode
+
+    z = encode.ZoneIds()
+    ids = [z(f"v{i}") for i in range(254)]
+    assert ids == list(range(1, 255)) and z("v0") == 1 and z(None) == 0
+    with pytest.raises(ValueError):
+        z("one-too-many")
