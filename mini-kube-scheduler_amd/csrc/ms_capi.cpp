@@ -63,11 +63,6 @@ void free_all(ms_ctx *c) {
     if (c->h_deltas) (void)hipHostFree(c->h_deltas);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_back) (void)hipEventDestroy(c->ev_back);
-    for (int i = 0; i < kSeqBufs; ++i) {
-        if (c->ev_valid[i]) (void)hipEventDestroy(c->ev_valid[i]);
-        if (c->ev_swept[i]) (void)hipEventDestroy(c->ev_swept[i]);
-    }
-    if (c->ev_seq) (void)hipEventDestroy(c->ev_seq);
     if (c->ev_tt) (void)hipEventDestroy(c->ev_tt);
     if (c->copy_stream) {
         (void)hipStreamSynchronize(c->copy_stream);
@@ -77,10 +72,6 @@ void free_all(ms_ctx *c) {
     for (int i = 0; i < 4; ++i) {
         if (c->ev_copy[i]) (void)hipEventDestroy(c->ev_copy[i]);
         if (c->ev_cyc[i]) (void)hipEventDestroy(c->ev_cyc[i]);
-    }
-    if (c->seq_stream) {
-        (void)hipStreamSynchronize(c->seq_stream);
-        (void)hipStreamDestroy(c->seq_stream);
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
 }
@@ -179,29 +170,12 @@ int chain_back(ms_ctx *c, hipStream_t s, bool recorded) {
     return MS_OK;
 }
 
-// The in-step merge's counter: MINISCHED_CTR_FINE=1 allocates it fine-grained
-// (atomics and polls at the memory side, coherent across XCDs without L2
-// maintenance; A/B), else plain device memory.
-hipError_t ctr_alloc(uint32_t **p) {
-    static const bool fine = [] {
-        const char *e = getenv("MINISCHED_CTR_FINE");
-        return e && e[0] == '1';
-    }();
-    // (a counter, or one slot per sweep workgroup: at most 255)
-    if (fine) return hipExtMallocWithFlags((void **)p, 1024, hipDeviceMallocFinegrained);
-    return hipMalloc((void **)p, 1024);
-}
+// The in-step merge's counter (a counter, or one slot per sweep workgroup: at most 255).
+hipError_t ctr_alloc(uint32_t **p) { return hipMalloc((void **)p, 1024); }
 
-// Sequential-engine scratch for n_tiles tiles, kSeqBufs batches deep (pipelining).
+// Sequential-engine scratch for n_tiles tiles, kSeqBufs batches deep (the
+// single-stream steps use two sets; the node-sharded candidates up to three).
 int ensure_tiles(ms_ctx *c, uint32_t n_tiles) {
-    if (!c->seq_stream) {
-        MS_HIP(c, hipStreamCreateWithFlags(&c->seq_stream, hipStreamNonBlocking));
-        for (int i = 0; i < kSeqBufs; ++i) {
-            MS_HIP(c, hipEventCreateWithFlags(&c->ev_valid[i], hipEventDisableTiming));
-            MS_HIP(c, hipEventCreateWithFlags(&c->ev_swept[i], hipEventDisableTiming));
-        }
-        MS_HIP(c, hipEventCreateWithFlags(&c->ev_seq, hipEventDisableTiming));
-    }
     if (n_tiles <= c->tile_cap) return MS_OK;
     MS_HIP(c, hipDeviceSynchronize());  // no batch still reads the old buffers
     void *old[] = {c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev,
@@ -278,97 +252,28 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     NodeTable tq = c->t;
     tq.drow = c->d_drow;
     MS_HIP(c, launch_build_drows(tq, rows, n_tiles * kFullWaveTile, s));
-    // Batch k: speculative sweep + top-4 merge on seq_stream into buffer set
-    // k % kSeqBufs, after validation k-D (D = the pipeline depth: every bind up
-    // to batch k-D is in the table the sweep reads; validations k-D+1 .. k-1,
-    // which may be running, read the other buffer sets); validation k on s
-    // after merge k (stream events only: a device-side wait would stall
-    // wherever dispatches are serialised, e.g. under counter profiling; an
-    // event costs ~6 us when already signalled, ~11 us otherwise,
-    // tools/ubench/xstream). Validation k treats the nodes batches k-D+1 .. k-1
-    // bound as stale (their prev lists): its sweep may predate those binds.
-    // D = 3 (default) keeps the sweep of batch k+1 off validation k-1's
-    // critical path: each chain then runs back to back instead of paying a
-    // cross-stream event per batch (profiles/r02j_e_timeline*.json).
+    // Step k = ONE launch (launch_seq_step): validation of batch k on workgroup
+    // 0 while the other workgroups sweep batch k+1 and then merge its tile lists
+    // (the in-step merge); batch k+1 treats batch k's binds as stale. No
+    // cross-stream hand-off: each cost ~12 us per batch, and a validation launched
+    // beside a sweep waited for a SIMD to drain (two-stream modes and a depth-2
+    // step measured slower and removed in round 6: profiles/r02j_e_modes.txt,
+    // r04w_e_fused2_ab.txt).
     const uint32_t B = seq_batch(c), SB = seq_batch_limit();
-    // ranks 4..7 of the merge for the validator's slow pods (MINISCHED_SEQ_EXT=0: top-4 only, A/B)
-    static const bool use_ext = [] {
-        const char *e = getenv("MINISCHED_SEQ_EXT");
-        return !(e && e[0] == '0');
-    }();
-    unsigned long long *const top_ext = use_ext ? c->d_top_ext : nullptr;
+    // ranks 4..7 of the merge for the validator's slow pods (profiles/r03v_e_rank8_ab.txt)
+    unsigned long long *const top_ext = c->d_top_ext;
     const size_t prev_words = 2 + seq_prev_cap(), prev_fields = (size_t)seq_prev_cap() * seq_rec_fields();
     const size_t cells_per_set = (size_t)SB * n_tiles, recs_per_set = (size_t)SB * seq_topk() * seq_rec_fields();
-    const char *pipe_env = getenv("MINISCHED_SEQ_PIPE");
-    if (pipe_env && std::string(pipe_env) == "fused2") {
-        // Single stream, depth 2 (MINISCHED_SEQ_PIPE=fused2, A/B; not the default:
-        // the deeper speculation doubled the recomputes and re-swept 18x the tiles,
-        // 54.9 vs 45.9 ms at config E, 48.2 ms at its best batch of 64,
-        // profiles/r04w_e_fused2_ab.txt). Step k = ONE launch validating batch
-        // k, merging batch k+1 (its tile lists came from step k-1) and sweeping
-        // batch k+2, so no merge launch sits between steps. Batch k's
-        // speculation predates batches k-1 and k-2 (carry: the prev lists hold
-        // both); three tile-list sets (validation k may re-scan its own lists
-        // while sweep k+2 writes), two merge-output sets.
-        auto tiles = [&](uint32_t k, unsigned long long *&tk, uint32_t *&tf) {
-            tk = c->d_tile_keys + cells_per_set * seq_topk() * (k % 3u);
-            tf = c->d_tile_flags + cells_per_set * (k % 3u);
-        };
-        auto out_top = [&](uint32_t k) { return c->d_top4 + (size_t)SB * seq_topk() * (k & 1u); };
-        auto out_ext = [&](uint32_t k) { return top_ext ? top_ext + (size_t)SB * seq_topk() * (k & 1u) : nullptr; };
-        const uint32_t nb0 = std::min(B, n_pods), nb1 = n_pods > B ? std::min(B, n_pods - B) : 0u;
-        unsigned long long *tk = nullptr;
-        uint32_t *tf = nullptr;
-        tiles(0, tk, tf);
-        MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods, nb0, seed32, tk, tf, n_tiles, s));
-        MS_HIP(c, launch_topk_merge(tk, tf, nb0, n_tiles, out_top(0), c->d_spec, c->d_spec_flags, tq, c->d_top4_rec,
-                                    s, out_ext(0)));
-        if (nb1) {
-            tiles(1, tk, tf);
-            MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods + B, nb1, seed32, tk, tf, n_tiles, s));
-        }
-        uint32_t k = 0;
-        for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
-            const uint32_t nb = std::min(B, n_pods - s0), cur = k & 1u, nxt = cur ^ 1u;
-            const uint32_t s1 = s0 + B, n1 = s1 < n_pods ? std::min(B, n_pods - s1) : 0u;
-            const uint32_t s2 = s1 + B, n2 = s2 < n_pods ? std::min(B, n_pods - s2) : 0u;
-            unsigned long long *tk0, *tk1, *tk2;
-            uint32_t *tf0, *tf1, *tf2;
-            tiles(k, tk0, tf0);
-            tiles(k + 1, tk1, tf1);
-            tiles(k + 2, tk2, tf2);
-            SeqMerge mg = {tk1, tf1, n1, out_top(k + 1), c->d_spec + SB * nxt, out_ext(k + 1),
-                           c->d_spec_flags + SB * nxt, c->d_top4_rec + recs_per_set * nxt};
-            MS_HIP(c, launch_seq_step(tq, rows, n_tiles, seed32, d_pods + s0, nb, tk0, tf0, c->d_spec + SB * cur,
-                                      c->d_spec_flags + SB * cur, out_top(k), c->d_top4_rec + recs_per_set * cur,
-                                      k ? c->d_prev + prev_words * nxt : nullptr,
-                                      k ? c->d_prev_rec + prev_fields * nxt : nullptr, c->d_prev + prev_words * cur,
-                                      c->d_prev_rec + prev_fields * cur, d_res + s0, c->d_overflow,
-                                      n2 ? d_pods + s2 : nullptr, n2, tk2, tf2, c->num_cus, s, out_ext(k), &mg, 1));
-        }
-        return MS_OK;
-    }
-    if (!pipe_env || std::string(pipe_env) == "fused") {
-        // Single stream, depth 1 (default): step k = one launch validating batch
-        // k while sweeping batch k+1 (launch_seq_step), then batch k+1's top-4 merge.
-        // No cross-stream hand-off (each cost ~12 us per batch, and a
-        // validation launched beside a sweep waited for a SIMD to drain);
-        // batch k+1 treats batch k's binds as stale.
+    {
         // Warm-up batches: the first 8,192 pods of the queue in batches of 64. On an
         // empty cluster every pod prefers the same emptiest nodes, so early batches
         // touch each other's speculative winners most (the slow-path burst of
         // batches 20-30); half-size batches there cut the re-sweeps to 0 and the
         // recomputes by 10 %: config E 39.7 -> 38.5 ms (profiles/r05l_e_ab.txt;
         // 4096:32 / 8192:32 / 16384:32 / 16384:64 / 32768:64 measured slower,
-        // r05k_e_warm.txt). MINISCHED_SEQ_WARM=<pods>:<batch> overrides (0:0 off).
-        static const std::pair<uint32_t, uint32_t> warm = [] {
-            uint32_t wp = 8192, wb = 64;
-            if (const char *e = getenv("MINISCHED_SEQ_WARM")) (void)std::sscanf(e, "%u:%u", &wp, &wb);
-            return std::make_pair(wp, wb);
-        }();
-        auto batch_at = [&](uint32_t s0) {
-            return (s0 < warm.first && warm.second) ? std::min(warm.second, B) : B;
-        };
+        // r05k_e_warm.txt).
+        constexpr uint32_t kWarmPods = 8192, kWarmBatch = 64;
+        auto batch_at = [&](uint32_t s0) { return s0 < kWarmPods ? std::min(kWarmBatch, B) : B; };
         const uint32_t nb0 = std::min(batch_at(0), n_pods);
         const char *merge_env = getenv("MINISCHED_SEQ_MERGE");
         const std::string merge_mode = merge_env ? merge_env : "instep";
@@ -408,12 +313,13 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
             unsigned long long *tk1 = c->d_tile_keys + cells_per_set * seq_topk() * nxt;
             uint32_t *tf = c->d_tile_flags + cells_per_set * cur, *tf1 = c->d_tile_flags + cells_per_set * nxt;
             SeqMergeIO mio;
-            // timeline of steps 0 .. kTimelineSteps - 1 (MS_TIMELINE=<file>; recorded
-            // by the MS_VSTAMPS / MS_TIMELINE_ONLY diagnostic kernels only)
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
+            // diagnostic builds: timeline of steps 0 .. kTimelineSteps - 1 (MS_TIMELINE=<file>)
             static const bool want_tl = getenv("MS_TIMELINE") != nullptr;
             if (want_tl && !c->d_tl &&
                 hipMalloc((void **)&c->d_tl, (size_t)kTimelineSteps * kTimelineWgs * 8 * 8) == hipSuccess)
                 MS_HIP(c, hipMemsetAsync(c->d_tl, 0, (size_t)kTimelineSteps * kTimelineWgs * 8 * 8, s));
+#endif
             mio.tl = c->d_tl;
             mio.tl_step = k;
             mio.in_tags = c->d_merge_tags + SB * cur;
@@ -427,7 +333,7 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
                 mio.spec = c->d_spec + SB * nxt;
                 mio.spec_flags = c->d_spec_flags + SB * nxt;
                 mio.recs = c->d_top4_rec + recs_per_set * nxt;
-                mio.ext = top_ext ? top_ext + (size_t)SB * seq_topk() * nxt : nullptr;
+                mio.ext = top_ext + (size_t)SB * seq_topk() * nxt;
                 mio.tags = c->d_merge_tags + SB * nxt;
                 mio.tag = c->merge_tag;
                 mio.skip = merge_mode == "fallback" ? 1 : 0;
@@ -439,47 +345,17 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
                                       k ? c->d_prev_rec + prev_fields * nxt : nullptr, c->d_prev + prev_words * cur,
                                       c->d_prev_rec + prev_fields * cur, d_res + s0, c->d_overflow,
                                       nn ? d_pods + s1 : nullptr, nn, tk1, tf1, c->num_cus, s,
-                                      top_ext ? top_ext + (size_t)SB * seq_topk() * cur : nullptr, nullptr, 0, &mio));
+                                      top_ext + (size_t)SB * seq_topk() * cur, &mio));
             target = mio.target;
             in_tag = in_step ? mio.tag : 0u;
             if (nn && !in_step)
                 MS_HIP(c, launch_topk_merge(tk1, tf1, nn, n_tiles, c->d_top4 + (size_t)SB * seq_topk() * nxt,
                                             c->d_spec + SB * nxt, c->d_spec_flags + SB * nxt, c->t,
                                             c->d_top4_rec + recs_per_set * nxt, s,
-                                            top_ext ? top_ext + (size_t)SB * seq_topk() * nxt : nullptr));
+                                            top_ext + (size_t)SB * seq_topk() * nxt));
         }
         return MS_OK;
     }
-    // Two streams (MINISCHED_SEQ_PIPE = 0: no overlap, 1: one stale batch, 2:
-    // two), handing off by stream events (measured slower than the single
-    // stream: profiles/r02j_e_modes.txt)
-    MS_HIP(c, hipEventRecord(c->ev_seq, s));
-    MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_seq, 0));
-    const uint32_t D = 1u + (uint32_t)std::min(2, std::max(0, atoi(pipe_env)));
-    uint32_t k = 0;
-    for (uint32_t s0 = 0; s0 < n_pods; s0 += B, ++k) {
-        const uint32_t nb = std::min(B, n_pods - s0), slot = k % kSeqBufs, par = k & 1u;
-        const size_t cells = cells_per_set * slot;
-        unsigned long long *tk = c->d_tile_keys + cells * seq_topk();
-        uint32_t *tf = c->d_tile_flags + cells;
-        unsigned long long *sp = c->d_spec + SB * slot, *top = c->d_top4 + (size_t)SB * seq_topk() * slot;
-        uint32_t *sf = c->d_spec_flags + SB * slot;
-        int64_t *trec = c->d_top4_rec + recs_per_set * slot;
-        if (k >= D) MS_HIP(c, hipStreamWaitEvent(c->seq_stream, c->ev_valid[(k - D) % kSeqBufs], 0));
-        MS_HIP(c, launch_sweep_full_tiles(tq, rows, d_pods + s0, nb, seed32, tk, tf, n_tiles, c->seq_stream));
-        unsigned long long *ext = top_ext ? top_ext + (size_t)SB * seq_topk() * slot : nullptr;
-        MS_HIP(c, launch_topk_merge(tk, tf, nb, n_tiles, top, sp, sf, c->t, trec, c->seq_stream, ext));
-        MS_HIP(c, hipEventRecord(c->ev_swept[slot], c->seq_stream));
-        MS_HIP(c, hipStreamWaitEvent(s, c->ev_swept[slot], 0));
-        const bool has_prev = D > 1 && k;
-        MS_HIP(c, launch_validate_seq(tq, rows, d_pods + s0, nb, seed32, tk, tf, sp, sf, top, trec, n_tiles,
-                                      has_prev ? c->d_prev + prev_words * (par ^ 1u) : nullptr,
-                                      has_prev ? c->d_prev_rec + prev_fields * (par ^ 1u) : nullptr,
-                                      c->d_prev + prev_words * par, c->d_prev_rec + prev_fields * par, D > 2 ? 1 : 0,
-                                      d_res + s0, c->d_overflow, s, ext));
-        MS_HIP(c, hipEventRecord(c->ev_valid[slot], s));
-    }
-    return MS_OK;
 }
 
 // Plugin sets whose filters and scores read no mutable node state (NU, NN,
@@ -510,14 +386,6 @@ int ensure_stage(ms_ctx *c, uint32_t n) {
     return MS_OK;
 }
 
-bool tt_two_pass() {
-    static const bool v2 = [] {
-        const char *e = getenv("MINISCHED_TT");
-        return !(e && std::string(e) == "v1");
-    }();
-    return v2;
-}
-
 // MS_PLUGINS_NU_TT_NN scratch: `need` bytes (summaries or the two-pass cycle's).
 int ensure_tt(ms_ctx *c, size_t need) {
     if (need <= c->tt_bytes) return MS_OK;
@@ -536,11 +404,11 @@ int ensure_tt(ms_ctx *c, size_t need) {
 // out (this shard's summary), or finalised into results (the single-shard
 // cycle; commit: the winners' NodeInfo.AddPod). Chunks of batch_cap pods.
 // A single-shard cycle (results) runs the two-pass bit-sliced form (round 5,
-// launch_tt2_cycle); MINISCHED_TT=v1: the per-pair summary sweep (A/B), which
-// the shard summaries (out) always use.
+// launch_tt2_cycle); the shard summaries (out, ms_tt_summaries_device) the
+// per-pair summary sweep.
 int tt_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, void *out, ms_result *results, int commit,
                     hipStream_t s) {
-    const bool two_pass = !out && tt_two_pass();
+    const bool two_pass = !out;
     const uint32_t B = c->batch_cap, segs = tt_segments(c->rows_dev), cap = std::min(B, n_pods);
     int rc = ensure_tt(c, two_pass ? tt2_scratch_bytes(c->rows_dev, cap)
                                    : (size_t)segs * cap * MS_TT_SUMMARY_BYTES);
@@ -712,16 +580,9 @@ int select_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resul
 // copies): chunk i+1's H2D (copy stream; the runtime stages pageable memory on
 // the calling thread, which here overlaps chunk i's fused cycle) and chunk i-1's
 // D2H overlap chunk i on the context stream; one cross-stream wait per chunk.
-// MINISCHED_E2E_CHUNKS: 1 turns it off, at most 4.
-constexpr uint32_t kE2eMinChunk = 16384;
+constexpr uint32_t kE2eMinChunk = 16384, kE2eChunks = 2;
 
-uint32_t e2e_chunks(uint32_t n) {
-    static const uint32_t k = [] {
-        const char *e = getenv("MINISCHED_E2E_CHUNKS");
-        return e ? (uint32_t)std::min(4, std::max(1, atoi(e))) : 2u;
-    }();
-    return std::max(1u, std::min(k, n / kE2eMinChunk));
-}
+uint32_t e2e_chunks(uint32_t n) { return std::max(1u, std::min(kE2eChunks, n / kE2eMinChunk)); }
 
 // The per-chunk events of the host-array paths, each created once whichever
 // path (zero-copy or chunked copies) runs first (no leak when a
@@ -824,21 +685,14 @@ int schedule_zc(ms_ctx *c, const PodIn *pods, uint32_t n, ResOut *out, CallClock
     ck.lap(MS_PH_ALLOC);
     MS_HIP(c, hipStreamSynchronize(s));  // (no earlier call still reads h_podz)
     ck.lap(MS_PH_WAIT);
-    static const uint32_t parts_env = [] {
-        const char *e = getenv("MINISCHED_ZC_PARTS");
-        return e ? (uint32_t)std::min(4, std::max(1, atoi(e))) : 0u;
-    }();
-    const uint32_t parts = parts_env ? std::min(parts_env, std::max(1u, n)) : std::max(1u, std::min(4u, n / kZcMinChunk));
+    const uint32_t parts = std::max(1u, std::min(4u, n / kZcMinChunk));
     const uint32_t per = cdiv(n, parts);
     auto beg = [&](uint32_t i) { return std::min(n, i * per); };
-    // Host copies split over the caller and the copy pool's helpers
-    // (MINISCHED_COPY_THREADS helpers, default 3; 0 = the caller alone): the first
-    // chunk's copy-in and the last one's copy-out are on the call's critical path.
-    static const unsigned helpers = [] {
-        const char *e = getenv("MINISCHED_COPY_THREADS");
-        return e ? (unsigned)std::min(15, std::max(0, atoi(e))) : 3u;
-    }();
-    if (helpers && per >= kZcParMin && !c->copy_pool) {
+    // Host copies split over the caller and the copy pool's 3 helpers (7 measured
+    // no better, profiles/r05v_e2e_ab.txt): the first chunk's copy-in and the last
+    // one's copy-out are on the call's critical path.
+    constexpr unsigned helpers = 3;
+    if (per >= kZcParMin && !c->copy_pool) {
         try {  // (no helper threads, e.g. none can be created: the caller copies alone)
             c->copy_pool.reset(new CopyPool(helpers));
         } catch (...) {
@@ -1043,12 +897,12 @@ int ms_destroy(ms_ctx *c) {
         }
     }
 #endif
+#if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
     {
         const char *tlf = getenv("MS_TIMELINE");
         if (tlf && c->d_tl) {
-            // (the last step kernels may still be writing the timeline)
-            if (c->stream) (void)hipStreamSynchronize(c->stream);
-            if (c->seq_stream) (void)hipStreamSynchronize(c->seq_stream);
+            // (the last step kernels, on any stream, may still be writing the timeline)
+            (void)hipDeviceSynchronize();
             std::vector<unsigned long long> tl((size_t)kTimelineSteps * kTimelineWgs * 8);
             if (hipMemcpy(tl.data(), c->d_tl, tl.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
                 if (FILE *f = std::fopen(tlf, "wb")) {
@@ -1060,6 +914,7 @@ int ms_destroy(ms_ctx *c) {
             c->d_tl = nullptr;
         }
     }
+#endif
     if (c->d_tl) (void)hipFree(c->d_tl);
     free_all(c);
     delete c;
@@ -1181,11 +1036,7 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     if (rc) return rc;
     ck.lap(MS_PH_LOCK_FLUSH);
     if (c->comm) return comm_schedule_host(c, n_pods, pods, mode, out, &ck);  // node-sharded over the communicator
-    static const bool zc_e2e = [] {
-        const char *e = getenv("MINISCHED_PAGEABLE_E2E");
-        return !(e && e[0] == '1');
-    }();
-    if (zc_e2e && !c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows)
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows)
         return schedule_zc(c, pods, n_pods, out, ck);  // (NU+NN: both modes are the batched cycle + binds)
     const hipStream_t s = c->stream;
     ++c->ctx_seq;  // binds below write the table on the context stream
@@ -1202,29 +1053,19 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
     // path, 0.56 ms for config C's 4 MB in + 2.4 MB out + cycle, against 0.72 ms
     // through a single-threaded memcpy into the pinned staging buffers;
     // profiles/r02u_e2e_ab.txt). The call waits for its copies before it
-    // returns, so no caller (cgo) pointer outlives it. MINISCHED_PAGEABLE=0
-    // keeps the pinned staging.
-    static const int pageable = [] {
-        const char *e = getenv("MINISCHED_PAGEABLE");
-        return !(e && e[0] == '0');
-    }();
+    // returns, so no caller (cgo) pointer outlives it.
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         MS_HIP(c, hipStreamSynchronize(s));  // h_pods / h_res free to reuse
         ck.lap(MS_PH_WAIT);
         const bool seq_full = (mode == MS_MODE_SEQUENTIAL && c->cfg.plugin_set == MS_PLUGINS_NU_NRF_NN_LA);
-        const uint32_t parts = (pageable && plugins_stateless(c)) ? e2e_chunks(nb) : 1u;
+        const uint32_t parts = plugins_stateless(c) ? e2e_chunks(nb) : 1u;
         if (parts > 1) {  // (NU+NN / NA: binds never change a later pod's keys, so chunks equal one batch)
             rc = schedule_chunked(c, pods + s0, nb, out + s0, parts, ck);
             if (rc) return rc;
             continue;
         }
-        if (pageable) {
-            MS_HIP(c, hipMemcpyAsync(c->d_pods, pods + s0, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
-        } else {
-            std::memcpy(c->h_pods, pods + s0, sizeof(ms_pod_rec) * nb);
-            MS_HIP(c, hipMemcpyAsync(c->d_pods, c->h_pods, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
-        }
+        MS_HIP(c, hipMemcpyAsync(c->d_pods, pods + s0, sizeof(ms_pod_rec) * nb, hipMemcpyHostToDevice, s));
         ck.count(MS_PH_CHUNKS);
         ck.lap(MS_PH_STAGE_IN);
         if (seq_full) {
@@ -1237,18 +1078,10 @@ int ms_schedule_batch(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods, int32_
             if (rc) return rc;
         }
         ck.lap(MS_PH_LAUNCH);
-        if (pageable) {
-            MS_HIP(c, hipMemcpyAsync(out + s0, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
-            ck.lap(MS_PH_STAGE_OUT);
-            MS_HIP(c, hipStreamSynchronize(s));
-            ck.lap(MS_PH_WAIT);
-        } else {
-            MS_HIP(c, hipMemcpyAsync(c->h_res, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
-            MS_HIP(c, hipStreamSynchronize(s));
-            ck.lap(MS_PH_WAIT);
-            std::memcpy(out + s0, c->h_res, sizeof(ms_result) * nb);
-            ck.lap(MS_PH_STAGE_OUT);
-        }
+        MS_HIP(c, hipMemcpyAsync(out + s0, c->d_res, sizeof(ms_result) * nb, hipMemcpyDeviceToHost, s));
+        ck.lap(MS_PH_STAGE_OUT);
+        MS_HIP(c, hipStreamSynchronize(s));
+        ck.lap(MS_PH_WAIT);
     }
     return MS_OK;
 }
@@ -1268,12 +1101,8 @@ int ms_schedule_batch_compact(ms_ctx *c, uint32_t n, const ms_pod_compact *pods,
     // Single-shard NU+NN: one launch reading the pods from and writing the
     // results to pinned host memory (8 B each way per pod over PCIe, no copy
     // commands, no widen / narrow passes); the host copies the caller's arrays
-    // in and out. MINISCHED_COMPACT_ZC=0: the staged path below (A/B).
-    static const bool zc = [] {
-        const char *e = getenv("MINISCHED_COMPACT_ZC");
-        return !(e && e[0] == '0');
-    }();
-    if (zc && !c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows)
+    // in and out (the staged path below: node shards, larger tables).
+    if (!c->comm && c->cfg.plugin_set == MS_PLUGINS_NU_NN && c->rows_dev <= kPpMaxFusedRows)
         return schedule_zc(c, pods, n, out, ck);
     rc = c->comm ? comm_stage(c, n) : ensure_stage(c, n);
     if (rc) return rc;
@@ -1614,7 +1443,9 @@ int ms_tt_final_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, u
     const uint32_t B = c->batch_cap, cap = std::min(B, n_pods), seed32 = seed32_of(c->cfg.seed);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
-        MS_HIP(c, launch_tt2_final_shard(c->t, c->rows_dev, pods_dev + s0, nb, seed32, c->d_tt, cap,
+        // (the scratch's plan records: ADVICE r5, its start holds the row planes)
+        MS_HIP(c, launch_tt2_final_shard(c->t, c->rows_dev, pods_dev + s0, nb, seed32,
+                                         tt2_plans(c->d_tt, c->rows_dev, cap), cap,
                                          static_cast<const char *>(census_all_dev) + (size_t)s0 * MS_TT_CENSUS_BYTES,
                                          n_pods, n_shards, keys_max_dev + s0, results_dev + s0, s));
     }

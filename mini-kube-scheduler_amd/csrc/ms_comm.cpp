@@ -78,10 +78,7 @@ struct ShardSlot {
     unsigned long long *keys = nullptr;       // G x cap: this shard's maxima, pod order
     unsigned long long *keys_mine = nullptr;  // cap: the cluster's maxima of this rank's slice
     uint32_t *flags = nullptr, *flags_mine = nullptr;
-    // MS_PLUGINS_NU_TT_NN: this shard's per-pod summaries (G x cap, pod order) and
-    // the slice's summaries from every shard (G x cap, shard order) after the all-to-all
-    void *summ = nullptr, *summ_mine = nullptr;
-    // the two-pass form (tt_two_pass()): this shard's census (G x cap records, pod
+    // MS_PLUGINS_NU_TT_NN, the two-pass form: this shard's census (G x cap records, pod
     // order), every shard's after the all-gather (G x G x cap, shard-major,
     // stride = the batch), and the slice's plans for the final pass
     void *cen_mine = nullptr, *cen_all = nullptr, *plans = nullptr;
@@ -153,7 +150,7 @@ namespace {
     } while (0)
 
 void free_slot(ShardSlot &sl) {
-    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.summ, sl.summ_mine, sl.cen_mine, sl.cen_all, sl.plans};
+    void *p[] = {sl.keys, sl.keys_mine, sl.flags, sl.flags_mine, sl.cen_mine, sl.cen_all, sl.plans};
     for (void *q : p)
         if (q) (void)hipFree(q);
     sl = ShardSlot{};
@@ -170,10 +167,7 @@ int slot_ensure(ms_ctx *c, ShardSlot &sl, uint32_t per) {
         hipMalloc((void **)&sl.keys_mine, cap * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void **)&sl.flags, G * cap * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc((void **)&sl.flags_mine, cap * sizeof(uint32_t)) != hipSuccess ||
-        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN && !tt_two_pass() &&
-         (hipMalloc(&sl.summ, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess ||
-          hipMalloc(&sl.summ_mine, G * cap * MS_TT_SUMMARY_BYTES) != hipSuccess)) ||
-        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN && tt_two_pass() &&
+        (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN &&
          (hipMalloc(&sl.cen_mine, G * cap * MS_TT_CENSUS_BYTES) != hipSuccess ||
           hipMalloc(&sl.cen_all, G * G * cap * MS_TT_CENSUS_BYTES) != hipSuccess ||
           hipMalloc(&sl.plans, cap * MS_TT_CENSUS_BYTES) != hipSuccess))) {
@@ -199,7 +193,7 @@ int drain_locked(ms_ctx *c, size_t k) {
     k = std::min(k, m.pending.size());
     if (k == 0) return MS_OK;
     MS_HIP(c, hipStreamWaitEvent(s, m.ev_comb[m.pending[k - 1].slot], 0));  // collectives run in issue order
-    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN && tt_two_pass()) {  // the slice's plans + the MAX of the picks
+    if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // the slice's plans + the MAX of the picks
         for (size_t i = 0; i < k; ++i) {
             const Pending &p = m.pending[i];
             const ShardSlot &sl = m.slot[p.slot];
@@ -207,13 +201,6 @@ int drain_locked(ms_ctx *c, size_t k) {
                                              sl.plans, p.count, static_cast<const char *>(sl.cen_all) +
                                                                     (size_t)p.first * MS_TT_CENSUS_BYTES,
                                              p.n, (uint32_t)m.world, sl.keys_mine, p.results, s));
-        }
-    } else if (c->cfg.plugin_set == MS_PLUGINS_NU_TT_NN) {  // the slice's G summaries merged in shard (LIST) order
-        for (size_t i = 0; i < k; ++i) {
-            const Pending &p = m.pending[i];
-            const ShardSlot &sl = m.slot[p.slot];
-            MS_HIP(c, launch_tt_combine(sl.summ_mine, cdiv(p.n, (uint32_t)m.world), (uint32_t)m.world, p.pods + p.first,
-                                        p.count, seed32_of(c->cfg.seed), nullptr, p.results, c->t, 0, s));
         }
     } else if (c->cfg.plugin_set == MS_PLUGINS_NU_NN_NA) {
         for (size_t i = 0; i < k; ++i) {
@@ -334,12 +321,8 @@ int collective_locked(ms_ctx *c, uint32_t si, hipEvent_t ev, uint32_t n, const m
     sl.used = true;
     host_tick(m, 2, tp);  // events to the collective stream
     ncclResult_t r = ncclSuccess;
-    if (ps == MS_PLUGINS_NU_NN || (ps == MS_PLUGINS_NU_TT_NN && tt_two_pass())) {  // the keys alone: one call
+    if (ps == MS_PLUGINS_NU_NN || ps == MS_PLUGINS_NU_TT_NN) {  // the keys alone: one call
         r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
-    } else if (ps == MS_PLUGINS_NU_TT_NN) {
-        // summaries do not combine by MAX: every rank sends each rank its pod slice's
-        // summaries ([q][per] in pod order) and receives its slice's from every shard
-        r = CCL(ncclAllToAll)(sl.summ, sl.summ_mine, (size_t)per * MS_TT_SUMMARY_BYTES, ncclUint8, m.comm, m.cs);
     } else {
         r = CCL(ncclGroupStart)();
         if (r == ncclSuccess) r = CCL(ncclReduceScatter)(sl.keys, sl.keys_mine, per, ncclUint64, ncclMax, m.comm, m.cs);
@@ -448,13 +431,10 @@ int submit_locked(ms_ctx *c, uint32_t n, const ms_pod_rec *pods, ms_result *resu
     const int ps = c->cfg.plugin_set;
     // (ev_swept recorded by the sweep's own dispatch for K1: no separate event
     // packet between consecutive sweeps on X)
-    if (ps == MS_PLUGINS_NU_TT_NN && tt_two_pass()) {
+    if (ps == MS_PLUGINS_NU_TT_NN) {
         // the two-pass form: this shard's census, every shard's by one all-gather,
         // then this shard's picks for every pod (keys, combined by the reduce-scatter)
         rc = tt2_sharded_sweep(c, si, n, pods, X);
-        if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
-    } else if (ps == MS_PLUGINS_NU_TT_NN) {  // per-pod summaries of this shard's nodes, no keys
-        rc = tt_summaries_locked(c, n, pods, sl.summ, X);
         if (rc == MS_OK && hipEventRecord(m.ev_swept[si], X) != hipSuccess) rc = fail(c, MS_E_HIP, "event record");
     } else {
         rc = sweep_locked(c, n, pods, sl.keys, ps == MS_PLUGINS_NU_NN ? nullptr : sl.flags, X, m.ev_swept[si]);
@@ -675,20 +655,15 @@ int comm_setup(ms_ctx *c, CommState &m, const ms_comm_id *id, int32_t rank, int3
     // streams are served by hardware queues of their own, so the caller's
     // (sweep) stream can never share a queue with them and serialise a
     // reduce-scatter or a decode behind the next sweep; their short kernels are
-    // dispatched ahead of the sweep's pending workgroups. MINISCHED_COMM_PRIO=0:
-    // normal priority (A/B).
+    // dispatched ahead of the sweep's pending workgroups (profiles/r03zc_comm_prio_ab.txt).
     int lo = 0, hi = 0;
     MS_HIP(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const char *cp = getenv("MINISCHED_COMM_PRIO");
-    const int cprio = (cp && cp[0] == '0') ? 0 : hi;
+    const int cprio = hi;
     MS_HIP(c, hipStreamCreateWithPriority(&m.cs, hipStreamNonBlocking, cprio));
-    // (MINISCHED_SHARD_STREAMS=2 only) two sweep streams; MINISCHED_SWEEP_PRIO=1
-    // creates them with the highest priority (A/B: the collectives then fell behind)
-    if (m.two_streams) {
-        const char *pe = getenv("MINISCHED_SWEEP_PRIO");
-        const int sprio = (pe && atoi(pe) == 1) ? hi : 0;
-        for (hipStream_t &q : m.ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, sprio));
-    }
+    // (MINISCHED_SHARD_STREAMS=2 only) two sweep streams at normal priority (at the
+    // highest, the collectives fell behind)
+    if (m.two_streams)
+        for (hipStream_t &q : m.ss) MS_HIP(c, hipStreamCreateWithPriority(&q, hipStreamNonBlocking, 0));
     MS_HIP(c, hipStreamCreateWithPriority(&m.ds, hipStreamNonBlocking, cprio));
     MS_HIP(c, hipEventCreateWithFlags(&m.ev_ds, hipEventDisableTiming));
     for (uint32_t i = 0; i < kPipeMax; ++i) {
@@ -735,11 +710,8 @@ int ms_comm_init(ms_ctx *c, const ms_comm_id *id, int32_t rank, int32_t world) {
     if (!m) return fail(c, MS_E_OOM, "ms_comm_init: host allocation");
     m->rank = rank;
     m->world = world;
-    if (const char *e = getenv("MINISCHED_PIPE_DEPTH")) m->depth = (uint32_t)std::max(1, atoi(e));
     m->depth = std::min<uint32_t>(m->depth, kPipeMax - 1);
     m->group = m->depth;
-    if (const char *e = getenv("MINISCHED_PIPE_GROUP")) m->group = (uint32_t)std::max(1, atoi(e));
-    m->group = std::min(m->group, m->depth);
     if (const char *e = getenv("MINISCHED_SHARD_STREAMS")) m->two_streams = atoi(e) == 2;
     if (const char *e = getenv("MINISCHED_HOST_PROF")) m->host_prof = atoi(e) == 1;
     if (const char *e = getenv("MINISCHED_SHARD_COALESCE")) m->coalesce = atoi(e) != 0;

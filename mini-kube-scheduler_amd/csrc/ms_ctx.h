@@ -78,15 +78,10 @@ struct ms_ctx {
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)
     int64_t *d_prev_rec = nullptr;         // and their final records (x2)
     DRow *d_drow = nullptr;                // derived rows of the binary64 sweep (tile_cap * kFullWaveTile)
-    // pipelined sequential engine: batch k+1's speculation (seq_stream) runs
-    // while batch k validates (caller stream); every buffer above is double-
-    // buffered by batch parity
-    hipStream_t seq_stream = nullptr;
+    // (every sequential-engine buffer above is double-buffered by batch parity)
     // ms_schedule_batch's chunked copies (schedule_chunked): H2D / D2H of host arrays beside the cycle
     hipStream_t copy_stream = nullptr;
     hipEvent_t ev_copy[4] = {nullptr, nullptr, nullptr, nullptr}, ev_cyc[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t ev_valid[3] = {nullptr, nullptr, nullptr}, ev_swept[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t ev_seq = nullptr;
     uint32_t tile_cap = 0;  // tiles allocated per pod
     uint32_t *d_overflow = nullptr;
     ms_pod_compact *h_podz = nullptr;      // pinned compact pods / results the compact cycle's
@@ -217,7 +212,6 @@ void comm_rank_world(const ms_ctx *c, int32_t *rank, int32_t *world);
 int comm_fence_reads(ms_ctx *c, hipStream_t writer);
 // MS_PLUGINS_NU_TT_NN: the two-pass bit-sliced cycle (default) or, with
 // MINISCHED_TT=v1, the per-pair summary sweep (read once per process).
-bool tt_two_pass();
 int ensure_tt(ms_ctx *c, size_t need);
 
 }  // namespace msgpu

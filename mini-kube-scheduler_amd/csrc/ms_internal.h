@@ -223,7 +223,7 @@ hipError_t launch_sweep_full(const NodeTable &t, uint32_t n_rows, const ms_pod_r
 // and its filter flags at tile_flags[p * n_tiles + t].
 // spec[p] accumulates (atomicMax) pod p's speculative global winner key and
 // spec_flags[p] the filter flags of tiles without a feasible row; both must be
-// zero on entry (k_validate_seq zeroes the entries it consumed).
+// zero on entry (the validator zeroes the entries it consumed).
 hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods,
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
                                    uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s);
@@ -236,33 +236,6 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
 hipError_t launch_topk_merge(const unsigned long long *tile_keys, const uint32_t *tile_flags, uint32_t n_pods,
                              uint32_t n_tiles, unsigned long long *top, unsigned long long *spec, uint32_t *spec_flags,
                              const NodeTable &t, int64_t *recs, hipStream_t s, unsigned long long *ext = nullptr);
-// In-order validation of a speculative batch (single workgroup); writes
-// results and commits binds to the table. prev_in / prev_recs_in: the stale
-// nodes (bound by the previous one or two batches) with their final records
-// ({n_own, n_carried, rows} of 2 + seq_prev_cap() words;
-// seq_prev_cap() * seq_rec_fields() i64), written by the previous batch's
-// validator into its prev_out / prev_recs_out; carry != 0 also carries the
-// previous batch's own binds into prev_out (the next sweep overlaps two
-// validations).
-// stats: u32[6] = overflow flags, re-swept tiles, recomputed entries, pods,
-// speculation misses, pods whose speculative winner was touched.
-hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                               uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
-                               const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
-                               const int64_t *top4_recs, uint32_t n_tiles, const uint32_t *prev_in,
-                               const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
-                               ms_result *results, uint32_t *stats, hipStream_t s,
-                               const unsigned long long *top_ext = nullptr);
-// A merge inside a step (launch_seq_step): batch k+1's tile lists -> its
-// global top-4, speculative winner, flags, records, ranks 4..7 (launch_topk_merge's outputs).
-struct SeqMerge {
-    const unsigned long long *tile_keys;
-    const uint32_t *tile_flags;
-    uint32_t n_pods;
-    unsigned long long *top, *spec, *ext;
-    uint32_t *spec_flags;
-    int64_t *recs;
-};
 // Batch k+1's merge inside step k at depth 1 (MINISCHED_SEQ_MERGE=instep):
 // once every sweep workgroup of the step has written batch k+1's tile lists
 // (write-through stores, counted on ctr), their waves merge its pods into these
@@ -289,11 +262,15 @@ struct SeqMergeIO {
 constexpr uint32_t kTimelineSteps = 2048, kTimelineWgs = 256;  // (a config E run: 1627 steps)
 // Whether launch_seq_step can merge n_next pods in-step (else launch_topk_merge follows).
 bool seq_step_merges(const NodeTable &t, uint32_t n_tiles, uint32_t n_next);
-// One single-stream step: validate batch k (n_pods) while sweeping the next
-// batch (n_next pods, tile lists only) and, with merge, merging the batch in
-// between (depth 2: carry 1, batch k's speculation predates batches k-1 and
-// k-2). Without merge (depth 1, carry 0), launch_topk_merge follows the step.
-// Any count may be 0.
+// One single-stream step: in-order validation of batch k (n_pods, workgroup 0;
+// writes results and commits binds to the table) while sweeping the next batch
+// (n_next pods: tile lists, and with mio their in-step merge; else
+// launch_topk_merge follows the step). prev_in / prev_recs_in: the stale nodes
+// (bound by the previous batch) with their final records ({n_own, n_carried,
+// rows} of 2 + seq_prev_cap() words; seq_prev_cap() * seq_rec_fields() i64),
+// written by the previous validation into its prev_out / prev_recs_out.
+// stats: u32[6] = overflow flags, re-swept tiles, recomputed entries, pods,
+// speculation misses, pods whose speculative winner was touched. Any count may be 0.
 hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles, uint32_t seed32,
                            const ms_pod_rec *pods, uint32_t n_pods, const unsigned long long *tile_keys,
                            const uint32_t *tile_flags, const unsigned long long *spec, const uint32_t *spec_flags,
@@ -301,8 +278,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s, const unsigned long long *top_ext = nullptr,
-                           const SeqMerge *merge = nullptr, int carry = 0, SeqMergeIO *mio = nullptr);
+                           hipStream_t s, const unsigned long long *top_ext = nullptr, SeqMergeIO *mio = nullptr);
 // Node-sharded sequential mode (minisched_gpu.h ms_seq_*): this shard's top-4
 // candidates with records + all-tile filter flags per pod, from the top-4 merge
 // output; and the replicated validation over the shards' gathered lists
@@ -359,6 +335,8 @@ hipError_t launch_tt2_pick_shard(const NodeTable &t, uint32_t n_rows, const ms_p
                                  uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
                                  uint32_t stride, uint32_t n_shards, uint32_t shard, unsigned long long *keys_out,
                                  hipStream_t s);
+// The plan records inside a two-pass scratch (tt2_scratch_bytes) for max_pods pods.
+void *tt2_plans(void *scratch, uint32_t n_rows, uint32_t max_pods);
 hipError_t launch_tt2_final_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                   uint32_t seed32, void *plans_buf, uint32_t max_pods, const void *census_all,
                                   uint32_t stride, uint32_t n_shards, const unsigned long long *keys_max,

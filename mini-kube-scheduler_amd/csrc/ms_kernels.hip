@@ -1173,17 +1173,6 @@ __global__ __launch_bounds__(64) void k_topk_merge(const u64 *__restrict__ tile_
     merge_pod<J>(tile_keys, tile_flags, p, n_tiles, top, spec, spec_flags, t, recs, ext, threadIdx.x);
 }
 
-// Batch k+1's merge inside step k (the depth-2 fused pipeline, run_sequential):
-// its tile lists were written by step k-1, so the merge workgroups need no wait.
-struct MergeArgs {
-    const u64 *tile_keys;
-    const uint32_t *tile_flags;
-    uint32_t n_pods, n_tiles;
-    u64 *top, *spec, *ext;
-    uint32_t *spec_flags;
-    int64_t *recs;
-};
-
 // ----------------------------------------------------------------------------
 // Exact sequential engine, in-order half: ONE wave walks the batch in queue
 // order, with no barriers. A bind only lowers keys of the node it lands on
@@ -1597,7 +1586,7 @@ __device__ __forceinline__ void put_stale(uint32_t *rows, int64_t *recs, uint32_
     for (int f = 0; f < kRecF; f += 2) d[f / 2] = make_longlong2(r[f], r[f + 1]);
 }
 
-// One speculative batch's in-order validation (k_validate_seq, k_seq_step).
+// One speculative batch's in-order validation (k_seq_step).
 // stats: [0] overflow flags, [1] re-swept tiles, [2] recomputed entries, [3] pods,
 //        [4] speculation misses (records loaded), [5] slow pods, [6] slow pods that scanned the tile lists
 // top4/top4_recs: k_topk_merge's per-pod top-4 keys and their batch-start records
@@ -1790,7 +1779,7 @@ __device__ __forceinline__ void prologue_wg_finish(SeqShared &S, const SeqArgs &
     __syncthreads();
 }
 
-// The validator's prologue on its one wave (k_validate_seq; k_seq_step with
+// The validator's prologue on its one wave (k_seq_step with
 // MS_WG_PROLOGUE=1, whose workgroup issued the bulk copies: wg_dma): the
 // batch's pods, top-4 keys and speculative winners into LDS, the stale nodes
 // mapped, each pod's speculative winner slot resolved. Returns prev_in[0].
@@ -2244,12 +2233,6 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 #endif
 }
 
-template <int J>
-__global__ __launch_bounds__(64) void k_validate_seq(SeqArgs va) {
-    __shared__ SeqShared S;
-    validate_batch<J>(S, va, threadIdx.x);
-}
-
 // One step of the single-stream sequential engine: workgroup 0 validates
 // batch k (one wave; the workgroup's LDS is the validator's, so it has a CU to
 // itself) while the other workgroups sweep batch k+1 (a (tile, pod chunk)
@@ -2370,8 +2353,7 @@ __device__ __forceinline__ bool step_merge_fallback(const SeqArgs &va, const Ste
 }
 
 template <int J, int W>
-__global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks, MergeArgs mg,
-                                                     uint32_t merge_wgs, StepMerge sm) {
+__global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, uint32_t n_tasks, StepMerge sm) {
     // (the untagged-pod check below reads one tag per thread)
     static_assert(kSeqBatch <= 64 * W, "k_seq_step: one in-step merge tag per thread of the validating workgroup");
     __shared__ SeqShared S;
@@ -2426,14 +2408,7 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
         return;
     }
     const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-    if (blockIdx.x <= merge_wgs) {  // workgroups 1 .. merge_wgs: batch k+1's merge, a pod per wave
-        const uint32_t p = (blockIdx.x - 1) * W + wave;
-        if (p < mg.n_pods)
-            merge_pod<J>(mg.tile_keys, mg.tile_flags, p, mg.n_tiles, mg.top, mg.spec, mg.spec_flags, va.t, mg.recs,
-                         mg.ext, lane);
-        return;
-    }
-    const uint32_t sb = blockIdx.x - 1 - merge_wgs, sg = gridDim.x - 1 - merge_wgs;  // sweep workgroup, count
+    const uint32_t sb = blockIdx.x - 1, sg = gridDim.x - 1;  // sweep workgroup, count
     if (sw.t.drow && sw.fast) {  // transposed form: a tile per workgroup, its rows in the validator's (idle) LDS
         DRow *rows = reinterpret_cast<DRow *>(&S);
         // Groups outside the binary64 range are taken after the tile loop, listed
@@ -3001,8 +2976,7 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
     if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
-    uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
-    if (const char *e = getenv("MINISCHED_SEQ_CHUNK")) chunk = (uint32_t)std::min(64, std::max(1, atoi(e)));
+    const uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
     if (t.drow && seq_fast()) {  // transposed form: one workgroup per tile
         const SweepArgs a = {t, n_rows, pods, n_pods, kTpPods, seed32, tile_keys, tile_flags, n_tiles, 1u};
         hipLaunchKernelGGL(k_sweep_tp_topk, dim3(n_tiles), dim3(64 * kTpWaves), 0, s, a);
@@ -3011,29 +2985,6 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
     const dim3 grid(gx, cdiv(n_pods, chunk));
     const SweepArgs a = {t, n_rows, pods, n_pods, chunk, seed32, tile_keys, tile_flags, n_tiles, seq_fast()};
     hipLaunchKernelGGL(k_sweep_full_topk, grid, dim3(kFullThreads), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_validate_seq(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                               uint32_t seed32, const unsigned long long *tile_keys, const uint32_t *tile_flags,
-                               const unsigned long long *spec, const uint32_t *spec_flags, const unsigned long long *top4,
-                               const int64_t *top4_recs, uint32_t n_tiles, const uint32_t *prev_in,
-                               const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out, int carry,
-                               ms_result *results, uint32_t *stats, hipStream_t s, const unsigned long long *top_ext) {
-    if (n_pods == 0) return hipSuccess;
-    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || !top4_recs || (prev_in && !prev_recs_in) ||
-        (prev_out && !prev_recs_out))
-        return hipErrorInvalidValue;
-    const SeqArgs va = {t,        n_rows,       pods,     n_pods,        seed32, tile_keys, tile_flags,
-                        spec,     spec_flags,   top4,     top4_recs,     top_ext, n_tiles, prev_in,  prev_recs_in,
-                        prev_out, prev_recs_out, carry,   results,       stats};
-#define MS_VAL(J) hipLaunchKernelGGL(k_validate_seq<J>, dim3(1), dim3(64), 0, s, va)
-    if (n_tiles <= 64) MS_VAL(1);
-    else if (n_tiles <= 128) MS_VAL(2);
-    else if (n_tiles <= 256) MS_VAL(4);
-    else if (n_tiles <= 512) MS_VAL(8);
-    else MS_VAL(16);
-#undef MS_VAL
     return hipGetLastError();
 }
 
@@ -3050,15 +3001,14 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            const int64_t *prev_recs_in, uint32_t *prev_out, int64_t *prev_recs_out,
                            ms_result *results, uint32_t *stats, const ms_pod_rec *next_pods, uint32_t n_next,
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
-                           hipStream_t s, const unsigned long long *top_ext, const SeqMerge *merge, int carry,
-                           SeqMergeIO *mio) {
-    if (n_pods == 0 && n_next == 0 && !(merge && merge->n_pods)) return hipSuccess;
+                           hipStream_t s, const unsigned long long *top_ext, SeqMergeIO *mio) {
+    if (n_pods == 0 && n_next == 0) return hipSuccess;
     if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
         (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
         return hipErrorInvalidValue;
     SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
                         spec,     spec_flags,   top4,    top4_recs,  top_ext, n_tiles, prev_in, prev_recs_in,
-                        prev_out, prev_recs_out, carry,  results,    stats};
+                        prev_out, prev_recs_out, 0,      results,    stats};
     // tasks: (tile, chunk of next pods) pairs, sized to fit one pass of the
     // sweep workgroups (one per CU beside the validator's)
     const uint32_t cus = (uint32_t)(num_cus > 1 ? num_cus : 256);
@@ -3071,21 +3021,13 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     SweepArgs sw = {t,       n_rows,         next_pods,       n_next,  chunk,
                     seed32,  next_tile_keys, next_tile_flags, n_tiles, seq_fast(), 0u};
     const uint32_t n_tasks = n_next ? n_tiles * cdiv(n_next, chunk) : 0u;
-    // merge workgroups (a pod per wave) between the validator's and the sweep's
-    MergeArgs mg = {};
-    uint32_t merge_wgs = 0;
-    if (merge && merge->n_pods) {
-        mg = {merge->tile_keys, merge->tile_flags, merge->n_pods, n_tiles, merge->top, merge->spec, merge->ext,
-              merge->spec_flags, merge->recs};
-        merge_wgs = cdiv(merge->n_pods, W);
-    }
-    const uint32_t room = cus > 1u + merge_wgs ? cus - 1u - merge_wgs : 1u;
-    const uint32_t grid = 1u + merge_wgs + (n_tasks ? std::min(room, tp ? n_tiles : cdiv(n_tasks, W)) : 0u);
+    const uint32_t room = cus > 1u ? cus - 1u : 1u;
+    const uint32_t grid = 1u + (n_tasks ? std::min(room, tp ? n_tiles : cdiv(n_tasks, W)) : 0u);
     StepMerge sm = {};
     if (mio) {
         sm.in_tags = mio->in_tags;
         sm.in_tag = mio->in_tags ? mio->in_tag : 0u;
-        if (mio->top && n_next && !merge_wgs && seq_step_merges(t, n_tiles, n_next)) {
+        if (mio->top && n_next && seq_step_merges(t, n_tiles, n_next)) {
             if (!mio->tags || !mio->ctr || !mio->spec || !mio->spec_flags) return hipErrorInvalidValue;
             mio->target += grid - 1u;  // every sweep workgroup counts once
             sm.top = mio->top;
@@ -3111,7 +3053,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     }
     va.tl = sm.tl;
 #define MS_STEP(JJ, WW) \
-    hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, mg, merge_wgs, sm)
+    hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, sm)
     if (J == 1) MS_STEP(1, 12);
     else if (J == 2) MS_STEP(2, 12);
     else if (J == 4) MS_STEP(4, 12);

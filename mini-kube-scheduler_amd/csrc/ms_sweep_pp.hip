@@ -647,7 +647,6 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // pipelined sharded step, whose collective and decode kernels then interleave with
     // a multi-round sweep: 74.6 -> 77.7 us at 25k, 136.3 -> 140 at 50k;
     // profiles/r04n_shard_shapes.txt, r04p_chunk56_probe.json. Not kept.)
-    if (const char *c = getenv("MINISCHED_PP_CHUNK")) chunk = cdiv((uint32_t)std::max(8, atoi(c)), 8) * 8;
     chunk = std::min(std::max(chunk, 8u), kPpMaxChunk);
     uint32_t nblk1 = cdiv(n_pods, chunk), xtra = 0;
     // Balanced split of a one-batch shard sweep (2- and 4-wave workgroups, one
@@ -657,13 +656,8 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
     // slot gets a workgroup: `chunk` pods each, 8 more for the first `xtra`
     // (4 x 48.8 pods on the busiest SIMD): the shard sweep alone 42.0 -> 38.7 us
     // at G = 8, 71.5 -> 67.5 at G = 4 (profiles/r05r_balance_ab.txt).
-    // MINISCHED_PP_BALANCE=0: off (A/B).
-    static const bool balance = [] {
-        const char *e = getenv("MINISCHED_PP_BALANCE");
-        return !e || atoi(e) != 0;
-    }();
     // A coalesced pair of equal batches splits the slots in halves, each balanced alike.
-    if (balance && (!pods2 || n_pods2 == n_pods) && gy == 1 && W <= 4u && !getenv("MINISCHED_PP_CHUNK")) {
+    if ((!pods2 || n_pods2 == n_pods) && gy == 1 && W <= 4u) {
         const uint32_t slots = (16u / W) * cus / (pods2 ? 2u : 1u);
         const uint32_t cb = (n_pods / slots) / 8u * 8u;
         if (cb >= 8u && cb + 8u <= kPpMaxChunk && n_pods > cb * slots) {
@@ -676,11 +670,8 @@ hipError_t sweep_pp_impl(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *
         }
     }
     const dim3 grid(nblk1 + (pods2 ? (xtra ? nblk1 : cdiv(n_pods2, chunk)) : 0u), gy);
-    // the fixed-slot form for digit-aligned waves (MINISCHED_PP_FIX=0: off, A/B)
-    static const int fix_ok = [] {
-        const char *e = getenv("MINISCHED_PP_FIX");
-        return e ? (atoi(e) != 0 ? 1 : 0) : 1;
-    }();
+    // the fixed-slot form for digit-aligned waves (profiles/r04j_fix_ab.txt)
+    constexpr int fix_ok = 1;
     const PpJob2 j2 = {pods2, reinterpret_cast<u64 *>(keys2), n_pods2, nblk1};
     if (pods2 && (gy > 1 || results || resc || !keys || !keys2)) return hipErrorInvalidValue;
     if (gy > 1) {

@@ -990,14 +990,18 @@ hipError_t launch_tt2_pick_shard(const NodeTable &t, uint32_t n_rows, const ms_p
     return hipGetLastError();
 }
 
+void *tt2_plans(void *scratch, uint32_t n_rows, uint32_t max_pods) {
+    return tt2_layout(scratch, n_rows, max_pods).plans;
+}
+
 hipError_t launch_tt2_final_shard(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                                  uint32_t seed32, void *scratch, uint32_t max_pods, const void *census_all,
+                                  uint32_t seed32, void *plans_buf, uint32_t max_pods, const void *census_all,
                                   uint32_t stride, uint32_t n_shards, const unsigned long long *keys_max,
                                   ms_result *results, hipStream_t s) {
+    (void)n_rows;
     if (n_pods == 0) return hipSuccess;
-    if (n_pods > max_pods || !results || !scratch) return hipErrorInvalidValue;
-    // the scratch's plan records (not its start, which holds the row planes)
-    TtPlan *plans = tt2_layout(scratch, n_rows, max_pods).plans;
+    if (n_pods > max_pods || !results || !plans_buf) return hipErrorInvalidValue;
+    TtPlan *plans = static_cast<TtPlan *>(plans_buf);  // (n_pods records)
     const dim3 g1(cdiv(n_pods, 128u));
     hipLaunchKernelGGL(k_tt2_plan, g1, dim3(128), 0, s, static_cast<const TtCensus *>(census_all), n_shards, stride,
                        pods, n_pods, seed32, plans, results, t, 0);

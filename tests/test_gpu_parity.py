@@ -412,17 +412,13 @@ def test_chunked_warm_runs(oracle, max_batch):
         assert_table_equal(e, o["cols"], 3000)
 
 
-@pytest.mark.parametrize("pipe", ["fused2", "fused", "2", "1", "0"])
-@pytest.mark.parametrize("batch", ["1", "7", "64", "256"])
-def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch, pipe):
+@pytest.mark.parametrize("batch", ["1", "7", "64", "128", "256"])
+def test_resource_sequential_batch_sizes(oracle, monkeypatch, batch):
     # speculative batch boundaries must not change placements: 50 nodes (one
-    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted); the
-    # default single-stream steps (validation k beside the sweep of k+1, merge
-    # launched after; "fused2": beside the merge of k+1 and the sweep of k+2), and
-    # two streams with the speculation overlapping two validations (2), one
-    # (1) or none (0); 256 is clamped to the validator's 128
+    # tile, heavy re-sweeps) and 2500 nodes (lists rarely exhausted); single-stream
+    # steps (validation k beside the sweep of k+1 and its in-step merge); 256 is
+    # clamped to the validator's 128
     monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
-    monkeypatch.setenv("MINISCHED_SEQ_PIPE", pipe)
     for n_nodes, n_pods in ((50, 600), (2500, 3000)):
         seed = 11 * n_nodes + int(batch)
         nr = synth.nodes(n_nodes, seed=seed, resources=True)
@@ -441,7 +437,6 @@ def test_resource_sequential_merge_forms(oracle, monkeypatch, batch, merge):
     # have written its tile lists), and the fallback where every in-step worker
     # skips and each validation merges its own batch first
     monkeypatch.setenv("MINISCHED_SEQ_BATCH", batch)
-    monkeypatch.setenv("MINISCHED_SEQ_PIPE", "fused")
     monkeypatch.setenv("MINISCHED_SEQ_MERGE", merge)
     for n_nodes, n_pods in ((50, 600), (2500, 3000)):
         seed = 13 * n_nodes + int(batch)

@@ -357,8 +357,8 @@ def test_library_sharded_cycle_1rank(oracle, plugin_set):
     _same(res, o, 0, len(pr), "library cycle")
 
 
-@pytest.mark.parametrize("coalesce,words", [("1", ""), ("0", ""), ("1", "8"), ("1", "4")])
-def test_library_submit_coalescing(oracle, monkeypatch, coalesce, words):
+@pytest.mark.parametrize("coalesce,words,prof", [("1", "", "1"), ("0", "", ""), ("1", "8", ""), ("1", "4", "")])
+def test_library_submit_coalescing(oracle, monkeypatch, capfd, coalesce, words, prof):
     # Consecutive NU+NN submits share one K1 launch (ms_comm.cpp submit_locked's
     # stash): distinct pod batches of distinct sizes, an odd count (the last one
     # swept alone at the drain), and a node delta between two submits (the
@@ -372,6 +372,8 @@ def test_library_submit_coalescing(oracle, monkeypatch, coalesce, words):
     monkeypatch.setenv("MINISCHED_SHARD_COALESCE", coalesce)
     if words:
         monkeypatch.setenv("MINISCHED_PP_WORDS", words)
+    if prof:  # the per-submit host clocks (tools/step_probe_lib.py reads them), printed at teardown
+        monkeypatch.setenv("MINISCHED_HOST_PROF", prof)
     nr = synth.nodes(5000, seed=81)
     batches = [synth.pods(n, seed=81 + i) for i, n in enumerate((700, 1200, 333, 2048, 901))]
     nr2 = nr.copy()
@@ -396,6 +398,8 @@ def test_library_submit_coalescing(oracle, monkeypatch, coalesce, words):
             _same(res[i].cpu().numpy().view(_lib.RESULT), want[i], 0, len(batches[i]), f"batch {i}")
     finally:
         e.close()
+    if prof:
+        assert "MS_HOST_PROF submits=5 " in capfd.readouterr().err
 
 
 def test_library_schedule_batch_1rank(oracle):
