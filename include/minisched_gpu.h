@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 6
+#define MS_ABI_VERSION 7
 
 /* ---- return codes -------------------------------------------------------- */
 #define MS_OK 0
@@ -72,7 +72,8 @@ extern "C" {
 /* Filter[NU]; Score[NN (weight w0), NodeAffinity with SEVERAL preferred terms
  * (weight w1), ScoreExtensions = DefaultNormalizeScore(MaxNodeScore,
  * reverse=false) run by the in-loop hook exactly as written]. A pod's terms are
- * a term set (ms_nam_term_set) registered with ms_nam_term_sets; the pod record
+ * a term set (ms_nam_term_set / ms_nam_term_set_ext) registered with
+ * ms_nam_term_sets(_ext); the pod record
  * names it by id = pref_zone | pref_weight << 8 (0 = no terms). Raw scores are
  * sums of matching term weights, up to 400, so the hook rescales earlier
  * entries whenever a later node's raw score exceeds 100. Terms
@@ -397,6 +398,29 @@ typedef struct ms_nam_term_set {
  * sets[s - 1]; ids above n_sets count as no terms. Copied; replaces the
  * previous table (stream-ordered after earlier calls). Up to 65535 sets. */
 int ms_nam_term_sets(ms_ctx *ctx, uint32_t n_sets, const ms_nam_term_set *sets);
+/* The same in general form (ABI 7): a PreferredSchedulingTerm whose
+ * NodeSelectorTerm holds any NodeSelectorRequirements (In, NotIn, Exists,
+ * DoesNotExist, Gt, Lt; several per term, ANDed) on the two encoded label keys
+ * (0: the zone label, ms_node_rec.zone; 1: the second label, label2). Per key,
+ * mask[key] is the set of value ids of nodes that satisfy every requirement of
+ * the term on that key: bit (v & 31) of mask[key][v >> 5] for value id v, id 0 =
+ * the node lacks the label; all ones when the term has no requirement on the
+ * key. The term matches a node when both masks hold the node's ids; a term with
+ * no requirement at all matches no node (k8s@v1.22.0 component-helpers
+ * nodeaffinity: an empty nodeSelectorTerm matches nothing), so the shim gives it
+ * zero masks. weight 1..100, 0 = unused slot. Value ids are the shim's (the same
+ * table as the node records'); it re-registers its sets when the table grows,
+ * since Exists, NotIn, DoesNotExist, Gt and Lt also cover ids it had not seen.
+ * ms_nam_term_sets' {key, value} terms are the masks {value} (In) or all ids
+ * but 0 (Exists, value 0xFF) on that key and all ones on the other. */
+typedef struct ms_pref_term_ext {
+    uint32_t mask[2][8];
+    uint8_t weight, _pad[3];
+} ms_pref_term_ext; /* 68 bytes */
+typedef struct ms_nam_term_set_ext {
+    ms_pref_term_ext term[MS_NAM_TERMS];
+} ms_nam_term_set_ext; /* 272 bytes */
+int ms_nam_term_sets_ext(ms_ctx *ctx, uint32_t n_sets, const ms_nam_term_set_ext *sets);
 /* Node shards (contexts with their own node_base, ordinals = LIST order) of
  * one MS_PLUGINS_NU_NN_NAM cycle, for a caller with its own collectives:
  *   1. ms_nam_segment_device: per pod, this shard's rescale composition (an

@@ -14,20 +14,36 @@
 // the composition of the rescales of every later feasible node (oracle/
 // ms_oracle.c nam_closed). Compositions of such maps on 0..100 are 101-entry
 // tables that compose associatively, so a LIST-ordered row segment summarises
-// as ONE table (its rescales composed) plus "has a non-zero node":
-//   k_nam_seg   per (segment, pod): that table, forward over the segment's rows
-//               (T <- f_r o T at each rescale);
-//   k_nam_keys  per (segment, pod): the suffix table of the later segments (and
-//               of the later node shards) composed, then the segment's rows in
-//               REVERSE order keeping T_{>j} (T <- T o f_r after each rescale)
-//               and the best packed key; the anchor decided by whether an
-//               earlier segment or shard has a non-zero node. atomicMax over the
-//               segments; node shards combine by uint64 MAX like NU+NN.
-// Lane = pod, rows streamed through LDS. A lane's table lives in LDS (a 108-B
-// row per lane); a rescale updates one table with all 64 lanes of the wave
-// (one lane per table entry, 2 passes), the lanes with a rescale on the same row
-// taken in turn by a ballot loop. Every f_r maps 1..100 below itself, so a table
-// is all 0 after at most 100 rescales; a lane whose T(100) is 0 stops updating.
+// as ONE table (its rescales composed) plus "has a non-zero node".
+//
+// Round 6: pod CLASSES. A node's NodeAffinity score depends on the pod only
+// through its term set and, via NodeUnschedulable's feasibility, its toleration
+// bit: pods with the same (term set, toleration) -- a class -- see the same
+// feasible list, the same raw scores and so the same normalised scores. So the
+// in-loop hook runs once per class, not per pod:
+//   k_nam_classes  one workgroup: the batch's classes (dense ids), each pod's
+//                  class, a representative pod per class, the pods in (class,
+//                  name digit) order;
+//   k_nam_seg      per (segment, class): the segment's composed rescale table
+//                  (forward over its rows, T <- f_r o T at each rescale);
+//   k_nam_fscore   per (segment, class): T_{>j} from the later segments (and
+//                  later node shards), then the segment's rows in REVERSE order
+//                  writing every row's normalised NodeAffinity score F[c][row]
+//                  (0..100; 0xFF infeasible), the anchor decided by whether an
+//                  earlier segment or shard has a non-zero node; and the
+//                  maximum of F per node-digit class (atomicMax);
+//   k_nam_pick     per pod (lane = pod, pods in class-digit order): the best
+//                  total S* = max(w_na F + w_nn NodeNumber) follows from its
+//                  class's maxima; then every (pod, row) pair is tested, four
+//                  rows per bit operation (the row's F against the value that
+//                  reaches S* given whether its name digit is the pod's), and
+//                  only the rows reaching S* are hashed for selectHost's
+//                  tie-break. Every pair is evaluated; only the hash is skipped
+//                  where it cannot win.
+// Terms (ABI 7, ms_nam_term_set_ext) are per-key value-id sets; the host turns
+// each set into a lookup table (NamTab: per value id a 4-bit "these terms' sets
+// hold it" mask per key, and the weight sum of every 4-bit term mask), so a
+// row's raw score is wsum[z[zone] & l[label2]] for any operators.
 #include <algorithm>
 
 #include "ms_device.h"
@@ -36,12 +52,14 @@ namespace msgpu {
 
 namespace {
 
-constexpr uint32_t kNamThreads = 256;  // pods per workgroup (one per lane)
-constexpr uint32_t kNamTile = 1024;    // rows staged in LDS per pass
-constexpr uint32_t kNamSegRows = 2048, kNamMaxSegs = 16;
-constexpr uint32_t kNamStride = 108;   // bytes per lane table in LDS: 27 words (odd: per-lane gathers spread banks)
-
+constexpr uint32_t kNamTile = 1024;      // rows staged in LDS per pass
+constexpr uint32_t kNamStride = 108;     // bytes per lane table in LDS: 27 words (odd: per-lane gathers spread banks)
+constexpr uint32_t kNamTabStride = 548;  // bytes per lane term table in LDS: 137 words (odd)
 constexpr uint32_t kNamComposeThreads = 128;
+constexpr uint32_t kNamPickThreads = 256;
+constexpr uint32_t kNamClsThreads = 1024;
+constexpr uint32_t kNamSortCap = 8192;   // (class, digit) buckets the class sort holds in LDS
+constexpr uint32_t kNamDigits = 11;      // node name digit 0..9, 10 = none
 
 struct NamSeg {
     uint8_t T[101];  // the composed rescale map on 0..100
@@ -49,6 +67,7 @@ struct NamSeg {
     uint8_t _pad[2];
 };
 static_assert(sizeof(NamSeg) == MS_NAM_SEG_BYTES, "NamSeg layout");
+static_assert(sizeof(NamTab) == 544 && kNamTabStride >= sizeof(NamTab), "NamTab layout");
 
 // Row word staged in LDS: bit 0 absent, bit 1 unschedulable, zone << 8,
 // label2 << 16, digit << 24 (15 = none).
@@ -59,89 +78,23 @@ __device__ __forceinline__ uint32_t nam_row_word(const NodeTable &t, uint32_t r)
            ((uint32_t)t.label2[r] << 16) | ((d <= 9u ? d : 15u) << 24);
 }
 
-// A pod's terms: term k matches a row whose label byte (zone: byte 1 of the
-// row word, label2: byte 2) lies in [lo, lo + span] (In: value, span 0;
-// Exists: 1..255, every labelled row) and adds weight (0: unused slot, or value 0 = "unlabelled",
-// which never matches).
-#ifndef MS_NAM_PACKED  // terms two per register in 16-bit halves (v_perm + v_pk_*_u16; 0: one at a time, A/B)
-#define MS_NAM_PACKED 1
-#endif
-#if MS_NAM_PACKED
-typedef unsigned short nam_u16x2 __attribute__((ext_vector_type(2)));
-// Terms (0, 1) and (2, 3) in the halves of one register each: sel picks the
-// terms' label bytes out of the row word into the low byte of each half
-// (v_perm_b32, 0x0C = a zero byte), lo / span + 1 / weight per half.
-struct NamTerms {
-    uint32_t sel[2];
-    nam_u16x2 lo[2], sp1[2], w[2];
-};
-#else
-struct NamTerms {
-    uint32_t sh[MS_NAM_TERMS], lo[MS_NAM_TERMS], span[MS_NAM_TERMS], w[MS_NAM_TERMS];
-};
-#endif
-
-__device__ __forceinline__ NamTerms load_terms(const ms_pod_rec &pod, const ms_nam_term_set *sets, uint32_t n_sets) {
-    NamTerms m;
-    const uint32_t sid = (uint32_t)pod.pref_zone | (uint32_t)pod.pref_weight << 8;
-    ms_nam_term_set st = {};
-    if (sid != 0u && sid <= n_sets) st = sets[sid - 1u];
-#pragma unroll
-    for (int k = 0; k < MS_NAM_TERMS; ++k) {
-        const ms_pref_term x = st.term[k];
-        const uint32_t lo = x.value == 0xFFu ? 1u : x.value, span = x.value == 0xFFu ? 254u : 0u;
-        const uint32_t w = x.value == 0u ? 0u : x.weight;
-#if MS_NAM_PACKED
-        const int h = k >> 1, half = k & 1;
-        const uint32_t b = x.key ? 2u : 1u;
-        if (half == 0) {
-            m.sel[h] = b | 0x0C0C0C00u;  // (bytes 1-3 zero until term k+1 fills byte 2)
-            m.lo[h].x = (unsigned short)lo;
-            m.sp1[h].x = (unsigned short)(span + 1u);
-            m.w[h].x = (unsigned short)w;
-        } else {
-            m.sel[h] = (m.sel[h] & 0xFF00FFFFu) | b << 16;
-            m.lo[h].y = (unsigned short)lo;
-            m.sp1[h].y = (unsigned short)(span + 1u);
-            m.w[h].y = (unsigned short)w;
-        }
-#else
-        m.sh[k] = x.key ? 16u : 8u;
-        m.lo[k] = lo;
-        m.span[k] = span;
-        m.w[k] = w;
-#endif
-    }
-    return m;
-}
-
-// NodeAffinity.Score: the sum of the weights of the matching terms.
-__device__ __forceinline__ uint32_t nam_raw(uint32_t w, const NamTerms &m) {
-#if MS_NAM_PACKED
-    // per half: d = label - lo (wrapping: a label below lo lands above 65280),
-    // s = sat(span + 1 - d) > 0 exactly when lo <= label <= lo + span, and
-    // min(s * weight, weight) (s * weight <= 255 * 100 < 2^16) the term's share
-    nam_u16x2 t = {0, 0};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t lab = __builtin_amdgcn_perm(0u, w, m.sel[h]);
-        const nam_u16x2 d = __builtin_bit_cast(nam_u16x2, lab) - m.lo[h];
-        const nam_u16x2 s = __builtin_elementwise_sub_sat(m.sp1[h], d);
-        t += __builtin_elementwise_min(s * m.w[h], m.w[h]);
-    }
-    return (uint32_t)t.x + (uint32_t)t.y;
-#else
-    uint32_t r = 0;
-#pragma unroll
-    for (int k = 0; k < MS_NAM_TERMS; ++k) {
-        const uint32_t lab = (w >> m.sh[k]) & 0xFFu;
-        r += (lab - m.lo[k] <= m.span[k]) ? m.w[k] : 0u;
-    }
-    return r;
-#endif
-}
-
 __device__ __forceinline__ bool nam_feasible(uint32_t w, uint32_t tol) { return (w & (tol ? 1u : 3u)) == 0u; }
+
+// NodeAffinity.Score of a row word under a term table in LDS.
+__device__ __forceinline__ uint32_t nam_raw(uint32_t w, const uint8_t *tab) {
+    const uint32_t m = tab[(w >> 8) & 0xFFu] & tab[256u + ((w >> 16) & 0xFFu)];
+    return reinterpret_cast<const uint16_t *>(tab + 512)[m & 15u];
+}
+
+// Class key (term set, toleration) of a pod: set ids past n_sets count as no terms.
+__device__ __forceinline__ uint32_t nam_key(const ms_pod_rec &p, uint32_t n_sets) {
+    uint32_t sid = (uint32_t)p.pref_zone | (uint32_t)p.pref_weight << 8;
+    if (sid > n_sets) sid = 0;
+    return sid * 2u + (p.tolerates_unschedulable ? 1u : 0u);
+}
+__device__ __forceinline__ uint32_t nam_pod_digit(const ms_pod_rec &p) {
+    return p.name_digit >= 0 && p.name_digit <= 9 ? (uint32_t)p.name_digit : 10u;
+}
 
 // The identity map in a lane's LDS table.
 __device__ __forceinline__ void table_identity(uint8_t *row) {
@@ -167,44 +120,154 @@ __device__ __forceinline__ void table_pre(uint8_t *row, uint32_t r, uint32_t lan
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void seg_bounds(uint32_t n_rows, uint32_t seg_rows, uint32_t seg, uint32_t &r0,
-                                           uint32_t &r1) {
-    r0 = seg * seg_rows;
-    r1 = min(n_rows, r0 + seg_rows);
+// The batch's classes, one workgroup (kNamClsThreads):
+//   used[key] (n_keys = 2 (n_sets + 1) words, zeroed here) -> dense class ids in
+//   key order; ctl[0] = the class count; cls_key[c], rep[c] (the first pod of
+//   class c); pcls[p]; perm = the pods in (class, name digit) order when the
+//   buckets fit kNamSortCap, else in batch order.
+__global__ __launch_bounds__(kNamClsThreads) void k_nam_classes(const ms_pod_rec *__restrict__ pods, uint32_t n,
+                                                                 uint32_t n_sets, uint32_t *__restrict__ used,
+                                                                 uint32_t *__restrict__ ctl,
+                                                                 uint32_t *__restrict__ cls_key,
+                                                                 uint32_t *__restrict__ rep,
+                                                                 uint32_t *__restrict__ pcls,
+                                                                 uint32_t *__restrict__ perm) {
+    __shared__ uint32_t cnt[kNamSortCap];
+    __shared__ uint32_t part[kNamClsThreads];
+    __shared__ uint32_t total;
+    const uint32_t tid = threadIdx.x, NT = kNamClsThreads;
+    const uint32_t n_keys = 2u * (n_sets + 1u);
+    for (uint32_t k = tid; k < n_keys; k += NT) used[k] = 0u;
+    __syncthreads();
+    __threadfence_block();
+    for (uint32_t i = tid; i < n; i += NT) used[nam_key(pods[i], n_sets)] = 1u;
+    __threadfence_block();
+    __syncthreads();
+    // exclusive scan of used[] in key order: thread t takes a contiguous range
+    const uint32_t per = (n_keys + NT - 1u) / NT, k0 = min(n_keys, tid * per), k1 = min(n_keys, k0 + per);
+    uint32_t s = 0;
+    for (uint32_t k = k0; k < k1; ++k) s += used[k];
+    part[tid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t a = 0;
+        for (uint32_t t = 0; t < NT; ++t) {
+            const uint32_t v = part[t];
+            part[t] = a;
+            a += v;
+        }
+        total = a;
+        ctl[0] = a;
+    }
+    __syncthreads();
+    uint32_t c = part[tid];
+    for (uint32_t k = k0; k < k1; ++k)
+        if (used[k]) {
+            cls_key[c] = k;
+            rep[c] = 0xFFFFFFFFu;
+            used[k] = c++;  // (used[] now maps a key to its class)
+        }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t n_cls = total;
+    const bool sort = n_cls * kNamDigits <= kNamSortCap;
+    const uint32_t nb = n_cls * kNamDigits;
+    if (sort)
+        for (uint32_t b = tid; b < nb; b += NT) cnt[b] = 0u;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += NT) {
+        const uint32_t cl = used[nam_key(pods[i], n_sets)];
+        pcls[i] = cl;
+        atomicMin(&rep[cl], i);
+        if (sort) atomicAdd(&cnt[cl * kNamDigits + nam_pod_digit(pods[i])], 1u);
+    }
+    __syncthreads();
+    if (!sort) {
+        for (uint32_t i = tid; i < n; i += NT) perm[i] = i;
+        return;
+    }
+    // exclusive scan of the bucket counts (contiguous ranges per thread)
+    const uint32_t bper = (nb + NT - 1u) / NT, b0 = min(nb, tid * bper), b1 = min(nb, b0 + bper);
+    s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += cnt[b];
+    part[tid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t a = 0;
+        for (uint32_t t = 0; t < NT; ++t) {
+            const uint32_t v = part[t];
+            part[t] = a;
+            a += v;
+        }
+    }
+    __syncthreads();
+    uint32_t a = part[tid];
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t v = cnt[b];
+        cnt[b] = a;
+        a += v;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += NT)
+        perm[atomicAdd(&cnt[pcls[i] * kNamDigits + nam_pod_digit(pods[i])], 1u)] = i;
 }
 
-// grid (pod blocks, segments): the segment's composed rescale table per pod.
-__global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
-                                                         const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
-                                                         const ms_nam_term_set *__restrict__ sets, uint32_t n_sets,
-                                                         NamSeg *__restrict__ out) {
+// A lane's class: its key's term table into the lane's LDS slot (kNamTabStride
+// apart: an odd word stride, so the per-lane lookups spread over the banks); all
+// 34 16-B loads issued before the stores. No terms: an all-zero table (raw 0).
+__device__ __forceinline__ void load_class_tab(uint8_t *tabs, const NamTab *__restrict__ sets,
+                                               const uint32_t *__restrict__ cls_key, uint32_t c, bool live,
+                                               uint32_t lane) {
+    constexpr uint32_t kVec = sizeof(NamTab) / 16;
+    const uint32_t sid = live ? cls_key[c] >> 1 : 0u;
+    const uint4 *src = reinterpret_cast<const uint4 *>(sets + (sid ? sid - 1u : 0u));
+    uint4 v[kVec];
+#pragma unroll
+    for (uint32_t k = 0; k < kVec; ++k) v[k] = sid ? src[k] : make_uint4(0, 0, 0, 0);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(tabs + lane * kNamTabStride);
+#pragma unroll
+    for (uint32_t k = 0; k < kVec; ++k) {
+        dst[4 * k] = v[k].x;
+        dst[4 * k + 1] = v[k].y;
+        dst[4 * k + 2] = v[k].z;
+        dst[4 * k + 3] = v[k].w;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// grid (class blocks of 64, segments): the segment's composed rescale table per
+// class, out[seg * stride + c].
+__global__ __launch_bounds__(64) void k_nam_seg(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
+                                                const NamTab *__restrict__ sets, uint32_t n_sets,
+                                                const uint32_t *__restrict__ ctl, const uint32_t *__restrict__ cls_key,
+                                                uint32_t stride, NamSeg *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t tile[kNamTile];
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
-    const uint32_t p = blockIdx.x * kNamThreads + tid;
-    uint32_t r0, r1;
-    seg_bounds(n_rows, seg_rows, blockIdx.y, r0, r1);
-    ms_pod_rec pod = {};
-    if (p < n_pods) pod = pods[p];
-    const NamTerms m = load_terms(pod, sets, n_sets);
-    const uint32_t tol = pod.tolerates_unschedulable ? 1u : 0u;
-    uint8_t *mine = tabs + tid * kNamStride;
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[64 * kNamStride];
+    __shared__ __attribute__((aligned(16))) uint8_t terms[64 * kNamTabStride];
+    const uint32_t lane = threadIdx.x, n_cls = ctl[0], c0 = blockIdx.x * 64u;
+    if (c0 >= n_cls) return;  // (workgroup-uniform)
+    const uint32_t c = c0 + lane;
+    const bool live = c < n_cls;
+    load_class_tab(terms, sets, cls_key, c, live, lane);
+    const uint8_t *tb = terms + lane * kNamTabStride;
+    const uint32_t tol = live ? (cls_key[c] & 1u) : 0u;
+    const uint32_t r0 = blockIdx.y * seg_rows, r1 = min(n_rows, r0 + seg_rows);
+    uint8_t *mine = tabs + lane * kNamStride;
     table_identity(mine);
     uint32_t any = 0, top = 100;  // top = T(100): 0 once the table is all 0
     for (uint32_t base = r0; base < r1; base += kNamTile) {
         const uint32_t nt = min(kNamTile, r1 - base);
-        // a lane is done once its table is all 0 and it has seen a non-zero node:
-        // nothing later in the segment changes its record (the workgroup stops
-        // when all its lanes are, a wave skips the tile's rows)
-        const bool done = p >= n_pods || (top == 0u && any);
-        if (__syncthreads_and(done)) break;
-        // (rows past nt up to a multiple of 4: absent, never feasible)
-        const uint32_t nt4 = (nt + 3u) & ~3u;
-        for (uint32_t i = tid; i < nt4; i += kNamThreads) tile[i] = i < nt ? nam_row_word(t, base + i) : 1u;
-        __syncthreads();
-        if (__ballot(!done) == 0) continue;  // (wave-uniform)
-        // four rows per step (one 16-B LDS broadcast): when no lane rescales at any
-        // of them (one ballot), their only effect is `any`; else they go one by one
+        // a lane is done once its table is all 0 and it has seen a non-zero node
+        const bool done = !live || (top == 0u && any);
+        if (__ballot(!done) == 0) break;  // (one wave: wave-uniform)
+        const uint32_t nt4 = (nt + 3u) & ~3u;  // (rows past nt: absent, never feasible)
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < nt4; i += 64u) tile[i] = i < nt ? nam_row_word(t, base + i) : 1u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // four rows per step: when no lane rescales at any of them (one ballot)
+        // their only effect is `any`; else they go one by one
         for (uint32_t i = 0; i < nt4; i += 4) {
             const uint4 w4 = *reinterpret_cast<const uint4 *>(tile + i);
             const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
@@ -212,12 +275,12 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n
             bool fv[4], resc = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                fv[k] = nam_feasible(wv[k], tol);
-                rv[k] = nam_raw(wv[k], m);
+                fv[k] = live && nam_feasible(wv[k], tol);
+                rv[k] = nam_raw(wv[k], tb);
                 any |= (fv[k] && rv[k] > 0u) ? 1u : 0u;
                 resc = resc || (fv[k] && rv[k] > 100u);
             }
-            if (__ballot(resc && top != 0u) == 0) continue;  // (wave-uniform)
+            if (__ballot(resc && top != 0u) == 0) continue;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t r = rv[k];
@@ -226,31 +289,32 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_seg(NodeTable t, uint32_t n
                     const uint32_t L = (uint32_t)__builtin_ctzll(b);
                     b &= b - 1u;
                     const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
-                    table_post(tabs + (wbase + L) * kNamStride, rl, lane);
+                    table_post(tabs + L * kNamStride, rl, lane);
                     __builtin_amdgcn_wave_barrier();
                     if (lane == L) top = mine[100];
                 }
             }
         }
     }
-    if (p >= n_pods) return;
+    if (!live) return;
     mine[101] = (uint8_t)any;
     mine[102] = mine[103] = 0;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(mine);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(out + (size_t)blockIdx.y * n_pods + p);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(out + (size_t)blockIdx.y * stride + c);
 #pragma unroll
     for (int k = 0; k < (int)(MS_NAM_SEG_BYTES / 4); ++k) dst[k] = src[k];
 }
 
-// Per pod: out = the composition of n segment records in order (in[s * stride + p], s
+// Per lane p < n_lanes: out = the composition of n records in order (in[s * stride + p], s
 // ascending: out.T = T_{n-1} o .. o T_0) and the OR of their "any". With skip_to:
 // only the records s > skip_to (a shard's suffix), and m_in gets the OR of the
-// records s < skip_to.
-__global__ void k_nam_compose(const NamSeg *__restrict__ in, uint32_t stride, uint32_t n, uint32_t n_pods,
-                              int32_t skip_to, NamSeg *__restrict__ out, uint8_t *__restrict__ m_in) {
+// records s < skip_to. n_live (optional): lanes past *n_live skip.
+__global__ void k_nam_compose(const NamSeg *__restrict__ in, uint32_t stride, uint32_t n, uint32_t n_lanes,
+                              int32_t skip_to, NamSeg *__restrict__ out, uint8_t *__restrict__ m_in,
+                              const uint32_t *__restrict__ n_live) {
     __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamComposeThreads * kNamStride];
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_pods) return;
+    if (p >= n_lanes || (n_live && p >= *n_live)) return;
     uint8_t *U = tabs + threadIdx.x * kNamStride;  // (LDS, not a dynamically indexed private array)
     table_identity(U);
     uint32_t any = 0, before = 0;
@@ -274,86 +338,91 @@ __global__ void k_nam_compose(const NamSeg *__restrict__ in, uint32_t stride, ui
     if (m_in) m_in[p] = (uint8_t)before;
 }
 
-// grid (pod blocks, segments): the segment's best packed key per pod (atomicMax
-// into keys). local: this context's segment records [n_segs][n_pods]; after /
-// m_in (node shards): the later shards' composed table and "an earlier shard has
-// a non-zero node" per pod, or null (single shard).
-__global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
-                                                          const ms_pod_rec *__restrict__ pods, uint32_t n_pods,
-                                                          const ms_nam_term_set *__restrict__ sets, uint32_t n_sets,
-                                                          uint32_t seed32, uint32_t w_nn, uint32_t w_na,
-                                                          const NamSeg *__restrict__ local, uint32_t n_segs,
-                                                          const NamSeg *__restrict__ after,
-                                                          const uint8_t *__restrict__ m_in, u64 *__restrict__ keys,
-                                                          const uint32_t *__restrict__ perm) {
+// Identity records (a shard without rows: no rescale, no non-zero node).
+__global__ void k_nam_identity(NamSeg *__restrict__ out, uint32_t n) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    uint8_t *o = out[p].T;
+    for (uint32_t v = 0; v <= 100u; ++v) o[v] = (uint8_t)v;
+    o[101] = o[102] = o[103] = 0;
+}
+
+// Per pod: out[p] = cls_rec[pcls[p]] (a shard's per-class records as the ABI's per-pod ones).
+__global__ void k_nam_expand(const NamSeg *__restrict__ cls_rec, const uint32_t *__restrict__ pcls, uint32_t n,
+                             NamSeg *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // (one thread per 4-B word)
+    constexpr uint32_t kW = MS_NAM_SEG_BYTES / 4;
+    if (i >= n * kW) return;
+    const uint32_t p = i / kW, w = i % kW;
+    reinterpret_cast<uint32_t *>(out + p)[w] = reinterpret_cast<const uint32_t *>(cls_rec + pcls[p])[w];
+}
+
+// Node name digit of a row word (0..9; 10 = none).
+__device__ __forceinline__ uint32_t word_digit(uint32_t w) {
+    const uint32_t d = w >> 24;
+    return d <= 9u ? d : 10u;
+}
+
+// grid (class blocks of 64, segments): every row's normalised NodeAffinity
+// score F[c * fpitch + row] for this class (0xFF: infeasible) and, per node
+// digit class, the class's maximum of F + 1 (fmax[c * 11 + d], atomicMax; 0:
+// no feasible row). local: k_nam_seg's records [seg][stride]; after / m_in
+// (node shards): the later shards' composed table and "an earlier shard has a
+// non-zero node", read at the class's representative pod, or null.
+__global__ __launch_bounds__(64) void k_nam_fscore(NodeTable t, uint32_t n_rows, uint32_t seg_rows,
+                                                   const NamTab *__restrict__ sets, uint32_t n_sets,
+                                                   const uint32_t *__restrict__ ctl,
+                                                   const uint32_t *__restrict__ cls_key,
+                                                   const uint32_t *__restrict__ rep, const NamSeg *__restrict__ local,
+                                                   uint32_t stride, uint32_t n_segs, const NamSeg *__restrict__ after,
+                                                   const uint8_t *__restrict__ m_in, uint8_t *__restrict__ F,
+                                                   uint32_t fpitch, uint32_t *__restrict__ fmax) {
     __shared__ __attribute__((aligned(16))) uint32_t tile[kNamTile];
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamThreads * kNamStride];
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wbase = tid & ~63u;
-    const uint32_t pi = blockIdx.x * kNamThreads + tid;
-    const bool live = pi < n_pods;
-    // lanes take the pods in name-digit order (perm, k_nam_perm): a wave's pods then
-    // mostly share the rows that can score NodeNumber's 10
-    const uint32_t p = live ? (perm ? perm[pi] : pi) : pi;
-    const uint32_t seg = blockIdx.y;
-    uint32_t r0, r1;
-    seg_bounds(n_rows, seg_rows, seg, r0, r1);
-    ms_pod_rec pod = {};
-    if (live) pod = pods[p];
-    const NamTerms m = load_terms(pod, sets, n_sets);
-    const uint32_t tol = pod.tolerates_unschedulable ? 1u : 0u;
-    const uint32_t pd = pod.name_digit >= 0 && pod.name_digit <= 9 ? (uint32_t)pod.name_digit : 14u;
-    const uint32_t A = tb_pod(seed32, pod.ordinal);
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[64 * kNamStride];
+    __shared__ __attribute__((aligned(16))) uint8_t terms[64 * kNamTabStride];
+    __shared__ uint32_t fm[64][12];
+    const uint32_t lane = threadIdx.x, n_cls = ctl[0], c0 = blockIdx.x * 64u, seg = blockIdx.y;
+    if (c0 >= n_cls) return;  // (workgroup-uniform)
+    const uint32_t c = c0 + lane;
+    const bool live = c < n_cls;
+    load_class_tab(terms, sets, cls_key, c, live, lane);
+    const uint8_t *tb = terms + lane * kNamTabStride;
+    const uint32_t tol = live ? (cls_key[c] & 1u) : 0u;
+    for (uint32_t d = 0; d < 12u; ++d) fm[lane][d] = 0u;
     // T_{>segment}: the later segments' tables, then the later shards'
-    uint8_t *mine = tabs + tid * kNamStride;
+    uint8_t *mine = tabs + lane * kNamStride;
     table_identity(mine);
-    uint32_t before = (live && m_in) ? m_in[p] : 0u;
+    const uint32_t rp = live ? rep[c] : 0u;
+    uint32_t before = (live && m_in) ? m_in[rp] : 0u;
     if (live) {
-        for (uint32_t s = 0; s < seg; ++s) before |= local[(size_t)s * n_pods + p].any;
+        for (uint32_t s = 0; s < seg; ++s) before |= local[(size_t)s * stride + c].any;
         for (uint32_t s = seg + 1; s < n_segs && mine[100] != 0; ++s) {
-            const uint8_t *T = local[(size_t)s * n_pods + p].T;
+            const uint8_t *T = local[(size_t)s * stride + c].T;
             for (uint32_t v = 0; v <= 100u; ++v) mine[v] = T[mine[v]];
         }
         if (after && mine[100] != 0) {
-            const uint8_t *T = after[p].T;
+            const uint8_t *T = after[rp].T;
             for (uint32_t v = 0; v <= 100u; ++v) mine[v] = T[mine[v]];
         }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     uint32_t top = mine[100];
-    // A row's key is hashed only when its score can reach the best so far (a lower
-    // score cannot win; an equal one needs its hash). The latest non-zero row
-    // (the anchor candidate) keeps its two scores and ordinal; it is hashed when
-    // committed.
-    u64 best = 0;
-    uint32_t cand_sreg = 0, cand_sanc = 0, cand_ord = 0;
+    // the latest non-zero row seen (in reverse: the earliest so far) is the anchor
+    // candidate: its T_{>j}(100) and row are kept; if it stays the first non-zero
+    // row of the cluster its F becomes that value
     bool cand = false;
+    uint32_t cand_row = 0, cand_top = 0, cand_dig = 0;
+    uint8_t *Fc = F + (size_t)c * fpitch;
+    const uint32_t r0 = seg * seg_rows, r1 = min(n_rows, r0 + seg_rows);
     const uint32_t n_tiles = r1 > r0 ? (r1 - r0 + kNamTile - 1u) / kNamTile : 0u;
-    // one row's candidate update (before its own rescale, which applies to earlier rows)
-    // Branch-light: at most one key is hashed per row (the row's own with a
-    // zero raw score, T(0) = 0, or -- a later non-zero node is not the anchor --
-    // the previous candidate's regular key), the candidate update is selects.
-    auto row_key = [&](uint32_t w, bool f, uint32_t r, uint32_t ord) {
-        const uint32_t sn = ((w >> 24) == pd) ? 10u * w_nn : 0u;
-        const uint32_t bs = (uint32_t)(best >> 52);
-        const bool nz = f && r != 0u;
-        const bool h0 = f && r == 0u && sn >= bs, h1 = nz && cand && cand_sreg >= bs;
-        if (h0 || h1) {
-            const uint32_t o = h0 ? ord : cand_ord, sc = h0 ? sn : cand_sreg;
-            best = umax64(best, make_key(sc, tb_hash(A, o), o));
-        }
-        const uint32_t mv = mine[min(r, 100u)];
-        cand = cand || nz;
-        cand_sreg = nz ? sn + w_na * mv : cand_sreg;
-        cand_sanc = nz ? sn + w_na * top : cand_sanc;
-        cand_ord = nz ? ord : cand_ord;
-    };
     for (uint32_t ti = n_tiles; ti-- > 0;) {  // tiles and rows in reverse LIST order
         const uint32_t base = r0 + ti * kNamTile, nt = min(kNamTile, r1 - base);
         const uint32_t nt4 = (nt + 3u) & ~3u;  // (rows past nt: absent, never feasible)
-        __syncthreads();
-        for (uint32_t i = tid; i < nt4; i += kNamThreads) tile[i] = i < nt ? nam_row_word(t, base + i) : 1u;
-        __syncthreads();
-        // four rows per step (one 16-B LDS broadcast, one ballot): while no lane
-        // rescales at any of them the table is fixed across the four
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < nt4; i += 64u) tile[i] = i < nt ? nam_row_word(t, base + i) : 1u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         for (uint32_t i4 = nt4; i4 > 0; i4 -= 4) {
             const uint4 w4 = *reinterpret_cast<const uint4 *>(tile + i4 - 4);
             const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
@@ -361,106 +430,263 @@ __global__ __launch_bounds__(kNamThreads) void k_nam_keys(NodeTable t, uint32_t 
             bool fv[4], resc = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                fv[k] = nam_feasible(wv[k], tol);
-                rv[k] = nam_raw(wv[k], m);
+                fv[k] = live && nam_feasible(wv[k], tol);
+                rv[k] = nam_raw(wv[k], tb);
                 resc = resc || (fv[k] && rv[k] > 100u);
             }
-            const uint32_t ord0 = t.base + base + i4 - 4;
-            if (__ballot(resc && top != 0u) == 0) {  // (wave-uniform)
-#pragma unroll
-                for (int k = 3; k >= 0; --k) row_key(wv[k], fv[k], rv[k], ord0 + k);
-                continue;
-            }
+            const bool fix = __ballot(resc && top != 0u) == 0;  // (wave-uniform) the table is fixed across the four
+            uint32_t packed = 0;
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
-                row_key(wv[k], fv[k], rv[k], ord0 + k);
                 const uint32_t r = rv[k];
-                uint64_t b = __ballot(fv[k] && r > 100u && top != 0u);
-                while (b) {  // (wave-uniform) this row's rescale applies to the earlier rows
-                    const uint32_t L = (uint32_t)__builtin_ctzll(b);
+                uint32_t f = 0xFFu;
+                if (fv[k]) {
+                    f = mine[min(r, 100u)];
+                    if (r != 0u) {
+                        cand = true;
+                        cand_row = base + i4 - 4 + (uint32_t)k;
+                        cand_top = top;
+                        cand_dig = word_digit(wv[k]);
+                    }
+                    atomicMax(&fm[lane][word_digit(wv[k])], f + 1u);
+                }
+                packed |= f << (8 * k);
+                if (!fix) {
+                    uint64_t b = __ballot(fv[k] && r > 100u && top != 0u);
+                    while (b) {  // (wave-uniform) this row's rescale applies to the earlier rows
+                        const uint32_t L = (uint32_t)__builtin_ctzll(b);
+                        b &= b - 1u;
+                        const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
+                        table_pre(tabs + L * kNamStride, rl, lane);
+                        if (lane == L) top = mine[100];
+                    }
+                }
+            }
+            if (live) *reinterpret_cast<uint32_t *>(Fc + base + i4 - 4) = packed;
+        }
+    }
+    if (!live) return;
+    // the segment's first non-zero row is the anchor unless an earlier segment or shard has one
+    if (cand && !before) {
+        Fc[cand_row] = (uint8_t)cand_top;
+        atomicMax(&fm[lane][cand_dig], cand_top + 1u);
+    }
+    for (uint32_t d = 0; d < kNamDigits; ++d)
+        if (fm[lane][d]) atomicMax(&fmax[(size_t)c * kNamDigits + d], fm[lane][d]);
+}
+
+// Bytes of a word that are zero: 0x80 in each (exact: no carries across bytes).
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t y) {
+    const uint32_t t = (y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return ~(t | y) & 0x80808080u;
+}
+
+// Per pod (lane = pod, pods in class-digit order): the packed key of the best
+// total over this context's rows. Row j's total is w_na F_j + w_nn 10 [digit_j
+// = the pod's]; the best S* follows from the class's maxima per digit, and
+// the rows reaching S* are the ones whose F equals t_nn (digit = the pod's) or
+// t_plain (else): compared four rows per word against a per-byte target chosen
+// by the digit mask dmask[d][row] (0xFF where the row's name digit is d), then
+// only those rows are hashed. keys[p] = the best key, or kKeyListed / 0 (this
+// context lists rows but none is feasible / lists none).
+__global__ __launch_bounds__(kNamPickThreads) void k_nam_pick(
+    const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const uint32_t *__restrict__ perm,
+    const uint32_t *__restrict__ pcls, const uint8_t *__restrict__ F, uint32_t fpitch,
+    const uint32_t *__restrict__ fmax, const uint8_t *__restrict__ dmask, uint32_t n_rows, uint32_t base,
+    uint32_t seed32, uint32_t w_nn, uint32_t w_na, uint32_t listed, u64 *__restrict__ keys) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < n_pods;
+    const uint32_t p = live ? perm[i] : 0u;
+    const ms_pod_rec pod = pods[p];
+    const uint32_t c = pcls[p], pd = nam_pod_digit(pod);
+    uint32_t fm[kNamDigits];
+    uint32_t fall = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < kNamDigits; ++d) {
+        fm[d] = fmax[(size_t)c * kNamDigits + d];
+        fall = max(fall, fm[d]);
+    }
+    const u64 best = listed ? kKeyListed : 0ull;
+    if (!live) return;
+    if (fall == 0u) {  // no feasible row here
+        keys[p] = best;
+        return;
+    }
+    uint32_t fpd = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 10u; ++d) fpd = d == pd ? fm[d] : fpd;
+    const uint32_t nn = 10u * w_nn;
+    const uint32_t s_plain = w_na * (fall - 1u), s_nn = fpd ? w_na * (fpd - 1u) + nn : 0u;
+    const uint32_t S = max(s_plain, fpd ? s_nn : 0u);
+    // the F a row needs to reach S: without / with the NodeNumber match (0xFE: none;
+    // 0xFF, infeasible, never equals either)
+    const uint32_t t_plain = (S % w_na == 0u && S / w_na <= 100u) ? S / w_na : 0xFEu;
+    const uint32_t t_nn = (pd <= 9u && S >= nn && (S - nn) % w_na == 0u && (S - nn) / w_na <= 100u) ? (S - nn) / w_na
+                                                                                                   : 0xFEu;
+    const uint32_t tp4 = t_plain * 0x01010101u, tn4 = t_nn * 0x01010101u;
+    const uint32_t A = tb_pod(seed32, pod.ordinal);
+    const uint8_t *Fc = F + (size_t)c * fpitch;
+    const uint8_t *Dd = dmask + (size_t)pd * fpitch;  // (row 10: all zero)
+    u64 top = 0;
+    for (uint32_t j = 0; j < n_rows; j += 16u) {
+        const uint4 f = *reinterpret_cast<const uint4 *>(Fc + j);
+        const uint4 m = *reinterpret_cast<const uint4 *>(Dd + j);
+        const uint32_t fw[4] = {f.x, f.y, f.z, f.w}, mw[4] = {m.x, m.y, m.z, m.w};
+        uint32_t z[4], any = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            z[k] = zero_bytes(fw[k] ^ ((tn4 & mw[k]) | (tp4 & ~mw[k])));
+            any |= z[k];
+        }
+        if (any) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t b = z[k];
+                while (b) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(b);
                     b &= b - 1u;
-                    const uint32_t rl = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)L);
-                    table_pre(tabs + (wbase + L) * kNamStride, rl, lane);
-                    if (lane == L) top = mine[100];
+                    const uint32_t ord = base + j + 4u * (uint32_t)k + (bit >> 3);
+                    top = umax64(top, make_key(S, tb_hash(A, ord), ord));
                 }
             }
         }
     }
-    if (!live) return;
-    // the segment's first non-zero node is the anchor unless an earlier segment or shard has one
-    if (cand) {
-        const uint32_t sc = before ? cand_sreg : cand_sanc;
-        best = umax64(best, make_key(sc, tb_hash(A, cand_ord), cand_ord));
-    }
-    if (best) atomicMax(keys + p, best);
+    keys[p] = umax64(best, top);
 }
 
-// The pods of a chunk in name-digit order (digits 0..9, then the rest): perm[i]
-// = the pod index lane i of k_nam_keys takes. One workgroup, LDS counting sort.
-__global__ __launch_bounds__(1024) void k_nam_perm(const ms_pod_rec *__restrict__ pods, uint32_t n,
-                                                   uint32_t *__restrict__ perm) {
-    __shared__ uint32_t cnt[11], off[11];
-    const uint32_t tid = threadIdx.x;
-    if (tid < 11u) cnt[tid] = 0u;
-    __syncthreads();
-    auto cls = [&](uint32_t i) {
-        const int d = pods[i].name_digit;
-        return d >= 0 && d <= 9 ? (uint32_t)d : 10u;
-    };
-    for (uint32_t i = tid; i < n; i += 1024u) atomicAdd(&cnt[cls(i)], 1u);
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t a = 0;
-        for (int k = 0; k < 11; ++k) {
-            off[k] = a;
-            a += cnt[k];
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += 1024u) perm[atomicAdd(&off[cls(i)], 1u)] = i;
+// dmask[d * fpitch + row] = 0xFF where row's name digit is d (d < 10), rows
+// past n_rows and row 10 all zero.
+__global__ void k_nam_dmask(NodeTable t, uint32_t n_rows, uint32_t fpitch, uint8_t *__restrict__ dmask) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= fpitch) return;
+    const uint32_t d = j < n_rows ? (uint32_t)t.digit[j] : 0xFFu;
+#pragma unroll
+    for (uint32_t k = 0; k < kNamDigits; ++k) dmask[(size_t)k * fpitch + j] = (k < 10u && d == k) ? 0xFFu : 0u;
 }
 
 inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
 }  // namespace
 
-uint32_t nam_segments(uint32_t n_rows, uint32_t *seg_rows) {
-    uint32_t sr = std::max(kNamSegRows, cdiv(std::max(n_rows, 1u), kNamMaxSegs));
-    sr = cdiv(sr, kNamTile) * kNamTile;
-    if (seg_rows) *seg_rows = sr;
-    return std::max(1u, cdiv(n_rows, sr));
+// Row segments for the per-class passes: enough (segment, class-block) waves to
+// spread over the chip, 64-row multiples (F is written four rows per word and
+// read sixteen per load; a segment never writes its neighbour's rows).
+NamLayout nam_layout(uint32_t n_rows, uint32_t cls_max) {
+    NamLayout L;
+    const uint32_t blocks = std::max(1u, cdiv(cls_max, 64u));
+    uint32_t segs = std::min(128u, std::max(16u, cdiv(512u, blocks)));
+    L.seg_rows = std::max(64u, cdiv(cdiv(std::max(n_rows, 1u), segs), 64u) * 64u);
+    L.segs = std::max(1u, cdiv(std::max(n_rows, 1u), L.seg_rows));
+    L.fpitch = cdiv(std::max(n_rows, 1u), 64u) * 64u;
+    L.cls_max = cls_max;
+    return L;
 }
 
-hipError_t launch_nam_seg(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                          const void *sets, uint32_t n_sets, void *segs, hipStream_t s) {
+size_t nam_scratch_bytes(const NamLayout &L, uint32_t n_pods, uint32_t n_sets) {
+    const size_t keys = 2ull * (n_sets + 1u);
+    return (size_t)L.segs * L.cls_max * sizeof(NamSeg)   // local
+           + (size_t)L.cls_max * sizeof(NamSeg)          // per-class composition (segment records)
+           + (size_t)L.cls_max * L.fpitch                // F
+           + (size_t)kNamDigits * L.fpitch               // dmask
+           + (size_t)L.cls_max * kNamDigits * 4          // fmax
+           + (keys + 16 + 3ull * L.cls_max + 2ull * n_pods) * 4 + 256;
+}
+
+namespace {
+struct NamScratch {
+    NamSeg *local, *comp;
+    uint8_t *F, *dmask;
+    uint32_t *fmax, *used, *ctl, *cls_key, *rep, *pcls, *perm;
+};
+NamScratch nam_carve(void *scratch, const NamLayout &L, uint32_t n_pods, uint32_t n_sets) {
+    char *b = static_cast<char *>(scratch);
+    NamScratch x;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        char *p = b + o;
+        o += (bytes + 255u) & ~size_t(255);
+        return p;
+    };
+    x.local = reinterpret_cast<NamSeg *>(take((size_t)L.segs * L.cls_max * sizeof(NamSeg)));
+    x.comp = reinterpret_cast<NamSeg *>(take((size_t)L.cls_max * sizeof(NamSeg)));
+    x.F = reinterpret_cast<uint8_t *>(take((size_t)L.cls_max * L.fpitch));
+    x.dmask = reinterpret_cast<uint8_t *>(take((size_t)kNamDigits * L.fpitch));
+    x.fmax = reinterpret_cast<uint32_t *>(take((size_t)L.cls_max * kNamDigits * 4));
+    x.used = reinterpret_cast<uint32_t *>(take(2ull * (n_sets + 1u) * 4));
+    x.ctl = reinterpret_cast<uint32_t *>(take(16 * 4));
+    x.cls_key = reinterpret_cast<uint32_t *>(take((size_t)L.cls_max * 4));
+    x.rep = reinterpret_cast<uint32_t *>(take((size_t)L.cls_max * 4));
+    x.pcls = reinterpret_cast<uint32_t *>(take((size_t)n_pods * 4));
+    x.perm = reinterpret_cast<uint32_t *>(take((size_t)n_pods * 4));
+    return x;
+}
+
+hipError_t nam_classes_and_segs(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                                const void *sets, uint32_t n_sets, const NamLayout &L, const NamScratch &x,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(k_nam_classes, dim3(1), dim3(kNamClsThreads), 0, s, pods, n_pods, n_sets, x.used, x.ctl,
+                       x.cls_key, x.rep, x.pcls, x.perm);
+    hipLaunchKernelGGL(k_nam_seg, dim3(cdiv(L.cls_max, 64u), L.segs), dim3(64), 0, s, t, n_rows, L.seg_rows,
+                       static_cast<const NamTab *>(sets), n_sets, (const uint32_t *)x.ctl,
+                       (const uint32_t *)x.cls_key, L.cls_max, x.local);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_nam_segment(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                              const void *sets, uint32_t n_sets, const NamLayout &L, void *scratch, void *out,
+                              hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
-    uint32_t sr = 0;
-    const uint32_t ns = nam_segments(n_rows, &sr);
-    hipLaunchKernelGGL(k_nam_seg, dim3(cdiv(n_pods, kNamThreads), ns), dim3(kNamThreads), 0, s, t, n_rows, sr, pods,
-                       n_pods, static_cast<const ms_nam_term_set *>(sets), n_sets, static_cast<NamSeg *>(segs));
+    if (n_pods > L.cls_max && L.cls_max < 2u * (n_sets + 1u)) return hipErrorInvalidValue;
+    const NamScratch x = nam_carve(scratch, L, n_pods, n_sets);
+    hipError_t e = nam_classes_and_segs(t, n_rows, pods, n_pods, sets, n_sets, L, x, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nam_compose, dim3(cdiv(L.cls_max, kNamComposeThreads)), dim3(kNamComposeThreads), 0, s,
+                       (const NamSeg *)x.local, L.cls_max, L.segs, L.cls_max, -1, x.comp, (uint8_t *)nullptr,
+                       (const uint32_t *)x.ctl);
+    const uint32_t words = n_pods * (MS_NAM_SEG_BYTES / 4);
+    hipLaunchKernelGGL(k_nam_expand, dim3(cdiv(words, 256u)), dim3(256), 0, s, (const NamSeg *)x.comp,
+                       (const uint32_t *)x.pcls, n_pods, static_cast<NamSeg *>(out));
+    return hipGetLastError();
+}
+
+hipError_t launch_nam_identity(void *out, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nam_identity, dim3(cdiv(n, 256u)), dim3(256), 0, s, static_cast<NamSeg *>(out), n);
     return hipGetLastError();
 }
 
 hipError_t launch_nam_compose(const void *in, uint32_t stride, uint32_t n, uint32_t n_pods, int32_t skip_to,
                               void *out, uint8_t *m_in, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_nam_compose, dim3(cdiv(n_pods, kNamComposeThreads)), dim3(kNamComposeThreads), 0, s, static_cast<const NamSeg *>(in),
-                       stride, n, n_pods, skip_to, static_cast<NamSeg *>(out), m_in);
+    hipLaunchKernelGGL(k_nam_compose, dim3(cdiv(n_pods, kNamComposeThreads)), dim3(kNamComposeThreads), 0, s,
+                       static_cast<const NamSeg *>(in), stride, n, n_pods, skip_to, static_cast<NamSeg *>(out), m_in,
+                       (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            const void *sets, uint32_t n_sets, uint32_t seed32, uint32_t w_nn, uint32_t w_na,
-                           const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys,
-                           uint32_t *perm, hipStream_t s) {
+                           const void *after, const uint8_t *m_in, uint32_t listed, const NamLayout &L,
+                           void *scratch, unsigned long long *keys, hipStream_t s) {
     if (n_pods == 0) return hipSuccess;
-    uint32_t sr = 0;
-    const uint32_t ns = nam_segments(n_rows, &sr);
-    if (perm) hipLaunchKernelGGL(k_nam_perm, dim3(1), dim3(1024), 0, s, pods, n_pods, perm);
-    hipLaunchKernelGGL(k_nam_keys, dim3(cdiv(n_pods, kNamThreads), ns), dim3(kNamThreads), 0, s, t, n_rows, sr, pods,
-                       n_pods, static_cast<const ms_nam_term_set *>(sets), n_sets, seed32, w_nn, w_na,
-                       static_cast<const NamSeg *>(local), ns, static_cast<const NamSeg *>(after), m_in, keys,
-                       static_cast<const uint32_t *>(perm));
+    if (n_pods > L.cls_max && L.cls_max < 2u * (n_sets + 1u)) return hipErrorInvalidValue;
+    const NamScratch x = nam_carve(scratch, L, n_pods, n_sets);
+    hipError_t e = nam_classes_and_segs(t, n_rows, pods, n_pods, sets, n_sets, L, x, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(x.fmax, 0, (size_t)L.cls_max * kNamDigits * 4, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(x.F, 0xFF, (size_t)L.cls_max * L.fpitch, s);  // (rows past n_rows: never tied)
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nam_dmask, dim3(cdiv(L.fpitch, 256u)), dim3(256), 0, s, t, n_rows, L.fpitch, x.dmask);
+    hipLaunchKernelGGL(k_nam_fscore, dim3(cdiv(L.cls_max, 64u), L.segs), dim3(64), 0, s, t, n_rows, L.seg_rows,
+                       static_cast<const NamTab *>(sets), n_sets, (const uint32_t *)x.ctl, (const uint32_t *)x.cls_key,
+                       (const uint32_t *)x.rep, (const NamSeg *)x.local, L.cls_max, L.segs,
+                       static_cast<const NamSeg *>(after), m_in, x.F, L.fpitch, x.fmax);
+    hipLaunchKernelGGL(k_nam_pick, dim3(cdiv(n_pods, kNamPickThreads)), dim3(kNamPickThreads), 0, s, pods, n_pods,
+                       (const uint32_t *)x.perm, (const uint32_t *)x.pcls, (const uint8_t *)x.F, L.fpitch,
+                       (const uint32_t *)x.fmax, (const uint8_t *)x.dmask, n_rows, t.base, seed32, w_nn, w_na, listed,
+                       reinterpret_cast<u64 *>(keys));
     return hipGetLastError();
 }
 

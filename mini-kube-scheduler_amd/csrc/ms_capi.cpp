@@ -47,7 +47,7 @@ void free_all(ms_ctx *c) {
     (void)hipSetDevice(c->cfg.device);
     comm_free(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void *dev[] = {c->t.planes, c->t.zone, c->t.label2, c->d_terms, c->d_nam, c->d_nam_perm, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
+    void *dev[] = {c->t.planes, c->t.zone, c->t.label2, c->d_terms, c->d_nam, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
                    c->d_tile_keys, c->d_tile_flags, c->d_spec, c->d_spec_flags, c->d_top4, c->d_top4_rec, c->d_prev, c->d_prev_rec, c->d_overflow,
@@ -439,36 +439,59 @@ int tt_summaries_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, vo
     return tt_cycle_locked(c, n_pods, d_pods, out, nullptr, 0, s);
 }
 
-// MS_PLUGINS_NU_NN_NAM scratch for chunks of n pods: the per-(segment, pod)
-// rescale tables, then one record (the later shards' table) and one byte (an
-// earlier shard has a non-zero node) per pod. Every NAM call runs on the
-// context stream or chains back into it, so one scratch serves them in order.
-int ensure_nam(ms_ctx *c, uint32_t n) {
-    const size_t need = ((size_t)nam_segments(c->rows_dev) + 1u) * n * MS_NAM_SEG_BYTES + n;
+// MS_PLUGINS_NU_NN_NAM: pods per chunk and the per-class passes' layout. A chunk
+// holds at most min(pods, 2 (n_sets + 1)) classes, and the per-class scores F
+// take classes x rows bytes: chunks shrink so F stays within kNamFBudget (only
+// with very many term sets; 64 sets at 50k rows: 130 classes, 6.5 MB).
+constexpr size_t kNamFBudget = 512ull << 20;
+
+uint32_t nam_chunk(const ms_ctx *c, uint32_t n_pods) {
+    uint32_t nb = std::min(c->batch_cap, n_pods);
+    const size_t rows = std::max<uint32_t>(64u, c->rows_dev);
+    const uint32_t cls_sets = 2u * (c->n_terms + 1u);
+    if ((size_t)std::min(nb, cls_sets) * rows > kNamFBudget)
+        nb = std::max<uint32_t>(256u, (uint32_t)std::min<size_t>(nb, kNamFBudget / rows));
+    return std::max(1u, nb);
+}
+
+NamLayout nam_layout_for(const ms_ctx *c, uint32_t nb) {
+    return nam_layout(c->rows_dev, std::max(1u, std::min(nb, 2u * (c->n_terms + 1u))));
+}
+
+// Scratch for chunks of nb pods (NamLayout), plus one record (the later shards'
+// table) and one byte (an earlier shard has a non-zero node) per pod. Every NAM
+// call runs on the context stream or chains back into it, so one scratch serves
+// them in order.
+int ensure_nam(ms_ctx *c, uint32_t nb) {
+    const size_t need = nam_scratch_bytes(nam_layout_for(c, nb), nb, c->n_terms) + (size_t)nb * (MS_NAM_SEG_BYTES + 1) + 512;
     if (need <= c->nam_bytes) return MS_OK;
     // (growing: a NodeAffinity call on a caller stream may still read the tables; as ensure_tt)
     if (c->d_nam) MS_HIP(c, hipDeviceSynchronize());
     if (c->d_nam) (void)hipFree(c->d_nam);
     c->d_nam = nullptr;
     c->nam_bytes = 0;
-    if (c->d_nam_perm) (void)hipFree(c->d_nam_perm);
-    c->d_nam_perm = nullptr;
-    if (hipMalloc(&c->d_nam, need) != hipSuccess ||
-        hipMalloc((void **)&c->d_nam_perm, sizeof(uint32_t) * std::max(1u, n)) != hipSuccess)
-        return fail(c, MS_E_OOM, "NodeAffinity rescale tables");
+    if (hipMalloc(&c->d_nam, need) != hipSuccess) return fail(c, MS_E_OOM, "NodeAffinity scratch");
     c->nam_bytes = need;
     return MS_OK;
 }
+// The per-pod shard inputs (after: nb records, m_in: nb bytes) past the layout's scratch.
+char *nam_after(ms_ctx *c, uint32_t nb) {
+    const size_t o = (nam_scratch_bytes(nam_layout_for(c, nb), nb, c->n_terms) + 255u) & ~size_t(255);
+    return static_cast<char *>(c->d_nam) + o;
+}
 
-// This shard's packed keys of nb pods into keys (chunk already sized): its row
-// segments' tables, then per segment the best key under the later segments' and
-// (after / m_in, node shards) the later shards' rescales.
+// This shard's packed keys of nb pods into keys (scratch sized for the chunk):
+// per class its rows' normalised scores under the later segments' and (after /
+// m_in, node shards) the later shards' rescales, then per pod the best key.
 int nam_keys_locked(ms_ctx *c, uint32_t nb, const ms_pod_rec *d_pods, const void *after, const uint8_t *m_in,
                     unsigned long long *keys, hipStream_t s) {
-    MS_HIP(c, launch_fill_keys(keys, nb, c->present_dev ? kKeyListed : 0ull, s));
-    MS_HIP(c, launch_nam_seg(c->t, c->rows_dev, d_pods, nb, c->d_terms, c->n_terms, c->d_nam, s));
+    if (c->rows_dev == 0) {
+        MS_HIP(c, launch_fill_keys(keys, nb, 0ull, s));
+        return MS_OK;
+    }
     MS_HIP(c, launch_nam_keys(c->t, c->rows_dev, d_pods, nb, c->d_terms, c->n_terms, seed32_of(c->cfg.seed), c->w_nn,
-                              c->w_na, c->d_nam, after, m_in, keys, c->d_nam_perm, s));
+                              c->w_na, after, m_in, c->present_dev ? 1u : 0u, nam_layout_for(c, nb), c->d_nam, keys,
+                              s));
     return MS_OK;
 }
 
@@ -476,8 +499,8 @@ int nam_keys_locked(ms_ctx *c, uint32_t nb, const ms_pod_rec *d_pods, const void
 // winner's NodeInfo.AddPod (stateless: no later pod reads it).
 int nam_cycle_locked(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_result *d_res, int commit,
                      hipStream_t s) {
-    const uint32_t B = c->batch_cap;
-    int rc = ensure_nam(c, std::min(B, n_pods));
+    const uint32_t B = nam_chunk(c, n_pods);
+    int rc = ensure_nam(c, B);
     if (rc) return rc;
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
@@ -1452,18 +1475,49 @@ int ms_tt_final_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, u
     return tt2_shard_epilogue(c, s);
 }
 
-int ms_nam_term_sets(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set *sets) {
-    if (!valid_ctx(c) || (n_sets && !sets) || n_sets > 0xFFFFu) return MS_E_INVAL;
-    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)
-        return fail(c, MS_E_INVAL, "ms_nam_term_sets: the multi-term NodeAffinity plugin set only");
-    for (uint32_t i = 0; i < n_sets; ++i)
-        for (int k = 0; k < MS_NAM_TERMS; ++k) {
-            const ms_pref_term &x = sets[i].term[k];
-            if (x.key > 1 || x.weight > 100)
-                return fail(c, MS_E_INVAL, "ms_nam_term_sets: term key must be 0 or 1 and weight 0..100");
-            // (value 0xFF is Exists; an In term names a value id 1..254, so a node label id
-            // of 255 matches Exists only: ZoneIds hands out at most 254 ids, ADVICE r5)
+// A term set in general form -> the device's lookup table (NamTab).
+static NamTab nam_tab_of(const ms_nam_term_set_ext &x) {
+    NamTab t{};
+    for (int k = 0; k < MS_NAM_TERMS; ++k) {
+        const ms_pref_term_ext &e = x.term[k];
+        if (e.weight == 0) continue;
+        for (uint32_t v = 0; v < 256u; ++v) {
+            if ((e.mask[0][v >> 5] >> (v & 31u)) & 1u) t.z[v] |= (uint8_t)(1u << k);
+            if ((e.mask[1][v >> 5] >> (v & 31u)) & 1u) t.l[v] |= (uint8_t)(1u << k);
         }
+    }
+    for (uint32_t m = 0; m < 16u; ++m) {
+        uint32_t w = 0;
+        for (int k = 0; k < MS_NAM_TERMS; ++k)
+            if ((m >> k) & 1u) w += x.term[k].weight;
+        t.wsum[m] = (uint16_t)w;
+    }
+    return t;
+}
+
+// ms_nam_term_set's {key, value} terms: In [value] (1..254) or Exists (0xFF) on
+// one key, all ids on the other; value 0 ("unlabelled") never matches.
+static ms_nam_term_set_ext nam_ext_of(const ms_nam_term_set &x) {
+    ms_nam_term_set_ext e{};
+    for (int k = 0; k < MS_NAM_TERMS; ++k) {
+        const ms_pref_term &t = x.term[k];
+        if (t.weight == 0 || t.value == 0) continue;
+        ms_pref_term_ext &o = e.term[k];
+        const int key = t.key ? 1 : 0;
+        for (int w = 0; w < 8; ++w) o.mask[1 - key][w] = ~0u;
+        if (t.value == 0xFFu) {
+            for (int w = 0; w < 8; ++w) o.mask[key][w] = ~0u;
+            o.mask[key][0] &= ~1u;
+        } else {
+            o.mask[key][t.value >> 5] |= 1u << (t.value & 31u);
+        }
+        o.weight = t.weight;
+    }
+    return e;
+}
+
+static int nam_install(ms_ctx *c, const std::vector<NamTab> &tabs, const char *who) {
+    const uint32_t n_sets = (uint32_t)tabs.size();
     std::lock_guard<std::mutex> g(c->sched_mu);
     MS_HIP(c, hipSetDevice(c->cfg.device));
     MS_HIP(c, hipDeviceSynchronize());  // (no cycle still reads the previous table; a configuration call)
@@ -1471,13 +1525,44 @@ int ms_nam_term_sets(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set *sets) {
         if (c->d_terms) (void)hipFree(c->d_terms);
         c->d_terms = nullptr;
         c->terms_cap = 0;
-        if (hipMalloc(&c->d_terms, (size_t)n_sets * sizeof(ms_nam_term_set)) != hipSuccess)
-            return fail(c, MS_E_OOM, "ms_nam_term_sets: term table");
+        if (hipMalloc(&c->d_terms, (size_t)n_sets * sizeof(NamTab)) != hipSuccess)
+            return fail(c, MS_E_OOM, std::string(who) + ": term table");
         c->terms_cap = n_sets;
     }
-    if (n_sets) MS_HIP(c, hipMemcpy(c->d_terms, sets, (size_t)n_sets * sizeof(ms_nam_term_set), hipMemcpyHostToDevice));
+    if (n_sets) MS_HIP(c, hipMemcpy(c->d_terms, tabs.data(), (size_t)n_sets * sizeof(NamTab), hipMemcpyHostToDevice));
     c->n_terms = n_sets;
     return MS_OK;
+}
+
+int ms_nam_term_sets(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set *sets) {
+    if (!valid_ctx(c) || (n_sets && !sets) || n_sets > 0xFFFFu) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)
+        return fail(c, MS_E_INVAL, "ms_nam_term_sets: the multi-term NodeAffinity plugin set only");
+    std::vector<NamTab> tabs(n_sets);
+    for (uint32_t i = 0; i < n_sets; ++i) {
+        for (int k = 0; k < MS_NAM_TERMS; ++k) {
+            const ms_pref_term &x = sets[i].term[k];
+            if (x.key > 1 || x.weight > 100)
+                return fail(c, MS_E_INVAL, "ms_nam_term_sets: term key must be 0 or 1 and weight 0..100");
+            // (value 0xFF is Exists; an In term names a value id 1..254, so a node label id
+            // of 255 matches Exists only: ZoneIds hands out at most 254 ids, ADVICE r5)
+        }
+        tabs[i] = nam_tab_of(nam_ext_of(sets[i]));
+    }
+    return nam_install(c, tabs, "ms_nam_term_sets");
+}
+
+int ms_nam_term_sets_ext(ms_ctx *c, uint32_t n_sets, const ms_nam_term_set_ext *sets) {
+    if (!valid_ctx(c) || (n_sets && !sets) || n_sets > 0xFFFFu) return MS_E_INVAL;
+    if (c->cfg.plugin_set != MS_PLUGINS_NU_NN_NAM)
+        return fail(c, MS_E_INVAL, "ms_nam_term_sets_ext: the multi-term NodeAffinity plugin set only");
+    std::vector<NamTab> tabs(n_sets);
+    for (uint32_t i = 0; i < n_sets; ++i) {
+        for (int k = 0; k < MS_NAM_TERMS; ++k)
+            if (sets[i].term[k].weight > 100) return fail(c, MS_E_INVAL, "ms_nam_term_sets_ext: weight 0..100");
+        tabs[i] = nam_tab_of(sets[i]);
+    }
+    return nam_install(c, tabs, "ms_nam_term_sets_ext");
 }
 
 int ms_nam_segment_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, void *seg_dev, void *stream) {
@@ -1492,14 +1577,18 @@ int ms_nam_segment_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);
     if (rc) return rc;
-    const uint32_t B = c->batch_cap, ns = nam_segments(c->rows_dev);
-    rc = ensure_nam(c, std::min(B, n_pods));
+    const uint32_t B = nam_chunk(c, n_pods);
+    rc = ensure_nam(c, B);
     if (rc) return rc;
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
-        MS_HIP(c, launch_nam_seg(c->t, c->rows_dev, pods_dev + s0, nb, c->d_terms, c->n_terms, c->d_nam, s));
-        MS_HIP(c, launch_nam_compose(c->d_nam, nb, ns, nb, -1, static_cast<char *>(seg_dev) + (size_t)s0 * MS_NAM_SEG_BYTES,
-                                     nullptr, s));
+        char *out = static_cast<char *>(seg_dev) + (size_t)s0 * MS_NAM_SEG_BYTES;
+        if (c->rows_dev == 0) {  // no rows: the identity map, no non-zero node
+            MS_HIP(c, launch_nam_identity(out, nb, s));
+            continue;
+        }
+        MS_HIP(c, launch_nam_segment(c->t, c->rows_dev, pods_dev + s0, nb, c->d_terms, c->n_terms,
+                                     nam_layout_for(c, nb), c->d_nam, out, s));
     }
     return chain_back(c, s);
 }
@@ -1519,12 +1608,11 @@ int ms_nam_keys_device(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *pods_dev, u
     hipStream_t s = pick_stream(c, stream);
     rc = order_after_ctx_stream(c, s);
     if (rc) return rc;
-    const uint32_t B = c->batch_cap, ns = nam_segments(c->rows_dev);
-    rc = ensure_nam(c, std::min(B, n_pods));
+    const uint32_t B = nam_chunk(c, n_pods);
+    rc = ensure_nam(c, B);
     if (rc) return rc;
-    const uint32_t nb_max = std::min(B, n_pods);
-    char *after = static_cast<char *>(c->d_nam) + (size_t)ns * nb_max * MS_NAM_SEG_BYTES;
-    uint8_t *m_in = reinterpret_cast<uint8_t *>(after + (size_t)nb_max * MS_NAM_SEG_BYTES);
+    char *after = nam_after(c, B);
+    uint8_t *m_in = reinterpret_cast<uint8_t *>(after + (size_t)B * MS_NAM_SEG_BYTES);
     for (uint32_t s0 = 0; s0 < n_pods; s0 += B) {
         const uint32_t nb = std::min(B, n_pods - s0);
         // the later shards' tables composed, and whether an earlier shard has a non-zero node

@@ -96,12 +96,11 @@ struct ms_ctx {
     // chained through the context stream)
     hipEvent_t ev_tt = nullptr;
     hipStream_t tt_stream = nullptr;
-    // MS_PLUGINS_NU_NN_NAM: the registered term sets (16 B each) and the per-(segment,
-    // pod) rescale compositions of a batch (nam_bytes allocated)
+    // MS_PLUGINS_NU_NN_NAM: the registered term sets as lookup tables (NamTab) and the
+    // per-class passes' scratch of a chunk (nam_bytes allocated)
     void *d_terms = nullptr;
     uint32_t n_terms = 0, terms_cap = 0;
     void *d_nam = nullptr;
-    uint32_t *d_nam_perm = nullptr;  // pods in name-digit order per chunk (k_nam_perm)
     size_t nam_bytes = 0;
     // node-sharded sequential mode: merged candidate lists (ms_seq_validate_device)
     ms_seq_cand *d_merged = nullptr;

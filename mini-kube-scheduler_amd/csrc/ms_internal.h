@@ -152,21 +152,39 @@ __host__ __device__ inline uint32_t tb_hash(uint32_t A, uint32_t node_ordinal) {
 __host__ __device__ inline uint32_t tb_unhash(uint32_t A, uint32_t h) { return (unmix32(h) - A) * kG24Inv; }
 
 // ---- MS_PLUGINS_NU_NN_NAM launchers (ms_affinity.hip) ----------------------
-// Row segments of a context (<= 16, >= 2048 rows each) and their rows per segment.
-uint32_t nam_segments(uint32_t n_rows, uint32_t *seg_rows = nullptr);
-// Per (segment, pod) composed rescale tables (MS_NAM_SEG_BYTES each, [seg][n_pods]).
-hipError_t launch_nam_seg(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
-                          const void *sets, uint32_t n_sets, void *segs, hipStream_t s);
+// A term set as the device reads it (built on the host from ms_nam_term_set(_ext)):
+// z[v] / l[v] bit t = term t (weight > 0) holds zone / label2 value id v; wsum[m]
+// = the weight sum of the terms in 4-bit mask m. raw = wsum[z[zone] & l[label2]].
+struct NamTab {
+    uint8_t z[256];
+    uint8_t l[256];
+    uint16_t wsum[16];
+};
+// Row segments and scratch shape of one call's per-class passes (cls_max = the
+// most classes a chunk can hold: min(pods, 2 (n_sets + 1))).
+struct NamLayout {
+    uint32_t segs = 1, seg_rows = 64, fpitch = 64, cls_max = 1;
+};
+NamLayout nam_layout(uint32_t n_rows, uint32_t cls_max);
+size_t nam_scratch_bytes(const NamLayout &L, uint32_t n_pods, uint32_t n_sets);
+// Node shards, step 1: per pod this context's composed rescale record (out:
+// MS_NAM_SEG_BYTES per pod), computed per class.
+hipError_t launch_nam_segment(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
+                              const void *sets, uint32_t n_sets, const NamLayout &L, void *scratch, void *out,
+                              hipStream_t s);
+// n identity records (a shard without rows).
+hipError_t launch_nam_identity(void *out, uint32_t n, hipStream_t s);
 // Per pod the composition of n records in[s * stride + p] (s ascending); skip_to >= 0:
 // only the records after skip_to, and m_in[p] = the OR of "any" of those before it.
 hipError_t launch_nam_compose(const void *in, uint32_t stride, uint32_t n, uint32_t n_pods, int32_t skip_to,
                               void *out, uint8_t *m_in, hipStream_t s);
-// Per pod the best packed key of this context's rows (atomicMax into keys): local =
-// launch_nam_seg's records; after / m_in as launch_nam_compose's outputs, or null.
+// Per pod the best packed key over this context's rows (keys[p] written; listed:
+// the context lists a row, so a pod with none feasible gets kKeyListed); after /
+// m_in: launch_nam_compose's outputs for these pods (node shards), or null.
 hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                            const void *sets, uint32_t n_sets, uint32_t seed32, uint32_t w_nn, uint32_t w_na,
-                           const void *local, const void *after, const uint8_t *m_in, unsigned long long *keys, uint32_t *perm,
-                           hipStream_t s);
+                           const void *after, const uint8_t *m_in, uint32_t listed, const NamLayout &L,
+                           void *scratch, unsigned long long *keys, hipStream_t s);
 
 // ---- launchers (ms_kernels.hip) -------------------------------------------
 // All return hipError_t of the launch; none synchronises.

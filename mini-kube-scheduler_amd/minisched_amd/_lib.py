@@ -108,6 +108,49 @@ NAM_SEG_BYTES = 104  # MS_NAM_SEG_BYTES
 NAM_TERMS = 4  # MS_NAM_TERMS
 
 
+NAM_TERM_EXT_BYTES = 68  # ms_pref_term_ext
+NAM_SET_EXT_BYTES = NAM_TERMS * NAM_TERM_EXT_BYTES  # ms_nam_term_set_ext
+_ALL_IDS = (1 << 256) - 1
+
+
+def nam_term_sets_ext_array(sets):
+    """ms_nam_term_set_ext records (uint8 (n, 272)) from a list of term lists
+    [(weight 0..100, zone id set, label2 id set), ...] (at most MS_NAM_TERMS
+    each); an id set is a Python int whose bit v holds value id v (0..255; bit 0:
+    the label is absent), e.g. encode.NamTerms builds them from requirements."""
+    out = np.zeros((len(sets), NAM_SET_EXT_BYTES), dtype=np.uint8)
+    for i, terms in enumerate(sets):
+        if len(terms) > NAM_TERMS:
+            raise ValueError(f"at most {NAM_TERMS} preferred terms per set")
+        for k, (weight, zmask, lmask) in enumerate(terms):
+            if not 0 <= weight <= 100 or not 0 <= zmask <= _ALL_IDS or not 0 <= lmask <= _ALL_IDS:
+                raise ValueError("term: weight 0..100, id sets within 256 bits")
+            b = k * NAM_TERM_EXT_BYTES
+            out[i, b:b + 32] = np.frombuffer(int(zmask).to_bytes(32, "little"), dtype=np.uint8)
+            out[i, b + 32:b + 64] = np.frombuffer(int(lmask).to_bytes(32, "little"), dtype=np.uint8)
+            out[i, b + 64] = weight
+    return out
+
+
+def nam_term_sets_to_ext(sets16):
+    """The 16-B form (nam_term_sets_array: {key, value, weight, 0} x 4, In [value] or
+    Exists = 0xFF on one key) as ms_nam_term_set_ext records: that key's set is
+    {value} or every id but 0, the other key's all ids (the library's own conversion)."""
+    a = np.asarray(sets16, dtype=np.uint8).reshape(-1, NAM_TERMS, 4)
+    sets = []
+    for row in a:
+        terms = []
+        for key, value, weight, _ in row:
+            key, value, weight = int(key), int(value), int(weight)
+            if weight == 0 or value == 0:
+                terms.append((0, 0, 0))
+                continue
+            m = (_ALL_IDS & ~1) if value == 0xFF else 1 << value
+            terms.append((weight, m, _ALL_IDS) if key == 0 else (weight, _ALL_IDS, m))
+        sets.append(terms)
+    return nam_term_sets_ext_array(sets)
+
+
 def nam_term_sets_array(sets):
     """ms_nam_term_set records (uint8 (n, 16)) from a list of term lists
     [(label key 0|1, value id 1..254 or 0xFF for Exists, weight 1..100), ...]
@@ -212,6 +255,7 @@ SIGNATURES = {
     "ms_tt_pick_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _u32, _vp, _vp, _vp]),
     "ms_tt_final_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp]),
     "ms_nam_term_sets": (ctypes.c_int, [_vp, _u32, _vp]),
+    "ms_nam_term_sets_ext": (ctypes.c_int, [_vp, _u32, _vp]),
     "ms_nam_segment_device": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp]),
     "ms_nam_keys_device": (ctypes.c_int, [_vp, _u32, _vp, _u32, _u32, _vp, _vp, _vp]),
     "ms_comm_id_create": (ctypes.c_int, [ctypes.POINTER(ms_comm_id)]),
@@ -484,6 +528,13 @@ class Engine:
         array); pod term set id s is row s - 1."""
         raw = np.ascontiguousarray(np.asarray(sets, dtype=np.uint8).reshape(-1, 16))
         self._check("ms_nam_term_sets", self.lib.ms_nam_term_sets(self.h, len(raw), raw.ctypes.data if len(raw) else None))
+
+    def nam_term_sets_ext(self, sets):
+        """The general form (ABI 7): uint8 (n, 272) ms_nam_term_set_ext records
+        (nam_term_sets_ext_array)."""
+        raw = np.ascontiguousarray(np.asarray(sets, dtype=np.uint8).reshape(-1, NAM_SET_EXT_BYTES))
+        self._check("ms_nam_term_sets_ext",
+                    self.lib.ms_nam_term_sets_ext(self.h, len(raw), raw.ctypes.data if len(raw) else None))
 
     def nam_segment_device(self, n_pods, pods_dev, seg_dev, stream=0):
         """Node-sharded multi-term NodeAffinity, step 1: this shard's rescale record per pod."""

@@ -33,6 +33,7 @@ NodeResourcesFit read no resources at all (pod_records(check_resources=False)).
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -227,6 +228,111 @@ def unsupported_request(p: Pod) -> Optional[str]:
             if name not in DEVICE_RESOURCES:
                 return name
     return None
+
+
+# ---- MS_PLUGINS_NU_NN_NAM: preferred NodeAffinity terms in general form (ABI 7) ----
+NAM_OPERATORS = ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt")
+_INT64 = re.compile(r"^[+-]?[0-9]+$")
+
+
+class UnsupportedTerm(ValueError):
+    """A preferred term the device records cannot express (a requirement on a
+    label key other than the two encoded ones, more than MS_NAM_TERMS terms)."""
+
+
+@dataclass(frozen=True)
+class NodeSelectorRequirement:
+    key: str
+    operator: str  # In, NotIn, Exists, DoesNotExist, Gt, Lt
+    values: Tuple[str, ...] = ()
+
+
+@dataclass
+class PreferredTerm:
+    weight: int  # 1..100 (API validation)
+    requirements: List[NodeSelectorRequirement] = field(default_factory=list)
+
+
+def parse_int64(v: str) -> Optional[int]:
+    """strconv.ParseInt(v, 10, 64), None on error."""
+    if not _INT64.match(v):
+        return None
+    x = int(v)
+    return x if -(1 << 63) <= x < (1 << 63) else None
+
+
+def requirement_holds(req: NodeSelectorRequirement, value: Optional[str]) -> bool:
+    """k8s.io/apimachinery labels.Requirement.Matches on one label (value None:
+    the node lacks the key), for the operators NodeSelectorRequirement maps to
+    (k8s@v1.22.0 component-helpers nodeaffinity nodeSelectorRequirementsAsSelector)."""
+    op = req.operator
+    if op == "In":
+        return value is not None and value in req.values
+    if op == "NotIn":
+        return value is None or value not in req.values
+    if op == "Exists":
+        return value is not None
+    if op == "DoesNotExist":
+        return value is None
+    if op in ("Gt", "Lt"):
+        if value is None:
+            return False
+        x = parse_int64(value)
+        if x is None:
+            return False
+        bound = parse_int64(req.values[0])
+        return x > bound if op == "Gt" else x < bound
+    raise UnsupportedTerm(f"operator {op!r}")
+
+
+class NamTerms:
+    """Term sets of MS_PLUGINS_NU_NN_NAM in general form (ms_nam_term_set_ext):
+    label key 0 is the zone label, key 1 `label2_key`; value ids come from the two
+    tables the node records use (ZoneIds). Per term and key the id set holds id v
+    when every requirement of the term on that key holds for value v (bit 0: for
+    a node without the label); a key without requirements holds every id. A term
+    with no requirement matches no node (an empty nodeSelectorTerm). Ids a table
+    has not handed out yet are left out: the shim re-registers its sets when a
+    table grows (NotIn, Exists, DoesNotExist, Gt and Lt cover new values too)."""
+
+    def __init__(self, label2_key: str, zone_ids: "ZoneIds", label2_ids: "ZoneIds"):
+        self.keys = (ZONE_LABEL, label2_key)
+        self.tables = (zone_ids, label2_ids)
+
+    def id_set(self, k: int, reqs: List[NodeSelectorRequirement]) -> int:
+        m = 0
+        for value, vid in [(None, 0)] + list(self.tables[k].ids.items()):
+            if all(requirement_holds(r, value) for r in reqs):
+                m |= 1 << vid
+        return m
+
+    def term(self, t: PreferredTerm) -> Tuple[int, int, int]:
+        if not 1 <= t.weight <= 100:
+            raise ValueError("PreferredSchedulingTerm weight must be in 1..100 (API validation)")
+        for r in t.requirements:
+            if r.key not in self.keys:
+                raise UnsupportedTerm(f"requirement on label {r.key!r}: the records carry {self.keys} only")
+            if r.operator not in NAM_OPERATORS:
+                raise UnsupportedTerm(f"operator {r.operator!r}")
+            if r.operator in ("In", "NotIn") and not r.values:
+                raise ValueError(f"{r.operator} needs values (API validation)")
+            if r.operator in ("Exists", "DoesNotExist") and r.values:
+                raise ValueError(f"{r.operator} takes no values (API validation)")
+            if r.operator in ("Gt", "Lt") and (len(r.values) != 1 or parse_int64(r.values[0]) is None):
+                raise ValueError(f"{r.operator} needs one integer value (API validation)")
+        if not t.requirements:
+            return (t.weight, 0, 0)
+        return (t.weight,) + tuple(self.id_set(k, [r for r in t.requirements if r.key == self.keys[k]])
+                                   for k in (0, 1))
+
+    def term_sets(self, sets: List[List[PreferredTerm]]) -> np.ndarray:
+        """uint8 (n, 272) ms_nam_term_set_ext records; set i is term set id i + 1."""
+        from ._lib import NAM_TERMS, nam_term_sets_ext_array
+
+        for terms in sets:
+            if len(terms) > NAM_TERMS:
+                raise UnsupportedTerm(f"more than {NAM_TERMS} preferred terms")
+        return nam_term_sets_ext_array([[self.term(t) for t in terms] for terms in sets])
 
 
 def pod_requests(p: Pod, check_resources: bool = True):

@@ -154,6 +154,54 @@ def nam_term_sets(k: int, seed: int = 1) -> np.ndarray:
     return nam_term_sets_array(sets)
 
 
+def nam_term_sets_ext(k: int, seed: int = 1, n_zone: int = N_ZONES, n_label2: int = N_LABEL2) -> np.ndarray:
+    """K random term sets in general form (uint8 (K, 272), ms_nam_term_set_ext): 1..4
+    terms with requirements on one or both keys, each In (1-3 ids), NotIn (all
+    but 1-3 ids, the absent label included), Exists, DoesNotExist, or Gt / Lt
+    (the ids above / below a threshold, as a shim whose value ids follow the
+    numeric label values would give them); about 1 term in 16 has no requirement
+    (matches nothing); weights 1..100. Value ids up to 255 (id 255 appears)."""
+    from ._lib import nam_term_sets_ext_array
+
+    rng = np.random.default_rng(int(seed) * 7919 + k)
+    top = {0: n_zone, 1: n_label2}
+
+    def ids(kk):
+        pool = list(range(1, top[kk] + 1)) + [255]
+        return [int(x) for x in rng.choice(pool, size=int(rng.integers(1, 4)), replace=False)]
+
+    def req_mask(kk):
+        op = int(rng.integers(0, 6))
+        full = (1 << 256) - 1
+        if op == 0:  # In
+            return sum(1 << v for v in set(ids(kk)))
+        if op == 1:  # NotIn
+            return full & ~sum(1 << v for v in set(ids(kk)))
+        if op == 2:  # Exists
+            return full & ~1
+        if op == 3:  # DoesNotExist
+            return 1
+        t = int(rng.integers(0, top[kk] + 1))
+        return sum(1 << v for v in range(t + 1, 256)) if op == 4 else sum(1 << v for v in range(1, t))
+
+    sets = []
+    for _ in range(k):
+        terms = []
+        for _ in range(int(rng.integers(1, 5))):
+            w = int(rng.integers(1, 101))
+            if rng.integers(0, 16) == 0:
+                terms.append((w, 0, 0))
+                continue
+            which = int(rng.integers(0, 3))  # 0: zone only, 1: label2 only, 2: both
+            zm = req_mask(0) if which in (0, 2) else (1 << 256) - 1
+            lm = req_mask(1) if which in (1, 2) else (1 << 256) - 1
+            if which == 2 and rng.integers(0, 3) == 0:
+                zm &= req_mask(0)  # two requirements on one key: ANDed
+            terms.append((w, zm, lm))
+        sets.append(terms)
+    return nam_term_sets_ext_array(sets)
+
+
 def set_tolerations(rec: np.ndarray, tol_hard, tol_soft) -> None:
     """MS_PLUGINS_NU_TT_NN: bit t of tol_hard / tol_soft = some toleration of the
     pod tolerates NoSchedule / PreferNoSchedule taint id t (ms_pod_rec.tol_hard,

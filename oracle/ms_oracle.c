@@ -407,18 +407,44 @@ int msor_schedule_na(const msor_nodes *nd, const msor_pods *pd, int64_t w_nn, in
 
 /* k8s@v1.22.0:pkg/scheduler/framework/plugins/nodeaffinity/node_affinity.go
  * Score: for each PreferredSchedulingTerm with a non-zero weight whose
- * NodeSelectorTerm matches the node, count += weight. Terms here test one
- * label key (0: topology.kubernetes.io/zone, 1: the second label) with
- * operator In [one value] or Exists (value 0xFF). */
+ * NodeSelectorTerm matches the node, count += weight. A term (general form,
+ * MSOR_NAM_EXT_BYTES per set) holds per label key (0: the zone label, 1: the
+ * second label) the set of value ids for which every requirement of the term on
+ * that key holds (id 0 = the label is absent; the shim derives the sets from
+ * In / NotIn / Exists / DoesNotExist / Gt / Lt, tests/_pyref.py restates those
+ * on label strings); it matches a node whose two ids are both in its sets. */
+static int nam_bit(const uint8_t *mask, uint32_t v) { /* bit v of 8 little-endian u32 words */
+    return (mask[4 * (v >> 5) + ((v & 31u) >> 3)] >> (v & 7u)) & 1;
+}
 static int64_t nam_raw(const msor_nodes *nd, uint32_t i, const uint8_t *set) {
     int64_t r = 0;
     for (int t = 0; t < MSOR_NAM_TERMS; ++t) {
-        const uint8_t key = set[4 * t], val = set[4 * t + 1], w = set[4 * t + 2];
+        const uint8_t *term = set + MSOR_NAM_TERM_BYTES * t;
+        const uint8_t w = term[64];
         if (w == 0) continue;
-        const uint8_t lab = key == 0 ? nd->zone[i] : nd->label2[i];
-        if (lab != 0 && (val == 0xFF || lab == val)) r += w;
+        if (nam_bit(term, nd->zone[i]) && nam_bit(term + 32, nd->label2[i])) r += w;
     }
     return r;
+}
+
+/* The 16-B form {key, value, weight, 0} x 4 (In [value] or Exists on one key) as
+ * the general form: that key's set is {value} or every id but 0, the other's all. */
+static void nam_set_to_ext(const uint8_t *set, uint8_t *ext) {
+    memset(ext, 0, MSOR_NAM_EXT_BYTES);
+    for (int t = 0; t < MSOR_NAM_TERMS; ++t) {
+        const uint8_t key = set[4 * t], val = set[4 * t + 1], w = set[4 * t + 2];
+        uint8_t *term = ext + MSOR_NAM_TERM_BYTES * t;
+        if (w == 0 || val == 0) continue; /* unused slot, or "unlabelled": never matches */
+        uint8_t *km = term + 32 * (key ? 1 : 0), *om = term + 32 * (key ? 0 : 1);
+        memset(om, 0xFF, 32);
+        if (val == 0xFF) {
+            memset(km, 0xFF, 32);
+            km[0] &= 0xFEu;
+        } else {
+            km[val >> 3] |= (uint8_t)(1u << (val & 7u));
+        }
+        term[64] = w;
+    }
 }
 
 /* Closed form of the in-loop hook for reverse=false: once an
@@ -464,11 +490,25 @@ int msor_nam_inloop(const int64_t *r, uint32_t F, int literal, int64_t *out) {
 int msor_schedule_nam(const msor_nodes *nd, const msor_pods *pd, const uint8_t *term_sets, uint32_t n_sets,
                       int64_t w_nn, int64_t w_na, int literal, uint64_t seed, uint32_t node_base, int32_t *out_node,
                       int64_t *out_score, int32_t *out_code, uint32_t *out_mask, uint64_t *out_key) {
+    if (n_sets && !term_sets) return -1;
+    uint8_t *ext = (uint8_t *)malloc((size_t)MSOR_NAM_EXT_BYTES * (n_sets ? n_sets : 1));
+    if (!ext) return -1;
+    for (uint32_t s = 0; s < n_sets; ++s) nam_set_to_ext(term_sets + 16u * s, ext + (size_t)MSOR_NAM_EXT_BYTES * s);
+    const int rc = msor_schedule_nam_ext(nd, pd, ext, n_sets, w_nn, w_na, literal, seed, node_base, out_node,
+                                         out_score, out_code, out_mask, out_key);
+    free(ext);
+    return rc;
+}
+
+int msor_schedule_nam_ext(const msor_nodes *nd, const msor_pods *pd, const uint8_t *term_sets, uint32_t n_sets,
+                          int64_t w_nn, int64_t w_na, int literal, uint64_t seed, uint32_t node_base,
+                          int32_t *out_node, int64_t *out_score, int32_t *out_code, uint32_t *out_mask,
+                          uint64_t *out_key) {
     if (!nd || !pd || !nd->flags || !nd->digit || !nd->zone || !nd->label2 || !pd->ordinal || !pd->digit || !pd->tol ||
         !pd->pref_zone || !pd->pref_weight || (n_sets && !term_sets))
         return -1;
     if ((uint64_t)node_base + nd->n >= 0xFFFFFu) return -1;
-    static const uint8_t none[4 * MSOR_NAM_TERMS] = {0};
+    static const uint8_t none[MSOR_NAM_EXT_BYTES] = {0};
     uint32_t *feas = (uint32_t *)malloc(sizeof(uint32_t) * (nd->n ? nd->n : 1));
     int64_t *raw = (int64_t *)malloc(sizeof(int64_t) * (nd->n ? nd->n : 1));
     int64_t *na = (int64_t *)malloc(sizeof(int64_t) * (nd->n ? nd->n : 1));
@@ -476,8 +516,8 @@ int msor_schedule_nam(const msor_nodes *nd, const msor_pods *pd, const uint8_t *
     int rc = 0;
     for (uint32_t j = 0; j < pd->n; ++j) {
         const uint32_t sid = (uint32_t)pd->pref_zone[j] | (uint32_t)pd->pref_weight[j] << 8;
-        if (sid > n_sets) { rc = -1; break; }
-        const uint8_t *set = sid ? term_sets + 16u * (sid - 1u) : none;
+        /* (ids past the registered sets count as no terms: minisched_gpu.h ms_nam_term_sets) */
+        const uint8_t *set = (sid && sid <= n_sets) ? term_sets + (size_t)MSOR_NAM_EXT_BYTES * (sid - 1u) : none;
         /* RunFilterPlugins (minisched.go:115-151): NodeUnschedulable only */
         uint32_t F = 0, mask = 0;
         for (uint32_t i = 0; i < nd->n; ++i) {

@@ -141,6 +141,17 @@ int msor_schedule_na(const msor_nodes *nodes, const msor_pods *pods, int64_t w_n
 int msor_schedule_nam(const msor_nodes *nodes, const msor_pods *pods, const uint8_t *term_sets, uint32_t n_sets,
                       int64_t w_nn, int64_t w_na, int literal, uint64_t seed, uint32_t node_base, int32_t *out_node,
                       int64_t *out_score, int32_t *out_code, uint32_t *out_mask, uint64_t *out_key);
+/* The same with term sets in general form (minisched_gpu.h ms_nam_term_set_ext):
+ * MSOR_NAM_EXT_BYTES per set, four terms of MSOR_NAM_TERM_BYTES: two 256-bit
+ * value-id sets (8 little-endian u32 each: the zone label's, then label2's; bit
+ * 0 = the label is absent), weight (0..100), 3 pad bytes. A term matches a node
+ * whose zone id and label2 id are both in its sets. */
+#define MSOR_NAM_TERM_BYTES 68
+#define MSOR_NAM_EXT_BYTES (4 * MSOR_NAM_TERM_BYTES)
+int msor_schedule_nam_ext(const msor_nodes *nodes, const msor_pods *pods, const uint8_t *term_sets, uint32_t n_sets,
+                          int64_t w_nn, int64_t w_na, int literal, uint64_t seed, uint32_t node_base,
+                          int32_t *out_node, int64_t *out_score, int32_t *out_code, uint32_t *out_mask,
+                          uint64_t *out_key);
 /* The in-loop reverse=false hook on one list of raw scores r[0..F) (any
  * non-negative values): literal=1 the loop as written, 0 the closed form
  * (out[k] = T_{>k}(v_k), T_{>k} the composition of v -> floor(100 v / r_i) over

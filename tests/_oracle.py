@@ -110,6 +110,8 @@ def lib():
             ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ]
+        L.msor_schedule_nam_ext.restype = ctypes.c_int
+        L.msor_schedule_nam_ext.argtypes = L.msor_schedule_nam.argtypes
         L.msor_nam_inloop.restype = ctypes.c_int
         L.msor_nam_inloop.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
         L.msor_tt_inloop.restype = ctypes.c_int
@@ -268,6 +270,24 @@ def schedule_nam(node_recs, pods, term_sets, weights=(1, 1), literal=True, seed=
     ts = np.ascontiguousarray(np.asarray(term_sets, dtype=np.uint8).reshape(-1, 16))
     o = _outs(len(pods))
     rc = L.msor_schedule_nam(
+        ctypes.byref(nst), ctypes.byref(pst), ts.ctypes.data if len(ts) else None, len(ts), int(weights[0]),
+        int(weights[1]), 1 if literal else 0, seed, node_base,
+        _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),
+    )
+    assert rc == 0, "oracle rejected its arguments"
+    return o
+
+
+def schedule_nam_ext(node_recs, pods, term_sets_ext, weights=(1, 1), literal=True, seed=1, node_base=0):
+    """msor_schedule_nam_ext: the same with general term sets (uint8 (n, 272)
+    ms_nam_term_set_ext records, _lib.nam_term_sets_ext_array)."""
+    L = lib()
+    cols = NodeCols(node_recs)
+    nst = cols.struct()
+    pc, pst = _pod_cols(pods)
+    ts = np.ascontiguousarray(np.asarray(term_sets_ext, dtype=np.uint8).reshape(-1, 272))
+    o = _outs(len(pods))
+    rc = L.msor_schedule_nam_ext(
         ctypes.byref(nst), ctypes.byref(pst), ts.ctypes.data if len(ts) else None, len(ts), int(weights[0]),
         int(weights[1]), 1 if literal else 0, seed, node_base,
         _p(o["node"]), _p(o["score"]), _p(o["code"]), _p(o["mask"]), _p(o["key"]),

@@ -180,3 +180,84 @@ def schedule_na(nodes, pods, weights=(1, 1), seed=1):
                 best, best_k = kk, k
         out.append((0, feasible[best_k], total[best_k], 0))
     return out
+
+
+# ---- MS_PLUGINS_NU_NN_NAM on v1-style objects --------------------------------
+def _parse_int64(v):
+    """strconv.ParseInt(v, 10, 64); None on error (restated here on purpose, not
+    imported: the encoder's id sets are checked against this)."""
+    s = v[1:] if v[:1] in ("+", "-") else v
+    if not s or not all("0" <= c <= "9" for c in s):
+        return None
+    x = int(v)
+    return x if -(1 << 63) <= x <= (1 << 63) - 1 else None
+
+
+def requirement_matches(req, labels):
+    """labels.Requirement.Matches (k8s.io/apimachinery, the operators a
+    NodeSelectorRequirement maps to in k8s@v1.22.0 component-helpers)."""
+    has = req.key in labels
+    v = labels.get(req.key)
+    if req.operator == "In":
+        return has and v in req.values
+    if req.operator == "NotIn":
+        return (not has) or v not in req.values
+    if req.operator == "Exists":
+        return has
+    if req.operator == "DoesNotExist":
+        return not has
+    if req.operator in ("Gt", "Lt"):
+        if not has:
+            return False
+        x, b = _parse_int64(v), _parse_int64(req.values[0])
+        if x is None or b is None:
+            return False
+        return x > b if req.operator == "Gt" else x < b
+    raise ValueError(req.operator)
+
+
+def term_matches(term, labels):
+    """nodeSelectorTerm.match: an empty term matches nothing; else every requirement."""
+    return bool(term.requirements) and all(requirement_matches(r, labels) for r in term.requirements)
+
+
+def nam_raw(terms, labels):
+    """NodeAffinity.Score: the sum of the weights of the matching preferred terms."""
+    return sum(t.weight for t in terms if t.weight > 0 and term_matches(t, labels))
+
+
+def schedule_nam(nodes, pods, pod_terms, weights=(1, 1), seed=1):
+    """MS_PLUGINS_NU_NN_NAM, minisched.go:164-199 as written (the in-loop
+    DefaultNormalizeScore on the whole NodeAffinity list after every node):
+    pod_terms[j] = the pod's list of PreferredTerm objects."""
+    out = []
+    for j, pod in enumerate(pods):
+        tol = tolerates_unschedulable(pod.tolerations)
+        feasible, plugins = [], 0
+        for i, n in enumerate(nodes):
+            if n.unschedulable and not tol:
+                plugins |= MASK_NU
+                continue
+            feasible.append(i)
+        if not feasible:
+            out.append((2, -1, 0, plugins))
+            continue
+        podnum = name_digit(pod.name)
+        if podnum < 0:
+            out.append((1, -1, 0, 0))
+            continue
+        nn = [0] * len(feasible)
+        na = [0] * len(feasible)
+        for k, i in enumerate(feasible):
+            d = name_digit(nodes[i].name)
+            nn[k] = 10 if (d >= 0 and d == podnum) else 0
+            na[k] = nam_raw(pod_terms[j], nodes[i].labels)
+            default_normalize_score(100, False, na)
+        total = [weights[0] * a + weights[1] * b for a, b in zip(nn, na)]
+        best, best_k = -1, -1
+        for k, i in enumerate(feasible):
+            kk = key(total[k], h32(seed, pod.ordinal, i), i)
+            if kk > best:
+                best, best_k = kk, k
+        out.append((0, feasible[best_k], total[best_k], 0))
+    return out

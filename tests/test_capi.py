@@ -69,7 +69,7 @@ def test_library_links_rccl():
 
 def test_abi_version_and_no_device_error_path():
     lib = _lib.load()
-    assert lib.ms_abi_version() == 6  # round 5: MS_PLUGINS_NU_NN_NAM, label2 (5); two-pass TT shard calls (6)
+    assert lib.ms_abi_version() == 7  # round 5: NAM, label2 (5); two-pass TT shard calls (6); round 6: ext term sets (7)
     if _lib.device_count() > 0:
         pytest.skip("a device is visible; the no-device path is exercised on CPU hosts")
     cfg = _lib.ms_config(0, 0, 16, 0, 64, (ctypes.c_uint16 * 2)(), 1)

@@ -34,20 +34,28 @@ def _cluster(n_nodes, n_pods, n_sets, seed):
     return nr, pr, synth.nam_term_sets(n_sets, seed=seed)
 
 
+def _ext(ts):
+    return np.asarray(ts).ndim == 2 and np.asarray(ts).shape[1] == _lib.NAM_SET_EXT_BYTES
+
+
 def _oracle(oracle, nr, pr, ts, seed, weights=(1, 1), dead=()):
     # the literal loop is O(F^2) per pod: up to 3,000 nodes; above, its closed form
     # (checked against the loop in tests/test_oracle_nam.py and here on the small ones)
     nr = nr.copy()
     if len(dead):
         nr["allowed_pods"][np.asarray(dead)] = -1
-    return oracle.schedule_nam(nr, pr, ts, weights=weights, literal=len(nr) <= 3000, seed=seed)
+    run = oracle.schedule_nam_ext if _ext(ts) else oracle.schedule_nam
+    return run(nr, pr, ts, weights=weights, literal=len(nr) <= 3000, seed=seed)
 
 
 def _engine(nr, ts, seed, lo=0, hi=None, dead=(), weights=(0, 0), max_batch=1 << 16):
     hi = len(nr) if hi is None else hi
     e = _lib.Engine(max_nodes=max(1, hi - lo), plugin_set=NAM, node_base=lo, seed=seed, score_weights=weights,
                     max_batch=max_batch)
-    e.nam_term_sets(ts)
+    if _ext(ts):
+        e.nam_term_sets_ext(ts)
+    else:
+        e.nam_term_sets(ts)
     e.upsert(np.arange(lo, hi), nr[lo:hi])
     gone = np.asarray([d for d in dead if lo <= d < hi], dtype=np.uint32)
     if len(gone):
@@ -168,3 +176,79 @@ def test_nam_label_id_255_matches_exists(oracle, key):
     o = _oracle(oracle, nr, pr, ts, 7)
     with _engine(nr, ts, 7) as e:
         _same(_device_cycle(e, pr), o, f"label id 255 on key {key}")
+
+
+
+# ---- general terms (ABI 7): In / NotIn / Exists / DoesNotExist / Gt / Lt as value-id sets ----
+def _ext_cluster(n_nodes, n_pods, n_sets, seed):
+    nr, pr, _ = _cluster(n_nodes, n_pods, n_sets, seed)
+    nr["zone"][::17] = 255  # (id 255: a labelled node)
+    nr["label2"][5::23] = 255
+    return nr, pr, synth.nam_term_sets_ext(n_sets, seed=seed)
+
+
+@pytest.mark.parametrize("n_nodes,n_pods,n_sets,seed", [(1, 60, 5, 61), (40, 300, 12, 62), (700, 900, 40, 63),
+                                                        (2900, 400, 64, 64), (12000, 700, 64, 65)])
+def test_nam_ext_against_literal_loop(oracle, n_nodes, n_pods, n_sets, seed):
+    nr, pr, ts = _ext_cluster(n_nodes, n_pods, n_sets, seed)
+    o = _oracle(oracle, nr, pr, ts, seed)
+    with _engine(nr, ts, seed) as e:
+        _same(_device_cycle(e, pr), o, f"ext {n_nodes}x{n_pods}")
+
+
+def test_nam_ext_many_classes_and_unknown_sets(oracle):
+    # more (term set, toleration) classes than the class sort holds (pods then in batch
+    # order), term set ids past the registered ones (no terms), a chunked host call
+    seed = 66
+    nr, pr, ts = _ext_cluster(1500, 5000, 1200, seed)
+    sid = (np.arange(len(pr)) * 7919) % 1400  # ids 1201..1399: not registered
+    pr["pref_zone"], pr["pref_weight"] = sid & 0xFF, sid >> 8
+    o = _oracle(oracle, nr, pr, ts, seed)
+    with _engine(nr, ts, seed) as e:
+        _same(_device_cycle(e, pr), o, "many classes")
+    with _engine(nr, ts, seed, max_batch=1700) as e:
+        _same(e.schedule(pr, _lib.MODE_BATCHED), o, "many classes, host chunks")
+
+
+@pytest.mark.parametrize("weights", [(1, 1), (3, 2)])
+def test_nam_ext_node_shards(oracle, weights):
+    import torch
+
+    seed = 67 + weights[0]
+    cuts = (0, 1, 2200, 2201, 5000)
+    n = cuts[-1]
+    nr, pr, ts = _ext_cluster(n, 900, 48, seed)
+    dead = np.arange(0, n, 11)
+    o = _oracle(oracle, nr, pr, ts, seed, weights=weights, dead=dead)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    G, P, SB = len(cuts) - 1, len(pr), _lib.NAM_SEG_BYTES
+    segs = torch.zeros(G * P * SB, dtype=torch.uint8, device=dev)
+    keys = torch.zeros((G, P), dtype=torch.int64, device=dev)
+    out = torch.zeros(P * 24, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    engines = [_engine(nr, ts, seed, lo, hi, dead, weights=weights) for lo, hi in zip(cuts[:-1], cuts[1:])]
+    try:
+        for g, e in enumerate(engines):
+            e.nam_segment_device(P, pods.data_ptr(), segs.data_ptr() + g * P * SB, s.cuda_stream)
+        for g, e in enumerate(engines):
+            e.nam_keys_device(P, pods.data_ptr(), G, g, segs.data_ptr(), keys[g].data_ptr(), s.cuda_stream)
+        s.synchronize()
+        best = keys.max(dim=0).values.contiguous()
+        present = sum(int(e.info().present_nodes) for e in engines)
+        torch.cuda.synchronize()
+        engines[0].decode_device(P, pods.data_ptr(), best.data_ptr(), 0, present, out.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        _same(out.cpu().numpy().view(_lib.RESULT), o, f"ext shards {weights}")
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_nam_ext_rejects_weights_above_100():
+    ts = synth.nam_term_sets_ext(2, seed=3)
+    ts[1, 64] = 101
+    with _lib.Engine(max_nodes=10, plugin_set=NAM, seed=1) as e:
+        with pytest.raises(_lib.MSError):
+            e.nam_term_sets_ext(ts)

@@ -116,11 +116,15 @@ def test_terms_match_keys_values_and_exists(oracle):
     assert o["score"][0] == 0
 
 
-def test_set_id_beyond_the_table_is_rejected_by_the_oracle(oracle):
+def test_set_id_beyond_the_table_counts_as_no_terms(oracle):
+    # minisched_gpu.h ms_nam_term_sets: "ids above n_sets count as no terms" (the device's rule)
     nr, pr, ts = _cluster(20, 5, 2, 3)
     pr["pref_zone"][0] = 7
-    with pytest.raises(AssertionError):
-        oracle.schedule_nam(nr, pr, ts)
+    a = oracle.schedule_nam(nr, pr, ts)
+    pr["pref_zone"][0] = 0
+    b = oracle.schedule_nam(nr, pr, ts)
+    for k in ("node", "code", "score", "mask"):
+        assert np.array_equal(a[k], b[k])
 
 
 def test_term_set_encoder_validates():
