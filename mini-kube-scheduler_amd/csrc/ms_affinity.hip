@@ -582,23 +582,13 @@ NamLayout nam_layout(uint32_t n_rows, uint32_t cls_max) {
     return L;
 }
 
-size_t nam_scratch_bytes(const NamLayout &L, uint32_t n_pods, uint32_t n_sets) {
-    const size_t keys = 2ull * (n_sets + 1u);
-    return (size_t)L.segs * L.cls_max * sizeof(NamSeg)   // local
-           + (size_t)L.cls_max * sizeof(NamSeg)          // per-class composition (segment records)
-           + (size_t)L.cls_max * L.fpitch                // F
-           + (size_t)kNamDigits * L.fpitch               // dmask
-           + (size_t)L.cls_max * kNamDigits * 4          // fmax
-           + (keys + 16 + 3ull * L.cls_max + 2ull * n_pods) * 4 + 256;
-}
-
 namespace {
 struct NamScratch {
     NamSeg *local, *comp;
     uint8_t *F, *dmask;
     uint32_t *fmax, *used, *ctl, *cls_key, *rep, *pcls, *perm;
 };
-NamScratch nam_carve(void *scratch, const NamLayout &L, uint32_t n_pods, uint32_t n_sets) {
+NamScratch nam_carve(void *scratch, const NamLayout &L, uint32_t n_pods, uint32_t n_sets, size_t *bytes = nullptr) {
     char *b = static_cast<char *>(scratch);
     NamScratch x;
     size_t o = 0;
@@ -618,9 +608,19 @@ NamScratch nam_carve(void *scratch, const NamLayout &L, uint32_t n_pods, uint32_
     x.rep = reinterpret_cast<uint32_t *>(take((size_t)L.cls_max * 4));
     x.pcls = reinterpret_cast<uint32_t *>(take((size_t)n_pods * 4));
     x.perm = reinterpret_cast<uint32_t *>(take((size_t)n_pods * 4));
+    if (bytes) *bytes = o;
     return x;
 }
 
+}  // namespace
+
+size_t nam_scratch_bytes(const NamLayout &L, uint32_t n_pods, uint32_t n_sets) {
+    size_t o = 0;
+    (void)nam_carve(nullptr, L, n_pods, n_sets, &o);
+    return o;
+}
+
+namespace {
 hipError_t nam_classes_and_segs(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                 const void *sets, uint32_t n_sets, const NamLayout &L, const NamScratch &x,
                                 hipStream_t s) {
