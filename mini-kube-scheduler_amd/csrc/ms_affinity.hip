@@ -56,9 +56,10 @@ constexpr uint32_t kNamTile = 1024;      // rows staged in LDS per pass
 constexpr uint32_t kNamStride = 108;     // bytes per lane table in LDS: 27 words (odd: per-lane gathers spread banks)
 constexpr uint32_t kNamTabStride = 548;  // bytes per lane term table in LDS: 137 words (odd)
 constexpr uint32_t kNamComposeThreads = 128;
-constexpr uint32_t kNamPickThreads = 256;
 constexpr uint32_t kNamClsThreads = 1024;
-constexpr uint32_t kNamSortCap = 8192;   // (class, digit) buckets the class sort holds in LDS
+constexpr uint32_t kNamPickRows = 32;  // rows per k_nam_pick step: two 16-B loads of F and two of the digit mask
+constexpr uint32_t kNamSortCap = 65536;  // (class, digit) buckets the class sort takes (else batch order)
+constexpr uint32_t kNamPickParts = 4;    // row parts per pod in a k_nam_pick workgroup (one per wave)
 constexpr uint32_t kNamDigits = 11;      // node name digit 0..9, 10 = none
 
 struct NamSeg {
@@ -120,30 +121,32 @@ __device__ __forceinline__ void table_pre(uint8_t *row, uint32_t r, uint32_t lan
     __builtin_amdgcn_wave_barrier();
 }
 
-// The batch's classes, one workgroup (kNamClsThreads):
-//   used[key] (n_keys = 2 (n_sets + 1) words, zeroed here) -> dense class ids in
-//   key order; ctl[0] = the class count; cls_key[c], rep[c] (the first pod of
-//   class c); pcls[p]; perm = the pods in (class, name digit) order when the
-//   buckets fit kNamSortCap, else in batch order.
-__global__ __launch_bounds__(kNamClsThreads) void k_nam_classes(const ms_pod_rec *__restrict__ pods, uint32_t n,
-                                                                 uint32_t n_sets, uint32_t *__restrict__ used,
-                                                                 uint32_t *__restrict__ ctl,
-                                                                 uint32_t *__restrict__ cls_key,
-                                                                 uint32_t *__restrict__ rep,
-                                                                 uint32_t *__restrict__ pcls,
-                                                                 uint32_t *__restrict__ perm) {
-    __shared__ uint32_t cnt[kNamSortCap];
+// The batch's classes (round 6), in five small launches:
+//   k_nam_mark    used[key] = 1 for every pod's class key (used zeroed before);
+//   k_nam_index   one workgroup: dense class ids in key order (used[key] becomes
+//                 the class id), ctl[0] = the class count, cls_key[c], and the
+//                 (class, name digit) bucket counters zeroed when they fit;
+//   k_nam_count   pcls[p], and each bucket's pod count;
+//   k_nam_offsets one workgroup: the buckets' start offsets (exclusive scan)
+//                 into bstart and bcur;
+//   k_nam_scatter perm = the pods in bucket order (class, then digit), and
+//                 rep[c] = a pod of class c (its first bucket's first pod).
+// With more buckets than kNamSortCap the pods keep batch order and rep[c] is
+// the lowest pod index of the class (atomicMin in k_nam_count).
+__global__ void k_nam_mark(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t n_sets,
+                           uint32_t *__restrict__ used) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) used[nam_key(pods[i], n_sets)] = 1u;
+}
+
+__global__ __launch_bounds__(kNamClsThreads) void k_nam_index(uint32_t n_sets, uint32_t *__restrict__ used,
+                                                               uint32_t *__restrict__ ctl,
+                                                               uint32_t *__restrict__ cls_key,
+                                                               uint32_t *__restrict__ rep,
+                                                               uint32_t *__restrict__ bcnt) {
     __shared__ uint32_t part[kNamClsThreads];
-    __shared__ uint32_t total;
     const uint32_t tid = threadIdx.x, NT = kNamClsThreads;
     const uint32_t n_keys = 2u * (n_sets + 1u);
-    for (uint32_t k = tid; k < n_keys; k += NT) used[k] = 0u;
-    __syncthreads();
-    __threadfence_block();
-    for (uint32_t i = tid; i < n; i += NT) used[nam_key(pods[i], n_sets)] = 1u;
-    __threadfence_block();
-    __syncthreads();
-    // exclusive scan of used[] in key order: thread t takes a contiguous range
     const uint32_t per = (n_keys + NT - 1u) / NT, k0 = min(n_keys, tid * per), k1 = min(n_keys, k0 + per);
     uint32_t s = 0;
     for (uint32_t k = k0; k < k1; ++k) s += used[k];
@@ -156,8 +159,8 @@ __global__ __launch_bounds__(kNamClsThreads) void k_nam_classes(const ms_pod_rec
             part[t] = a;
             a += v;
         }
-        total = a;
         ctl[0] = a;
+        ctl[1] = a * kNamDigits <= kNamSortCap ? 1u : 0u;  // sorted
     }
     __syncthreads();
     uint32_t c = part[tid];
@@ -167,29 +170,32 @@ __global__ __launch_bounds__(kNamClsThreads) void k_nam_classes(const ms_pod_rec
             rep[c] = 0xFFFFFFFFu;
             used[k] = c++;  // (used[] now maps a key to its class)
         }
-    __threadfence_block();
     __syncthreads();
-    const uint32_t n_cls = total;
-    const bool sort = n_cls * kNamDigits <= kNamSortCap;
-    const uint32_t nb = n_cls * kNamDigits;
-    if (sort)
-        for (uint32_t b = tid; b < nb; b += NT) cnt[b] = 0u;
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += NT) {
-        const uint32_t cl = used[nam_key(pods[i], n_sets)];
-        pcls[i] = cl;
-        atomicMin(&rep[cl], i);
-        if (sort) atomicAdd(&cnt[cl * kNamDigits + nam_pod_digit(pods[i])], 1u);
-    }
-    __syncthreads();
-    if (!sort) {
-        for (uint32_t i = tid; i < n; i += NT) perm[i] = i;
-        return;
-    }
-    // exclusive scan of the bucket counts (contiguous ranges per thread)
-    const uint32_t bper = (nb + NT - 1u) / NT, b0 = min(nb, tid * bper), b1 = min(nb, b0 + bper);
-    s = 0;
-    for (uint32_t b = b0; b < b1; ++b) s += cnt[b];
+    const uint32_t nb = ctl[1] ? ctl[0] * kNamDigits : 0u;
+    for (uint32_t b = tid; b < nb; b += NT) bcnt[b] = 0u;
+}
+
+__global__ void k_nam_count(const ms_pod_rec *__restrict__ pods, uint32_t n, uint32_t n_sets,
+                            const uint32_t *__restrict__ used, const uint32_t *__restrict__ ctl,
+                            uint32_t *__restrict__ pcls, uint32_t *__restrict__ rep, uint32_t *__restrict__ bcnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ms_pod_rec p = pods[i];
+    const uint32_t cl = used[nam_key(p, n_sets)];
+    pcls[i] = cl;
+    if (ctl[1]) atomicAdd(&bcnt[cl * kNamDigits + nam_pod_digit(p)], 1u);
+    else atomicMin(&rep[cl], i);
+}
+
+__global__ __launch_bounds__(kNamClsThreads) void k_nam_offsets(const uint32_t *__restrict__ ctl,
+                                                                 uint32_t *__restrict__ bcnt,
+                                                                 uint32_t *__restrict__ bstart) {
+    __shared__ uint32_t part[kNamClsThreads];
+    if (!ctl[1]) return;  // (workgroup-uniform)
+    const uint32_t tid = threadIdx.x, NT = kNamClsThreads, nb = ctl[0] * kNamDigits;
+    const uint32_t per = (nb + NT - 1u) / NT, b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+    uint32_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += bcnt[b];
     part[tid] = s;
     __syncthreads();
     if (tid == 0) {
@@ -203,13 +209,26 @@ __global__ __launch_bounds__(kNamClsThreads) void k_nam_classes(const ms_pod_rec
     __syncthreads();
     uint32_t a = part[tid];
     for (uint32_t b = b0; b < b1; ++b) {
-        const uint32_t v = cnt[b];
-        cnt[b] = a;
+        const uint32_t v = bcnt[b];
+        bcnt[b] = a;  // (the scatter's running cursor)
+        bstart[b] = a;
         a += v;
     }
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += NT)
-        perm[atomicAdd(&cnt[pcls[i] * kNamDigits + nam_pod_digit(pods[i])], 1u)] = i;
+}
+
+__global__ void k_nam_scatter(const ms_pod_rec *__restrict__ pods, uint32_t n, const uint32_t *__restrict__ ctl,
+                              const uint32_t *__restrict__ pcls, uint32_t *__restrict__ bcnt,
+                              uint32_t *__restrict__ perm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    perm[ctl[1] ? atomicAdd(&bcnt[pcls[i] * kNamDigits + nam_pod_digit(pods[i])], 1u) : i] = i;
+}
+
+__global__ void k_nam_rep(const uint32_t *__restrict__ ctl, const uint32_t *__restrict__ bstart,
+                          const uint32_t *__restrict__ perm, uint32_t *__restrict__ rep) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!ctl[1] || c >= ctl[0]) return;
+    rep[c] = perm[bstart[c * kNamDigits]];  // (class c's buckets are contiguous and not all empty)
 }
 
 // A lane's class: its key's term table into the lane's LDS slot (kNamTabStride
@@ -313,9 +332,11 @@ __global__ void k_nam_compose(const NamSeg *__restrict__ in, uint32_t stride, ui
                               int32_t skip_to, NamSeg *__restrict__ out, uint8_t *__restrict__ m_in,
                               const uint32_t *__restrict__ n_live) {
     __shared__ __attribute__((aligned(16))) uint8_t tabs[kNamComposeThreads * kNamStride];
+    __shared__ __attribute__((aligned(16))) uint8_t stg[kNamComposeThreads * kNamStride];
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_lanes || (n_live && p >= *n_live)) return;
     uint8_t *U = tabs + threadIdx.x * kNamStride;  // (LDS, not a dynamically indexed private array)
+    uint8_t *st = stg + threadIdx.x * kNamStride;  // the record being composed, staged as words
     table_identity(U);
     uint32_t any = 0, before = 0;
     for (uint32_t s = 0; s < n; ++s) {
@@ -327,7 +348,12 @@ __global__ void k_nam_compose(const NamSeg *__restrict__ in, uint32_t stride, ui
         if (skip_to >= 0 && (int32_t)s == skip_to) continue;
         any |= x->any;
         if (U[100] == 0) continue;  // (all 0 stays all 0)
-        for (uint32_t v = 0; v <= 100u; ++v) U[v] = x->T[U[v]];
+        uint32_t w[MS_NAM_SEG_BYTES / 4];
+#pragma unroll
+        for (uint32_t k = 0; k < MS_NAM_SEG_BYTES / 4; ++k) w[k] = reinterpret_cast<const uint32_t *>(x)[k];
+#pragma unroll
+        for (uint32_t k = 0; k < MS_NAM_SEG_BYTES / 4; ++k) reinterpret_cast<uint32_t *>(st)[k] = w[k];
+        for (uint32_t v = 0; v <= 100u; ++v) U[v] = st[U[v]];
     }
     U[101] = (uint8_t)any;
     U[102] = U[103] = 0;
@@ -381,6 +407,7 @@ __global__ __launch_bounds__(64) void k_nam_fscore(NodeTable t, uint32_t n_rows,
     __shared__ __attribute__((aligned(16))) uint8_t tabs[64 * kNamStride];
     __shared__ __attribute__((aligned(16))) uint8_t terms[64 * kNamTabStride];
     __shared__ uint32_t fm[64][12];
+    __shared__ __attribute__((aligned(16))) uint8_t stg[64 * kNamStride];  // a later segment's table, staged
     const uint32_t lane = threadIdx.x, n_cls = ctl[0], c0 = blockIdx.x * 64u, seg = blockIdx.y;
     if (c0 >= n_cls) return;  // (workgroup-uniform)
     const uint32_t c = c0 + lane;
@@ -396,14 +423,20 @@ __global__ __launch_bounds__(64) void k_nam_fscore(NodeTable t, uint32_t n_rows,
     uint32_t before = (live && m_in) ? m_in[rp] : 0u;
     if (live) {
         for (uint32_t s = 0; s < seg; ++s) before |= local[(size_t)s * stride + c].any;
-        for (uint32_t s = seg + 1; s < n_segs && mine[100] != 0; ++s) {
-            const uint8_t *T = local[(size_t)s * stride + c].T;
-            for (uint32_t v = 0; v <= 100u; ++v) mine[v] = T[mine[v]];
-        }
-        if (after && mine[100] != 0) {
-            const uint8_t *T = after[rp].T;
-            for (uint32_t v = 0; v <= 100u; ++v) mine[v] = T[mine[v]];
-        }
+        // T <- T_s o T for the later segments, then the later shards: each record's
+        // 104 B loaded as words into the lane's LDS row, then 101 lookups there
+        uint8_t *st = stg + lane * kNamStride;
+        auto compose = [&](const NamSeg *x) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(x);
+            uint32_t w[MS_NAM_SEG_BYTES / 4];
+#pragma unroll
+            for (uint32_t k = 0; k < MS_NAM_SEG_BYTES / 4; ++k) w[k] = src[k];
+#pragma unroll
+            for (uint32_t k = 0; k < MS_NAM_SEG_BYTES / 4; ++k) reinterpret_cast<uint32_t *>(st)[k] = w[k];
+            for (uint32_t v = 0; v <= 100u; ++v) mine[v] = st[mine[v]];
+        };
+        for (uint32_t s = seg + 1; s < n_segs && mine[100] != 0; ++s) compose(local + (size_t)s * stride + c);
+        if (after && mine[100] != 0) compose(static_cast<const NamSeg *>(after) + rp);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -481,77 +514,91 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t y) {
     return ~(t | y) & 0x80808080u;
 }
 
-// Per pod (lane = pod, pods in class-digit order): the packed key of the best
-// total over this context's rows. Row j's total is w_na F_j + w_nn 10 [digit_j
-// = the pod's]; the best S* follows from the class's maxima per digit, and
-// the rows reaching S* are the ones whose F equals t_nn (digit = the pod's) or
-// t_plain (else): compared four rows per word against a per-byte target chosen
-// by the digit mask dmask[d][row] (0xFF where the row's name digit is d), then
-// only those rows are hashed. keys[p] = the best key, or kKeyListed / 0 (this
-// context lists rows but none is feasible / lists none).
-__global__ __launch_bounds__(kNamPickThreads) void k_nam_pick(
+// Per pod (lane = pod, pods in class-digit order, so a wave's pods mostly share
+// one class and digit): the packed key of the best total over this context's
+// rows. Row j's total is w_na F_j + w_nn 10 [digit_j = the pod's]; the best S*
+// follows from the class's maxima per digit, and the rows reaching S* are the
+// ones whose F equals t_nn (digit = the pod's) or t_plain (else): compared four
+// rows per word against a per-byte target chosen by the digit mask dmask[d][row]
+// (0xFF where the row's name digit is d), then only those rows are hashed.
+// Workgroup = 64 pods x kNamPickParts waves (wave w: row part w of the
+// workgroup's grid.y slice), combined in LDS, then one atomicMax per pod into
+// keys[p] (filled before with kKeyListed / 0: this context lists rows but none is
+// feasible / lists none). grid.y x kNamPickParts parts keep many waves in flight
+// over the row stream (lane = pod alone gives one wave per 64 pods).
+__global__ __launch_bounds__(64 * kNamPickParts) void k_nam_pick(
     const ms_pod_rec *__restrict__ pods, uint32_t n_pods, const uint32_t *__restrict__ perm,
     const uint32_t *__restrict__ pcls, const uint8_t *__restrict__ F, uint32_t fpitch,
-    const uint32_t *__restrict__ fmax, const uint8_t *__restrict__ dmask, uint32_t n_rows, uint32_t base,
-    uint32_t seed32, uint32_t w_nn, uint32_t w_na, uint32_t listed, u64 *__restrict__ keys) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t *__restrict__ fmax, const uint8_t *__restrict__ dmask, uint32_t n_rows, uint32_t rows_per_part,
+    uint32_t base, uint32_t seed32, uint32_t w_nn, uint32_t w_na, u64 *__restrict__ keys) {
+    __shared__ u64 part_best[kNamPickParts][64];
+    const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * 64u + lane;
     const bool live = i < n_pods;
     const uint32_t p = live ? perm[i] : 0u;
     const ms_pod_rec pod = pods[p];
     const uint32_t c = pcls[p], pd = nam_pod_digit(pod);
-    uint32_t fm[kNamDigits];
-    uint32_t fall = 0;
+    uint32_t fall = 0, fpd = 0;
 #pragma unroll
     for (uint32_t d = 0; d < kNamDigits; ++d) {
-        fm[d] = fmax[(size_t)c * kNamDigits + d];
-        fall = max(fall, fm[d]);
+        const uint32_t v = fmax[(size_t)c * kNamDigits + d];
+        fall = max(fall, v);
+        fpd = d == pd ? v : fpd;  // (pd 10: non-digit pod, never matches)
     }
-    const u64 best = listed ? kKeyListed : 0ull;
-    if (!live) return;
-    if (fall == 0u) {  // no feasible row here
-        keys[p] = best;
-        return;
-    }
-    uint32_t fpd = 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 10u; ++d) fpd = d == pd ? fm[d] : fpd;
+    if (pd > 9u) fpd = 0u;
     const uint32_t nn = 10u * w_nn;
-    const uint32_t s_plain = w_na * (fall - 1u), s_nn = fpd ? w_na * (fpd - 1u) + nn : 0u;
-    const uint32_t S = max(s_plain, fpd ? s_nn : 0u);
-    // the F a row needs to reach S: without / with the NodeNumber match (0xFE: none;
+    const uint32_t s_plain = fall ? w_na * (fall - 1u) : 0u, s_nn = fpd ? w_na * (fpd - 1u) + nn : 0u;
+    const uint32_t S = max(s_plain, s_nn);
+    // the F a row needs to reach S without / with the NodeNumber match (0xFE: none;
     // 0xFF, infeasible, never equals either)
     const uint32_t t_plain = (S % w_na == 0u && S / w_na <= 100u) ? S / w_na : 0xFEu;
-    const uint32_t t_nn = (pd <= 9u && S >= nn && (S - nn) % w_na == 0u && (S - nn) / w_na <= 100u) ? (S - nn) / w_na
-                                                                                                   : 0xFEu;
+    const uint32_t t_nn = (pd <= 9u && S >= nn && (S - nn) % w_na == 0u && (S - nn) / w_na <= 100u)
+                              ? (S - nn) / w_na : 0xFEu;
     const uint32_t tp4 = t_plain * 0x01010101u, tn4 = t_nn * 0x01010101u;
     const uint32_t A = tb_pod(seed32, pod.ordinal);
     const uint8_t *Fc = F + (size_t)c * fpitch;
     const uint8_t *Dd = dmask + (size_t)pd * fpitch;  // (row 10: all zero)
+    const uint32_t part = blockIdx.y * kNamPickParts + wave;
+    const uint32_t j0 = part * rows_per_part, j1 = min(n_rows, j0 + rows_per_part);
     u64 top = 0;
-    for (uint32_t j = 0; j < n_rows; j += 16u) {
-        const uint4 f = *reinterpret_cast<const uint4 *>(Fc + j);
-        const uint4 m = *reinterpret_cast<const uint4 *>(Dd + j);
-        const uint32_t fw[4] = {f.x, f.y, f.z, f.w}, mw[4] = {m.x, m.y, m.z, m.w};
-        uint32_t z[4], any = 0;
+    if (live && fall)
+        for (uint32_t j = j0; j < j1; j += kNamPickRows) {
+            const uint4 f0 = *reinterpret_cast<const uint4 *>(Fc + j), f1 = *reinterpret_cast<const uint4 *>(Fc + j + 16);
+            const uint4 m0 = *reinterpret_cast<const uint4 *>(Dd + j), m1 = *reinterpret_cast<const uint4 *>(Dd + j + 16);
+            const uint32_t fw[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            const uint32_t mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+            uint32_t z[8], any = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            z[k] = zero_bytes(fw[k] ^ ((tn4 & mw[k]) | (tp4 & ~mw[k])));
-            any |= z[k];
-        }
-        if (any) {
+            for (int k = 0; k < 8; ++k) {
+                z[k] = zero_bytes(fw[k] ^ ((tn4 & mw[k]) | (tp4 & ~mw[k])));
+                any |= z[k];
+            }
+            if (any) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint32_t b = z[k];
-                while (b) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(b);
-                    b &= b - 1u;
-                    const uint32_t ord = base + j + 4u * (uint32_t)k + (bit >> 3);
-                    top = umax64(top, make_key(S, tb_hash(A, ord), ord));
+                for (int k = 0; k < 8; ++k) {
+                    uint32_t b = z[k];
+                    while (b) {
+                        const uint32_t bit = (uint32_t)__builtin_ctz(b);
+                        b &= b - 1u;
+                        const uint32_t ord = base + j + 4u * (uint32_t)k + (bit >> 3);
+                        top = umax64(top, make_key(S, tb_hash(A, ord), ord));
+                    }
                 }
             }
         }
+    part_best[wave][lane] = top;
+    __syncthreads();
+    if (wave == 0 && live) {
+        u64 b = top;
+#pragma unroll
+        for (uint32_t w = 1; w < kNamPickParts; ++w) b = umax64(b, part_best[w][lane]);
+        if (b) atomicMax(reinterpret_cast<unsigned long long *>(keys + p), (unsigned long long)b);
     }
-    keys[p] = umax64(best, top);
+}
+
+__global__ void k_nam_fill(u64 *__restrict__ keys, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = kKeyListed;
 }
 
 // dmask[d * fpitch + row] = 0xFF where row's name digit is d (d < 10), rows
@@ -574,7 +621,9 @@ inline uint32_t cdiv(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 NamLayout nam_layout(uint32_t n_rows, uint32_t cls_max) {
     NamLayout L;
     const uint32_t blocks = std::max(1u, cdiv(cls_max, 64u));
-    uint32_t segs = std::min(128u, std::max(16u, cdiv(512u, blocks)));
+    // (per class and segment: rows / segs row steps, and up to segs compositions of
+    // the later segments' 101-entry tables, so a few tens of segments)
+    uint32_t segs = std::min(32u, std::max(8u, cdiv(128u, blocks)));
     L.seg_rows = std::max(64u, cdiv(cdiv(std::max(n_rows, 1u), segs), 64u) * 64u);
     L.segs = std::max(1u, cdiv(std::max(n_rows, 1u), L.seg_rows));
     L.fpitch = cdiv(std::max(n_rows, 1u), 64u) * 64u;
@@ -586,7 +635,7 @@ namespace {
 struct NamScratch {
     NamSeg *local, *comp;
     uint8_t *F, *dmask;
-    uint32_t *fmax, *used, *ctl, *cls_key, *rep, *pcls, *perm;
+    uint32_t *fmax, *used, *ctl, *cls_key, *rep, *pcls, *perm, *bcnt, *bstart;
 };
 NamScratch nam_carve(void *scratch, const NamLayout &L, uint32_t n_pods, uint32_t n_sets, size_t *bytes = nullptr) {
     char *b = static_cast<char *>(scratch);
@@ -608,6 +657,9 @@ NamScratch nam_carve(void *scratch, const NamLayout &L, uint32_t n_pods, uint32_
     x.rep = reinterpret_cast<uint32_t *>(take((size_t)L.cls_max * 4));
     x.pcls = reinterpret_cast<uint32_t *>(take((size_t)n_pods * 4));
     x.perm = reinterpret_cast<uint32_t *>(take((size_t)n_pods * 4));
+    const size_t nb = std::min<size_t>((size_t)L.cls_max * kNamDigits, kNamSortCap);
+    x.bcnt = reinterpret_cast<uint32_t *>(take(nb * 4));
+    x.bstart = reinterpret_cast<uint32_t *>(take(nb * 4));
     if (bytes) *bytes = o;
     return x;
 }
@@ -624,8 +676,19 @@ namespace {
 hipError_t nam_classes_and_segs(const NodeTable &t, uint32_t n_rows, const ms_pod_rec *pods, uint32_t n_pods,
                                 const void *sets, uint32_t n_sets, const NamLayout &L, const NamScratch &x,
                                 hipStream_t s) {
-    hipLaunchKernelGGL(k_nam_classes, dim3(1), dim3(kNamClsThreads), 0, s, pods, n_pods, n_sets, x.used, x.ctl,
-                       x.cls_key, x.rep, x.pcls, x.perm);
+    hipError_t e = hipMemsetAsync(x.used, 0, 2ull * (n_sets + 1u) * 4, s);
+    if (e != hipSuccess) return e;
+    const dim3 pg(cdiv(n_pods, 256u));
+    hipLaunchKernelGGL(k_nam_mark, pg, dim3(256), 0, s, pods, n_pods, n_sets, x.used);
+    hipLaunchKernelGGL(k_nam_index, dim3(1), dim3(kNamClsThreads), 0, s, n_sets, x.used, x.ctl, x.cls_key, x.rep,
+                       x.bcnt);
+    hipLaunchKernelGGL(k_nam_count, pg, dim3(256), 0, s, pods, n_pods, n_sets, (const uint32_t *)x.used,
+                       (const uint32_t *)x.ctl, x.pcls, x.rep, x.bcnt);
+    hipLaunchKernelGGL(k_nam_offsets, dim3(1), dim3(kNamClsThreads), 0, s, (const uint32_t *)x.ctl, x.bcnt, x.bstart);
+    hipLaunchKernelGGL(k_nam_scatter, pg, dim3(256), 0, s, pods, n_pods, (const uint32_t *)x.ctl,
+                       (const uint32_t *)x.pcls, x.bcnt, x.perm);
+    hipLaunchKernelGGL(k_nam_rep, dim3(cdiv(L.cls_max, 256u)), dim3(256), 0, s, (const uint32_t *)x.ctl,
+                       (const uint32_t *)x.bstart, (const uint32_t *)x.perm, x.rep);
     hipLaunchKernelGGL(k_nam_seg, dim3(cdiv(L.cls_max, 64u), L.segs), dim3(64), 0, s, t, n_rows, L.seg_rows,
                        static_cast<const NamTab *>(sets), n_sets, (const uint32_t *)x.ctl,
                        (const uint32_t *)x.cls_key, L.cls_max, x.local);
@@ -683,10 +746,20 @@ hipError_t launch_nam_keys(const NodeTable &t, uint32_t n_rows, const ms_pod_rec
                        static_cast<const NamTab *>(sets), n_sets, (const uint32_t *)x.ctl, (const uint32_t *)x.cls_key,
                        (const uint32_t *)x.rep, (const NamSeg *)x.local, L.cls_max, L.segs,
                        static_cast<const NamSeg *>(after), m_in, x.F, L.fpitch, x.fmax);
-    hipLaunchKernelGGL(k_nam_pick, dim3(cdiv(n_pods, kNamPickThreads)), dim3(kNamPickThreads), 0, s, pods, n_pods,
+    // row parts: enough waves to keep the row stream busy (~16 per SIMD at 50k pods),
+    // each part a multiple of kNamPickRows rows
+    const uint32_t pod_blocks = cdiv(n_pods, 64u);
+    uint32_t gy = std::max(1u, std::min(cdiv(16384u, pod_blocks * kNamPickParts), cdiv(n_rows, 256u * kNamPickParts)));
+    const uint32_t parts = gy * kNamPickParts;
+    const uint32_t rows_per_part = cdiv(cdiv(n_rows, parts), kNamPickRows) * kNamPickRows;
+    gy = cdiv(cdiv(n_rows, rows_per_part), kNamPickParts);
+    e = hipMemsetAsync(keys, 0, sizeof(u64) * n_pods, s);
+    if (e != hipSuccess) return e;
+    if (listed) hipLaunchKernelGGL(k_nam_fill, dim3(cdiv(n_pods, 256u)), dim3(256), 0, s, reinterpret_cast<u64 *>(keys), n_pods);
+    hipLaunchKernelGGL(k_nam_pick, dim3(pod_blocks, gy), dim3(64 * kNamPickParts), 0, s, pods, n_pods,
                        (const uint32_t *)x.perm, (const uint32_t *)x.pcls, (const uint8_t *)x.F, L.fpitch,
-                       (const uint32_t *)x.fmax, (const uint8_t *)x.dmask, n_rows, t.base, seed32, w_nn, w_na, listed,
-                       reinterpret_cast<u64 *>(keys));
+                       (const uint32_t *)x.fmax, (const uint8_t *)x.dmask, n_rows, rows_per_part, t.base, seed32, w_nn,
+                       w_na, reinterpret_cast<u64 *>(keys));
     return hipGetLastError();
 }
 
