@@ -534,6 +534,34 @@ def other_configs(args, dev, stream):
                              sample=f"oracle msor_schedule_nam closed form (1 thread), first {n_pre} pods "
                                     f"({cpu_nam:.2f} s)", pods_per_s=n_pre / cpu_nam, **_cpu_info(1)),
     }
+    # ---- NAM_ext: the same shape with term sets in general form (ABI 7: In / NotIn / Exists /
+    # DoesNotExist / Gt / Lt value-id sets, several requirements per term, synth.nam_term_sets_ext)
+    nr = synth.nodes(N, seed=args.seed, labels=True)
+    pr = synth.pods(P, seed=args.seed, term_sets=n_sets)
+    tse = synth.nam_term_sets_ext(n_sets, seed=args.seed)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    res = torch.empty(P * 24, dtype=torch.uint8, device=dev)
+    with _lib.Engine(max_nodes=N, plugin_set=_lib.PLUGINS_NU_NN_NAM, seed=args.seed, device=dev.index) as e:
+        e.nam_term_sets_ext(tse)
+        e.upsert(np.arange(N), nr)
+        e.flush()
+        med, ts_run = _median_time(lambda: e.select_batch_device(P, pods.data_ptr(), res.data_ptr()), sync=sync)
+        got = res.cpu().numpy().view(_lib.RESULT)
+    t0 = time.perf_counter()
+    o = _oracle.schedule_nam_ext(nr, pr[:n_pre], tse, literal=False, seed=args.seed)
+    cpu_name = time.perf_counter() - t0
+    out["NAM_ext"] = {
+        "workload": "NAM_ext (extension): NAM's shape with general preferred terms (In / NotIn / Exists / "
+                    f"DoesNotExist / Gt / Lt, several requirements per term; {n_sets} term sets), batched",
+        "ms": med * 1e3, "runs_ms": [t * 1e3 for t in ts_run], "evals_per_s": N * P / med, "pods_per_s": P / med,
+        "parity_vs_oracle_prefix": bool(np.array_equal(got["node"][:n_pre], o["node"])
+                                        and np.array_equal(got["code"][:n_pre], o["code"])
+                                        and np.array_equal(got["score"][:n_pre].astype(np.int64),
+                                                           o["score"].astype(np.int64))),
+        "cpu_baseline": dict(value=N * n_pre / cpu_name, unit="pod×node evals/s", kind="port",
+                             sample=f"oracle msor_schedule_nam_ext closed form (1 thread), first {n_pre} pods "
+                                    f"({cpu_name:.2f} s)", pods_per_s=n_pre / cpu_name, **_cpu_info(1)),
+    }
     return out
 
 

@@ -4,6 +4,7 @@
 #include "ms_comm_loopback.h"
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -29,6 +30,7 @@ struct Post {
 
 struct Group {
     int world = 0;
+    bool solo = false;  // MS_LB_SOLO: one rank of `world` stands alone (per-rank probes)
     std::mutex mu;
     std::condition_variable cv;
     int joined = 0, left = 0;
@@ -50,6 +52,7 @@ std::atomic<unsigned long long> g_id_counter{1};
 
 // Generation barrier over the group's ranks; false on timeout.
 bool barrier(Group &g) {
+    if (g.solo) return true;
     std::unique_lock<std::mutex> lk(g.mu);
     const uint64_t my = g.gen;
     if (++g.arrived == g.world) {
@@ -97,9 +100,35 @@ hipError_t launch_max(const Srcs &s, int G, size_t base, size_t n, void *out, hi
 
 // One collective on rank r: post, barrier, wait for every rank's send event,
 // combine this rank's output, barrier, wait for every rank's done event.
+// Solo (MS_LB_SOLO, per-rank probes): every other rank is taken to have sent
+// this rank's own buffer, so a reduce-scatter combines G copies of its block r
+// (the G-way MAX a real rank computes), an all-gather writes its block into all
+// G slots, an all-to-all its block r into all G; the work and bytes of one rank
+// of a G-rank collective, without the others.
 ncclResult_t collective(Comm *c, const Post &p, hipStream_t st) {
     Group &g = *c->g;
     const int r = c->rank, G = g.world;
+    if (g.solo) {
+        const size_t es = dt_size(p.dt), bytes = p.count * es;
+        hipError_t e = hipSuccess;
+        if (p.kind == 1) {
+            Srcs s{};
+            for (int j = 0; j < G; ++j) s.p[j] = p.send;
+            const size_t base = (size_t)r * p.count;
+            if (es == 1) e = launch_max<uint8_t>(s, G, base, p.count, p.recv, st);
+            else if (es == 4) e = launch_max<uint32_t>(s, G, base, p.count, p.recv, st);
+            else e = launch_max<unsigned long long>(s, G, base, p.count, p.recv, st);
+        } else {
+            const char *src = static_cast<const char *>(p.send) + (p.kind == 3 ? (size_t)r * bytes : 0);
+            for (int j = 0; j < G && e == hipSuccess; ++j) {
+                char *dst = static_cast<char *>(p.recv) + (size_t)j * bytes;
+                if (dst != src && bytes) e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st);
+            }
+        }
+        if (e != hipSuccess) return ncclUnhandledCudaError;
+        g_issued.fetch_add(1);
+        return ncclSuccess;
+    }
     if (hipEventRecord(g.ev_send[r], st) != hipSuccess) return ncclUnhandledCudaError;
     g.post[r] = p;
     if (!barrier(g)) return ncclSystemError;  // a rank never issued this collective
@@ -159,6 +188,16 @@ ncclResult_t lb_ncclGetUniqueId(ncclUniqueId *id) {
 
 ncclResult_t lb_ncclCommInitRank(ncclComm_t *comm, int nranks, ncclUniqueId id, int rank) {
     if (!comm || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+    if (const char *solo = getenv("MS_LB_SOLO"); solo && solo[0] == '1') {  // (test / probe builds only)
+        auto g = std::make_shared<Group>();
+        g->world = nranks;
+        g->solo = true;
+        if (hipEventCreateWithFlags(&g->ev_send[rank], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->ev_done[rank], hipEventDisableTiming) != hipSuccess)
+            return ncclUnhandledCudaError;
+        *comm = reinterpret_cast<ncclComm_t>(new Comm{g, rank});
+        return ncclSuccess;
+    }
     const std::string key(id.internal, sizeof(id.internal));
     std::shared_ptr<Group> g;
     {

@@ -396,3 +396,38 @@ def test_loopback_mismatched_collectives_fail_cleanly(lb):
             e.close()
 
     run_ranks(G, rank_fn, timeout=300)
+
+
+@pytest.mark.parametrize("G,r", [(4, 2), (8, 7)])
+def test_solo_rank_probe_mode(lb, oracle, monkeypatch, G, r):
+    # MS_LB_SOLO=1 (tools/step_probe_rank.py): ONE rank of a G-rank
+    # communicator on its own -- its shard sweep, its ceil(P/G)-pod slice, a G-way MAX
+    # reduce-scatter over G copies of its own keys, the slice decode -- the per-rank work
+    # of the driver's G-GPU run. Its slice therefore holds the best over ITS shard only:
+    # the oracle over that shard's rows equals it
+    import torch
+
+    monkeypatch.setenv("MS_LB_SOLO", "1")
+    N, P, seed = 24_000, 9_001, 5
+    lo, hi = sharded.shard_bounds(N, r, G)
+    nr, pr = synth.nodes(N, seed=seed), synth.pods(P, seed=seed)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream(device=dev)
+    pods = torch.from_numpy(pr.view(np.uint8).copy()).to(dev)
+    e = _lib.Engine(max_nodes=hi - lo, node_base=lo, seed=seed, lib=lb)
+    try:
+        e.upsert(np.arange(lo, hi), nr[lo:hi])
+        e.flush()
+        e.comm_init(_lib.comm_id_create(lb), r, G)
+        cyc = sharded.ShardedCycle(e, N, P, pods, s)
+        assert cyc.library and (cyc.a, cyc.b) == (r * -(-P // G), min(P, (r + 1) * -(-P // G)))
+        for _ in range(3):  # (pipelined submits, then the drain)
+            cyc.step()
+        cyc.finish()
+        s.synchronize()
+        got = cyc.results.cpu().numpy().view(_lib.RESULT)[: cyc.b - cyc.a]
+    finally:
+        e.close()
+    o = oracle.schedule(nr[lo:hi], pr[cyc.a:cyc.b], seed=seed, node_base=lo)
+    _same(got, {k: np.concatenate([np.zeros(cyc.a, v.dtype), v]) for k, v in o.items() if k != "cols"},
+          cyc.a, cyc.b, f"solo rank {r} of {G}")

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B builds of libminisched_gpu.so with extra -D flags on ms_kernels.hip, for
 # MINISCHED_LIB=... runs (tools/gpu_*.sh). Usage: tools/build_variants.sh NAME "-DFOO=1 ..." [vst]
-# -> mini-kube-scheduler_amd/minisched_amd/libminisched_gpu_NAME.so (vst: with the MS_VSTAMPS stamps)
+# -> mini-kube-scheduler_amd/minisched_amd/libminisched_gpu_NAME.so (vst: with the MS_VSTAMPS stamps;
+# tl: the per-workgroup step timeline only, e.g. tools/build_variants.sh tl "" tl)
 set -e
 cd "$(dirname "$0")/../mini-kube-scheduler_amd"
 NAME=$1; DEFS=$2; VST=$3
@@ -9,8 +10,12 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unu
 mkdir -p build
 if [ "$VST" = vst ]; then
   $H -DMS_VSTAMPS $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
-  [ -f build/ms_capi_vst.o ] || $H -DMS_VSTAMPS -c csrc/ms_capi.cpp -o build/ms_capi_vst.o
+  $H -DMS_VSTAMPS -c csrc/ms_capi.cpp -o build/ms_capi_vst.o
   CAPI=build/ms_capi_vst.o
+elif [ "$VST" = tl ]; then  # step timeline only (MS_TIMELINE=<file>; the host side reads it since round 6)
+  $H -DMS_TIMELINE_ONLY $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
+  $H -DMS_TIMELINE_ONLY -c csrc/ms_capi.cpp -o build/ms_capi_tl.o
+  CAPI=build/ms_capi_tl.o
 else
   $H $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
   CAPI=build/ms_capi.o
