@@ -105,16 +105,24 @@ __device__ __forceinline__ void table_identity(uint8_t *row) {
     }
 }
 
+// floor(100 v / r) for v <= 100 (r > 100) as a multiply-high by m = floor((2^32 - 1) / r) + 1
+// (one division per rescale, not per entry): m exceeds 2^32 / r by at most 1, so the
+// product overshoots 100 v / r by at most 10^4 / 2^32 < 1 / r, less than the gap from any
+// fraction k / r (k < r) to the next integer: the floor is exact.
+__device__ __forceinline__ uint32_t div_magic(uint32_t r) { return 0xFFFFFFFFu / r + 1u; }
+__device__ __forceinline__ uint32_t f_r(uint32_t v, uint32_t m) { return __umulhi(100u * v, m); }
+
 // f_r o T on table `row` (every lane of the wave: entries lane, lane + 64).
 __device__ __forceinline__ void table_post(uint8_t *row, uint32_t r, uint32_t lane) {
-    for (uint32_t v = lane; v <= 100u; v += 64u) row[v] = (uint8_t)((100u * row[v]) / r);
+    const uint32_t m = div_magic(r);
+    for (uint32_t v = lane; v <= 100u; v += 64u) row[v] = (uint8_t)f_r(row[v], m);
 }
 
 // T o f_r on table `row` (reads of both passes before the writes).
 __device__ __forceinline__ void table_pre(uint8_t *row, uint32_t r, uint32_t lane) {
-    const uint32_t v0 = lane, v1 = lane + 64u;
-    const uint8_t a = row[(100u * v0) / r];
-    const uint8_t b = v1 <= 100u ? row[(100u * v1) / r] : 0;
+    const uint32_t v0 = lane, v1 = lane + 64u, m = div_magic(r);
+    const uint8_t a = row[f_r(v0, m)];
+    const uint8_t b = v1 <= 100u ? row[f_r(v1, m)] : 0;
     __builtin_amdgcn_wave_barrier();
     row[v0] = a;
     if (v1 <= 100u) row[v1] = b;

@@ -161,3 +161,12 @@ def test_random_ext_sets_generator_covers_the_operators():
     assert ts.shape == (64, _lib.NAM_SET_EXT_BYTES)
     w = ts.reshape(64, 4, 68)[:, :, 64]
     assert (w > 0).sum() > 64 and w.max() <= 100
+
+
+def test_rescale_multiply_high_is_exact():
+    # ms_affinity.hip f_r: floor(100 v / r) as umulhi(100 v, floor((2^32 - 1) / r) + 1) for the
+    # rescale of every table entry (v <= 100; a rescale has r > 100, raw scores reach 400)
+    r = np.arange(101, 65536, dtype=np.uint64)[:, None]
+    v = np.arange(0, 101, dtype=np.uint64)[None, :]
+    m = np.uint64(0xFFFFFFFF) // r + np.uint64(1)
+    assert np.array_equal((np.uint64(100) * v * m) >> np.uint64(32), (np.uint64(100) * v) // r)
