@@ -272,7 +272,10 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
         // recomputes by 10 %: config E 39.7 -> 38.5 ms (profiles/r05l_e_ab.txt;
         // 4096:32 / 8192:32 / 16384:32 / 16384:64 / 32768:64 measured slower,
         // r05k_e_warm.txt).
-        constexpr uint32_t kWarmPods = 8192, kWarmBatch = 64;
+#ifndef MS_WARM_PODS
+#define MS_WARM_PODS 8192
+#endif
+        constexpr uint32_t kWarmPods = MS_WARM_PODS, kWarmBatch = 64;
         auto batch_at = [&](uint32_t s0) { return s0 < kWarmPods ? std::min(kWarmBatch, B) : B; };
         const uint32_t nb0 = std::min(batch_at(0), n_pods);
         const char *merge_env = getenv("MINISCHED_SEQ_MERGE");

@@ -1465,7 +1465,15 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
 // inserts the map entry) and need (four touched entries in a full list: the
 // tile lists decide). ck == 0 without need: the list ended and none of its
 // nodes is feasible now, so no node is (a FitError).
+// EXT: a pod whose four entries are all touched continues into the merge's
+// ranks 4..cert-1 (S.top_ext) by the same rule, 16 pods per pass: the first
+// untouched one is exact (its record is fetched from the table into the pod's
+// slot 4 pod, dead since all four of its top-4 nodes are touched) and bounds
+// every row below it; `need` stays only when every certified entry is touched
+// in a full list (the serial path then scans the tile lists). Without it those
+// pods were resolved one at a time, each ending its round (round 6).
 // Called by the whole wave (wave-uniform passes); clears `walk`.
+template <bool EXT = false>
 __device__ __forceinline__ void walk_top4(SeqShared &S, const NodeTable &t, uint32_t seed32, bool &walk, uint32_t pod,
                                           u64 &ck, uint32_t &cslot, bool &cins, bool &need, SeqCounters &ctr) {
     const uint32_t lane = lane_id();
@@ -1520,6 +1528,67 @@ __device__ __forceinline__ void walk_top4(SeqShared &S, const NodeTable &t, uint
         }
         __builtin_amdgcn_wave_barrier();
         wm = __ballot(walk);
+    }
+    if (!EXT) return;
+    bool ext = need && S.cert[pod] > (uint8_t)kTopK;  // (need is set only on walking lanes)
+    for (u64 wm = __ballot(ext); wm;) {
+        const uint32_t nw = min(16u, (uint32_t)__builtin_popcountll(wm));
+        const uint32_t rank = (uint32_t)__builtin_popcountll(wm & ((1ull << lane) - 1ull));
+        if (ext && rank < 16u) S.walk[rank] = pod;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t qi = lane >> 2, r = lane & 3u;
+        u64 v = 0;
+        uint32_t vs = 0;
+        bool unt = false, end = false, known = false;
+        if (qi < nw) {
+            const uint32_t pw = S.walk[qi];
+            known = (uint32_t)kTopK + r < (uint32_t)S.cert[pw];
+            const u64 e = known ? S.top_ext[pw][r] : 0ull;
+            if (known && e == 0) {
+                end = true;  // list ended within the certified ranks
+            } else if (known) {
+                const uint32_t er = row_of_key(e, t.base);
+                const int es = map_find(S, er);
+                if (es < 0) {
+                    unt = true;
+                    v = e;
+                    vs = kTopK * pw;  // (the record is fetched below if this entry wins)
+                } else {
+                    uint32_t nu, nrf;
+                    v = eval_full(slot_row(S, es), er + t.base, load_pod(S.pods[pw], seed32), nu, nrf);
+                    vs = (uint32_t)es;
+                    ++ctr.recompute;
+                }
+            }
+        }
+        const uint32_t qb = (uint32_t)(__ballot(known && (unt || end)) >> (4u * qi)) & 0xFu;
+        const uint32_t f = qb ? (uint32_t)__builtin_ctz(qb) : 4u;
+        const bool valid = known && !end && (r < f || (r == f && unt));
+        const u64 ve = valid ? v : 0ull;
+        const u64 m = quad_max_u64(ve);
+        const uint32_t own = (uint32_t)(__ballot(valid && m != 0 && ve == m) >> (4u * qi)) & 0xFu;
+        if (qi < nw && r == (own ? (uint32_t)__builtin_ctz(own) : 0u))
+            S.walkres[qi] = {m, vs, (unt && m != 0 ? 1u : 0u) | (qb == 0u ? 2u : 0u)};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        bool fetch = false;
+        if (ext && rank < 16u) {
+            const WalkResult w = S.walkres[rank];
+            if (w.key > ck) {  // (distinct nodes: keys never tie)
+                ck = w.key;
+                cslot = w.slot;
+                cins = (w.flags & 1u) != 0;
+                fetch = cins;
+            }
+            need = (w.flags & 2u) != 0;
+            ext = false;
+        }
+        ctr.miss += (uint32_t)__builtin_popcountll(__ballot(fetch));
+        if (fetch) store_merged_rec(t, ck, S.rec[cslot]);  // the untouched winner's current record
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        wm = __ballot(ext);
     }
 }
 
@@ -1931,7 +2000,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     MS_VST_DECL
     SeqCounters ctr = {0, 0, 0, 0, 0, 0};
     // (pro 2: the whole prologue ran on the workgroup: prologue_wg_issue / _finish)
-    const uint32_t n_own_in = pro == 2 ? (prev_in ? prev_in[0] : 0u) : validate_prologue_wave(S, va, lane, pro == 1, ctr);
+    // (pro 2: prev_in[0] is read only where it is used, in the carry branch at the end: a
+    // scalar load issued here would hold every LDS wait of the decisions until it landed)
+    const uint32_t n_own_wave = pro == 2 ? 0u : validate_prologue_wave(S, va, lane, pro == 1, ctr);
     if (pro == 2 && lane == 0) ctr.recompute = S.n_prorec;  // (summed over lanes at the end)
     uint32_t tiles = 0;  // tiles: bit j <=> this lane owns tile lane + 64 j
 #pragma unroll
@@ -1998,7 +2069,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
                     walk = true;
                 }
             }
-            walk_top4(S, t, seed32, walk, pl, ck, cslot, cins, need, ctr);
+            walk_top4<true>(S, t, seed32, walk, pl, ck, cslot, cins, need, ctr);
             if (act && cvalid) crow = ck ? row_of_key(ck, t.base) : 0xFFFFFFFEu;
             MS_VST(7);
             const bool claims = act && !need && ck != 0 && dig_l >= 0;  // binds at ck if decided this round
@@ -2212,6 +2283,7 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     if (prev_out) {
         // carried: the previous batch's own binds that this batch did not bind again
         const uint32_t n_own = S.n_out;
+        const uint32_t n_own_in = carry ? (pro == 2 ? (prev_in ? prev_in[0] : 0u) : n_own_wave) : 0u;
         if (carry)
             for (uint32_t i = lane; i < min(n_own_in, (uint32_t)kSeqBatch); i += 64) {
                 const uint32_t sl = kPrevSlot0 + i;

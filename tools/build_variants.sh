@@ -19,6 +19,10 @@ elif [ "$VST" = tl ]; then  # step timeline only (MS_TIMELINE=<file>; the host s
 else
   $H $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
   CAPI=build/ms_capi.o
+  if [ -n "$DEFS" ]; then  # (host-side constants such as MS_WARM_PODS take the same -D flags)
+    $H $DEFS -c csrc/ms_capi.cpp -o build/ms_capi_$NAME.o
+    CAPI=build/ms_capi_$NAME.o
+  fi
 fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o minisched_amd/libminisched_gpu_$NAME.so build/ms_kernels_$NAME.o build/ms_sweep_pp.o build/ms_taint.o build/ms_affinity.o $CAPI build/ms_comm.o -L/opt/rocm/lib -lrccl
 echo built minisched_amd/libminisched_gpu_$NAME.so
