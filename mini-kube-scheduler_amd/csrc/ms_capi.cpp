@@ -265,15 +265,16 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     const size_t prev_words = 2 + seq_prev_cap(), prev_fields = (size_t)seq_prev_cap() * seq_rec_fields();
     const size_t cells_per_set = (size_t)SB * n_tiles, recs_per_set = (size_t)SB * seq_topk() * seq_rec_fields();
     {
-        // Warm-up batches: the first 8,192 pods of the queue in batches of 64. On an
+        // Warm-up batches: the first 4,096 pods of the queue in batches of 64. On an
         // empty cluster every pod prefers the same emptiest nodes, so early batches
         // touch each other's speculative winners most (the slow-path burst of
         // batches 20-30); half-size batches there cut the re-sweeps to 0 and the
         // recomputes by 10 %: config E 39.7 -> 38.5 ms (profiles/r05l_e_ab.txt;
         // 4096:32 / 8192:32 / 16384:32 / 16384:64 / 32768:64 measured slower,
-        // r05k_e_warm.txt).
+        // r05k_e_warm.txt). Round 6, with the validator's ranks 4..7 walk: none /
+        // 4,096 / 8,192 pods 32.3 / 31.1 / 31.2 ms (profiles/r06j_e_warm_ab.txt).
 #ifndef MS_WARM_PODS
-#define MS_WARM_PODS 8192
+#define MS_WARM_PODS 4096
 #endif
         constexpr uint32_t kWarmPods = MS_WARM_PODS, kWarmBatch = 64;
         auto batch_at = [&](uint32_t s0) { return s0 < kWarmPods ? std::min(kWarmBatch, B) : B; };
