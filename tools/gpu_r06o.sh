@@ -1,0 +1,14 @@
+# round 6 closing profiles on the final kernels: K1 (config C) kernel stats + counters, config E kernel
+# stats + counters + validator stamps, config E whole-run step timeline (the bench's E step_split)
+set -o pipefail
+T=${1:-r06o}
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+L=$PWD/mini-kube-scheduler_amd/minisched_amd
+bash tools/profile_pp.sh $T > gpurun_out/${T}_pp.log 2>&1 || { tail -20 gpurun_out/${T}_pp.log; exit 1; }
+tail -3 gpurun_out/${T}_pp.log
+bash tools/profile_e.sh $T > gpurun_out/${T}_pe.log 2>&1 || { tail -20 gpurun_out/${T}_pe.log; exit 1; }
+tail -3 gpurun_out/${T}_pe.log
+MS_TIMELINE=gpurun_out/${T}_tl.bin MINISCHED_LIB=$L/libminisched_gpu_tl.so timeout -k 10 200 python tools/bench_configs.py --configs E --reps 1 > gpurun_out/${T}_tl.jsonl 2> gpurun_out/${T}_tl.err || { tail gpurun_out/${T}_tl.err; exit 1; }
+python tools/e_wg_timeline.py gpurun_out/${T}_tl.bin gpurun_out/${T}_e_wg_timeline_run.json | tail -1
+rm -f gpurun_out/${T}_tl.bin
