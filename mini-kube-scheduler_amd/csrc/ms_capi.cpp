@@ -243,15 +243,26 @@ int run_sequential(ms_ctx *c, uint32_t n_pods, const ms_pod_rec *d_pods, ms_resu
     if (rows > seq_max_rows())
         return fail(c, MS_E_CAPACITY, "resource-aware sequential mode supports at most " +
                                           std::to_string(seq_max_rows()) + " rows per context (shard the nodes)");
-    const uint32_t n_tiles = cdiv(rows, kFullWaveTile);
+    // Tiles of the speculative sweep: one per CU beside the validator's where the
+    // table allows (rows per tile a multiple of 16, 64..256): at 50k nodes 241
+    // tiles of 208 rows on 241 CUs instead of 196 of 256 on 196 (round 6).
+    NodeTable tq = c->t;
+    {
+        const uint32_t room = (uint32_t)std::max(2, c->num_cus) - 1u;
+        const uint32_t tr = (cdiv(rows, room) + 15u) / 16u * 16u;
+        tq.tile_rows = std::min<uint32_t>((uint32_t)kFullWaveTile, std::max<uint32_t>(64u, tr));
+#ifdef MS_TILE_ROWS  // (A/B builds: a fixed tile height)
+        tq.tile_rows = MS_TILE_ROWS;
+#endif
+    }
+    const uint32_t n_tiles = cdiv(rows, tq.tile_rows);
     int rc = ensure_tiles(c, n_tiles);
     if (rc) return rc;
     // the engine's table copy carries the derived rows of the binary64 sweep,
     // rebuilt here (deltas and binds since the last run) and kept current by
     // the validator's write-back
-    NodeTable tq = c->t;
     tq.drow = c->d_drow;
-    MS_HIP(c, launch_build_drows(tq, rows, n_tiles * kFullWaveTile, s));
+    MS_HIP(c, launch_build_drows(tq, rows, n_tiles * tq.tile_rows, s));
     // Step k = ONE launch (launch_seq_step): validation of batch k on workgroup
     // 0 while the other workgroups sweep batch k+1 and then merge its tile lists
     // (the in-step merge); batch k+1 treats batch k's binds as stale. No

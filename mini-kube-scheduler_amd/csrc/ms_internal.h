@@ -21,7 +21,7 @@ constexpr int kNunnTile = kNunnThreads * kNunnSlots;  // nodes per block
 // K3 (resource-aware sweep) geometry.
 constexpr int kFullThreads = 256;
 constexpr int kFullSlots = 4;
-constexpr int kFullWaveTile = 64 * kFullSlots;            // nodes per wave  (validator tile)
+constexpr int kFullWaveTile = 64 * kFullSlots;            // nodes per wave  (validator tile; the most rows a tile holds)
 constexpr int kFullTile = kFullThreads * kFullSlots;      // nodes per block
 
 constexpr uint32_t kGolden32 = 0x9E3779B1u;  // LDS map hashing in the validator
@@ -49,12 +49,21 @@ struct NodeTable {
     // kGroupRows consecutive rows (bit s = row g*kGroupRows + s).
     uint32_t *planes;
     uint32_t gcap;  // groups allocated = cdiv(cap, kGroupRows)
+    // Rows per tile of the config-E sweep (the engine's table copy; 0 = kFullWaveTile).
+    // run_sequential sizes tiles so that every CU beside the validator's gets one
+    // (a multiple of 16, 64..256): 208 rows at 50k nodes = 241 tiles, not 196 x 256.
+    // (In the 4 bytes of padding before drow: the structure's size is unchanged.)
+    uint32_t tile_rows;
     // Derived rows of the config-E sweep's binary64 form (DRow), set only in the
     // table copy the sequential engine passes to its launches: rebuilt at the
     // start of each run (k_build_drows) and kept current by the validator's
     // write-back of the rows it binds. nullptr everywhere else.
     struct DRow *drow;
 };
+
+__host__ __device__ inline uint32_t tile_rows_of(const NodeTable &t) {
+    return t.tile_rows ? t.tile_rows : (uint32_t)kFullWaveTile;
+}
 
 // One node as the config-E sweep's binary64 LeastAllocated form reads it
 // (ms_kernels.hip make_drow; 64 B, one row per lane and load).

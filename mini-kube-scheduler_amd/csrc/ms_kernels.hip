@@ -583,16 +583,23 @@ struct SweepArgs {
 // One wave, lane = row: tile `tile`'s top-4 lists and filter flags for pods
 // [pbeg, pbeg + cnt), cnt <= 64. The binary64 fast form unless a row or pod of
 // the task is outside its exact range (MINISCHED_SEQ_FAST=0: a.fast == 0).
+// Row `slot` (lane * kFullSlots + s) of tile `tile`, or an absent row (~0u) past
+// the tile's height (t.tile_rows < kFullWaveTile: the next tile's rows).
+__device__ __forceinline__ uint32_t tile_slot_row(const NodeTable &t, uint32_t tile, uint32_t slot) {
+    const uint32_t tr = tile_rows_of(t);
+    return slot < tr ? tile * tr + slot : ~0u;
+}
+
 __device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t tile, uint32_t pbeg, uint32_t cnt,
                                                 uint32_t lane) {
-    const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
+    const uint32_t row0 = tile * tile_rows_of(a.t) + lane * kFullSlots;
     const uint32_t ord0 = a.t.base + row0;
     if (a.fast) {
         FastRow x[kFullSlots];
         bool ok = true;
 #pragma unroll
         for (int s = 0; s < kFullSlots; ++s) {
-            x[s] = load_fast_row(a.t, row0 + s, a.n_rows);
+            x[s] = load_fast_row(a.t, tile_slot_row(a.t, tile, lane * kFullSlots + s), a.n_rows);
             ok = ok && !(x[s].rbits & kRbSlow);
         }
         ms_pod_rec z = {};
@@ -605,7 +612,7 @@ __device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t til
     }
     FullRow x[kFullSlots];
 #pragma unroll
-    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, tile_slot_row(a.t, tile, lane * kFullSlots + s), a.n_rows);
     const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
     if (rows_huge(x)) sweep_topk_pods<1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags, a.coh);
     else sweep_topk_pods<0>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys, a.tile_flags, a.coh);
@@ -615,11 +622,11 @@ __device__ __forceinline__ void sweep_rows_task(const SweepArgs &a, uint32_t til
 // rare): the general int64 form one pod at a time, lean on registers.
 __device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_t tile, uint32_t pbeg, uint32_t cnt,
                                                      uint32_t lane) {
-    const uint32_t row0 = tile * kFullWaveTile + lane * kFullSlots;
+    const uint32_t row0 = tile * tile_rows_of(a.t) + lane * kFullSlots;
     const uint32_t ord0 = a.t.base + row0;
     FullRow x[kFullSlots];
 #pragma unroll
-    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, row0 + s, a.n_rows);
+    for (int s = 0; s < kFullSlots; ++s) x[s] = load_row(a.t, tile_slot_row(a.t, tile, lane * kFullSlots + s), a.n_rows);
     const PodLanes m = stage_pods(a.pods, pbeg, cnt, lane, a.seed32);
     if (rows_huge(x))
         sweep_topk_pods<1, FullRow, PodLanes, 1>(x, ord0, m, pbeg, cnt, lane, tile, a.n_tiles, a.tile_keys,
@@ -640,9 +647,6 @@ __device__ __forceinline__ void sweep_rows_task_lean(const SweepArgs &a, uint32_
 // where the lane = row form paid a sort plus four wave-wide max extractions
 // per (pod, tile) on top of its evaluations.
 constexpr uint32_t kTpPods = 16;
-#ifndef MS_TP_UNROLL
-#define MS_TP_UNROLL 2  // row blocks unrolled in sweep_tp_task (round 5, binary64 keys + ld_drow: 2 vs 1 = 33.87 vs 34.16 ms at config E, profiles/r05ay_e_unroll_ab.txt; round 4 form: 1 / 2 / 4 / 8 = 44.4 / 45.2 / 44.9 / 44.9 ms, r04s_e_unroll.txt)
-#endif
 #define MS_PRAGMA(x) _Pragma(#x)
 #define MS_UNROLL(n) MS_PRAGMA(unroll n)
 
@@ -812,10 +816,11 @@ struct TileBits {
     uint32_t any, all;
 };
 
-__device__ __forceinline__ TileBits tile_bits(const DRow *rows, uint32_t lane) {
+__device__ __forceinline__ TileBits tile_bits(const DRow *rows, uint32_t lane, uint32_t tr) {
     uint32_t o = 0, a = ~0u;
 #pragma unroll
     for (int k = 0; k < (int)kFullWaveTile / 64; ++k) {
+        if (lane + 64u * k >= tr) continue;  // (a tile of tr < kFullWaveTile rows)
         const uint32_t r = rows[lane + 64u * k].rbits;
         o |= r;
         a &= r;
@@ -845,13 +850,18 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     ms_pod_rec z = {};
     const PodFast q = load_pod_fast(pi < cnt ? a.pods[pbeg + pi] : z, a.seed32);
     if ((tb.any & kRbSlow) || __ballot(pi < cnt && !(q.bits & kPfOk))) return false;
-    const uint32_t row0 = tile * kFullWaveTile + part;
+    // (tr: a multiple of 16, so every part's rows come in whole 4-row blocks; a
+    // runtime trip count, not unrolled: unroll 2 gained 0.6 % at a fixed 256 rows,
+    // profiles/r05ay_e_unroll_ab.txt, but written out by hand, or left to the
+    // compiler's runtime unrolling, it made k_seq_step spill 121 VGPRs)
+    const uint32_t tr = tile_rows_of(a.t);
+    const uint32_t row0 = tile * tr + part;
     const uint32_t ord0 = a.t.base + row0;
     const DRow *d = rows + part;  // the tile's rows, staged in LDS
 #if MS_TP_F64KEYS
     double k[4] = {0.0, 0.0, 0.0, 0.0};
-    MS_UNROLL(MS_TP_UNROLL)
-    for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
+#pragma unroll 1
+    for (uint32_t i = 0; i < tr / 4u; i += 4) {
         double x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -866,7 +876,7 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
     if (pi < cnt) {
         const size_t cell = (size_t)(pbeg + pi) * a.n_tiles + tile;
         const double mine = part == 0 ? k[0] : part == 1 ? k[1] : part == 2 ? k[2] : k[3];
-        const u64 g = global_key(mine, a.t.base + tile * kFullWaveTile);
+        const u64 g = global_key(mine, a.t.base + tile * tr);
         if (a.coh) {  // (launch-uniform)
             st_coh(a.tile_keys + cell * kTopK + part, g | (u64)a.coh << kListTagShift);
             if (part == 0) st_coh(a.tile_flags + cell, f | a.coh << 16);
@@ -879,8 +889,8 @@ __device__ __forceinline__ bool sweep_tp_task(const SweepArgs &a, uint32_t tile,
 #else
     u64 k[4] = {0ull, 0ull, 0ull, 0ull};
     // rows 4 at a time (LDS reads issued together at the top of each block)
-    MS_UNROLL(MS_TP_UNROLL)
-    for (uint32_t i = 0; i < (uint32_t)kFullWaveTile / 4u; i += 4) {
+#pragma unroll 1
+    for (uint32_t i = 0; i < tr / 4u; i += 4) {
         u64 x[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) x[u] = eval_tp(d[4 * (i + u)], ord0 + 4 * (i + u), q);
@@ -919,13 +929,14 @@ template <int W>
 __device__ __forceinline__ uint32_t sweep_tp_tile(const SweepArgs &a, uint32_t tile, DRow *rows, uint32_t wave,
                                                   uint32_t lane, u64 *tl = nullptr) {
     __syncthreads();  // the previous tile's readers are done
-    const uint4 *src = reinterpret_cast<const uint4 *>(a.t.drow + (size_t)tile * kFullWaveTile);
+    const uint32_t tr = tile_rows_of(a.t);
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.t.drow + (size_t)tile * tr);
     uint4 *dst = reinterpret_cast<uint4 *>(rows);
-    constexpr uint32_t kVec = kFullWaveTile * sizeof(DRow) / sizeof(uint4);
-    for (uint32_t i = threadIdx.x; i < kVec; i += 64u * W) dst[i] = src[i];
+    const uint32_t n_vec = tr * (uint32_t)(sizeof(DRow) / sizeof(uint4));
+    for (uint32_t i = threadIdx.x; i < n_vec; i += 64u * W) dst[i] = src[i];
     __syncthreads();
     if (tl && threadIdx.x == 0) tl[kTlStaged] = __builtin_amdgcn_s_memrealtime();  // (diagnostic builds)
-    const TileBits tb = tile_bits(rows, lane);
+    const TileBits tb = tile_bits(rows, lane, tr);
     // (a batch holds at most kSeqBatch <= 256 pods, i.e. 16 groups)
     uint32_t redo = 0;
     for (uint32_t grp = wave, i = 0; grp * kTpPods < a.n_pods; grp += W, ++i)
@@ -1435,7 +1446,7 @@ __device__ __forceinline__ void validate_scan(SeqShared &S, const NodeTable &t, 
         ++ctr.resweep;
 #pragma unroll
         for (int sidx = 0; sidx < kFullSlots; ++sidx) {
-            const uint32_t r = tile * kFullWaveTile + lane * kFullSlots + sidx;
+            const uint32_t r = tile_slot_row(t, tile, lane * kFullSlots + sidx);  // (~0u past the tile: absent)
             FullRow x = load_row(t, r, n_rows);
             int sl = -1;
             if (r < n_rows) {
@@ -2310,8 +2321,9 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
 // itself) while the other workgroups sweep batch k+1 (a (tile, pod chunk)
 // task per wave, k_sweep_full_topk's work). One launch per batch and no
 // cross-stream hand-off: batch k+1's speculation may predate batch k's binds,
-// which its validation treats as stale (prev lists). W waves per workgroup:
-// the most that fit the validator's VGPRs at one workgroup per CU.
+// which its validation treats as stale (prev lists). W waves per workgroup
+// (launch_seq_step: 8 up to 256 tiles, MS_STEP_W4; the validator's VGPRs at
+// one workgroup per CU).
 // Batch k+1's in-step merge (SeqMergeIO, depth 1): n = 0 none.
 struct StepMerge {
     u64 *top, *spec, *ext;
@@ -2326,8 +2338,9 @@ struct StepMerge {
 
 constexpr uint64_t kMergeSpinTicks = 10000;  // a worker's wait for the sweep, s_memrealtime (100 MHz): 100 us
 
-// Worker wid (wave W-1 of every sweep workgroup first: idle in the transposed
-// sweep, which keeps 8 of the 12 waves busy) merges pods wid, wid + W * nsw, ..
+// Worker wid (wave W-1 of every sweep workgroup first: idle in a 12-wave
+// transposed sweep, which keeps 8 busy; with 8 waves it merges after its own
+// pod group) merges pods wid, wid + W * nsw, ..
 // of the next batch and tags each. MS_MERGE_TAGS: it polls the tagged lists
 // themselves from the start of the step (merge_pod_lists); otherwise every
 // sweep workgroup counts itself done on sm.ctr once its stores landed and the
@@ -2509,10 +2522,9 @@ __global__ __launch_bounds__(64 * W) void k_seq_step(SeqArgs va, SweepArgs sw, u
             for (uint32_t grp = wave, i = 0; grp * kTpPods < sw.n_pods; grp += W, ++i) all |= 1u << i;
             for (uint32_t tile = sb; tile < sw.n_tiles; tile += sg) sweep_tp_redo<W>(sw, tile, all, wave, lane);
         }
-        if (tlw) {  // (launch-uniform: diagnostic builds only)
-            __syncthreads();
-            if (threadIdx.x == 0) tlw[kTlTasks] = __builtin_amdgcn_s_memrealtime();
-        }
+        if (tlw && lane == 0)  // (diagnostic builds: the last wave's end, without a barrier that would hold the merging wave)
+            atomicMax(reinterpret_cast<unsigned long long *>(tlw + kTlTasks),
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());
     } else {
         for (uint32_t task = sb * W + wave; task < n_tasks; task += sg * W)
             sweep_topk_task(sw, task % sw.n_tiles, task / sw.n_tiles, lane);
@@ -3046,7 +3058,7 @@ hipError_t launch_sweep_full_tiles(const NodeTable &t, uint32_t n_rows, const ms
                                    uint32_t n_pods, uint32_t seed32, unsigned long long *tile_keys,
                                    uint32_t *tile_flags, uint32_t n_tiles, hipStream_t s) {
     if (n_pods == 0 || n_rows == 0) return hipSuccess;
-    if (n_tiles != cdiv(n_rows, kFullWaveTile)) return hipErrorInvalidValue;
+    if (n_tiles != cdiv(n_rows, tile_rows_of(t))) return hipErrorInvalidValue;
     const uint32_t gx = cdiv(n_tiles, kFullThreads / 64);
     const uint32_t chunk = 8;  // pods per wave: node rows amortised against enough waves to fill the chip
     if (t.drow && seq_fast()) {  // transposed form: one workgroup per tile
@@ -3075,7 +3087,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
                            unsigned long long *next_tile_keys, uint32_t *next_tile_flags, int num_cus,
                            hipStream_t s, const unsigned long long *top_ext, SeqMergeIO *mio) {
     if (n_pods == 0 && n_next == 0) return hipSuccess;
-    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, kFullWaveTile) ||
+    if (n_pods > (uint32_t)kSeqBatch || n_tiles > 64u * kSeqMaxJ || n_tiles != cdiv(n_rows, tile_rows_of(t)) ||
         (n_pods && (!top4_recs || (prev_in && !prev_recs_in) || (prev_out && !prev_recs_out))))
         return hipErrorInvalidValue;
     SeqArgs va = {t,        n_rows,       pods,    n_pods,     seed32, tile_keys, tile_flags,
@@ -3085,7 +3097,15 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     // sweep workgroups (one per CU beside the validator's)
     const uint32_t cus = (uint32_t)(num_cus > 1 ? num_cus : 256);
     const int J = n_tiles <= 64 ? 1 : n_tiles <= 128 ? 2 : n_tiles <= 256 ? 4 : n_tiles <= 512 ? 8 : 16;
-    const uint32_t W = J <= 4 ? 12u : J == 8 ? 8u : 4u;
+#ifndef MS_STEP_W4
+// Waves per workgroup for n_tiles <= 256. 8 (round 6): with tiles sized to the
+// CUs (t.tile_rows) the 12-wave form's 168 VGPRs spilled 121 in the merge; 8
+// waves (the transposed sweep's busy ones, the 8th merging after its sweep)
+// take 238 without spilling: config E 31.13 -> 30.3 ms with 208-row tiles,
+// 31.3 with 256 (profiles/r06q_e_tiles_ab.txt).
+#define MS_STEP_W4 8
+#endif
+    const uint32_t W = J <= 4 ? (uint32_t)MS_STEP_W4 : J == 8 ? 8u : 4u;
     uint32_t chunk = 8;
     if (n_next) chunk = std::min(64u, std::max(8u, cdiv(n_tiles * n_next, (cus - 1) * W)));
     const bool tp = t.drow && seq_fast();
@@ -3128,7 +3148,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, sm)
     if (J == 1) MS_STEP(1, 12);
     else if (J == 2) MS_STEP(2, 12);
-    else if (J == 4) MS_STEP(4, 12);
+    else if (J == 4) MS_STEP(4, MS_STEP_W4);
     else if (J == 8) MS_STEP(8, 8);
     else MS_STEP(16, 4);
 #undef MS_STEP
