@@ -1092,7 +1092,10 @@ __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_key
         }
         if (!COH || !tag || __ballot(!ok) == 0) break;
         if (__builtin_amdgcn_s_memrealtime() > deadline) return false;
-        __builtin_amdgcn_s_sleep(2);
+#ifndef MS_MERGE_SLEEP
+#define MS_MERGE_SLEEP 2  // s_sleep between a merge worker's list polls (x 64 cycles)
+#endif
+        __builtin_amdgcn_s_sleep(MS_MERGE_SLEEP);
     }
 #pragma unroll
     for (int j = 0; j < J; ++j) {
