@@ -1002,23 +1002,41 @@ __device__ __forceinline__ int64_t rec_field(const NodeTable &t, uint32_t r, uin
 
 // The validator's record of key k's node (F_ROW = -1 for an empty entry),
 // written with 16-byte stores so the validator copies it as is.
-__device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int64_t *dst) {
+struct MergedRec {
+    int64_t v[kSpecF];
+    uint32_t row;  // ~0u: an empty entry
+};
+
+// The table loads of key k's record, issued (nothing waits for them here).
+__device__ __forceinline__ MergedRec load_merged_rec(const NodeTable &t, u64 k) {
+    MergedRec m;
+    m.row = k ? row_of_key(k, t.base) : ~0u;
+    const uint32_t r = k ? m.row : 0u;  // (row 0 is a valid address)
+#pragma unroll
+    for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) m.v[f] = rec_field(t, r, f);
+    return m;
+}
+
+__device__ __forceinline__ void store_rec(const MergedRec &m, int64_t *dst) {
     int64_t v[kRecF];
+    const bool e = m.row != ~0u;
 #pragma unroll
-    for (int f = 0; f < kRecF; ++f) v[f] = 0;
-    v[F_ROW] = -1;
-    if (k) {
-        const uint32_t r = row_of_key(k, t.base);
-#pragma unroll
-        for (uint32_t f = 0; f < (uint32_t)kSpecF; ++f) v[f] = rec_field(t, r, f);
-        v[F_ROW] = r;
-        v[F_INV_CPU] = __float_as_uint(r100(v[F_ALLOC_CPU]));
-        v[F_INV_MEM] = __float_as_uint(r100(v[F_ALLOC_MEM]));
-    }
+    for (int f = 0; f < kSpecF; ++f) v[f] = e ? m.v[f] : 0;
+    v[F_ROW] = e ? (int64_t)m.row : -1;
+    v[F_INV_CPU] = e ? __float_as_uint(r100(m.v[F_ALLOC_CPU])) : 0;
+    v[F_INV_MEM] = e ? __float_as_uint(r100(m.v[F_ALLOC_MEM])) : 0;
     longlong2 *d = reinterpret_cast<longlong2 *>(dst);
 #pragma unroll
     for (int f = 0; f < kRecF; f += 2) d[f / 2] = make_longlong2(v[f], v[f + 1]);
 }
+
+__device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int64_t *dst) {
+    store_rec(load_merged_rec(t, k), dst);
+}
+
+struct NoTop4Hook {
+    __device__ __forceinline__ void operator()(u64) const {}
+};
 
 // One wave merges pod p's tile lists: lane r < R gets the global rank-r key
 // (out, 0 past the feasible rows), f the filters of the tiles with no feasible
@@ -1031,11 +1049,14 @@ __device__ __forceinline__ void store_merged_rec(const NodeTable &t, u64 k, int6
 // COH: the lists are written in the same launch (ld_coh); with tag != 0 the
 // lists carry it (MS_MERGE_TAGS) and the loads repeat until every list read
 // has it, or until `deadline` (s_memrealtime) passes: then false, nothing out.
-template <int J, int R = kTopK, bool COH = false>
+// at4(out): called on every lane once ranks 0..3 are final (lane r < 4 holds
+// rank r), before the ranks past them are merged: the caller's record loads for
+// those entries overlap the later rounds.
+template <int J, int R = kTopK, bool COH = false, typename H = NoTop4Hook>
 __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_keys,
                                                 const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
                                                 uint32_t lane, u64 &out, uint32_t &f, uint32_t *cert_out = nullptr,
-                                                uint32_t tag = 0, uint64_t deadline = 0) {
+                                                uint32_t tag = 0, uint64_t deadline = 0, const H &at4 = H()) {
     u64 e[J][kTopK];
     uint32_t pos[J];
     uint32_t tfs[J];
@@ -1135,6 +1156,7 @@ __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_key
                 }
         }
         if (R > kTopK && cert == (uint32_t)R && __ballot(used_up)) cert = (uint32_t)r + 1u;
+        if (r == kTopK - 1) at4(out);
     }
     if (cert_out) *cert_out = cert;
     f = (__ballot((fl & 0xFFu) != 0) ? 1u : 0u) | (__ballot((fl & 0xFF00u) != 0) ? 0x100u : 0u) |
@@ -1158,16 +1180,26 @@ __device__ __forceinline__ bool merge_pod(const u64 *__restrict__ tile_keys, con
                                           uint32_t tag = 0, uint64_t deadline = 0) {
     u64 out;
     uint32_t f, cert = 0;
+#ifndef MS_MERGE_REC_EARLY
+#define MS_MERGE_REC_EARLY 1  // the four records' table loads issued right after rank 3
+#endif
+    MergedRec mr;  // lanes 0..3: their entry's record
+    const auto at4 = [&](u64 o) {
+        if (MS_MERGE_REC_EARLY && recs && lane < (uint32_t)kTopK) mr = load_merged_rec(t, o);
+    };
     if (ext) {
-        if (!merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert, tag, deadline))
+        if (!merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert, tag, deadline, at4))
             return false;
         if (lane >= (uint32_t)kTopK && lane < (uint32_t)kTopExt) ext[(size_t)p * kTopK + lane - kTopK] = out;
     } else {
-        if (!merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, nullptr, tag, deadline))
+        if (!merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, nullptr, tag, deadline, at4))
             return false;
     }
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
-    if (recs && lane < (uint32_t)kTopK) store_merged_rec(t, out, recs + ((size_t)p * kTopK + lane) * kRecF);
+    if (recs && lane < (uint32_t)kTopK) {
+        if (!MS_MERGE_REC_EARLY) mr = load_merged_rec(t, out);
+        store_rec(mr, recs + ((size_t)p * kTopK + lane) * kRecF);
+    }
     // the speculative winner (rank 0) and, when no row is feasible, the filters
     if (lane == 0) {
         spec[p] = out;
