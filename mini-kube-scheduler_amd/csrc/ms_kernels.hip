@@ -3133,7 +3133,7 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     const uint32_t cus = (uint32_t)(num_cus > 1 ? num_cus : 256);
     const int J = n_tiles <= 64 ? 1 : n_tiles <= 128 ? 2 : n_tiles <= 256 ? 4 : n_tiles <= 512 ? 8 : 16;
 #ifndef MS_STEP_W4
-// Waves per workgroup for n_tiles <= 256. 8 (round 6): with tiles sized to the
+// Waves per workgroup for n_tiles <= 256 (J <= 4). 8 (round 6): with tiles sized to the
 // CUs (t.tile_rows) the 12-wave form's 168 VGPRs spilled 121 in the merge; 8
 // waves (the transposed sweep's busy ones, the 8th merging after its sweep)
 // take 238 without spilling: config E 31.13 -> 30.3 ms with 208-row tiles,
@@ -3181,8 +3181,8 @@ hipError_t launch_seq_step(const NodeTable &t, uint32_t n_rows, uint32_t n_tiles
     va.tl = sm.tl;
 #define MS_STEP(JJ, WW) \
     hipLaunchKernelGGL((k_seq_step<JJ, WW>), dim3(grid), dim3(64 * WW), 0, s, va, sw, n_tasks, sm)
-    if (J == 1) MS_STEP(1, 12);
-    else if (J == 2) MS_STEP(2, 12);
+    if (J == 1) MS_STEP(1, MS_STEP_W4);  // (12 waves spilled 119 VGPRs here too)
+    else if (J == 2) MS_STEP(2, MS_STEP_W4);
     else if (J == 4) MS_STEP(4, MS_STEP_W4);
     else if (J == 8) MS_STEP(8, 8);
     else MS_STEP(16, 4);
