@@ -1056,7 +1056,8 @@ template <int J, int R = kTopK, bool COH = false, typename H = NoTop4Hook>
 __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_keys,
                                                 const uint32_t *__restrict__ tile_flags, uint32_t p, uint32_t n_tiles,
                                                 uint32_t lane, u64 &out, uint32_t &f, uint32_t *cert_out = nullptr,
-                                                uint32_t tag = 0, uint64_t deadline = 0, const H &at4 = H()) {
+                                                uint32_t tag = 0, uint64_t deadline = 0, const H &at4 = H(),
+                                                uint64_t *t_poll = nullptr) {
     u64 e[J][kTopK];
     uint32_t pos[J];
     uint32_t tfs[J];
@@ -1118,6 +1119,7 @@ __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_key
 #endif
         __builtin_amdgcn_s_sleep(MS_MERGE_SLEEP);
     }
+    if (t_poll) *t_poll = __builtin_amdgcn_s_memrealtime();  // (timeline build: every list arrived)
 #pragma unroll
     for (int j = 0; j < J; ++j) {
         const uint32_t tt = lane + 64u * j;
@@ -1130,6 +1132,59 @@ __device__ __forceinline__ bool merge_pod_lists(const u64 *__restrict__ tile_key
     }
     out = 0;
     uint32_t cert = R;
+#ifndef MS_MERGE_SORTED
+#define MS_MERGE_SORTED 1  // each lane's lists merged into one sorted top-8 first; a round pops by a shift
+#endif
+    if (MS_MERGE_SORTED) {
+        // The lane's own J lists (each sorted, best first) merged into its top
+        // 8, best first: list j joins by Batcher's half merge (the elementwise
+        // max of L and the list reversed is bitonic and holds the top 8), then a
+        // bitonic sort of 8. A round then reads L[0] and the popping lane shifts:
+        // a few independent selects instead of J list heads picked by position.
+        u64 L[8];
+        u64 sp[J];  // the last entry of each full list: popping it ends the certified ranks
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const bool in = lane + 64u * (uint32_t)j < n_tiles;  // (past n_tiles: the clamped tile's copy)
+#pragma unroll
+            for (int k = 0; k < kTopK; ++k) e[j][k] = in ? e[j][k] : 0ull;
+            sp[j] = e[j][kTopK - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) L[k] = k < kTopK ? e[0][k] : 0ull;
+        const auto ce = [](u64 &a, u64 &b) {  // max to a
+            const u64 x = a > b ? a : b, y = a > b ? b : a;
+            a = x;
+            b = y;
+        };
+#pragma unroll
+        for (int j = 1; j < J; ++j) {
+#pragma unroll
+            for (int i = 8 - kTopK; i < 8; ++i) L[i] = L[i] > e[j][7 - i] ? L[i] : e[j][7 - i];
+#pragma unroll
+            for (int d = 4; d >= 1; d >>= 1)
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if ((i & d) == 0) ce(L[i], L[i + d]);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const u64 head = L[0];
+            const u64 m = MS_MERGE_WMAX(head);
+            if (lane == (uint32_t)r) out = m;
+            const bool pop = m != 0 && head == m;  // keys are unique: exactly one lane pops
+            bool used_up = false;
+            if (R > kTopK) {
+#pragma unroll
+                for (int j = 0; j < J; ++j) used_up = used_up || (pop && head == sp[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < 7; ++i) L[i] = pop ? L[i + 1] : L[i];
+            L[7] = pop ? 0ull : L[7];
+            if (R > kTopK && cert == (uint32_t)R && __ballot(used_up)) cert = (uint32_t)r + 1u;
+            if (r == kTopK - 1) at4(out);
+        }
+    } else
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         u64 head = 0;  // this lane's best list head
@@ -1177,7 +1232,8 @@ __device__ __forceinline__ bool merge_pod(const u64 *__restrict__ tile_keys, con
                                           uint32_t p, uint32_t n_tiles, u64 *__restrict__ top, u64 *__restrict__ spec,
                                           uint32_t *__restrict__ spec_flags, const NodeTable &t,
                                           int64_t *__restrict__ recs, u64 *__restrict__ ext, uint32_t lane,
-                                          uint32_t tag = 0, uint64_t deadline = 0) {
+                                          uint32_t tag = 0, uint64_t deadline = 0, uint64_t *t_poll = nullptr,
+                                          uint64_t *t_rank = nullptr) {
     u64 out;
     uint32_t f, cert = 0;
 #ifndef MS_MERGE_REC_EARLY
@@ -1188,13 +1244,16 @@ __device__ __forceinline__ bool merge_pod(const u64 *__restrict__ tile_keys, con
         if (MS_MERGE_REC_EARLY && recs && lane < (uint32_t)kTopK) mr = load_merged_rec(t, o);
     };
     if (ext) {
-        if (!merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert, tag, deadline, at4))
+        if (!merge_pod_lists<J, kTopExt, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, &cert, tag, deadline, at4,
+                                              t_poll))
             return false;
         if (lane >= (uint32_t)kTopK && lane < (uint32_t)kTopExt) ext[(size_t)p * kTopK + lane - kTopK] = out;
     } else {
-        if (!merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, nullptr, tag, deadline, at4))
+        if (!merge_pod_lists<J, kTopK, COH>(tile_keys, tile_flags, p, n_tiles, lane, out, f, nullptr, tag, deadline, at4,
+                                            t_poll))
             return false;
     }
+    if (t_rank) *t_rank = __builtin_amdgcn_s_memrealtime();  // (timeline build: ranks merged)
     if (lane < (uint32_t)kTopK) top[(size_t)p * kTopK + lane] = out;
     if (recs && lane < (uint32_t)kTopK) {
         if (!MS_MERGE_REC_EARLY) mr = load_merged_rec(t, out);
@@ -2424,17 +2483,24 @@ __device__ __forceinline__ void step_merge(const SweepArgs &sw, const StepMerge 
 #endif
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
     const uint64_t t_waited = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_poll = 0, t_rank = 0;  // the first pod's lists all arrived / its ranks merged
+#define MS_TL_MERGE_STAMPS , p == wid ? &t_poll : nullptr, p == wid ? &t_rank : nullptr
+#else
+#define MS_TL_MERGE_STAMPS
 #endif
     for (uint32_t p = wid; p < sm.n; p += W * nsw) {
         if (!merge_pod<J, true>(sw.tile_keys, sw.tile_flags, p, sw.n_tiles, sm.top, sm.spec, sm.spec_flags, sw.t,
-                                sm.recs, sm.ext, lane, tag, deadline))
+                                sm.recs, sm.ext, lane, tag, deadline MS_TL_MERGE_STAMPS))
             return;  // (untagged: the next validation merges it)
+#undef MS_TL_MERGE_STAMPS
         if (lane == 0) sm.tags[p] = sm.tag;
     }
 #if defined(MS_VSTAMPS) || defined(MS_TIMELINE_ONLY)
     __builtin_amdgcn_s_waitcnt(0);
     if (lane == 0 && sm.tl) {
         sm.tl[blockIdx.x * 8 + kTlWaited] = t_waited;
+        sm.tl[blockIdx.x * 8 + kTlSwept] = t_rank;  // (tagged lists: slot 1 holds the first pod's ranks merged)
+        sm.tl[blockIdx.x * 8 + kTlValidated] = t_poll;  // (and slot 4 its lists' arrival)
         sm.tl[blockIdx.x * 8 + kTlMerged] = __builtin_amdgcn_s_memrealtime();
     }
 #endif

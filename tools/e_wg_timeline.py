@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-workgroup timeline of config-E steps from the diagnostic timeline build
 (MS_TIMELINE=<file>: u64 [steps][256 workgroups][8], s_memrealtime ticks of
-10 ns, steps 0 .. 2047 of the last run; fields: 0 start, 1 swept + counted,
-2 worker wait done, 3 worker merges done, 4 validator done (workgroup 0)).
+10 ns, steps 0 .. 2047 of the last run; fields: 0 start, 2 sweep done / merge
+worker starts, 3 worker merges stored, 4 validator done (workgroup 0); merge
+workers (since r06aa) also 4 the first pod's lists all arrived, 1 its ranks merged).
 Workgroup 0 (the validator's) also stamps 1 bulk LDS copies landed, 2 wave-0
 loads landed (single-wave prologue), 3 stale nodes mapped, 6 prologue done,
 5 decisions done, 7 write-back issued; sweep workgroups 5 tile staged, 6 wave
@@ -29,7 +30,9 @@ def step_row(tl, s):
     t0 = b[live].min()
     us = lambda v: (v - t0) / 100.0  # noqa: E731
     r = {"step": s, "workgroups": int(live.sum()), "start_spread_us": float(us(b[live].max())), "t0": int(t0)}
-    for f, name in ((1, "swept"), (2, "waited"), (3, "merged")):
+    # merge workgroups (tagged lists, the default since round 5): 2 = its sweep done, 4 = the first
+    # pod's lists all arrived, 1 = that pod's ranks merged (round 6 r06aa on), 3 = its merges stored
+    for f, name in ((1, "ranked"), (2, "waited"), (3, "merged"), (4, "polled")):
         x = tl[s, 1:, f][live[1:]]
         x = x[x > 0]
         if len(x):
@@ -56,7 +59,8 @@ def main(path, out=None):
     rows = [r for r in (step_row(tl, s) for s in range(n_steps)) if r]
     window = [r for r in rows if 200 <= r["step"] < 216]
     keys = ["start_spread_us", "staged_median", "staged_max", "wave0_tasks_median", "all_tasks_median",
-            "all_tasks_max", "swept_median", "swept_max", "waited_median", "waited_max",
+            "all_tasks_max", "waited_median", "waited_max", "polled_median", "polled_max", "ranked_median",
+            "ranked_max",
             "merged_median", "merged_max", "val_dma", "val_loads", "val_mapped", "val_prologue", "val_decided",
             "val_written", "validator_done"]
     med = {k: float(np.median([r[k] for r in window if k in r])) for k in keys if any(k in r for r in window)}
@@ -69,7 +73,7 @@ def main(path, out=None):
     full = [r for r in rows if "validator_done" in r]
     if len(full) > 1:
         V = np.array([r["validator_done"] for r in full])
-        M = np.array([r.get("merged_max", r.get("swept_max", 0.0)) for r in full])
+        M = np.array([r.get("merged_max", 0.0) for r in full])
         t0 = np.array([r["t0"] for r in full], dtype=np.int64)
         D = np.diff(t0) / 100.0
         V1, M1 = V[:-1], M[:-1]
@@ -86,7 +90,7 @@ def main(path, out=None):
         with open(out, "w") as f:
             json.dump({"steps": window, "median": med, "run": run,
                        "per_step": [{"step": r["step"], "V": r.get("validator_done"),
-                                     "M": r.get("merged_max", r.get("swept_max")),
+                                     "M": r.get("merged_max"),
                                      "prologue": r.get("val_prologue")} for r in full]}, f, indent=0)
 
 
