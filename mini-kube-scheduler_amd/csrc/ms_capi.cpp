@@ -47,6 +47,14 @@ void free_all(ms_ctx *c) {
     (void)hipSetDevice(c->cfg.device);
     comm_free(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_table) {  // the columns live in it
+        (void)hipFree(c->d_table);
+        c->d_table = nullptr;
+        c->t.flags = c->t.digit = c->t.zone = c->t.label2 = nullptr;
+        c->t.taints = nullptr;
+        c->t.allowed_pods = c->t.pod_count = nullptr;
+        c->t.alloc_cpu = c->t.alloc_mem = c->t.req_cpu = c->t.req_mem = c->t.nz_cpu = c->t.nz_mem = nullptr;
+    }
     void *dev[] = {c->t.planes, c->t.zone, c->t.label2, c->d_terms, c->d_nam, c->t.flags, c->t.digit, c->t.allowed_pods, c->t.pod_count, c->t.alloc_cpu,
                    c->t.alloc_mem, c->t.req_cpu, c->t.req_mem, c->t.nz_cpu, c->t.nz_mem,
                    c->d_pods, c->d_res, c->d_keys, c->d_flags, c->d_deltas, c->d_one,
@@ -879,19 +887,46 @@ int ms_create(const ms_config *cfg, ms_ctx **out) {
     NodeTable &t = c->t;
     t.cap = cfg->max_nodes;
     t.base = cfg->node_base;
-    bool ok = hipMalloc((void **)&t.flags, n + kColumnPad) == hipSuccess &&
-              hipMalloc((void **)&t.digit, n + kColumnPad) == hipSuccess &&
-              hipMalloc((void **)&t.zone, n + kColumnPad) == hipSuccess &&
-              hipMalloc((void **)&t.label2, n + kColumnPad) == hipSuccess &&
-              hipMalloc((void **)&t.taints, n * 4) == hipSuccess &&
-              hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
-              hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
-              hipMalloc((void **)&t.alloc_cpu, n * 8) == hipSuccess &&
-              hipMalloc((void **)&t.alloc_mem, n * 8) == hipSuccess &&
-              hipMalloc((void **)&t.req_cpu, n * 8) == hipSuccess &&
-              hipMalloc((void **)&t.req_mem, n * 8) == hipSuccess &&
-              hipMalloc((void **)&t.nz_cpu, n * 8) == hipSuccess &&
-              hipMalloc((void **)&t.nz_mem, n * 8) == hipSuccess;
+#ifndef MS_TABLE_ONE_ALLOC
+#define MS_TABLE_ONE_ALLOC 1
+#endif
+    bool ok;
+    if (MS_TABLE_ONE_ALLOC) {
+        // Every column in one allocation, 2 MB-rounded: the validator's write-back
+        // stores one scattered row per lane into five of them each step, and
+        // separate allocations spread those rows over many more translation entries.
+        void **cols[] = {(void **)&t.flags,     (void **)&t.digit,     (void **)&t.zone,    (void **)&t.label2,
+                         (void **)&t.taints,    (void **)&t.allowed_pods, (void **)&t.pod_count, (void **)&t.alloc_cpu,
+                         (void **)&t.alloc_mem, (void **)&t.req_cpu,   (void **)&t.req_mem, (void **)&t.nz_cpu,
+                         (void **)&t.nz_mem};
+        const size_t bytes[] = {n + kColumnPad, n + kColumnPad, n + kColumnPad, n + kColumnPad, n * 4, n * 4, n * 4,
+                                n * 8,          n * 8,          n * 8,          n * 8,          n * 8, n * 8};
+        static_assert(sizeof(cols) / sizeof(cols[0]) == sizeof(bytes) / sizeof(bytes[0]), "one size per column");
+        size_t off[sizeof(bytes) / sizeof(bytes[0])], total = 0;
+        for (size_t i = 0; i < sizeof(bytes) / sizeof(bytes[0]); ++i) {
+            off[i] = total;
+            total += (bytes[i] + 255) & ~(size_t)255;
+        }
+        total = (total + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        ok = hipMalloc(&c->d_table, total) == hipSuccess;
+        if (ok)
+            for (size_t i = 0; i < sizeof(bytes) / sizeof(bytes[0]); ++i)
+                *cols[i] = static_cast<char *>(c->d_table) + off[i];
+    } else {
+        ok = hipMalloc((void **)&t.flags, n + kColumnPad) == hipSuccess &&
+             hipMalloc((void **)&t.digit, n + kColumnPad) == hipSuccess &&
+             hipMalloc((void **)&t.zone, n + kColumnPad) == hipSuccess &&
+             hipMalloc((void **)&t.label2, n + kColumnPad) == hipSuccess &&
+             hipMalloc((void **)&t.taints, n * 4) == hipSuccess &&
+             hipMalloc((void **)&t.allowed_pods, n * 4) == hipSuccess &&
+             hipMalloc((void **)&t.pod_count, n * 4) == hipSuccess &&
+             hipMalloc((void **)&t.alloc_cpu, n * 8) == hipSuccess &&
+             hipMalloc((void **)&t.alloc_mem, n * 8) == hipSuccess &&
+             hipMalloc((void **)&t.req_cpu, n * 8) == hipSuccess &&
+             hipMalloc((void **)&t.req_mem, n * 8) == hipSuccess &&
+             hipMalloc((void **)&t.nz_cpu, n * 8) == hipSuccess &&
+             hipMalloc((void **)&t.nz_mem, n * 8) == hipSuccess;
+    }
     t.gcap = (uint32_t)((n + kGroupRows - 1) / kGroupRows);
     ok = ok && hipMalloc((void **)&t.planes, sizeof(uint32_t) * kPlanes * t.gcap) == hipSuccess;
     if (!ok) return bail(MS_E_OOM, "node table allocation");

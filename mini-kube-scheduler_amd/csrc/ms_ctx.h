@@ -73,6 +73,7 @@ struct ms_ctx {
     unsigned long long *d_top_ext = nullptr;  // ranks 4..7 per pod (the validator's slow pods)
     uint32_t *d_merge_tags = nullptr;         // per pod of both merge-output sets: the in-step merge's tag
     uint32_t *d_merge_ctr = nullptr;          // the in-step merge's sweep-done counter
+    void *d_table = nullptr;                  // the node table's columns, one allocation (ms_create)
     uint32_t merge_tag = 0;                   // last in-step merge tag issued
     unsigned long long *d_tl = nullptr;       // MS_VSTAMPS: step timeline (MS_TIMELINE=<file> dumps it at ms_destroy)
     uint32_t *d_prev = nullptr;            // {count, rows} of the nodes each batch bound (x2)

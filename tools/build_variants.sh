@@ -10,12 +10,12 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unu
 mkdir -p build
 if [ "$VST" = vst ]; then
   $H -DMS_VSTAMPS $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
-  $H -DMS_VSTAMPS -c csrc/ms_capi.cpp -o build/ms_capi_vst.o
-  CAPI=build/ms_capi_vst.o
+  $H -DMS_VSTAMPS $DEFS -c csrc/ms_capi.cpp -o build/ms_capi_vst_$NAME.o  # (host-side -D flags too)
+  CAPI=build/ms_capi_vst_$NAME.o
 elif [ "$VST" = tl ]; then  # step timeline only (MS_TIMELINE=<file>; the host side reads it since round 6)
   $H -DMS_TIMELINE_ONLY $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
-  $H -DMS_TIMELINE_ONLY -c csrc/ms_capi.cpp -o build/ms_capi_tl.o
-  CAPI=build/ms_capi_tl.o
+  $H -DMS_TIMELINE_ONLY $DEFS -c csrc/ms_capi.cpp -o build/ms_capi_tl_$NAME.o
+  CAPI=build/ms_capi_tl_$NAME.o
 else
   $H $DEFS -c csrc/ms_kernels.hip -o build/ms_kernels_$NAME.o
   CAPI=build/ms_capi.o
