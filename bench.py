@@ -95,7 +95,7 @@ def parse():
                     help="rocprofv3 counter summary of the timed kernel (tools/profile_pp.sh)")
     ap.add_argument("--profile-shard-prefix", default=os.path.join(ROOT, "profiles", "r04zh_pmc_shard"),
                     help="N > 1: per-shard K1 counters <prefix><rows>.json (tools/profile_shards.sh)")
-    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r06w_pmc_E.json"),
+    ap.add_argument("--profile-json-e", default=os.path.join(ROOT, "profiles", "r06ag_pmc_E.json"),
                     help="rocprofv3 counter summary of config E's step kernel (tools/profile_e.sh)")
     return ap.parse_args()
 
@@ -450,11 +450,11 @@ def other_configs(args, dev, stream):
     # validator end V and merge-path end M from the step's start, and how often V is later
     step_split = None
     try:
-        with open(os.path.join(ROOT, "profiles", "r06w_e_wg_timeline_run.json")) as f:
+        with open(os.path.join(ROOT, "profiles", "r06ag_e_wg_timeline_run.json")) as f:
             run = json.load(f)["run"]
         step_split = {k: run[k] for k in ("step_us_mean", "V_mean", "M_mean", "frac_validator_critical",
                                           "gap_us_mean")}
-        step_split["profile"] = "profiles/r06w_e_wg_timeline_run.json"
+        step_split["profile"] = "profiles/r06ag_e_wg_timeline_run.json"
     except Exception:
         pass
     if pj and pj.get("nodes") == N and pj.get("pods") == P:
