@@ -2368,17 +2368,12 @@ __device__ __forceinline__ void validate_batch(SeqShared &S, const SeqArgs &va, 
     for (uint32_t o = lane; o < n_bl; o += 64) {
         const int64_t *r = S.rec[S.bl[o]];
         const uint32_t row = (uint32_t)r[F_ROW];
-#ifndef MS_DIAG_WB_SKIP
-#define MS_DIAG_WB_SKIP 0  // diagnostic builds only (wrong results): 1 no derived-row stores, 2 no column stores
-#endif
-        if (MS_DIAG_WB_SKIP != 2) {
-            t.req_cpu[row] = r[F_REQ_CPU];
-            t.req_mem[row] = r[F_REQ_MEM];
-            t.nz_cpu[row] = r[F_NZ_CPU];
-            t.nz_mem[row] = r[F_NZ_MEM];
-            t.pod_count[row] = (int32_t)r[F_CNT];
-        }
-        if (t.drow && MS_DIAG_WB_SKIP != 1)  // the next sweep's derived row (a sweep reading it now treats the row as stale)
+        t.req_cpu[row] = r[F_REQ_CPU];
+        t.req_mem[row] = r[F_REQ_MEM];
+        t.nz_cpu[row] = r[F_NZ_CPU];
+        t.nz_mem[row] = r[F_NZ_MEM];
+        t.pod_count[row] = (int32_t)r[F_CNT];
+        if (t.drow)  // the next sweep's derived row (a sweep reading it now treats the row as stale)
             t.drow[row] = make_drow(r[F_ALLOC_CPU], r[F_ALLOC_MEM], r[F_REQ_CPU], r[F_REQ_MEM], r[F_NZ_CPU],
                                     r[F_NZ_MEM], (int32_t)(r[F_ALLOWED] - r[F_CNT]), (uint32_t)r[F_FD]);
         if (prev_out) put_stale(prev_out, prev_recs_out, o, row, r);

@@ -1,4 +1,4 @@
-# round 6 diagnostic (wrong results by design): the validator's write-back phase with the derived-row
+# round 6 diagnostic (wrong results by design): the validator's write-back phase with the derived-row (the MS_DIAG_WB_SKIP switch it builds with was removed after the run; patch: git show 29227c1)
 # stores (vsk1) or the table-column stores (vsk2) left out, against the full write-back (vstamps);
 # validator phase stamps, and the timeline build without derived-row stores (tlsk1)
 set -o pipefail
